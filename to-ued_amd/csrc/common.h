@@ -1,0 +1,166 @@
+// Shared device helpers for the TO-UED MI355X hot path (gfx950 / CDNA4).
+//
+//  * threefry2x32-20 and the jax.random key-derivation helpers (split, random
+//    bits, uniform) — integer-exact restatement of jax 0.4.13's PRNG, the one
+//    every env transition and level index depends on.
+//  * Portable f32 exp/log: the exact op sequence of oracle/pmath.py, so that
+//    GPU and oracle agree bit-for-bit on everything that steers sampling.
+//    This TU family is compiled with -ffp-contract=off.
+//  * The packed level layout (int32[64] per level) and env-state SoA layout.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define TOUED_DEV __device__ __forceinline__
+
+// ----------------------------------------------------------------------------
+// Packed level record (oracle/levels.py pack_levels)
+enum {
+  L_MAX_STEPS = 0, L_GRID = 1, L_START = 2, L_NOBJS = 3, L_RANDRESP = 4, L_LIFETIME = 5,
+  L_BUFID = 6, L_OBJ_IDS = 8, L_STATIC = 16, L_REW = 24, L_PTERM = 32, L_PRESP = 40,
+  L_WALLS = 48, LEVEL_WORDS = 64
+};
+// Env state, SoA over workers: field f of worker i at state[f * n + i].
+enum { S_TIME = 0, S_POS = 1, S_EXISTS = 2, S_TERM = 3, S_OBJ = 4, S_FIELDS = 12 };
+#define TOUED_MAX_OBJS 8
+
+struct EnvSpec {
+  int max_grid;   // max_grid_size
+  int n_max;      // max_n_objs
+  int n_types;    // max_n_obj_types
+  int tabular;    // 1 = tabular observation / static respawn
+};
+
+// ----------------------------------------------------------------------------
+// threefry2x32-20 (jax/_src/prng.py _threefry2x32_lowering)
+TOUED_DEV uint32_t rotl32(uint32_t v, uint32_t r) { return (v << r) | (v >> (32u - r)); }
+
+TOUED_DEV uint2 threefry(uint32_t k0, uint32_t k1, uint32_t x0, uint32_t x1) {
+  const uint32_t k2 = k0 ^ k1 ^ 0x1BD11BDAu;
+  x0 += k0;
+  x1 += k1;
+#define TF_R(r) { x0 += x1; x1 = rotl32(x1, r); x1 ^= x0; }
+  TF_R(13) TF_R(15) TF_R(26) TF_R(6)  x0 += k1; x1 += k2 + 1u;
+  TF_R(17) TF_R(29) TF_R(16) TF_R(24) x0 += k2; x1 += k0 + 2u;
+  TF_R(13) TF_R(15) TF_R(26) TF_R(6)  x0 += k0; x1 += k1 + 3u;
+  TF_R(17) TF_R(29) TF_R(16) TF_R(24) x0 += k1; x1 += k2 + 4u;
+  TF_R(13) TF_R(15) TF_R(26) TF_R(6)  x0 += k2; x1 += k0 + 5u;
+#undef TF_R
+  return make_uint2(x0, x1);
+}
+
+// Element j of threefry_2x32(key, iota(count)) (odd counts padded with a 0 counter).
+TOUED_DEV uint32_t random_bits_at(uint2 key, uint32_t count, uint32_t j) {
+  const uint32_t nb = (count + 1u) >> 1;
+  const uint32_t b = (j < nb) ? j : j - nb;
+  const uint32_t hi = b + nb;
+  const uint2 y = threefry(key.x, key.y, b, hi < count ? hi : 0u);
+  return (j < nb) ? y.x : y.y;
+}
+
+// jax.random.split(key, num)[i]
+TOUED_DEV uint2 split_at(uint2 key, uint32_t num, uint32_t i) {
+  return make_uint2(random_bits_at(key, 2u * num, 2u * i), random_bits_at(key, 2u * num, 2u * i + 1u));
+}
+
+// split(key) -> (a, b): blocks (0,2),(1,3); out = [b0.x, b1.x, b0.y, b1.y]
+TOUED_DEV void split2(uint2 key, uint2& a, uint2& b) {
+  const uint2 y0 = threefry(key.x, key.y, 0u, 2u);
+  const uint2 y1 = threefry(key.x, key.y, 1u, 3u);
+  a = make_uint2(y0.x, y1.x);
+  b = make_uint2(y0.y, y1.y);
+}
+
+// split(key, 3): blocks (0,3),(1,4),(2,5); out = [b0.x,b1.x,b2.x,b0.y,b1.y,b2.y]
+TOUED_DEV void split3(uint2 key, uint2& a, uint2& b, uint2& c) {
+  const uint2 y0 = threefry(key.x, key.y, 0u, 3u);
+  const uint2 y1 = threefry(key.x, key.y, 1u, 4u);
+  const uint2 y2 = threefry(key.x, key.y, 2u, 5u);
+  a = make_uint2(y0.x, y1.x);
+  b = make_uint2(y2.x, y0.y);
+  c = make_uint2(y1.y, y2.y);
+}
+
+// random_bits(key, 32, ()) : single element -> block (0, 0 pad), first output.
+TOUED_DEV uint32_t bits1(uint2 key) { return threefry(key.x, key.y, 0u, 0u).x; }
+
+TOUED_DEV float bits_to_unit(uint32_t bits) {
+  return __uint_as_float((bits >> 9) | 0x3F800000u) - 1.0f;
+}
+
+// jax.random.uniform(minval, maxval): max(lo, f*(hi-lo)+lo), no contraction.
+TOUED_DEV float uniform_from_bits(uint32_t bits, float lo, float hi) {
+  const float f = bits_to_unit(bits);
+  return fmaxf(lo, __fadd_rn(__fmul_rn(f, __fsub_rn(hi, lo)), lo));
+}
+
+// ----------------------------------------------------------------------------
+// Portable math (oracle/pmath.py)
+TOUED_DEV float pow2i(int k) { return __uint_as_float((uint32_t)(k + 127) << 23); }
+
+TOUED_DEV float pexp(float x) {
+  if (x != x) return x;
+  if (x > 88.72283905206835f) return __builtin_inff();
+  if (x < -103.972084f) return 0.0f;
+  const float k = rintf(__fmul_rn(x, 1.44269504088896341f));
+  float r = __fsub_rn(x, __fmul_rn(k, 0.693145751953125f));
+  r = __fsub_rn(r, __fmul_rn(k, 1.428606765330187045e-06f));
+  const float C[8] = {1.0f, 1.0f, 0.5f, (float)(1.0 / 6.0), (float)(1.0 / 24.0), (float)(1.0 / 120.0),
+                      (float)(1.0 / 720.0), (float)(1.0 / 5040.0)};
+  float p = C[7];
+#pragma unroll
+  for (int i = 6; i >= 0; --i) p = __fadd_rn(__fmul_rn(p, r), C[i]);
+  int ki = (int)k;
+  ki = ki < -200 ? -200 : (ki > 200 ? 200 : ki);
+  const int k1 = (ki >= 0) ? (ki / 2) : -((-ki + 1) / 2);  // floor division
+  const int k2 = ki - k1;
+  const int c1 = k1 < -126 ? -126 : (k1 > 127 ? 127 : k1);
+  const int c2 = k2 < -126 ? -126 : (k2 > 127 ? 127 : k2);
+  return __fmul_rn(__fmul_rn(p, pow2i(c1)), pow2i(c2));
+}
+
+TOUED_DEV float plog(float x) {
+  if (x != x) return x;
+  if (x == 0.0f) return -__builtin_inff();
+  if (x < 0.0f) return __builtin_nanf("");
+  if (__builtin_isinf(x)) return x;
+  const bool sub = x < 1.17549435e-38f;
+  const float xs = sub ? __fmul_rn(x, 8388608.0f) : x;
+  const uint32_t bits = __float_as_uint(xs);
+  int e = (int)((bits >> 23) & 0xFFu) - 127;
+  if (sub) e -= 23;
+  float m = __uint_as_float((bits & 0x7FFFFFu) | 0x3F800000u);
+  if (m > 1.41421356237f) { m = __fmul_rn(m, 0.5f); e += 1; }
+  const float f = __fsub_rn(m, 1.0f);
+  const float s = __fdiv_rn(f, __fadd_rn(2.0f, f));
+  const float z = __fmul_rn(s, s);
+  const float w = __fmul_rn(z, z);
+  const float t1 = __fmul_rn(w, __fadd_rn(0.40000972152f, __fmul_rn(w, 0.24279078841f)));
+  const float t2 = __fmul_rn(z, __fadd_rn(0.66666662693f, __fmul_rn(w, 0.28498786688f)));
+  const float R = __fadd_rn(t2, t1);
+  const float hfsq = __fmul_rn(__fmul_rn(0.5f, f), f);
+  const float dk = (float)e;
+  const float inner = __fadd_rn(__fmul_rn(s, __fadd_rn(hfsq, R)), __fmul_rn(dk, 1.428606765330187045e-06f));
+  return __fsub_rn(__fmul_rn(dk, 0.693145751953125f), __fsub_rn(__fsub_rn(hfsq, inner), f));
+}
+
+// ----------------------------------------------------------------------------
+// Error reporting for the C ABI
+namespace toued {
+void set_error(const char* fmt, ...);
+}
+#define TOUED_CHECK_LAUNCH()                                                   \
+  do {                                                                         \
+    hipError_t _e = hipGetLastError();                                         \
+    if (_e != hipSuccess) {                                                    \
+      toued::set_error("%s: launch failed: %s", __func__, hipGetErrorString(_e)); \
+      return -2;                                                               \
+    }                                                                          \
+  } while (0)
+#define TOUED_REQUIRE(cond, ...)                                               \
+  do {                                                                         \
+    if (!(cond)) {                                                             \
+      toued::set_error(__VA_ARGS__);                                           \
+      return -1;                                                               \
+    }                                                                          \
+  } while (0)

@@ -1,0 +1,464 @@
+// GridWorld env step/reset and the fused persistent rollout — HIP for gfx950.
+//
+// Restates environments/gridworld/gridworld.py:72-211 (step_env/reset_env/
+// get_obs), the gymnax 0.0.6 auto-reset wrapper (Environment.step), and
+// environments/rollout.py:38-102 (batch_reset / batch_rollout / policy_step)
+// with the linear-softmax tabular actor of models/agent.py:7-17.
+//
+// Mapping: one lane = one env worker.  With W % 64 == 0 every wavefront holds
+// the workers of a single agent, so the level record and the actor's
+// time-feature row are wave-uniform (readfirstlane -> scalar loads).  The env
+// state lives in VGPRs for the whole T-step scan; the trajectory is written
+// lane-contiguously ([agent][t][worker]) so every store is coalesced.
+#include "common.h"
+
+namespace {
+
+struct EnvState {
+  int time, pos, exists, early_term;
+  int obj[TOUED_MAX_OBJS];
+};
+
+TOUED_DEV int lev_i(const int* lev, int w) { return lev[w]; }
+TOUED_DEV float lev_f(const int* lev, int w) { return __int_as_float(lev[w]); }
+
+TOUED_DEV bool wall_at(const int* lev, int cell) {
+  return (((uint32_t)lev[L_WALLS + (cell >> 5)]) >> (cell & 31)) & 1u;
+}
+
+// _get_next_pos, gridworld.py:138-146
+TOUED_DEV int next_pos(const int* lev, int pos, int action) {
+  const int g = lev_i(lev, L_GRID);
+  const int top = pos < g, bottom = pos >= g * (g - 1);
+  const int left = (pos % g) == 0, right = (pos % g) == g - 1;
+  const int step = (action == 0) * (1 - top) * -g + (action == 1) * (1 - bottom) * g +
+                   (action == 2) * (1 - left) * -1 + (action == 3) * (1 - right) * 1;
+  const int nxt = pos + step;
+  return wall_at(lev, nxt) ? pos : nxt;
+}
+
+// Gumbel top-k choice over the max_grid^2 cells (jax.random.choice replace=False, p given):
+// g_c = -gumbel(key)_c - log(p_c), stable ascending argsort, first NMAX indices.
+// valid(c) decides p_c = valid/count.  Streaming insertion keeps (value, index) lexicographic order.
+template <int NMAX, typename ValidFn>
+TOUED_DEV void gumbel_topk(uint2 key, int g2, ValidFn valid, int* out) {
+  int cnt = 0;
+  for (int c = 0; c < g2; ++c) cnt += valid(c) ? 1 : 0;
+  const float pv = __fdiv_rn(1.0f, (float)cnt);
+  const float lp_valid = plog(pv);
+  float bv[NMAX];
+  int bi[NMAX];
+#pragma unroll
+  for (int j = 0; j < NMAX; ++j) { bv[j] = __builtin_inff(); bi[j] = 0x7fffffff; }
+  const float tiny = 1.17549435e-38f;
+  for (int c = 0; c < g2; ++c) {
+    const float u = uniform_from_bits(random_bits_at(key, (uint32_t)g2, (uint32_t)c), tiny, 1.0f);
+    const float gmb = -plog(-plog(u));
+    const float g = valid(c) ? __fsub_rn(-gmb, lp_valid) : __builtin_inff();
+    // insert (g, c) if it precedes the current last entry
+    if (g < bv[NMAX - 1] || (g == bv[NMAX - 1] && c < bi[NMAX - 1])) {
+      float cv = g;
+      int ci = c;
+#pragma unroll
+      for (int j = 0; j < NMAX; ++j) {
+        const bool before = (cv < bv[j]) || (cv == bv[j] && ci < bi[j]);
+        if (before) {
+          const float tv = bv[j]; const int ti = bi[j];
+          bv[j] = cv; bi[j] = ci; cv = tv; ci = ti;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NMAX; ++j) out[j] = bi[j];
+}
+
+// _get_valid_obj_idxs, gridworld.py:149-155, with the isin(idx, bool walls) quirk
+struct ValidCells {
+  const int* lev; int pos; int g2grid; bool has_false, has_true; int excl[TOUED_MAX_OBJS]; int n_excl;
+  TOUED_DEV bool operator()(int c) const {
+    bool v = (c != pos) && (c < g2grid);
+    v = v && !((c == 0 && has_false) || (c == 1 && has_true));
+    for (int i = 0; i < n_excl; ++i) v = v && (c != excl[i]);
+    return v;
+  }
+};
+
+TOUED_DEV ValidCells make_valid(const int* lev, int G2, int pos) {
+  ValidCells vc;
+  vc.lev = lev; vc.pos = pos;
+  const int g = lev_i(lev, L_GRID);
+  vc.g2grid = g * g;
+  bool any_t = false, any_f = false;
+  for (int w = 0; w < 8; ++w) {
+    const int lo = w * 32;
+    if (lo >= G2) break;
+    const int nb = (G2 - lo) < 32 ? (G2 - lo) : 32;
+    const uint32_t mask = nb == 32 ? 0xffffffffu : ((1u << nb) - 1u);
+    const uint32_t bits = (uint32_t)lev[L_WALLS + w] & mask;
+    any_t |= bits != 0u;
+    any_f |= bits != mask;
+  }
+  vc.has_true = any_t; vc.has_false = any_f; vc.n_excl = 0;
+  return vc;
+}
+
+// reset_env, gridworld.py:157-182
+template <int NMAX, bool TAB>
+TOUED_DEV void reset_env(const EnvSpec& sp, const int* lev, uint2 key, EnvState& s) {
+  const int G2 = sp.max_grid * sp.max_grid;
+  s.time = 0;
+  s.pos = lev_i(lev, L_START);
+  s.early_term = 0;
+  const int nobj = lev_i(lev, L_NOBJS);
+  s.exists = 0;
+#pragma unroll
+  for (int i = 0; i < NMAX; ++i) {
+    s.obj[i] = lev_i(lev, L_STATIC + i);
+    if (i < nobj) s.exists |= 1 << i;
+  }
+  if (!TAB) {
+    if (lev_i(lev, L_RANDRESP)) {
+      uint2 obj_key, pos_key;
+      split2(key, obj_key, pos_key);
+      ValidCells vc = make_valid(lev, G2, s.pos);
+      int pick[NMAX];
+      gumbel_topk<NMAX>(obj_key, G2, vc, pick);
+#pragma unroll
+      for (int i = 0; i < NMAX; ++i) s.obj[i] = pick[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NMAX; ++i) s.obj[i] += lev_i(lev, L_OBJ_IDS + i) * G2;
+}
+
+// gymnax Environment.step -> step_env (gridworld.py:72-136) + auto-reset select.
+template <int NMAX, bool TAB>
+TOUED_DEV void env_step(const EnvSpec& sp, const int* lev, uint2 key, EnvState& s, int action,
+                        float& reward, bool& done) {
+  const int G2 = sp.max_grid * sp.max_grid;
+  uint2 key_s, key_r;
+  split2(key, key_s, key_r);
+  uint2 term_key, respawn_key, obj_key;
+  split3(key_s, term_key, respawn_key, obj_key);
+
+  const int pos = next_pos(lev, s.pos, action);
+  int old[NMAX];
+  int collected = 0;
+#pragma unroll
+  for (int i = 0; i < NMAX; ++i) {
+    old[i] = s.obj[i] - lev_i(lev, L_OBJ_IDS + i) * G2;
+    if (((s.exists >> i) & 1) && old[i] == pos) collected |= 1 << i;
+  }
+  // respawn = bernoulli(respawn_key, p_respawn[obj_ids]) over NMAX draws
+  int respawn = 0;
+  {
+    constexpr uint32_t nb = (NMAX + 1) / 2;
+#pragma unroll
+    for (uint32_t b = 0; b < nb; ++b) {
+      const uint32_t hi = b + nb;
+      const uint2 y = threefry(respawn_key.x, respawn_key.y, b, hi < (uint32_t)NMAX ? hi : 0u);
+      const float u0 = bits_to_unit(y.x);
+      if (u0 < lev_f(lev, L_PRESP + b)) respawn |= 1 << b;
+      if (hi < (uint32_t)NMAX) {
+        const float u1 = bits_to_unit(y.y);
+        if (u1 < lev_f(lev, L_PRESP + hi)) respawn |= 1 << hi;
+      }
+    }
+  }
+  int exists = s.exists | respawn;
+  int newpos[NMAX];
+#pragma unroll
+  for (int i = 0; i < NMAX; ++i) newpos[i] = old[i];
+  if (!TAB) {
+    const int use_new = (~s.exists) & respawn & ((1 << NMAX) - 1);
+    if (lev_i(lev, L_RANDRESP) && use_new) {
+      ValidCells vc = make_valid(lev, G2, pos);
+#pragma unroll
+      for (int i = 0; i < NMAX; ++i) vc.excl[i] = old[i];
+      vc.n_excl = NMAX;
+      int pick[NMAX];
+      gumbel_topk<NMAX>(obj_key, G2, vc, pick);
+#pragma unroll
+      for (int i = 0; i < NMAX; ++i) if ((use_new >> i) & 1) newpos[i] = pick[i];
+    }
+  }
+  const int nobj = lev_i(lev, L_NOBJS);
+  const int used = nobj >= 32 ? -1 : ((1 << nobj) - 1);
+  exists = exists & ~collected & used;
+
+  float p_t = 0.0f, rew = 0.0f;
+#pragma unroll
+  for (int i = 0; i < NMAX; ++i) {
+    const float ci = ((collected >> i) & 1) ? 1.0f : 0.0f;
+    p_t = __fadd_rn(p_t, __fmul_rn(lev_f(lev, L_PTERM + i), ci));
+    if ((collected >> i) & 1) rew = __fadd_rn(rew, lev_f(lev, L_REW + i));
+  }
+  const float ut = bits_to_unit(bits1(term_key));
+  const int term = (ut < p_t) || s.early_term;
+  const int time = s.time + 1;
+  done = (time >= lev_i(lev, L_MAX_STEPS)) || term;
+  reward = rew;
+  if (done) {
+    reset_env<NMAX, TAB>(sp, lev, key_r, s);
+  } else {
+    s.time = time;
+    s.pos = pos;
+    s.exists = exists;
+    s.early_term = term;
+#pragma unroll
+    for (int i = 0; i < NMAX; ++i) s.obj[i] = newpos[i] + lev_i(lev, L_OBJ_IDS + i) * G2;
+  }
+}
+
+template <int NMAX>
+TOUED_DEV void load_state(const int* st, int n, int i, EnvState& s) {
+  s.time = st[S_TIME * n + i];
+  s.pos = st[S_POS * n + i];
+  s.exists = st[S_EXISTS * n + i];
+  s.early_term = st[S_TERM * n + i];
+#pragma unroll
+  for (int k = 0; k < NMAX; ++k) s.obj[k] = st[(S_OBJ + k) * n + i];
+}
+
+template <int NMAX>
+TOUED_DEV void store_state(int* st, int n, int i, const EnvState& s) {
+  st[S_TIME * n + i] = s.time;
+  st[S_POS * n + i] = s.pos;
+  st[S_EXISTS * n + i] = s.exists;
+  st[S_TERM * n + i] = s.early_term;
+#pragma unroll
+  for (int k = 0; k < NMAX; ++k) st[(S_OBJ + k) * n + i] = s.obj[k];
+}
+
+TOUED_DEV int tab_index(const EnvSpec& sp, const EnvState& s) {
+  return s.pos + sp.max_grid * sp.max_grid * s.exists;
+}
+
+// ---------------------------------------------------------------- kernels
+// gymnax reset for n independent (key, level) pairs; worker i uses level i / W.
+template <int NMAX, bool TAB>
+__global__ void __launch_bounds__(256) k_gw_reset(EnvSpec sp, const int* __restrict__ levels, int W,
+                                                  const uint32_t* __restrict__ keys, int* __restrict__ state,
+                                                  int* __restrict__ obs_idx, int* __restrict__ obs_time, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int* lev = levels + (size_t)(i / W) * LEVEL_WORDS;
+  EnvState s;
+  reset_env<NMAX, TAB>(sp, lev, make_uint2(keys[2 * i], keys[2 * i + 1]), s);
+  store_state<NMAX>(state, n, i, s);
+  obs_idx[i] = tab_index(sp, s);
+  obs_time[i] = s.time;
+}
+
+template <int NMAX, bool TAB>
+__global__ void __launch_bounds__(256) k_gw_step(EnvSpec sp, const int* __restrict__ levels, int W,
+                                                 const uint32_t* __restrict__ keys, int* __restrict__ state,
+                                                 const int* __restrict__ actions, int* __restrict__ obs_idx,
+                                                 int* __restrict__ obs_time, float* __restrict__ reward,
+                                                 uint8_t* __restrict__ done, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int* lev = levels + (size_t)(i / W) * LEVEL_WORDS;
+  EnvState s;
+  load_state<NMAX>(state, n, i, s);
+  float r; bool d;
+  env_step<NMAX, TAB>(sp, lev, make_uint2(keys[2 * i], keys[2 * i + 1]), s, actions[i], r, d);
+  store_state<NMAX>(state, n, i, s);
+  obs_idx[i] = tab_index(sp, s);
+  obs_time[i] = s.time;
+  reward[i] = r;
+  done[i] = d ? 1 : 0;
+}
+
+// RolloutWrapper.batch_reset: worker keys = split(agent_key, W)[w].
+template <int NMAX, bool TAB>
+__global__ void __launch_bounds__(256) k_batch_reset(EnvSpec sp, const int* __restrict__ levels,
+                                                     const uint32_t* __restrict__ agent_keys, int W,
+                                                     int* __restrict__ state, int* __restrict__ obs_idx,
+                                                     int* __restrict__ obs_time, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int a = i / W, w = i - a * W;
+  const int* lev = levels + (size_t)a * LEVEL_WORDS;
+  const uint2 key = split_at(make_uint2(agent_keys[2 * a], agent_keys[2 * a + 1]), (uint32_t)W, (uint32_t)w);
+  EnvState s;
+  reset_env<NMAX, TAB>(sp, lev, key, s);
+  store_state<NMAX>(state, n, i, s);
+  obs_idx[i] = tab_index(sp, s);
+  obs_time[i] = s.time;
+}
+
+// Linear softmax actor on a compact tabular obs: logits = W[idx] + (f32(t)*0.001)*W[D-1].
+TOUED_DEV void actor_probs5(const float* __restrict__ tab, const float* last, int idx, int t, float* p) {
+  const float c = __fmul_rn((float)t, 0.001f);
+  float l[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) l[j] = __fadd_rn(tab[(size_t)idx * 5 + j], __fmul_rn(c, last[j]));
+  float m = l[0];
+#pragma unroll
+  for (int j = 1; j < 5; ++j) m = fmaxf(m, l[j]);
+  float e[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) e[j] = pexp(__fsub_rn(l[j], m));
+  float s = e[0];
+#pragma unroll
+  for (int j = 1; j < 5; ++j) s = __fadd_rn(s, e[j]);
+#pragma unroll
+  for (int j = 0; j < 5; ++j) p[j] = __fdiv_rn(e[j], s);
+}
+
+// jax.random.choice(key, 5, p=p): searchsorted(cumsum_assoc(p), c4*(1-u), 'left')
+TOUED_DEV int choice5(uint2 key, const float* p) {
+  const float c0 = p[0];
+  const float c1 = __fadd_rn(p[0], p[1]);
+  const float c2 = __fadd_rn(c1, p[2]);
+  const float c3 = __fadd_rn(c1, __fadd_rn(p[2], p[3]));
+  const float c4 = __fadd_rn(c3, p[4]);
+  const float u = bits_to_unit(bits1(key));
+  const float r = __fmul_rn(c4, __fsub_rn(1.0f, u));
+  return (c0 < r) + (c1 < r) + (c2 < r) + (c3 < r) + (c4 < r);
+}
+
+// Fused rollout: T policy steps per worker, state in registers.
+// traj_idx/time: [N][T+1][W]; action/done u8 [N][T][W]; reward f32 [N][T][W].
+template <int NMAX, bool TAB, bool UNIFORM>
+__global__ void __launch_bounds__(256) k_rollout(EnvSpec sp, const int* __restrict__ levels,
+                                                 const float* __restrict__ theta, int D,
+                                                 const uint32_t* __restrict__ agent_keys, int* __restrict__ state,
+                                                 int T, int W, int n, int* __restrict__ traj_idx,
+                                                 int* __restrict__ traj_time, uint8_t* __restrict__ traj_action,
+                                                 float* __restrict__ traj_reward, uint8_t* __restrict__ traj_done,
+                                                 float* __restrict__ cum_return) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int a = i / W;
+  if (UNIFORM) a = __builtin_amdgcn_readfirstlane(a);
+  const int w = i - a * W;
+  const int* lev = levels + (size_t)a * LEVEL_WORDS;
+  const float* tab = theta + (size_t)a * D * 5;
+  float last[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) last[j] = tab[(size_t)(D - 1) * 5 + j];
+  uint2 rng = split_at(make_uint2(agent_keys[2 * a], agent_keys[2 * a + 1]), (uint32_t)W, (uint32_t)w);
+  EnvState s;
+  load_state<NMAX>(state, n, i, s);
+  float cum = 0.0f, valid = 1.0f;
+  const size_t base_o = (size_t)a * (T + 1) * W + w;
+  const size_t base_t = (size_t)a * T * W + w;
+  for (int t = 0; t < T; ++t) {
+    uint2 sub;
+    split2(rng, rng, sub);
+    const int idx = tab_index(sp, s);
+    const int tm = s.time;
+    float p[5];
+    actor_probs5(tab, last, idx, tm, p);
+    const int action = choice5(sub, p);
+    split2(rng, rng, sub);
+    float r; bool d;
+    env_step<NMAX, TAB>(sp, lev, sub, s, action, r, d);
+    cum = __fadd_rn(cum, __fmul_rn(r, valid));
+    valid = __fmul_rn(valid, d ? 0.0f : 1.0f);
+    traj_idx[base_o + (size_t)t * W] = idx;
+    traj_time[base_o + (size_t)t * W] = tm;
+    traj_action[base_t + (size_t)t * W] = (uint8_t)action;
+    traj_reward[base_t + (size_t)t * W] = r;
+    traj_done[base_t + (size_t)t * W] = d ? 1 : 0;
+  }
+  traj_idx[base_o + (size_t)T * W] = tab_index(sp, s);
+  traj_time[base_o + (size_t)T * W] = s.time;
+  store_state<NMAX>(state, n, i, s);
+  cum_return[i] = cum;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- dispatch
+#define TOUED_DISPATCH_NMAX(NM, TAB, ...)                    \
+  switch (NM) {                                              \
+    case 1: { constexpr int NMAX = 1; __VA_ARGS__; } break;  \
+    case 2: { constexpr int NMAX = 2; __VA_ARGS__; } break;  \
+    case 3: { constexpr int NMAX = 3; __VA_ARGS__; } break;  \
+    case 4: { constexpr int NMAX = 4; __VA_ARGS__; } break;  \
+    case 5: { constexpr int NMAX = 5; __VA_ARGS__; } break;  \
+    default: break;                                          \
+  }
+
+#define TOUED_DISPATCH(sp, ...)                                                  \
+  if ((sp).tabular) {                                                            \
+    constexpr bool TAB = true;                                                   \
+    TOUED_DISPATCH_NMAX((sp).n_max, TAB, __VA_ARGS__)                            \
+  } else {                                                                       \
+    constexpr bool TAB = false;                                                  \
+    TOUED_DISPATCH_NMAX((sp).n_max, TAB, __VA_ARGS__)                            \
+  }
+
+static int check_spec(const EnvSpec& sp) {
+  TOUED_REQUIRE(sp.n_max >= 1 && sp.n_max <= 5, "env spec: max_n_objs=%d unsupported (1..5)", sp.n_max);
+  TOUED_REQUIRE(sp.max_grid >= 1 && sp.max_grid * sp.max_grid <= 256, "env spec: max_grid_size=%d unsupported",
+                sp.max_grid);
+  TOUED_REQUIRE(sp.n_types >= 1 && sp.n_types <= 8, "env spec: max_n_obj_types=%d unsupported", sp.n_types);
+  return 0;
+}
+
+static inline int nblk(long n) { return (int)((n + 255) / 256); }
+
+extern "C" {
+
+int toued_gw_reset(EnvSpec sp, const int* levels, int W, const uint32_t* keys, int* state, int* obs_idx,
+                   int* obs_time, int n, hipStream_t stream) {
+  if (int e = check_spec(sp)) return e;
+  TOUED_REQUIRE(n >= 0 && W >= 1, "toued_gw_reset: bad sizes n=%d W=%d", n, W);
+  if (n == 0) return 0;
+  TOUED_DISPATCH(sp, hipLaunchKernelGGL((k_gw_reset<NMAX, TAB>), dim3(nblk(n)), dim3(256), 0, stream, sp, levels,
+                                        W, keys, state, obs_idx, obs_time, n));
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_gw_step(EnvSpec sp, const int* levels, int W, const uint32_t* keys, int* state, const int* actions,
+                  int* obs_idx, int* obs_time, float* reward, uint8_t* done, int n, hipStream_t stream) {
+  if (int e = check_spec(sp)) return e;
+  TOUED_REQUIRE(n >= 0 && W >= 1, "toued_gw_step: bad sizes n=%d W=%d", n, W);
+  if (n == 0) return 0;
+  TOUED_DISPATCH(sp, hipLaunchKernelGGL((k_gw_step<NMAX, TAB>), dim3(nblk(n)), dim3(256), 0, stream, sp, levels, W,
+                                        keys, state, actions, obs_idx, obs_time, reward, done, n));
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_batch_reset(EnvSpec sp, const int* levels, const uint32_t* agent_keys, int n_agents, int W, int* state,
+                      int* obs_idx, int* obs_time, hipStream_t stream) {
+  if (int e = check_spec(sp)) return e;
+  TOUED_REQUIRE(n_agents >= 0 && W >= 1, "toued_batch_reset: bad sizes N=%d W=%d", n_agents, W);
+  const int n = n_agents * W;
+  if (n == 0) return 0;
+  TOUED_DISPATCH(sp, hipLaunchKernelGGL((k_batch_reset<NMAX, TAB>), dim3(nblk(n)), dim3(256), 0, stream, sp, levels,
+                                        agent_keys, W, state, obs_idx, obs_time, n));
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_rollout(EnvSpec sp, const int* levels, const float* theta, int D, const uint32_t* agent_keys, int* state,
+                  int n_agents, int W, int T, int* traj_idx, int* traj_time, uint8_t* traj_action,
+                  float* traj_reward, uint8_t* traj_done, float* cum_return, hipStream_t stream) {
+  if (int e = check_spec(sp)) return e;
+  TOUED_REQUIRE(n_agents >= 0 && W >= 1 && T >= 0, "toued_rollout: bad sizes N=%d W=%d T=%d", n_agents, W, T);
+  TOUED_REQUIRE(sp.tabular, "toued_rollout: the linear tabular actor needs a tabular env");
+  TOUED_REQUIRE(D == sp.max_grid * sp.max_grid * (1 << sp.n_max) + 1, "toued_rollout: D=%d != obs_dim", D);
+  const int n = n_agents * W;
+  if (n == 0) return 0;
+  if (W % 64 == 0) {
+    TOUED_DISPATCH(sp, hipLaunchKernelGGL((k_rollout<NMAX, TAB, true>), dim3(nblk(n)), dim3(256), 0, stream, sp,
+                                          levels, theta, D, agent_keys, state, T, W, n, traj_idx, traj_time,
+                                          traj_action, traj_reward, traj_done, cum_return));
+  } else {
+    TOUED_DISPATCH(sp, hipLaunchKernelGGL((k_rollout<NMAX, TAB, false>), dim3(nblk(n)), dim3(256), 0, stream, sp,
+                                          levels, theta, D, agent_keys, state, T, W, n, traj_idx, traj_time,
+                                          traj_action, traj_reward, traj_done, cum_return));
+  }
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

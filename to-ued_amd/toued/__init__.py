@@ -1,0 +1,10 @@
+"""toued — MI355X-native hot path of nmonette/TO-UED (GROOVE / LPG / TA-LPG).
+
+Python host mirroring the reference's operator interfaces (gymnax GridWorld,
+RolloutWrapper, LevelSampler, make_lpg_train_step, train.py flags) over the C
+ABI of libtoued_hip.so (include/toued.h).  PyTorch provides device memory,
+streams and torch.distributed; the computation is in the HIP kernels.
+"""
+from ._lib import ToUEDError, lib  # noqa: F401
+
+__all__ = ["ToUEDError", "lib"]

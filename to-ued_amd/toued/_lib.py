@@ -1,0 +1,96 @@
+"""ctypes binding of libtoued_hip.so (the C ABI declared in include/toued.h).
+
+The product path has no CPU fallback: if the library is missing or a call
+fails, ``ToUEDError`` is raised.  Device buffers are torch tensors; the
+current torch HIP stream is passed to every call.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch
+
+LIB_PATH = Path(os.environ.get("TOUED_LIB", Path(__file__).resolve().parent / "libtoued_hip.so"))
+
+
+class ToUEDError(RuntimeError):
+    pass
+
+
+class EnvSpecC(ctypes.Structure):
+    _fields_ = [("max_grid", ctypes.c_int), ("n_max", ctypes.c_int), ("n_types", ctypes.c_int),
+                ("tabular", ctypes.c_int)]
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+_U = ctypes.c_uint32
+
+# name -> argtypes (restype int unless listed in _RESTYPES)
+_SIGS = {
+    "toued_split": [_P, _I, _I, _P, _P],
+    "toued_fold_in": [_P, _I, _U, _P, _P],
+    "toued_random_bits": [_P, _I, _I, _P, _P],
+    "toued_uniform": [_P, _I, _I, _F, _F, _P, _P],
+    "toued_mode_program_bytes": [],
+    "toued_level_gen": [_P, _P, _P, _P, _P, _I, _P],
+    "toued_gw_reset": [EnvSpecC, _P, _I, _P, _P, _P, _P, _I, _P],
+    "toued_gw_step": [EnvSpecC, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P],
+    "toued_batch_reset": [EnvSpecC, _P, _P, _I, _I, _P, _P, _P, _P],
+    "toued_rollout": [EnvSpecC, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "toued_last_error": [],
+    "toued_abi_version": [],
+}
+_RESTYPES = {"toued_last_error": ctypes.c_char_p, "toued_mode_program_bytes": ctypes.c_size_t}
+
+_lib = None
+
+
+def lib():
+    """Load the library once (raises ToUEDError if it is absent)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise ToUEDError(f"libtoued_hip.so not found at {LIB_PATH}; run `python to-ued_amd/build.py` "
+                             "(there is no CPU fallback for the hot path)")
+        L = ctypes.CDLL(str(LIB_PATH))
+        for name, args in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def ptr(t) -> int | None:
+    if t is None:
+        return None
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"expected a tensor, got {type(t)}")
+    if not t.is_contiguous():
+        raise ToUEDError("toued: tensor arguments must be contiguous")
+    return t.data_ptr()
+
+
+def stream_ptr():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def call(name: str, *args):
+    fn = getattr(lib(), name)
+    rc = fn(*args)
+    if rc != 0:
+        msg = lib().toued_last_error().decode(errors="replace")
+        raise ToUEDError(f"{name} failed ({rc}): {msg}")
+    return rc
+
+
+def env_spec_c(spec) -> EnvSpecC:
+    return EnvSpecC(spec.max_grid_size, spec.max_n_objs, spec.max_n_obj_types, int(spec.tabular))

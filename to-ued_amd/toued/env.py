@@ -1,0 +1,142 @@
+"""GridWorld on MI355X: level generation and the gymnax env API over the C ABI.
+
+Mirrors environments/gridworld/gridworld.py (GridWorld: reset/step),
+environments/environments.py:22-63 (get_env / reset_env_params / get_env_spec /
+get_agent_hypers) and configs.py's mode tables — batched ("vmapped") over
+levels/workers, with all state resident on the GPU.
+
+Levels are packed int32[n, 64] tensors (include/toued.h); env state is
+int32[12, n] SoA; observations are compact (tab_idx, time) int32 pairs.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from . import modes as M
+
+STATE_FIELDS = 12
+LEVEL_WORDS = 64
+# packed-level word offsets (csrc/common.h)
+L_MAX_STEPS, L_GRID, L_START, L_NOBJS, L_RANDRESP, L_LIFETIME, L_BUFID = 0, 1, 2, 3, 4, 5, 6
+L_OBJ_IDS, L_STATIC, L_REW, L_PTERM, L_PRESP, L_WALLS = 8, 16, 24, 32, 40, 48
+
+
+@dataclass(frozen=True)
+class EnvSpec:
+    """Static env kwargs (configs.py:430-544)."""
+    max_grid_size: int
+    max_n_objs: int
+    max_n_obj_types: int
+    tabular: bool
+
+    @property
+    def g2(self) -> int:
+        return self.max_grid_size ** 2
+
+    @property
+    def obs_dim(self) -> int:
+        # gridworld.py:230-235
+        if self.tabular:
+            return self.g2 * (2 ** self.max_n_objs) + 1
+        return self.g2 * (self.max_n_obj_types + 1) + 1
+
+    @property
+    def num_actions(self) -> int:
+        return 5  # gridworld.py:218-222
+
+
+def get_env_spec(env_mode: str):
+    """environments.py:40-55: (env spec, max_rollout_len, max_lifetime)."""
+    if env_mode not in M.ENV_MODE_KWARGS:
+        raise ValueError(f"Environment mode {env_mode} has no get env spec method.")
+    k = M.ENV_MODE_KWARGS[env_mode]
+    spec = EnvSpec(k["max_grid_size"], k["max_n_objs"], k["max_n_obj_types"], k["tabular"])
+    return spec, M.ENV_MODE_EPISODE_LEN[env_mode], M.ENV_MODE_LIFETIME_MAX[env_mode]
+
+
+def get_agent_hypers(env_mode: str) -> dict:
+    """environments.py:58-63 / configs.py:652-707."""
+    if env_mode not in M.MODE_AGENT_HYPERS:
+        raise ValueError(f"Environment mode {env_mode} has no get agent hyperparameters method.")
+    return dict(M.MODE_AGENT_HYPERS[env_mode])
+
+
+def _dev(device=None):
+    return torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+
+
+class LevelGenerator:
+    """Device ``reset_env_params`` (environments.py:22-37) for one env mode."""
+
+    def __init__(self, env_mode: str, device=None):
+        if env_mode not in M.ENV_MODE_PARAMS:
+            raise ValueError(f"Environment mode {env_mode} not registered.")
+        self.env_mode = env_mode
+        self.spec, _, _ = get_env_spec(env_mode)
+        prog = M.mode_program(env_mode)
+        nbytes = int(_lib.lib().toued_mode_program_bytes())
+        if prog.nbytes != nbytes:
+            raise _lib.ToUEDError(f"ModeProgram size mismatch: host {prog.nbytes} vs device {nbytes}")
+        self.program = torch.from_numpy(prog).to(_dev(device))
+
+    def __call__(self, keys: torch.Tensor, buffer_ids: torch.Tensor | None = None, with_sub_mode=False):
+        """keys int32[n,2] (threefry) -> levels int32[n,64] (lifetime and buffer_id packed in)."""
+        n = keys.shape[0]
+        levels = torch.empty((n, LEVEL_WORDS), dtype=torch.int32, device=keys.device)
+        sub = torch.empty((n,), dtype=torch.int32, device=keys.device) if with_sub_mode else None
+        if buffer_ids is not None:
+            buffer_ids = buffer_ids.to(torch.int32).contiguous()
+        _lib.call("toued_level_gen", _lib.ptr(self.program), _lib.ptr(keys.contiguous()), _lib.ptr(buffer_ids),
+                  _lib.ptr(levels), _lib.ptr(sub), n, _lib.stream_ptr())
+        return (levels, sub) if with_sub_mode else levels
+
+
+class GridWorld:
+    """gymnax ``Environment`` API for GridWorld (gridworld.py:38-236), vectorised.
+
+    ``reset(keys, levels, W)`` and ``step(keys, state, actions, levels, W)``
+    apply to n = keys.shape[0] workers; worker i uses level ``i // W``.
+    ``step`` includes gymnax's auto-reset (select(done, reset, stepped)).
+    """
+
+    def __init__(self, spec: EnvSpec):
+        self.spec = spec
+        self._c = _lib.env_spec_c(spec)
+
+    @property
+    def num_actions(self) -> int:
+        return 5
+
+    def reset(self, keys, levels, W: int = 1):
+        n = keys.shape[0]
+        dev = keys.device
+        state = torch.empty((STATE_FIELDS, n), dtype=torch.int32, device=dev)
+        idx = torch.empty(n, dtype=torch.int32, device=dev)
+        tm = torch.empty(n, dtype=torch.int32, device=dev)
+        _lib.call("toued_gw_reset", self._c, _lib.ptr(levels), W, _lib.ptr(keys), _lib.ptr(state), _lib.ptr(idx),
+                  _lib.ptr(tm), n, _lib.stream_ptr())
+        return (idx, tm), state
+
+    def step(self, keys, state, actions, levels, W: int = 1):
+        n = keys.shape[0]
+        dev = keys.device
+        state = state.clone()
+        idx = torch.empty(n, dtype=torch.int32, device=dev)
+        tm = torch.empty(n, dtype=torch.int32, device=dev)
+        rew = torch.empty(n, dtype=torch.float32, device=dev)
+        done = torch.empty(n, dtype=torch.uint8, device=dev)
+        _lib.call("toued_gw_step", self._c, _lib.ptr(levels), W, _lib.ptr(keys), _lib.ptr(state),
+                  _lib.ptr(actions.to(torch.int32).contiguous()), _lib.ptr(idx), _lib.ptr(tm), _lib.ptr(rew),
+                  _lib.ptr(done), n, _lib.stream_ptr())
+        return (idx, tm), state, rew, done.bool()
+
+    def obs_dense(self, idx, tm):
+        """Materialise the reference's dense observation (gridworld.py:184-199) — debugging only."""
+        D = self.spec.obs_dim
+        out = torch.zeros((idx.shape[0], D), dtype=torch.float32, device=idx.device)
+        out[torch.arange(idx.shape[0], device=idx.device), idx.long()] = 1.0
+        out[:, -1] = tm.float() * torch.tensor(0.001, dtype=torch.float32)
+        return out

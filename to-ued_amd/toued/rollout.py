@@ -1,0 +1,87 @@
+"""RolloutWrapper on MI355X (environments/rollout.py:13-102), vmapped over agents.
+
+The reference's ``RolloutWrapper`` works on one agent and is vmapped by its
+callers (agents/a2c.py:98, agents/lpg_agent.py:109, meta/train.py:48,
+agents/agents.py:101-105, level_sampler.py:276).  Here the agent axis is
+explicit: every call takes N agent keys, N packed levels and N actor tables,
+and runs one fused HIP launch (csrc/env.hip k_rollout).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from .env import STATE_FIELDS, EnvSpec, get_env_spec
+
+
+@dataclass
+class Transition:
+    """util/data.py:37-44 in compact, lane-contiguous layout.
+
+    obs_idx/obs_time: int32 [N, T+1, W] (obs_t for t<T; slot T is the end obs,
+    so next_obs_t == obs_{t+1}); action/done: uint8 [N, T, W]; reward: f32 [N, T, W].
+    """
+    obs_idx: torch.Tensor
+    obs_time: torch.Tensor
+    action: torch.Tensor
+    reward: torch.Tensor
+    done: torch.Tensor
+
+
+class RolloutWrapper:
+    def __init__(self, env_mode: str, train_rollout_len: int, eval_rollout_len: int | None = None,
+                 env_workers: int = 64):
+        self.env_mode = env_mode
+        self.spec, max_len, _ = get_env_spec(env_mode)
+        self.train_rollout_len = train_rollout_len
+        self.eval_rollout_len = max_len if eval_rollout_len is None else eval_rollout_len
+        self.env_workers = env_workers
+        self._c = _lib.env_spec_c(self.spec)
+
+    @property
+    def obs_dim(self) -> int:
+        return self.spec.obs_dim
+
+    def batch_reset(self, agent_keys: torch.Tensor, levels: torch.Tensor, num_workers: int | None = None):
+        """rollout.py:38-42 per agent: split(rng, W); vmap(env.reset).  Returns ((idx, time) [N*W], state)."""
+        W = self.env_workers if num_workers is None else num_workers
+        N = agent_keys.shape[0]
+        dev = agent_keys.device
+        n = N * W
+        state = torch.empty((STATE_FIELDS, n), dtype=torch.int32, device=dev)
+        idx = torch.empty(n, dtype=torch.int32, device=dev)
+        tm = torch.empty(n, dtype=torch.int32, device=dev)
+        _lib.call("toued_batch_reset", self._c, _lib.ptr(levels), _lib.ptr(agent_keys.contiguous()), N, W,
+                  _lib.ptr(state), _lib.ptr(idx), _lib.ptr(tm), _lib.stream_ptr())
+        return (idx, tm), state
+
+    def batch_rollout(self, agent_keys: torch.Tensor, theta: torch.Tensor, levels: torch.Tensor,
+                      state: torch.Tensor, eval: bool = False, out: Transition | None = None,
+                      inplace_state: bool = False):
+        """rollout.py:45-102.  theta: actor tables f32 [N, D, 5].
+
+        Returns (Transition, end_state, cum_return f32 [N, W]).
+        """
+        N = agent_keys.shape[0]
+        n = state.shape[1]
+        W = n // N
+        T = self.eval_rollout_len if eval else self.train_rollout_len
+        D = theta.shape[1]
+        dev = state.device
+        if not inplace_state:
+            state = state.clone()
+        if out is None:
+            out = Transition(
+                torch.empty((N, T + 1, W), dtype=torch.int32, device=dev),
+                torch.empty((N, T + 1, W), dtype=torch.int32, device=dev),
+                torch.empty((N, T, W), dtype=torch.uint8, device=dev),
+                torch.empty((N, T, W), dtype=torch.float32, device=dev),
+                torch.empty((N, T, W), dtype=torch.uint8, device=dev),
+            )
+        cum = torch.empty((N, W), dtype=torch.float32, device=dev)
+        _lib.call("toued_rollout", self._c, _lib.ptr(levels), _lib.ptr(theta), D, _lib.ptr(agent_keys.contiguous()),
+                  _lib.ptr(state), N, W, T, _lib.ptr(out.obs_idx), _lib.ptr(out.obs_time), _lib.ptr(out.action),
+                  _lib.ptr(out.reward), _lib.ptr(out.done), _lib.ptr(cum), _lib.stream_ptr())
+        return out, state, cum
