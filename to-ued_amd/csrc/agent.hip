@@ -1,0 +1,886 @@
+// Linear-softmax agent maths for the LPG meta-gradient step — HIP for gfx950.
+//
+// Forward (per inner update k):   agents/lpg_agent.py:31-85, :88-140
+//   k_lpg_inputs   LPG inputs x = [r, d, pi, e(y_t), e(y_tp1)(, step, lifetime)] (models/lpg.py:48-77)
+//   k_agent_grad   d/dtheta of mean(log(pi)*pi_hat), d/dphi of a_y*mean(KL(y_t||y_hat)), metrics
+//   k_agent_apply  optax clip_by_global_norm -> scale(lr) -> scale(-1); discard if step > lifetime
+//   k_entropy      util/metrics.py:5-9 batch_rollout_entropy (and its gradient, backward mode)
+//   k_eval_loss    meta/train.py:61-100: frozen value critic, GAE (util/metrics.py:17-38), normalised
+//                  advantage, lpg_loss with the [T] x [T,1] broadcast, value_loss
+// Reverse (explicit adjoint of jax.grad through the K clipped-SGD steps, meta/train.py:174):
+//   k_lpgloss_grad d lpg_loss / d theta_K
+//   k_clip_dot     <G_k, adjoint> per agent -> clip-VJP coefficients
+//   k_hvp          Hessian-vector products of the actor/critic losses through the linear-softmax
+//                  (row-gather) parameterisation + cotangents on pi_hat / y_hat (+ L2 regularisers)
+//   k_embed_bwd    embedding-MLP parameter gradient from the GRU input cotangents
+//   k_adam         optax scale_by_adam + scale(lr) + scale(-1)
+//
+// Sample index s = (a*T + t)*W + w (trajectory layout), GRU row r = a*W + w.
+// A tabular observation (idx, t) contributes logits table[idx] + (0.001 t) * table[D-1].
+#include <string.h>
+#include "common.h"
+
+#define EPSF 1e-8f
+
+namespace {
+
+TOUED_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// logits of a compact obs: W[idx] + c * W[D-1]
+template <int K>
+TOUED_DEV void probs_of(const float* __restrict__ tab, const float* __restrict__ last, int idx, float c, float* p) {
+  float l[K];
+  float m = -__builtin_inff();
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    l[j] = tab[(size_t)idx * K + j] + c * last[j];
+    m = fmaxf(m, l[j]);
+  }
+  float s = 0.0f;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    p[j] = __expf(l[j] - m);
+    s += p[j];
+  }
+  const float inv = 1.0f / s;
+#pragma unroll
+  for (int j = 0; j < K; ++j) p[j] *= inv;
+}
+
+// Scatter a K-vector d into rows idx and D-1 (times c) of a dense per-agent table.
+// UNIF: the whole wave shares one agent -> reduce the D-1 row contribution first.
+template <int K, bool UNIF>
+TOUED_DEV void scatter_rows(float* __restrict__ tab, int idx, int D, float c, const float* d) {
+#pragma unroll
+  for (int j = 0; j < K; ++j) atomicAdd(&tab[(size_t)idx * K + j], d[j]);
+  if (UNIF) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const float v = wave_sum(c * d[j]);
+      if (lane == 0) atomicAdd(&tab[(size_t)(D - 1) * K + j], v);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < K; ++j) atomicAdd(&tab[(size_t)(D - 1) * K + j], c * d[j]);
+  }
+}
+
+template <bool UNIF>
+TOUED_DEV void add_metric(float* met, int a, int slot, float v) {
+  if (UNIF) {
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&met[a * 8 + slot], v);
+  } else {
+    atomicAdd(&met[a * 8 + slot], v);
+  }
+}
+
+struct SampleRef {
+  int a, t, w, r, idx, idx1, act, done;
+  float c, c1, rew;
+};
+
+TOUED_DEV SampleRef load_sample(long s, int T, int W, const int* __restrict__ tidx, const int* __restrict__ ttime,
+                                const uint8_t* __restrict__ tact, const float* __restrict__ trew,
+                                const uint8_t* __restrict__ tdone, bool uniform) {
+  SampleRef q;
+  const long at = s / W;
+  q.w = (int)(s - at * W);
+  q.a = (int)(at / T);
+  q.t = (int)(at - (long)q.a * T);
+  if (uniform) q.a = __builtin_amdgcn_readfirstlane(q.a);
+  q.r = q.a * W + q.w;
+  const size_t o0 = ((size_t)q.a * (T + 1) + q.t) * W + q.w;
+  q.idx = tidx[o0];
+  q.idx1 = tidx[o0 + W];
+  q.c = (float)ttime[o0] * 0.001f;
+  q.c1 = (float)ttime[o0 + W] * 0.001f;
+  q.act = tact[s];
+  q.rew = trew[s];
+  q.done = tdone[s];
+  return q;
+}
+
+// ---------------------------------------------------------------------------- keys
+// Per agent key rng_a (already split(rng, N)[a]) -> the keys meta/train.py:88-170 consumes:
+//   _rng = split(rng_a)[1] -> train_lpg_agent; inside: (t, roll_k) = split(t) for k < K
+//   rng = split(rng_a)[0]; (rng, ev) = split(rng) -> eval rollout; (rng, ea) = split(rng) -> eval_agent
+//   eval_agent(ea): (x, reset) = split(ea); (x, roll) = split(x)
+__global__ void k_meta_keys(const uint32_t* __restrict__ agent_keys, int N, int K, uint32_t* __restrict__ roll_keys,
+                            uint32_t* __restrict__ eval_keys, uint32_t* __restrict__ ea_reset,
+                            uint32_t* __restrict__ ea_roll) {
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= N) return;
+  uint2 rng = make_uint2(agent_keys[2 * a], agent_keys[2 * a + 1]);
+  uint2 r0, tk;
+  split2(rng, r0, tk);
+  for (int k = 0; k < K; ++k) {
+    uint2 rk;
+    split2(tk, tk, rk);
+    roll_keys[2 * ((size_t)k * N + a)] = rk.x;
+    roll_keys[2 * ((size_t)k * N + a) + 1] = rk.y;
+  }
+  uint2 ev, ea;
+  split2(r0, r0, ev);
+  split2(r0, r0, ea);
+  eval_keys[2 * a] = ev.x;
+  eval_keys[2 * a + 1] = ev.y;
+  uint2 x, rs, rr;
+  split2(ea, x, rs);
+  split2(x, x, rr);
+  ea_reset[2 * a] = rs.x;
+  ea_reset[2 * a + 1] = rs.y;
+  ea_roll[2 * a] = rr.x;
+  ea_roll[2 * a + 1] = rr.y;
+}
+
+// ---------------------------------------------------------------------------- LPG inputs
+// X[f][t][r] (row stride xs_f between features) for one inner update.
+template <bool UNIF, int F>
+__global__ void __launch_bounds__(256) k_lpg_inputs(int N, int W, int T, int D, const float* __restrict__ theta,
+                                                    const float* __restrict__ phi, const int* __restrict__ tidx,
+                                                    const int* __restrict__ ttime, const uint8_t* __restrict__ tact,
+                                                    const float* __restrict__ trew, const uint8_t* __restrict__ tdone,
+                                                    const float* __restrict__ e1w, const float* __restrict__ e1b,
+                                                    const float* __restrict__ e2w, const float* __restrict__ e2b,
+                                                    const int* __restrict__ step, const int* __restrict__ levels,
+                                                    float* __restrict__ X, long xs_f) {
+  const long s = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= (long)N * T * W) return;
+  const SampleRef q = load_sample(s, T, W, tidx, ttime, tact, trew, tdone, UNIF);
+  const int R = N * W;
+  const float* th = theta + (size_t)q.a * D * 5;
+  const float* ph = phi + (size_t)q.a * D * 8;
+  float lastA[5], lastC[8];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
+  float p[5], y0[8], y1[8];
+  probs_of<5>(th, lastA, q.idx, q.c, p);
+  probs_of<8>(ph, lastC, q.idx, q.c, y0);
+  probs_of<8>(ph, lastC, q.idx1, q.c1, y1);
+  float pa = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) pa = (j == q.act) ? p[j] + EPSF : pa;
+  // embedding MLP [16, 1] (models/common.py:6-18) on y_t and y_tp1
+  float e0 = e2b[0], e1 = e2b[0];
+#pragma unroll
+  for (int h = 0; h < 16; ++h) {
+    float h0 = e1b[h], h1 = e1b[h];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      h0 += y0[i] * e1w[i * 16 + h];
+      h1 += y1[i] * e1w[i * 16 + h];
+    }
+    e0 += fmaxf(h0, 0.0f) * e2w[h];
+    e1 += fmaxf(h1, 0.0f) * e2w[h];
+  }
+  if (q.done) e1 = 0.0f;
+  const size_t o = (size_t)q.t * R + q.r;
+  X[0 * xs_f + o] = q.rew;
+  X[1 * xs_f + o] = q.done ? 1.0f : 0.0f;
+  X[2 * xs_f + o] = pa;
+  X[3 * xs_f + o] = e0;
+  X[4 * xs_f + o] = e1;
+  if (F == 7) {
+    X[5 * xs_f + o] = (float)step[q.a];
+    X[6 * xs_f + o] = (float)levels[(size_t)q.a * LEVEL_WORDS + L_LIFETIME];
+  }
+}
+
+// ---------------------------------------------------------------------------- agent gradient
+// met slots: 0 kl_sum, 1 pihat^2 sum, 2 sum_j yhat^2 sum, 3 actor entropy sum, 4 critic entropy sum
+template <bool UNIF>
+__global__ void __launch_bounds__(256) k_agent_grad(int N, int W, int T, int D, const float* __restrict__ theta,
+                                                    const float* __restrict__ phi, const int* __restrict__ tidx,
+                                                    const int* __restrict__ ttime, const uint8_t* __restrict__ tact,
+                                                    const float* __restrict__ trew, const uint8_t* __restrict__ tdone,
+                                                    const float* __restrict__ pi_hat, const float* __restrict__ y_hat,
+                                                    float alpha_y, float* __restrict__ Gth, float* __restrict__ Gph,
+                                                    float* __restrict__ met) {
+  const long s = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= (long)N * T * W) return;
+  const SampleRef q = load_sample(s, T, W, tidx, ttime, tact, trew, tdone, UNIF);
+  const int R = N * W;
+  const float inv_wt = 1.0f / (float)(W * T);
+  const float* th = theta + (size_t)q.a * D * 5;
+  const float* ph = phi + (size_t)q.a * D * 8;
+  float lastA[5], lastC[8];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
+  float p[5], y[8], yh[8];
+  probs_of<5>(th, lastA, q.idx, q.c, p);
+  probs_of<8>(ph, lastC, q.idx, q.c, y);
+  const size_t o = (size_t)q.t * R + q.r;
+  const float pih = pi_hat[o];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) yh[j] = y_hat[((size_t)q.t * 8 + j) * R + q.r];
+  // actor: d/dl [mean(log(pi_a + eps) * pi_hat)]
+  float pa = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) pa = (j == q.act) ? p[j] : pa;
+  const float rho = pa / (pa + EPSF);
+  float qa[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) qa[j] = pih * inv_wt * rho * ((j == q.act ? 1.0f : 0.0f) - p[j]);
+  // critic: d/dm [a_y * mean KL(y || y_hat)]
+  float av[8], ya = 0.0f, kl = 0.0f, y2 = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float ly = __logf(y[j] + EPSF), lq = __logf(yh[j] + EPSF);
+    kl += y[j] * (ly - lq);
+    av[j] = ly - lq + y[j] / (y[j] + EPSF);
+    ya += y[j] * av[j];
+    y2 += yh[j] * yh[j];
+  }
+  float qc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) qc[j] = alpha_y * inv_wt * y[j] * (av[j] - ya);
+  scatter_rows<5, UNIF>(Gth + (size_t)q.a * D * 5, q.idx, D, q.c, qa);
+  scatter_rows<8, UNIF>(Gph + (size_t)q.a * D * 8, q.idx, D, q.c, qc);
+  add_metric<UNIF>(met, q.a, 0, kl);
+  add_metric<UNIF>(met, q.a, 1, pih * pih);
+  add_metric<UNIF>(met, q.a, 2, y2);
+}
+
+// ---------------------------------------------------------------------------- apply (clipped SGD)
+// One block per agent.  gstat[a] = {|G_theta|, |G_phi|, applied}.
+__global__ void __launch_bounds__(256) k_agent_apply(int N, int D, const float* __restrict__ th0,
+                                                     const float* __restrict__ ph0, const float* __restrict__ Gth,
+                                                     const float* __restrict__ Gph, float lr_a, float lr_c,
+                                                     float max_norm, int* __restrict__ step,
+                                                     const int* __restrict__ levels, float* __restrict__ th1,
+                                                     float* __restrict__ ph1, float* __restrict__ gstat) {
+  const int a = blockIdx.x;
+  __shared__ float red[2][8];
+  const size_t na = (size_t)D * 5, nc = (size_t)D * 8;
+  const float* ga = Gth + (size_t)a * na;
+  const float* gc = Gph + (size_t)a * nc;
+  float sa = 0.0f, sc = 0.0f;
+  for (size_t i = threadIdx.x; i < na; i += blockDim.x) sa += ga[i] * ga[i];
+  for (size_t i = threadIdx.x; i < nc; i += blockDim.x) sc += gc[i] * gc[i];
+  sa = wave_sum(sa);
+  sc = wave_sum(sc);
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[0][wv] = sa; red[1][wv] = sc; }
+  __syncthreads();
+  float na2 = 0.0f, nc2 = 0.0f;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) { na2 += red[0][i]; nc2 += red[1][i]; }
+  const float gna = sqrtf(na2), gnc = sqrtf(nc2);
+  const int st = step[a];
+  const bool applied = (st + 1) <= levels[(size_t)a * LEVEL_WORDS + L_LIFETIME];
+  const bool clip_a = !(gna < max_norm), clip_c = !(gnc < max_norm);
+  const float* pa0 = th0 + (size_t)a * na;
+  const float* pc0 = ph0 + (size_t)a * nc;
+  float* pa1 = th1 + (size_t)a * na;
+  float* pc1 = ph1 + (size_t)a * nc;
+  for (size_t i = threadIdx.x; i < na; i += blockDim.x) {
+    const float g = clip_a ? (ga[i] / gna) * max_norm : ga[i];
+    pa1[i] = applied ? pa0[i] + (-(lr_a * g)) : pa0[i];
+  }
+  for (size_t i = threadIdx.x; i < nc; i += blockDim.x) {
+    const float g = clip_c ? (gc[i] / gnc) * max_norm : gc[i];
+    pc1[i] = applied ? pc0[i] + (-(lr_c * g)) : pc0[i];
+  }
+  if (threadIdx.x == 0) {
+    gstat[a * 4 + 0] = gna;
+    gstat[a * 4 + 1] = gnc;
+    gstat[a * 4 + 2] = applied ? 1.0f : 0.0f;
+    step[a] = applied ? st + 1 : st;
+  }
+}
+
+// ---------------------------------------------------------------------------- entropy
+// Forward: met[a][3|4] += sample entropies.  Backward (coef != 0): scatter coef * inv_wt * dH/dlogits.
+template <bool UNIF>
+__global__ void __launch_bounds__(256) k_entropy(int N, int W, int T, int D, const float* __restrict__ theta,
+                                                 const float* __restrict__ phi, const int* __restrict__ tidx,
+                                                 const int* __restrict__ ttime, float* __restrict__ met,
+                                                 float coef_a, float coef_c, float* __restrict__ adj_th,
+                                                 float* __restrict__ adj_ph) {
+  const long s = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= (long)N * T * W) return;
+  const long at = s / W;
+  const int w = (int)(s - at * W);
+  int a = (int)(at / T);
+  const int t = (int)(at - (long)a * T);
+  if (UNIF) a = __builtin_amdgcn_readfirstlane(a);
+  const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
+  const int idx = tidx[o0];
+  const float c = (float)ttime[o0] * 0.001f;
+  const float* th = theta + (size_t)a * D * 5;
+  const float* ph = phi + (size_t)a * D * 8;
+  float lastA[5], lastC[8];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
+  float p[5], y[8];
+  probs_of<5>(th, lastA, idx, c, p);
+  probs_of<8>(ph, lastC, idx, c, y);
+  float ha = 0.0f, hc = 0.0f, ga[5], gc[8];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) { const float l = __logf(p[j] + EPSF); ha -= (p[j] + EPSF) * l; ga[j] = -(l + 1.0f); }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { const float l = __logf(y[j] + EPSF); hc -= (y[j] + EPSF) * l; gc[j] = -(l + 1.0f); }
+  if (met) {
+    add_metric<UNIF>(met, a, 3, ha);
+    add_metric<UNIF>(met, a, 4, hc);
+  }
+  if (adj_th) {
+    const float inv_wt = 1.0f / (float)(W * T);
+    float pg = 0.0f, yg = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) pg += p[j] * ga[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) yg += y[j] * gc[j];
+    float da[5], dc[8];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) da[j] = coef_a * inv_wt * p[j] * (ga[j] - pg);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dc[j] = coef_c * inv_wt * y[j] * (gc[j] - yg);
+    scatter_rows<5, UNIF>(adj_th + (size_t)a * D * 5, idx, D, c, da);
+    scatter_rows<8, UNIF>(adj_ph + (size_t)a * D * 8, idx, D, c, dc);
+  }
+}
+
+// ---------------------------------------------------------------------------- eval loss
+// One block (64 threads) per agent; eval trajectory (T steps).  Outputs per agent:
+// out[a] = {lpg_loss, value_loss}; abar[a*W + w] = mean_t normalised advantage.
+__global__ void __launch_bounds__(64) k_eval_loss(int N, int W, int T, int D, const float* __restrict__ theta,
+                                                  const float* __restrict__ vcrit, const int* __restrict__ tidx,
+                                                  const int* __restrict__ ttime, const uint8_t* __restrict__ tact,
+                                                  const float* __restrict__ trew, const uint8_t* __restrict__ tdone,
+                                                  float gamma, float lam, float* __restrict__ adv_scratch,
+                                                  float* __restrict__ abar, float* __restrict__ out) {
+  const int a = blockIdx.x;
+  const int lane = threadIdx.x;
+  const float* v = vcrit + (size_t)a * D;
+  const float vlast = v[D - 1];
+  const float* th = theta + (size_t)a * D * 5;
+  float lastA[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
+  float* adv = adv_scratch + (size_t)a * W * T;
+  float s_adv = 0.0f, s_vl = 0.0f;
+  for (int w = lane; w < W; w += 64) {
+    float vn = v[tidx[((size_t)a * (T + 1) + T) * W + w]] + ((float)ttime[((size_t)a * (T + 1) + T) * W + w] * 0.001f) * vlast;
+    float g = 0.0f, vl = 0.0f;
+    for (int t = T - 1; t >= 0; --t) {
+      const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
+      const size_t s = ((size_t)a * T + t) * W + w;
+      const float vt = v[tidx[o0]] + ((float)ttime[o0] * 0.001f) * vlast;
+      const float nd = tdone[s] ? 0.0f : 1.0f;
+      const float delta = trew[s] + (gamma * vn * nd - vt);
+      g = delta + gamma * lam * nd * g;
+      adv[(size_t)w * T + t] = g;
+      const float tg = g + vt;
+      vl += (tg - vt) * (tg - vt);
+      s_adv += g;
+      vn = vt;
+    }
+    s_vl += vl / (float)T;
+  }
+  __shared__ float sh[4];
+  s_adv = wave_sum(s_adv);
+  s_vl = wave_sum(s_vl);
+  const float n = (float)(W * T);
+  const float mean = s_adv / n;
+  __syncthreads();
+  float s_var = 0.0f;
+  for (int i = lane; i < W * T; i += 64) { const float d = adv[i] - mean; s_var += d * d; }
+  s_var = wave_sum(s_var);
+  const float stdv = sqrtf(s_var / n);
+  float s_loss = 0.0f;
+  for (int w = lane; w < W; w += 64) {
+    float ab = 0.0f, lp = 0.0f;
+    for (int t = 0; t < T; ++t) {
+      ab += (adv[(size_t)w * T + t] - mean) / (stdv + EPSF);
+      const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
+      const size_t s = ((size_t)a * T + t) * W + w;
+      float p[5];
+      probs_of<5>(th, lastA, tidx[o0], (float)ttime[o0] * 0.001f, p);
+      float pa = p[0];
+#pragma unroll
+      for (int j = 1; j < 5; ++j) pa = (j == tact[s]) ? p[j] : pa;
+      lp += __logf(pa + EPSF);
+    }
+    ab /= (float)T;
+    lp /= (float)T;
+    abar[(size_t)a * W + w] = ab;
+    s_loss += -(lp * ab);
+  }
+  s_loss = wave_sum(s_loss);
+  if (lane == 0) {
+    out[a * 2 + 0] = s_loss / (float)W;
+    out[a * 2 + 1] = s_vl / (float)W;
+  }
+  (void)sh;
+}
+
+// ---------------------------------------------------------------------------- d lpg_loss / d theta_K
+template <bool UNIF>
+__global__ void __launch_bounds__(256) k_lpgloss_grad(int N, int W, int T, int D, const float* __restrict__ theta,
+                                                      const int* __restrict__ tidx, const int* __restrict__ ttime,
+                                                      const uint8_t* __restrict__ tact, const float* __restrict__ abar,
+                                                      float* __restrict__ adj_th) {
+  const long s = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= (long)N * T * W) return;
+  const long at = s / W;
+  const int w = (int)(s - at * W);
+  int a = (int)(at / T);
+  const int t = (int)(at - (long)a * T);
+  if (UNIF) a = __builtin_amdgcn_readfirstlane(a);
+  const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
+  const int idx = tidx[o0];
+  const float c = (float)ttime[o0] * 0.001f;
+  const float* th = theta + (size_t)a * D * 5;
+  float lastA[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
+  float p[5];
+  probs_of<5>(th, lastA, idx, c, p);
+  const int act = tact[s];
+  float pa = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) pa = (j == act) ? p[j] : pa;
+  const float rho = pa / (pa + EPSF);
+  const float kappa = -abar[(size_t)a * W + w] / (float)(W * T);
+  float d[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) d[j] = kappa * rho * ((j == act ? 1.0f : 0.0f) - p[j]);
+  scatter_rows<5, UNIF>(adj_th + (size_t)a * D * 5, idx, D, c, d);
+}
+
+// ---------------------------------------------------------------------------- clip VJP coefficients
+// coef[a] = {alpha_a, beta_a, alpha_c, beta_c}: gbar = alpha*u + beta*G with u = -lr * adjoint.
+__global__ void __launch_bounds__(256) k_clip_dot(int N, int D, const float* __restrict__ Gth,
+                                                  const float* __restrict__ Gph, const float* __restrict__ adj_th,
+                                                  const float* __restrict__ adj_ph, const float* __restrict__ gstat,
+                                                  float lr_a, float lr_c, float max_norm, float* __restrict__ coef) {
+  const int a = blockIdx.x;
+  __shared__ float red[2][8];
+  const size_t na = (size_t)D * 5, nc = (size_t)D * 8;
+  float da = 0.0f, dc = 0.0f;
+  for (size_t i = threadIdx.x; i < na; i += blockDim.x) da += Gth[(size_t)a * na + i] * adj_th[(size_t)a * na + i];
+  for (size_t i = threadIdx.x; i < nc; i += blockDim.x) dc += Gph[(size_t)a * nc + i] * adj_ph[(size_t)a * nc + i];
+  da = wave_sum(da);
+  dc = wave_sum(dc);
+  if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = da; red[1][threadIdx.x >> 6] = dc; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float sa = 0.0f, sc = 0.0f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) { sa += red[0][i]; sc += red[1][i]; }
+    const float gna = gstat[a * 4 + 0], gnc = gstat[a * 4 + 1];
+    const bool applied = gstat[a * 4 + 2] > 0.5f;
+    float aa = 0.0f, ba = 0.0f, ac = 0.0f, bc = 0.0f;
+    if (applied) {
+      if (gna < max_norm) { aa = 1.0f; }
+      else { aa = max_norm / gna; ba = -max_norm * (-lr_a * sa) / (gna * gna * gna); }
+      if (gnc < max_norm) { ac = 1.0f; }
+      else { ac = max_norm / gnc; bc = -max_norm * (-lr_c * sc) / (gnc * gnc * gnc); }
+    }
+    coef[a * 4 + 0] = aa;
+    coef[a * 4 + 1] = ba;
+    coef[a * 4 + 2] = ac;
+    coef[a * 4 + 3] = bc;
+  }
+}
+
+// ---------------------------------------------------------------------------- HVP + LPG-output cotangents
+template <bool UNIF>
+__global__ void __launch_bounds__(256) k_hvp(int N, int W, int T, int D, int K, const float* __restrict__ theta,
+                                             const float* __restrict__ phi, const int* __restrict__ tidx,
+                                             const int* __restrict__ ttime, const uint8_t* __restrict__ tact,
+                                             const float* __restrict__ pi_hat, const float* __restrict__ y_hat,
+                                             const float* __restrict__ Gth, const float* __restrict__ Gph,
+                                             const float* __restrict__ adj_th_in, const float* __restrict__ adj_ph_in,
+                                             const float* __restrict__ coef, float lr_a, float lr_c, float alpha_y,
+                                             float b2, float b3, float* __restrict__ adj_th_out,
+                                             float* __restrict__ adj_ph_out, float* __restrict__ d_pi_hat,
+                                             float* __restrict__ d_y_hat) {
+  const long s = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= (long)N * T * W) return;
+  const long at = s / W;
+  const int w = (int)(s - at * W);
+  int a = (int)(at / T);
+  const int t = (int)(at - (long)a * T);
+  if (UNIF) a = __builtin_amdgcn_readfirstlane(a);
+  const int R = N * W, r = a * W + w;
+  const float inv_wt = 1.0f / (float)(W * T);
+  const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
+  const int idx = tidx[o0];
+  const float c = (float)ttime[o0] * 0.001f;
+  const int act = tact[s];
+  const size_t o = (size_t)t * R + r;
+  const float pih = pi_hat[o];
+  float yh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) yh[j] = y_hat[((size_t)t * 8 + j) * R + r];
+  // regularisers beta_2 * mean(pi_hat^2), beta_3 * mean(sum y_hat^2), each averaged over K updates
+  float dpih = (b2 / (float)K) * 2.0f * pih * inv_wt;
+  float dyh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dyh[j] = (b3 / (float)K) * 2.0f * yh[j] * inv_wt;
+  const float aa = coef[a * 4 + 0], ba = coef[a * 4 + 1], ac = coef[a * 4 + 2], bc = coef[a * 4 + 3];
+  if (aa != 0.0f) {   // update k was applied
+    const size_t baseA = (size_t)a * D * 5, baseC = (size_t)a * D * 8;
+    const float* th = theta + baseA;
+    const float* ph = phi + baseC;
+    float lastA[5], lastC[8];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
+    float p[5], y[8];
+    probs_of<5>(th, lastA, idx, c, p);
+    probs_of<8>(ph, lastC, idx, c, y);
+    // ---- actor
+    float v[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const float adj = adj_th_in[baseA + (size_t)idx * 5 + j] + c * adj_th_in[baseA + (size_t)(D - 1) * 5 + j];
+      const float g = Gth[baseA + (size_t)idx * 5 + j] + c * Gth[baseA + (size_t)(D - 1) * 5 + j];
+      v[j] = -lr_a * aa * adj + ba * g;
+    }
+    float pa = 0.0f, va = 0.0f, pv = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      pa = (j == act) ? p[j] : pa;
+      va = (j == act) ? v[j] : va;
+      pv += p[j] * v[j];
+    }
+    const float rho = pa / (pa + EPSF);
+    dpih += inv_wt * rho * (va - pv);
+    const float ws = pih * inv_wt;
+    const float drs = EPSF * pa / ((pa + EPSF) * (pa + EPSF));
+    float da[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const float drho = drs * ((k == act ? 1.0f : 0.0f) - p[k]);
+      da[k] = ws * (drho * (va - pv) - rho * p[k] * (v[k] - pv));
+    }
+    scatter_rows<5, UNIF>(adj_th_out + baseA, idx, D, c, da);
+    // ---- critic
+    float vc[8], av[8], ay = 0.0f, yv = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float adj = adj_ph_in[baseC + (size_t)idx * 8 + j] + c * adj_ph_in[baseC + (size_t)(D - 1) * 8 + j];
+      const float g = Gph[baseC + (size_t)idx * 8 + j] + c * Gph[baseC + (size_t)(D - 1) * 8 + j];
+      vc[j] = -lr_c * ac * adj + bc * g;
+      av[j] = __logf(y[j] + EPSF) - __logf(yh[j] + EPSF) + y[j] / (y[j] + EPSF);
+      ay += av[j] * y[j];
+      yv += y[j] * vc[j];
+    }
+    const float scale = alpha_y * inv_wt;
+    float sv[8], ys = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float b = vc[j] - yv;
+      dyh[j] += scale * (-y[j] * b / (yh[j] + EPSF));
+      const float ye = y[j] + EPSF;
+      const float adash = 1.0f / ye + EPSF / (ye * ye);
+      sv[j] = y[j] * b * adash + av[j] * b - vc[j] * ay;
+      ys += y[j] * sv[j];
+    }
+    float dc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dc[j] = scale * y[j] * (sv[j] - ys);
+    scatter_rows<8, UNIF>(adj_ph_out + baseC, idx, D, c, dc);
+  }
+  d_pi_hat[o] = dpih;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) d_y_hat[((size_t)t * 8 + j) * R + r] = dyh[j];
+}
+
+// ---------------------------------------------------------------------------- embedding MLP backward
+// grad layout (161 floats): e1_b[16], e1_w[8*16], e2_b[1], e2_w[16] (flat-eta order within MLP_0)
+// Inputs: y_t / y_tp1 recomputed from phi_k; cotangents dX3 (pyt), dX4 (pyt1, masked by done).
+template <bool UNIF>
+__global__ void __launch_bounds__(256) k_embed_bwd(int N, int W, int T, int D, int K, const float* __restrict__ phi_hist,
+                                                   long phi_stride, const int* __restrict__ tidx_hist, long tidx_stride,
+                                                   const int* __restrict__ ttime_hist, const uint8_t* __restrict__ tdone_hist,
+                                                   long tstep_stride, const float* __restrict__ dX3,
+                                                   const float* __restrict__ dX4, long dx_stride_k,
+                                                   const float* __restrict__ e1w, const float* __restrict__ e1b,
+                                                   const float* __restrict__ e2w, float* __restrict__ partial) {
+  float acc[161];
+#pragma unroll
+  for (int i = 0; i < 161; ++i) acc[i] = 0.0f;
+  const long total = (long)K * N * T * W;
+  const int R = N * W;
+  for (long g = (long)blockIdx.x * blockDim.x + threadIdx.x; g < total; g += (long)gridDim.x * blockDim.x) {
+    const int k = (int)(g / ((long)N * T * W));
+    const long s = g - (long)k * N * T * W;
+    const long at = s / W;
+    const int w = (int)(s - at * W);
+    const int a = (int)(at / T);
+    const int t = (int)(at - (long)a * T);
+    const int r = a * W + w;
+    const int* tidx = tidx_hist + k * tidx_stride;
+    const int* ttime = ttime_hist + k * tidx_stride;
+    const uint8_t* tdone = tdone_hist + k * tstep_stride;
+    const float* ph = phi_hist + k * phi_stride + (size_t)a * D * 8;
+    const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
+    float lastC[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
+    const size_t o = (size_t)k * dx_stride_k + (size_t)t * R + r;
+    for (int which = 0; which < 2; ++which) {
+      float cg = which == 0 ? dX3[o] : (tdone[s] ? 0.0f : dX4[o]);
+      if (cg == 0.0f) continue;
+      float y[8];
+      probs_of<8>(ph, lastC, which == 0 ? tidx[o0] : tidx[o0 + W],
+                  (float)ttime[which == 0 ? o0 : o0 + W] * 0.001f, y);
+      acc[144] += cg;  // e2_b
+#pragma unroll
+      for (int h = 0; h < 16; ++h) {
+        float pre = e1b[h];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) pre += y[i] * e1w[i * 16 + h];
+        const float hid = fmaxf(pre, 0.0f);
+        acc[145 + h] += hid * cg;  // e2_w
+        const float dh = pre > 0.0f ? e2w[h] * cg : 0.0f;
+        acc[h] += dh;  // e1_b
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[16 + i * 16 + h] += y[i] * dh;  // e1_w
+      }
+    }
+  }
+  __shared__ float red[4][161];
+  const int wv = threadIdx.x >> 6;
+  for (int i = 0; i < 161; ++i) {
+    const float v = wave_sum(acc[i]);
+    if ((threadIdx.x & 63) == 0) red[wv][i] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 161; i += blockDim.x) {
+    float v = 0.0f;
+    for (int q = 0; q < (int)(blockDim.x >> 6); ++q) v += red[q][i];
+    partial[(size_t)blockIdx.x * 161 + i] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------- Adam
+__global__ void __launch_bounds__(256) k_adam(int P, float* __restrict__ eta, const float* __restrict__ grad,
+                                              float* __restrict__ m, float* __restrict__ v, float scale, float lr,
+                                              float b1, float b2, float eps, float bc1, float bc2) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  const float g = grad[i] * scale;
+  const float mi = b1 * m[i] + (1.0f - b1) * g;
+  const float vi = b2 * v[i] + (1.0f - b2) * g * g;
+  m[i] = mi;
+  v[i] = vi;
+  const float mh = mi / bc1, vh = vi / bc2;
+  eta[i] = eta[i] + (-(lr * (mh / (sqrtf(vh) + eps))));
+}
+
+// ---------------------------------------------------------------------------- agent init
+// agents/agents.py:31-95 create_agent / create_value_critic: bias-free Dense kernels with flax's
+// lecun_normal (truncated normal in [-2, 2], stddev sqrt(1/fan_in)/0.87962566).  Here the kernel of
+// table i is drawn from keys[i] directly (flax's per-module key derivation is not reproduced: parity
+// unpinned).  u = uniform(lo=erf(-sqrt2), hi=erf(sqrt2)); z = sqrt2*erfinv(u), clipped.
+TOUED_DEV float erfinv_giles(float x) {
+  float w = -plog((1.0f - x) * (1.0f + x));
+  float p;
+  if (w < 5.0f) {
+    w = w - 2.5f;
+    p = 2.81022636e-08f;
+    p = 3.43273939e-07f + p * w; p = -3.5233877e-06f + p * w; p = -4.39150654e-06f + p * w;
+    p = 0.00021858087f + p * w; p = -0.00125372503f + p * w; p = -0.00417768164f + p * w;
+    p = 0.246640727f + p * w; p = 1.50140941f + p * w;
+  } else {
+    w = sqrtf(w) - 3.0f;
+    p = -0.000200214257f;
+    p = 0.000100950558f + p * w; p = 0.00134934322f + p * w; p = -0.00367342844f + p * w;
+    p = 0.00573950773f + p * w; p = -0.0076224613f + p * w; p = 0.00943887047f + p * w;
+    p = 1.00167406f + p * w; p = 2.83297682f + p * w;
+  }
+  return p * x;
+}
+
+__global__ void __launch_bounds__(256) k_init_tables(const uint32_t* __restrict__ keys, int n, int cols, int D,
+                                                     float lo, float hi, float stddev, float* __restrict__ out) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long per = (long)D * cols;
+  if (e >= (long)n * per) return;
+  const int i = (int)(e / per);
+  const long j = e - (long)i * per;
+  const uint2 key = make_uint2(keys[2 * i], keys[2 * i + 1]);
+  const float u = uniform_from_bits(random_bits_at(key, (uint32_t)per, (uint32_t)j), lo, hi);
+  float z = 1.41421356237f * erfinv_giles(u);
+  z = fminf(fmaxf(z, -1.99999988f), 1.99999988f);
+  out[e] = z * stddev;
+}
+
+}  // namespace
+
+// ============================================================================ C ABI
+static inline unsigned nb256(long n) { return (unsigned)((n + 255) / 256); }
+
+extern "C" {
+
+int toued_meta_keys(const uint32_t* agent_keys, int N, int K, uint32_t* roll_keys, uint32_t* eval_keys,
+                    uint32_t* ea_reset, uint32_t* ea_roll, hipStream_t stream) {
+  TOUED_REQUIRE(N >= 1 && K >= 0, "toued_meta_keys: N=%d K=%d", N, K);
+  hipLaunchKernelGGL(k_meta_keys, dim3((N + 63) / 64), dim3(64), 0, stream, agent_keys, N, K, roll_keys, eval_keys,
+                     ea_reset, ea_roll);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_lpg_inputs(int N, int W, int T, int D, int F, const float* theta, const float* phi, const int* tidx,
+                     const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone, const float* eta_e1w,
+                     const float* eta_e1b, const float* eta_e2w, const float* eta_e2b, const int* step,
+                     const int* levels, float* X, long xs_f, hipStream_t stream) {
+  TOUED_REQUIRE(F == 5 || F == 7, "toued_lpg_inputs: F=%d", F);
+  const long n = (long)N * T * W;
+  if (n == 0) return 0;
+#define L_(U, FF) hipLaunchKernelGGL((k_lpg_inputs<U, FF>), dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, theta, \
+                                     phi, tidx, ttime, tact, trew, tdone, eta_e1w, eta_e1b, eta_e2w, eta_e2b, step,   \
+                                     levels, X, xs_f)
+  if (W % 64 == 0) { if (F == 5) L_(true, 5); else L_(true, 7); }
+  else { if (F == 5) L_(false, 5); else L_(false, 7); }
+#undef L_
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_agent_grad(int N, int W, int T, int D, const float* theta, const float* phi, const int* tidx,
+                     const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
+                     const float* pi_hat, const float* y_hat, float alpha_y, float* Gth, float* Gph, float* met,
+                     hipStream_t stream) {
+  const long n = (long)N * T * W;
+  if (n == 0) return 0;
+  if (W % 64 == 0)
+    hipLaunchKernelGGL(k_agent_grad<true>, dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, theta, phi, tidx, ttime,
+                       tact, trew, tdone, pi_hat, y_hat, alpha_y, Gth, Gph, met);
+  else
+    hipLaunchKernelGGL(k_agent_grad<false>, dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, theta, phi, tidx,
+                       ttime, tact, trew, tdone, pi_hat, y_hat, alpha_y, Gth, Gph, met);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_agent_apply(int N, int D, const float* th0, const float* ph0, const float* Gth, const float* Gph,
+                      float lr_a, float lr_c, float max_norm, int* step, const int* levels, float* th1, float* ph1,
+                      float* gstat, hipStream_t stream) {
+  if (N == 0) return 0;
+  hipLaunchKernelGGL(k_agent_apply, dim3(N), dim3(256), 0, stream, N, D, th0, ph0, Gth, Gph, lr_a, lr_c, max_norm,
+                     step, levels, th1, ph1, gstat);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_entropy(int N, int W, int T, int D, const float* theta, const float* phi, const int* tidx, const int* ttime,
+                  float* met, float coef_a, float coef_c, float* adj_th, float* adj_ph, hipStream_t stream) {
+  const long n = (long)N * T * W;
+  if (n == 0) return 0;
+  if (W % 64 == 0)
+    hipLaunchKernelGGL(k_entropy<true>, dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, theta, phi, tidx, ttime,
+                       met, coef_a, coef_c, adj_th, adj_ph);
+  else
+    hipLaunchKernelGGL(k_entropy<false>, dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, theta, phi, tidx, ttime,
+                       met, coef_a, coef_c, adj_th, adj_ph);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_eval_loss(int N, int W, int T, int D, const float* theta, const float* vcrit, const int* tidx,
+                    const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone, float gamma,
+                    float lam, float* adv_scratch, float* abar, float* out, hipStream_t stream) {
+  if (N == 0) return 0;
+  hipLaunchKernelGGL(k_eval_loss, dim3(N), dim3(64), 0, stream, N, W, T, D, theta, vcrit, tidx, ttime, tact, trew,
+                     tdone, gamma, lam, adv_scratch, abar, out);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_lpgloss_grad(int N, int W, int T, int D, const float* theta, const int* tidx, const int* ttime,
+                       const uint8_t* tact, const float* abar, float* adj_th, hipStream_t stream) {
+  const long n = (long)N * T * W;
+  if (n == 0) return 0;
+  if (W % 64 == 0)
+    hipLaunchKernelGGL(k_lpgloss_grad<true>, dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, theta, tidx, ttime,
+                       tact, abar, adj_th);
+  else
+    hipLaunchKernelGGL(k_lpgloss_grad<false>, dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, theta, tidx, ttime,
+                       tact, abar, adj_th);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_clip_dot(int N, int D, const float* Gth, const float* Gph, const float* adj_th, const float* adj_ph,
+                   const float* gstat, float lr_a, float lr_c, float max_norm, float* coef, hipStream_t stream) {
+  if (N == 0) return 0;
+  hipLaunchKernelGGL(k_clip_dot, dim3(N), dim3(256), 0, stream, N, D, Gth, Gph, adj_th, adj_ph, gstat, lr_a, lr_c,
+                     max_norm, coef);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_hvp(int N, int W, int T, int D, int K, const float* theta, const float* phi, const int* tidx,
+              const int* ttime, const uint8_t* tact, const float* pi_hat, const float* y_hat, const float* Gth,
+              const float* Gph, const float* adj_th_in, const float* adj_ph_in, const float* coef, float lr_a,
+              float lr_c, float alpha_y, float b2, float b3, float* adj_th_out, float* adj_ph_out, float* d_pi_hat,
+              float* d_y_hat, hipStream_t stream) {
+  const long n = (long)N * T * W;
+  if (n == 0) return 0;
+  if (W % 64 == 0)
+    hipLaunchKernelGGL(k_hvp<true>, dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, K, theta, phi, tidx, ttime, tact,
+                       pi_hat, y_hat, Gth, Gph, adj_th_in, adj_ph_in, coef, lr_a, lr_c, alpha_y, b2, b3, adj_th_out,
+                       adj_ph_out, d_pi_hat, d_y_hat);
+  else
+    hipLaunchKernelGGL(k_hvp<false>, dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, K, theta, phi, tidx, ttime,
+                       tact, pi_hat, y_hat, Gth, Gph, adj_th_in, adj_ph_in, coef, lr_a, lr_c, alpha_y, b2, b3,
+                       adj_th_out, adj_ph_out, d_pi_hat, d_y_hat);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_embed_bwd(int N, int W, int T, int D, int K, const float* phi_hist, long phi_stride, const int* tidx_hist,
+                    long tidx_stride, const int* ttime_hist, const uint8_t* tdone_hist, long tstep_stride,
+                    const float* dX3, const float* dX4, long dx_stride_k, const float* e1w, const float* e1b,
+                    const float* e2w, float* partial, int n_blocks, hipStream_t stream) {
+  if ((long)K * N * T * W == 0) return 0;
+  if (W % 64 == 0)
+    hipLaunchKernelGGL(k_embed_bwd<true>, dim3(n_blocks), dim3(256), 0, stream, N, W, T, D, K, phi_hist, phi_stride,
+                       tidx_hist, tidx_stride, ttime_hist, tdone_hist, tstep_stride, dX3, dX4, dx_stride_k, e1w, e1b,
+                       e2w, partial);
+  else
+    hipLaunchKernelGGL(k_embed_bwd<false>, dim3(n_blocks), dim3(256), 0, stream, N, W, T, D, K, phi_hist, phi_stride,
+                       tidx_hist, tidx_stride, ttime_hist, tdone_hist, tstep_stride, dX3, dX4, dx_stride_k, e1w, e1b,
+                       e2w, partial);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_init_tables(const uint32_t* keys, int n, int cols, int D, float lo, float hi, float stddev, float* out,
+                      hipStream_t stream) {
+  const long tot = (long)n * D * cols;
+  if (tot == 0) return 0;
+  hipLaunchKernelGGL(k_init_tables, dim3(nb256(tot)), dim3(256), 0, stream, keys, n, cols, D, lo, hi, stddev, out);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_adam(int P, float* eta, const float* grad, float* m, float* v, float scale, float lr, float b1, float b2,
+               float eps, int count, hipStream_t stream) {
+  if (P == 0) return 0;
+  const float bc1 = 1.0f - powf(b1, (float)count), bc2 = 1.0f - powf(b2, (float)count);
+  hipLaunchKernelGGL(k_adam, dim3(nb256(P)), dim3(256), 0, stream, P, eta, grad, m, v, scale, lr, b1, b2, eps, bc1,
+                     bc2);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

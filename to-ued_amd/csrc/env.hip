@@ -359,14 +359,18 @@ __global__ void __launch_bounds__(256) k_rollout(EnvSpec sp, const int* __restri
     env_step<NMAX, TAB>(sp, lev, sub, s, action, r, d);
     cum = __fadd_rn(cum, __fmul_rn(r, valid));
     valid = __fmul_rn(valid, d ? 0.0f : 1.0f);
-    traj_idx[base_o + (size_t)t * W] = idx;
-    traj_time[base_o + (size_t)t * W] = tm;
-    traj_action[base_t + (size_t)t * W] = (uint8_t)action;
-    traj_reward[base_t + (size_t)t * W] = r;
-    traj_done[base_t + (size_t)t * W] = d ? 1 : 0;
+    if (traj_idx) {   // eval_agent only needs the return (agents/agents.py:98-106)
+      traj_idx[base_o + (size_t)t * W] = idx;
+      traj_time[base_o + (size_t)t * W] = tm;
+      traj_action[base_t + (size_t)t * W] = (uint8_t)action;
+      traj_reward[base_t + (size_t)t * W] = r;
+      traj_done[base_t + (size_t)t * W] = d ? 1 : 0;
+    }
   }
-  traj_idx[base_o + (size_t)T * W] = tab_index(sp, s);
-  traj_time[base_o + (size_t)T * W] = s.time;
+  if (traj_idx) {
+    traj_idx[base_o + (size_t)T * W] = tab_index(sp, s);
+    traj_time[base_o + (size_t)T * W] = s.time;
+  }
   store_state<NMAX>(state, n, i, s);
   cum_return[i] = cum;
 }

@@ -1,0 +1,447 @@
+// LPG reverse-time GRU (models/lpg.py:11-36 LPGGRU + :79-85 heads) on CDNA4 matrix cores.
+//
+// Forward: rows = agents x workers (32,768 at N=512) share the LPG parameters,
+// so every time step is a dense [rows x 264] x [264 x 1024] f32 contraction
+// (h: 256 recurrent units, + x features, + a bias row; columns = r | z | W_hn h + b_hn
+// | W_in x + b_in).  One workgroup owns 32 rows for the whole T-step reverse
+// scan: h^T lives in LDS (k-major, padded to 33 columns: conflict-free
+// ds_read_b32 B-fragments), the weights stream from L2 as pre-packed A-fragment
+// float4s (one dwordx4 per lane feeds four v_mfma_f32_32x32x2_f32), and the
+// gate maths happens in the accumulator registers (lane = batch row, registers
+// = 16 gate columns; the r, z, n tiles of a unit line up lane-for-lane).
+// Each wave owns 64 units = 2 unit tiles x {r, z, nh, ni} accumulators.
+// Saved for the backward: h_in (masked carry), r, z, n, W_hn h + b_hn.
+//
+// Backward: one workgroup per (k, 32 rows), t ascending; three LDS phases
+// (dr_pre, dz_pre, d(W_hn h + b_hn)) each contracted with W_h^T on MFMA give
+// dh_prev; writes the gate-pre-activation cotangents DG[4][256][M], relu(h_out)
+// and the head cotangents for the weight-gradient GEMMs, and dX for the
+// embedding inputs.
+//
+// MFMA f32 32x32x2 operand/result maps (cdna_hip_programming.md §3):
+//   A: lane l holds A[i = l&31][k = l>>5];  B: lane l holds B[k = l>>5][j = l&31]
+//   D: reg q of lane l is D[i = (q&3) + 8*(q>>2) + 4*(l>>5)][j = l&31]
+#include <string.h>
+#include "common.h"
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+#define HU 256          // GRU width (lpg_gru_width)
+#define RB 32           // batch rows per workgroup
+#define LDH 33          // padded LDS row length
+#define NAUG 8          // augmented K rows: x (F <= 7) + bias row
+#define KQF 33          // fwd k-quads: 32 over h + 1 over the augmented rows
+#define NTILE_F 32      // fwd A tiles: r[8] z[8] nh[8] ni[8]
+
+struct EtaOff {         // flat LPG parameter offsets (oracle/lpg.py layout)
+  int pi_b, pi_w, y_b, y_w, hn_b, hn_w, hr_w, hz_w, in_b, in_w, ir_b, ir_w, iz_b, iz_w, e1_b, e1_w, e2_b, e2_w;
+};
+
+namespace {
+
+TOUED_DEV floatx16 mfma32(float a, float b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// Streamed [256][M] tensors: uniform (SGPR) base for the register's unit + a 32-bit per-lane
+// byte offset, so every access is a single saddr+voffset global instruction.
+TOUED_DEV float ld_u(const float* base_q, unsigned vbyte) {
+  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base_q) + vbyte);
+}
+TOUED_DEV void st_u(float* base_q, unsigned vbyte, float v) {
+  *reinterpret_cast<float*>(reinterpret_cast<char*>(base_q) + vbyte) = v;
+}
+TOUED_DEV int qunit(int q) { return (q & 3) + 8 * (q >> 2); }
+
+TOUED_DEV float sigm(float x) { return 1.0f / (1.0f + __expf(-x)); }
+TOUED_DEV float tanh_f(float x) {
+  const float e = __expf(-2.0f * fabsf(x));
+  const float t = (1.0f - e) / (1.0f + e);
+  return copysignf(t, x);
+}
+
+// ------------------------------------------------------------------ packing
+// fwdA[(tile*KQF + kq)*64 + lane] = float4 over kk = 4kq..4kq+3 of A[i=l&31][k=2kk+(l>>5)]
+__global__ void k_pack_fwd(const float* __restrict__ eta, EtaOff o, int F, float4* __restrict__ out) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= NTILE_F * KQF * 64) return;
+  const int lane = gid & 63, kq = (gid >> 6) % KQF, tile = gid / (64 * KQF);
+  const int g = tile >> 3, u = 32 * (tile & 7) + (lane & 31);
+  float v[4];
+  for (int e = 0; e < 4; ++e) {
+    const int k = 2 * (4 * kq + e) + (lane >> 5);
+    float x = 0.0f;
+    if (k < HU) {
+      if (g == 0) x = eta[o.hr_w + k * HU + u];
+      else if (g == 1) x = eta[o.hz_w + k * HU + u];
+      else if (g == 2) x = eta[o.hn_w + k * HU + u];
+    } else {
+      const int f = k - HU;
+      if (f < F) {
+        if (g == 0) x = eta[o.ir_w + f * HU + u];
+        else if (g == 1) x = eta[o.iz_w + f * HU + u];
+        else if (g == 3) x = eta[o.in_w + f * HU + u];
+      } else if (f == F) {
+        x = g == 0 ? eta[o.ir_b + u] : g == 1 ? eta[o.iz_b + u] : g == 2 ? eta[o.hn_b + u] : eta[o.in_b + u];
+      }
+    }
+    v[e] = x;
+  }
+  out[gid] = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// bwdA[((ut*3 + g)*32 + kq)*64 + lane]: A[i = u (input unit) ][k = c (gate unit)] = W_g[u][c]
+__global__ void k_pack_bwd(const float* __restrict__ eta, EtaOff o, float4* __restrict__ out) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= 8 * 3 * 32 * 64) return;
+  const int lane = gid & 63, kq = (gid >> 6) & 31, g = (gid >> 11) % 3, ut = gid / (64 * 32 * 3);
+  const int u = 32 * ut + (lane & 31);
+  const int base = g == 0 ? o.hr_w : g == 1 ? o.hz_w : o.hn_w;
+  float v[4];
+  for (int e = 0; e < 4; ++e) {
+    const int c = 2 * (4 * kq + e) + (lane >> 5);
+    v[e] = eta[base + u * HU + c];
+  }
+  out[gid] = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// ------------------------------------------------------------------ forward
+struct FwdArgs {
+  int R, T, W, F;
+  const float* X; long xs_f;           // X[f*xs_f + t*R + r]
+  const uint8_t* done;                 // [N][T][W]
+  const float4* A;                     // packed fwd fragments
+  const float* eta; EtaOff o;
+  float* pi_hat; float* y_hat;         // [T][R], [T][8][R]
+  float* s_hin; float* s_r; float* s_z; float* s_n; float* s_hn;  // [256][M] with column base added
+  long M;
+};
+
+#define NWAVE 8         // 512-thread workgroups: wave w owns units [32w, 32w+32)
+#define NGRP (2 * NWAVE)
+
+__global__ void __launch_bounds__(512, 2) k_gru_fwd(FwdArgs p) {
+  __shared__ float hT[(HU + NAUG) * LDH];
+  __shared__ float wh[HU * 9];
+  __shared__ float hp[NGRP * 9 * RB];
+  __shared__ float hout[9 * RB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hi = lane >> 5, col = lane & 31;
+  const int r0 = blockIdx.x * RB, row = r0 + col;
+  const int R = p.R, T = p.T, W = p.W, F = p.F;
+  const int a = r0 / W, w = row - a * W;
+  for (int i = tid; i < HU * 9; i += 512) {
+    const int u = i / 9, oo = i - u * 9;
+    wh[i] = oo == 0 ? p.eta[p.o.pi_w + u] : p.eta[p.o.y_w + u * 8 + (oo - 1)];
+  }
+  for (int i = tid; i < (HU + NAUG) * LDH; i += 512) hT[i] = 0.0f;
+  float hreg[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) hreg[q] = 0.0f;
+  __syncthreads();
+  if (tid < RB) {
+    const int t = T - 1;
+    for (int f = 0; f < NAUG; ++f)
+      hT[(HU + f) * LDH + tid] = f < F ? p.X[f * p.xs_f + (size_t)t * R + r0 + tid] : (f == F ? 1.0f : 0.0f);
+  }
+  __syncthreads();
+  const float bpi = p.eta[p.o.pi_b];
+  const float4* Ab = p.A + lane;
+  for (int s = 0; s < T; ++s) {
+    const int t = T - 1 - s;
+    floatx16 acc[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[g][q] = 0.0f;
+    // ---- recurrent contraction over the 256 h rows (kq 0..31): r, z, nh tiles of unit tile `wave`
+    float4 an[3];
+#pragma unroll
+    for (int g = 0; g < 3; ++g) an[g] = Ab[((8 * g + wave) * KQF + 0) * 64];
+#pragma unroll 2
+    for (int kq = 0; kq < 32; ++kq) {
+      float4 ac[3];
+#pragma unroll
+      for (int g = 0; g < 3; ++g) ac[g] = an[g];
+      if (kq + 1 < 32) {
+#pragma unroll
+        for (int g = 0; g < 3; ++g) an[g] = Ab[((8 * g + wave) * KQF + kq + 1) * 64];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float b = hT[(2 * (4 * kq + e) + hi) * LDH + col];
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          const float av = e == 0 ? ac[g].x : e == 1 ? ac[g].y : e == 2 ? ac[g].z : ac[g].w;
+          acc[g] = mfma32(av, b, acc[g]);
+        }
+      }
+    }
+    // ---- augmented rows (x features + bias): kq = 32 for all four gate kinds
+    {
+      float4 ag[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) ag[g] = Ab[((8 * g + wave) * KQF + 32) * 64];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float b = hT[(HU + 2 * e + hi) * LDH + col];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float av = e == 0 ? ag[g].x : e == 1 ? ag[g].y : e == 2 ? ag[g].z : ag[g].w;
+          acc[g] = mfma32(av, b, acc[g]);
+        }
+      }
+    }
+    // ---- gate maths (lane = row, register q = unit offset)
+    const long cbase = (long)t * R;                              // uniform column base
+    const unsigned vbyte = (unsigned)(((long)(32 * wave + 4 * hi) * p.M + row) * 4);
+    float hp_loc[9];
+#pragma unroll
+    for (int oo = 0; oo < 9; ++oo) hp_loc[oo] = 0.0f;
+    float hnew[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int u = 32 * wave + (q & 3) + 8 * (q >> 2) + 4 * hi;
+      const float rg = sigm(acc[0][q]);
+      const float zg = sigm(acc[1][q]);
+      const float hn = acc[2][q];
+      const float ng = tanh_f(acc[3][q] + rg * hn);
+      const float hin = hreg[q];
+      const float h = (1.0f - zg) * ng + zg * hin;
+      hnew[q] = h;
+      const long qo = (long)qunit(q) * p.M + cbase;
+      st_u(p.s_hin + qo, vbyte, hin);
+      st_u(p.s_r + qo, vbyte, rg);
+      st_u(p.s_z + qo, vbyte, zg);
+      st_u(p.s_n + qo, vbyte, ng);
+      st_u(p.s_hn + qo, vbyte, hn);
+      const float rl = fmaxf(h, 0.0f);
+#pragma unroll
+      for (int oo = 0; oo < 9; ++oo) hp_loc[oo] += rl * wh[u * 9 + oo];
+    }
+#pragma unroll
+    for (int oo = 0; oo < 9; ++oo) hp[((2 * wave + hi) * 9 + oo) * RB + col] = hp_loc[oo];
+    __syncthreads();   // all MFMA reads of hT done; head partials visible
+    // next-step carry: h_in(t-1) = where(d_{t-1}, 0, h_out(t))
+    const bool dn = (t >= 1) ? p.done[((size_t)a * T + (t - 1)) * W + w] != 0 : false;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int u = 32 * wave + (q & 3) + 8 * (q >> 2) + 4 * hi;
+      const float h = dn ? 0.0f : hnew[q];
+      hreg[q] = h;
+      hT[u * LDH + col] = h;
+    }
+    if (t >= 1 && tid < RB) {
+      for (int f = 0; f < F; ++f) hT[(HU + f) * LDH + tid] = p.X[f * p.xs_f + (size_t)(t - 1) * R + r0 + tid];
+    }
+    for (int i = tid; i < 9 * RB; i += 512) {
+      const int oo = i / RB, c = i - oo * RB;
+      float v = oo == 0 ? bpi : p.eta[p.o.y_b + oo - 1];
+#pragma unroll
+      for (int gq = 0; gq < NGRP; ++gq) v += hp[(gq * 9 + oo) * RB + c];
+      hout[i] = v;
+    }
+    __syncthreads();
+    if (tid < RB) {
+      const long ob = (long)t * R + r0 + tid;
+      p.pi_hat[ob] = hout[tid];
+      float m = -__builtin_inff();
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, hout[(j + 1) * RB + tid]);
+      float e[8], ssum = 0.0f;
+      for (int j = 0; j < 8; ++j) { e[j] = __expf(hout[(j + 1) * RB + tid] - m); ssum += e[j]; }
+      const float inv = 1.0f / ssum;
+      for (int j = 0; j < 8; ++j) p.y_hat[((long)t * 8 + j) * R + r0 + tid] = e[j] * inv;
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ backward
+struct BwdArgs {
+  int R, T, W, K;
+  const uint8_t* done; long done_stride_k;     // per k: [N][T][W]
+  const float4* A;                             // packed bwd fragments
+  const float* eta; EtaOff o;
+  const float* y_hat; const float* d_pi_hat; const float* d_y_hat;   // [K][T][(8)][R]
+  const float* s_hin; const float* s_r; const float* s_z; const float* s_n; const float* s_hn;  // [256][M]
+  long M;
+  float* DG;        // [4][256][M]: dr_pre, dz_pre, d(hn), dn_pre
+  float* RH;        // [256][M] relu(h_out)
+  float* DH;        // [9][M] head cotangents (d pi_hat, d y_logits)
+  float* dX3; float* dX4;   // [K][T][R]
+};
+
+__global__ void __launch_bounds__(512, 2) k_gru_bwd(BwdArgs p) {
+  __shared__ float dgT[HU * LDH];
+  __shared__ float wh[HU * 9];
+  __shared__ float wi34[2 * 3 * HU];
+  __shared__ float hv[9 * RB];
+  __shared__ float dxp[NGRP * 2 * RB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hi = lane >> 5, col = lane & 31;
+  const int nb = p.R / RB;
+  const int k = blockIdx.x / nb;
+  const int r0 = (blockIdx.x - k * nb) * RB, row = r0 + col;
+  const int R = p.R, T = p.T, W = p.W;
+  const int a = r0 / W, w = row - a * W;
+  for (int i = tid; i < HU * 9; i += 512) {
+    const int u = i / 9, oo = i - u * 9;
+    wh[i] = oo == 0 ? p.eta[p.o.pi_w + u] : p.eta[p.o.y_w + u * 8 + (oo - 1)];
+  }
+  // W_i rows for the embedding inputs (f = 3: pyt, f = 4: pyt1), per gate kind r, z, n
+  for (int i = tid; i < 2 * 3 * HU; i += 512) {
+    const int f = 3 + i / (3 * HU), g = (i / HU) % 3, u = i % HU;
+    const int base = g == 0 ? p.o.ir_w : g == 1 ? p.o.iz_w : p.o.in_w;
+    wi34[i] = p.eta[base + f * HU + u];
+  }
+  float dh[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) dh[q] = 0.0f;
+  const uint8_t* done = p.done + (long)k * p.done_stride_k;
+  const float4* Ab = p.A + lane;
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    const long ctr = ((long)k * T + t) * R;          // column base in [.][K*T*R]
+    if (tid < RB) {
+      const long o = ctr + r0 + tid;
+      float yh[8], dy[8], s = 0.0f;
+      for (int j = 0; j < 8; ++j) {
+        yh[j] = p.y_hat[((long)k * T * 8 + (long)t * 8 + j) * R + r0 + tid];
+        dy[j] = p.d_y_hat[((long)k * T * 8 + (long)t * 8 + j) * R + r0 + tid];
+        s += yh[j] * dy[j];
+      }
+      const float dpi = p.d_pi_hat[o];
+      hv[tid] = dpi;
+      p.DH[o] = dpi;
+      for (int j = 0; j < 8; ++j) {
+        const float v = yh[j] * (dy[j] - s);
+        hv[(j + 1) * RB + tid] = v;
+        p.DH[(long)(j + 1) * p.M + o] = v;
+      }
+    }
+    __syncthreads();
+    float hvl[9];
+#pragma unroll
+    for (int oo = 0; oo < 9; ++oo) hvl[oo] = hv[oo * RB + col];
+    const unsigned vbyte = (unsigned)(((long)(32 * wave + 4 * hi) * p.M + row) * 4);
+    float dx3 = 0.0f, dx4 = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int u = 32 * wave + (q & 3) + 8 * (q >> 2) + 4 * hi;
+      const long qo = (long)qunit(q) * p.M + ctr;
+      const float hin = ld_u(p.s_hin + qo, vbyte), rg = ld_u(p.s_r + qo, vbyte), zg = ld_u(p.s_z + qo, vbyte);
+      const float ng = ld_u(p.s_n + qo, vbyte), hn = ld_u(p.s_hn + qo, vbyte);
+      const float hout = (1.0f - zg) * ng + zg * hin;
+      float d = dh[q];
+      if (hout > 0.0f) {
+        float hs = 0.0f;
+#pragma unroll
+        for (int oo = 0; oo < 9; ++oo) hs += wh[u * 9 + oo] * hvl[oo];
+        d += hs;
+      }
+      st_u(p.RH + qo, vbyte, fmaxf(hout, 0.0f));
+      const float dn_ = d * (1.0f - zg);
+      const float dz = d * (hin - ng);
+      const float dnp = dn_ * (1.0f - ng * ng);
+      const float dhn = dnp * rg;
+      const float drp = dnp * hn * rg * (1.0f - rg);
+      const float dzp = dz * zg * (1.0f - zg);
+      dh[q] = d * zg;   // direct path; the W_h^T contraction is added below
+      st_u(p.DG + 0L * HU * p.M + qo, vbyte, drp);
+      st_u(p.DG + 1L * HU * p.M + qo, vbyte, dzp);
+      st_u(p.DG + 2L * HU * p.M + qo, vbyte, dhn);
+      st_u(p.DG + 3L * HU * p.M + qo, vbyte, dnp);
+      dx3 += drp * wi34[0 * HU + u] + dzp * wi34[1 * HU + u] + dnp * wi34[2 * HU + u];
+      dx4 += drp * wi34[3 * HU + u] + dzp * wi34[4 * HU + u] + dnp * wi34[5 * HU + u];
+    }
+    dxp[((2 * wave + hi) * 2 + 0) * RB + col] = dx3;
+    dxp[((2 * wave + hi) * 2 + 1) * RB + col] = dx4;
+    floatx16 acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+#pragma unroll 1
+    for (int g = 0; g < 3; ++g) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int u = 32 * wave + (q & 3) + 8 * (q >> 2) + 4 * hi;
+        dgT[u * LDH + col] = ld_u(p.DG + (long)g * HU * p.M + (long)qunit(q) * p.M + ctr, vbyte);  // own store
+      }
+      __syncthreads();
+      float4 an = Ab[((wave * 3 + g) * 32 + 0) * 64];
+#pragma unroll 2
+      for (int kq = 0; kq < 32; ++kq) {
+        const float4 av = an;
+        if (kq + 1 < 32) an = Ab[((wave * 3 + g) * 32 + kq + 1) * 64];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float b = dgT[(2 * (4 * kq + e) + hi) * LDH + col];
+          const float x = e == 0 ? av.x : e == 1 ? av.y : e == 2 ? av.z : av.w;
+          acc = mfma32(x, b, acc);
+        }
+      }
+      __syncthreads();
+    }
+    if (tid < RB) {
+      float s3 = 0.0f, s4 = 0.0f;
+      for (int gq = 0; gq < NGRP; ++gq) { s3 += dxp[(gq * 2 + 0) * RB + tid]; s4 += dxp[(gq * 2 + 1) * RB + tid]; }
+      p.dX3[ctr + r0 + tid] = s3;
+      p.dX4[ctr + r0 + tid] = s4;
+    }
+    // carry to h_out(t+1): h_in(t) = where(d_t, 0, h_out(t+1))
+    const bool dn = done[((size_t)a * T + t) * W + w] != 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dh[q] = dn ? 0.0f : dh[q] + acc[q];
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int toued_gru_pack(const float* eta, const int* off, int F, float* fwdA, float* bwdA, hipStream_t stream) {
+  TOUED_REQUIRE(F >= 1 && F <= 7, "toued_gru_pack: F=%d", F);
+  EtaOff o;
+  memcpy(&o, off, sizeof(EtaOff));
+  const int n1 = NTILE_F * KQF * 64, n2 = 8 * 3 * 32 * 64;
+  hipLaunchKernelGGL(k_pack_fwd, dim3((n1 + 255) / 256), dim3(256), 0, stream, eta, o, F,
+                     reinterpret_cast<float4*>(fwdA));
+  hipLaunchKernelGGL(k_pack_bwd, dim3((n2 + 255) / 256), dim3(256), 0, stream, eta, o,
+                     reinterpret_cast<float4*>(bwdA));
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+size_t toued_gru_packed_floats(int which) { return which == 0 ? (size_t)NTILE_F * KQF * 64 * 4 : (size_t)8 * 3 * 32 * 64 * 4; }
+
+int toued_gru_fwd(int R, int T, int W, int F, const float* X, long xs_f, const uint8_t* done, const float* fwdA,
+                  const float* eta, const int* off, float* pi_hat, float* y_hat, float* s_hin, float* s_r, float* s_z,
+                  float* s_n, float* s_hn, long M, hipStream_t stream) {
+  TOUED_REQUIRE(R % RB == 0 && W % RB == 0, "toued_gru_fwd: rows R=%d and workers W=%d must be multiples of 32", R, W);
+  TOUED_REQUIRE(F >= 1 && F <= 7 && T >= 1, "toued_gru_fwd: F=%d T=%d", F, T);
+  FwdArgs p;
+  p.R = R; p.T = T; p.W = W; p.F = F; p.X = X; p.xs_f = xs_f; p.done = done;
+  p.A = reinterpret_cast<const float4*>(fwdA); p.eta = eta;
+  memcpy(&p.o, off, sizeof(EtaOff));
+  p.pi_hat = pi_hat; p.y_hat = y_hat; p.s_hin = s_hin; p.s_r = s_r; p.s_z = s_z; p.s_n = s_n; p.s_hn = s_hn; p.M = M;
+  hipLaunchKernelGGL(k_gru_fwd, dim3(R / RB), dim3(512), 0, stream, p);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_stride_k, const float* bwdA,
+                  const float* eta, const int* off, const float* y_hat, const float* d_pi_hat, const float* d_y_hat,
+                  const float* s_hin, const float* s_r, const float* s_z, const float* s_n, const float* s_hn, long M,
+                  float* DG, float* RH, float* DH, float* dX3, float* dX4, hipStream_t stream) {
+  TOUED_REQUIRE(R % RB == 0 && W % RB == 0, "toued_gru_bwd: rows R=%d and workers W=%d must be multiples of 32", R, W);
+  BwdArgs p;
+  p.R = R; p.T = T; p.W = W; p.K = K; p.done = done; p.done_stride_k = done_stride_k;
+  p.A = reinterpret_cast<const float4*>(bwdA); p.eta = eta;
+  memcpy(&p.o, off, sizeof(EtaOff));
+  p.y_hat = y_hat; p.d_pi_hat = d_pi_hat; p.d_y_hat = d_y_hat;
+  p.s_hin = s_hin; p.s_r = s_r; p.s_z = s_z; p.s_n = s_n; p.s_hn = s_hn; p.M = M;
+  p.DG = DG; p.RH = RH; p.DH = DH; p.dX3 = dX3; p.dX4 = dX4;
+  hipLaunchKernelGGL(k_gru_bwd, dim3(K * (R / RB)), dim3(512), 0, stream, p);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

@@ -28,6 +28,7 @@ _P = ctypes.c_void_p
 _I = ctypes.c_int
 _F = ctypes.c_float
 _U = ctypes.c_uint32
+_L = ctypes.c_long
 
 # name -> argtypes (restype int unless listed in _RESTYPES)
 _SIGS = {
@@ -41,10 +42,29 @@ _SIGS = {
     "toued_gw_step": [EnvSpecC, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P],
     "toued_batch_reset": [EnvSpecC, _P, _P, _I, _I, _P, _P, _P, _P],
     "toued_rollout": [EnvSpecC, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "toued_meta_keys": [_P, _I, _I, _P, _P, _P, _P, _P],
+    "toued_lpg_inputs": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _P],
+    "toued_agent_grad": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P],
+    "toued_agent_apply": [_I, _I, _P, _P, _P, _P, _F, _F, _F, _P, _P, _P, _P, _P, _P],
+    "toued_entropy": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P],
+    "toued_eval_loss": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P],
+    "toued_lpgloss_grad": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "toued_clip_dot": [_I, _I, _P, _P, _P, _P, _P, _F, _F, _F, _P, _P],
+    "toued_hvp": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F,
+                  _P, _P, _P, _P, _P],
+    "toued_embed_bwd": [_I, _I, _I, _I, _I, _P, _L, _P, _L, _P, _P, _L, _P, _P, _L, _P, _P, _P, _P, _I, _P],
+    "toued_init_tables": [_P, _I, _I, _I, _F, _F, _F, _P, _P],
+    "toued_adam": [_I, _P, _P, _P, _P, _F, _F, _F, _F, _F, _I, _P],
+    "toued_gru_pack": [_P, _P, _I, _P, _P, _P],
+    "toued_gru_packed_floats": [_I],
+    "toued_gru_fwd": [_I, _I, _I, _I, _P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _P],
+    "toued_gru_bwd": [_I, _I, _I, _I, _P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _P, _P, _P, _P, _P,
+                      _P],
     "toued_last_error": [],
     "toued_abi_version": [],
 }
-_RESTYPES = {"toued_last_error": ctypes.c_char_p, "toued_mode_program_bytes": ctypes.c_size_t}
+_RESTYPES = {"toued_last_error": ctypes.c_char_p, "toued_mode_program_bytes": ctypes.c_size_t,
+             "toued_gru_packed_floats": ctypes.c_size_t}
 
 _lib = None
 

@@ -1,0 +1,164 @@
+"""LPG model on MI355X: flat parameter layout, initialisation, MFMA GRU forward/backward.
+
+models/lpg.py:11-96 (LPG, LPGGRU) + meta/meta.py:10-30 (create_lpg_train_state).
+The parameters are one flat f32 vector in jax ``tree_flatten`` order of the
+flax param dict (the layout evosax's ParameterReshaper ravels, and the one
+oracle/lpg.py uses):
+
+  Dense_0 {bias[1], kernel[H,1]}  Dense_1 {bias[Y], kernel[H,Y]}
+  LPGGRU_0/GRUCell_0: hn{bias,kernel[H,H]} hr{kernel} hz{kernel} in{bias,kernel[F,H]} ir{..} iz{..}
+  MLP_0: Dense_0 {bias[E], kernel[Y,E]}  Dense_1 {bias[1], kernel[E,1]}
+
+F = 5 input features, 7 with --lifetime_conditioning.  H = 256 (lpg_gru_width),
+Y = 8 (lpg_target_width), E = 16 (lpg_embedding_net_width) are what the HIP
+kernels are built for.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import _lib
+
+H, Y, E = 256, 8, 16
+_OFF_ORDER = ("pi_b", "pi_w", "y_b", "y_w", "hn_b", "hn_w", "hr_w", "hz_w", "in_b", "in_w", "ir_b", "ir_w",
+              "iz_b", "iz_w", "e1_b", "e1_w", "e2_b", "e2_w")
+
+
+def layout(F: int) -> "OrderedDict[str, tuple]":
+    L = OrderedDict()
+    L["pi_b"], L["pi_w"] = (1,), (H, 1)
+    L["y_b"], L["y_w"] = (Y,), (H, Y)
+    L["hn_b"], L["hn_w"], L["hr_w"], L["hz_w"] = (H,), (H, H), (H, H), (H, H)
+    L["in_b"], L["in_w"], L["ir_b"], L["ir_w"], L["iz_b"], L["iz_w"] = (H,), (F, H), (H,), (F, H), (H,), (F, H)
+    L["e1_b"], L["e1_w"], L["e2_b"], L["e2_w"] = (E,), (Y, E), (1,), (E, 1)
+    return L
+
+
+class LPGLayout:
+    def __init__(self, F: int):
+        if F not in (5, 7):
+            raise ValueError(f"LPG input width F={F} (5, or 7 with lifetime conditioning)")
+        self.F = F
+        self.shapes = layout(F)
+        self.offsets = {}
+        off = 0
+        for k, s in self.shapes.items():
+            self.offsets[k] = off
+            off += int(np.prod(s))
+        self.size = off
+        self.off_array = (ctypes_int_array := np.array([self.offsets[k] for k in _OFF_ORDER], np.int32))
+        self._c_off = (__import__("ctypes").c_int * len(_OFF_ORDER))(*ctypes_int_array.tolist())
+
+    def view(self, flat: torch.Tensor, name: str) -> torch.Tensor:
+        o = self.offsets[name]
+        s = self.shapes[name]
+        return flat[o:o + int(np.prod(s))].view(s)
+
+    @property
+    def c_offsets(self):
+        return self._c_off
+
+
+def init_lpg_params(seed: int, F: int, device=None) -> torch.Tensor:
+    """flax-like LPG initialisation (lecun-normal kernels, orthogonal recurrent kernels, zero biases).
+
+    flax's exact init RNG derivation (per-module fold_in of the init key) is not
+    reproduced — parity unpinned, documented in DESIGN.md; the distribution matches.
+    Runs once at start-up on the host (numpy), then lives on the GPU.
+    """
+    rs = np.random.RandomState(seed)
+    parts = []
+    for k, s in layout(F).items():
+        if k.endswith("_b"):
+            parts.append(np.zeros(s))
+        elif k in ("hn_w", "hr_w", "hz_w"):
+            q, r = np.linalg.qr(rs.randn(H, H))
+            parts.append(q * np.sign(np.diag(r))[None, :])
+        else:
+            std = math.sqrt(1.0 / s[0]) / 0.87962566103423978
+            parts.append(np.clip(rs.randn(*s), -2, 2) * std)
+    flat = np.concatenate([p.ravel() for p in parts]).astype(np.float32)
+    dev = torch.device(device) if device is not None else torch.device("cuda")
+    return torch.from_numpy(flat).to(dev)
+
+
+class LPGGRU:
+    """MFMA GRU forward/backward over K x R rows (csrc/gru.hip) with saved activations.
+
+    Saved tensors are [256][M] with M = K*T*R columns ordered (k, t, r): the exact
+    operand layout of the weight-gradient GEMMs.
+    """
+
+    def __init__(self, lay: LPGLayout, R: int, T: int, K: int, W: int, device):
+        self.lay, self.R, self.T, self.K, self.W = lay, R, T, K, W
+        self.M = K * T * R
+        L = _lib.lib()
+        dev = device
+        f32 = torch.float32
+        self.fwdA = torch.empty(int(L.toued_gru_packed_floats(0)), dtype=f32, device=dev)
+        self.bwdA = torch.empty(int(L.toued_gru_packed_floats(1)), dtype=f32, device=dev)
+        M = self.M
+        self.S = torch.empty((5, H, M), dtype=f32, device=dev)          # h_in, r, z, n, hn
+        self.DG = torch.empty((4, H, M), dtype=f32, device=dev)         # dr_pre, dz_pre, d(hn), dn_pre
+        self.RH = torch.empty((H, M), dtype=f32, device=dev)            # relu(h_out)
+        self.DH = torch.empty((9, M), dtype=f32, device=dev)            # head cotangents
+        self.dX3 = torch.empty((K, T, R), dtype=f32, device=dev)
+        self.dX4 = torch.empty((K, T, R), dtype=f32, device=dev)
+
+    def pack(self, eta: torch.Tensor):
+        _lib.call("toued_gru_pack", _lib.ptr(eta), self.lay.c_offsets, self.lay.F, _lib.ptr(self.fwdA),
+                  _lib.ptr(self.bwdA), _lib.stream_ptr())
+
+    def forward(self, k: int, X: torch.Tensor, done_k: torch.Tensor, eta: torch.Tensor, pi_hat: torch.Tensor,
+                y_hat: torch.Tensor):
+        """X: [F, K, T, R] (feature stride M); done_k: u8 [N, T, W]; pi_hat [K,T,R]; y_hat [K,T,8,R]."""
+        R, T, M = self.R, self.T, self.M
+        col = k * T * R
+        Xk = X[:, k]
+        S = self.S
+        _lib.call("toued_gru_fwd", R, T, self.W, self.lay.F, _lib.ptr(X) + 4 * col, M, _lib.ptr(done_k),
+                  _lib.ptr(self.fwdA), _lib.ptr(eta), self.lay.c_offsets, _lib.ptr(pi_hat[k]), _lib.ptr(y_hat[k]),
+                  _lib.ptr(S) + 4 * (0 * H * M + col), _lib.ptr(S) + 4 * (1 * H * M + col),
+                  _lib.ptr(S) + 4 * (2 * H * M + col), _lib.ptr(S) + 4 * (3 * H * M + col),
+                  _lib.ptr(S) + 4 * (4 * H * M + col), M, _lib.stream_ptr())
+        del Xk
+
+    def backward(self, done_all: torch.Tensor, eta: torch.Tensor, y_hat: torch.Tensor, d_pi_hat: torch.Tensor,
+                 d_y_hat: torch.Tensor, X: torch.Tensor, grad: torch.Tensor):
+        """done_all: u8 [K(+1), N, T, W] (first K slots used).  Accumulates d(loss)/d(eta) into ``grad``
+        (all parameters except the embedding MLP, which needs dX3/dX4 -> agent-side kernel)."""
+        R, T, K, M = self.R, self.T, self.K, self.M
+        S = self.S
+        stride_k = done_all[0].numel()
+        _lib.call("toued_gru_bwd", R, T, self.W, K, _lib.ptr(done_all), stride_k, _lib.ptr(self.bwdA), _lib.ptr(eta),
+                  self.lay.c_offsets, _lib.ptr(y_hat), _lib.ptr(d_pi_hat), _lib.ptr(d_y_hat),
+                  _lib.ptr(S[0]), _lib.ptr(S[1]), _lib.ptr(S[2]), _lib.ptr(S[3]), _lib.ptr(S[4]), M,
+                  _lib.ptr(self.DG), _lib.ptr(self.RH), _lib.ptr(self.DH), _lib.ptr(self.dX3), _lib.ptr(self.dX4),
+                  _lib.stream_ptr())
+        lay = self.lay
+        F = lay.F
+        DG = self.DG
+        # weight-gradient GEMMs (library GEMMs on the saved operands; reduction over M = K*T*R)
+        gh = torch.mm(S[0], DG[0:3].reshape(3 * H, M).t())                 # [256, 768]
+        lay.view(grad, "hr_w").add_(gh[:, 0:H])
+        lay.view(grad, "hz_w").add_(gh[:, H:2 * H])
+        lay.view(grad, "hn_w").add_(gh[:, 2 * H:3 * H])
+        X2 = X.reshape(F, M)
+        lay.view(grad, "ir_w").add_(torch.mm(X2, DG[0].t()))
+        lay.view(grad, "iz_w").add_(torch.mm(X2, DG[1].t()))
+        lay.view(grad, "in_w").add_(torch.mm(X2, DG[3].t()))
+        bsum = DG.sum(dim=2)                                                # [4, 256]
+        lay.view(grad, "ir_b").add_(bsum[0])
+        lay.view(grad, "iz_b").add_(bsum[1])
+        lay.view(grad, "hn_b").add_(bsum[2])
+        lay.view(grad, "in_b").add_(bsum[3])
+        heads = torch.mm(self.RH, self.DH.t())                             # [256, 9]
+        lay.view(grad, "pi_w").add_(heads[:, 0:1])
+        lay.view(grad, "y_w").add_(heads[:, 1:9])
+        hb = self.DH.sum(dim=1)
+        lay.view(grad, "pi_b").add_(hb[0:1])
+        lay.view(grad, "y_b").add_(hb[1:9])

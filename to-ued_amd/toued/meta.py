@@ -1,0 +1,238 @@
+"""LPG meta-gradient train step on MI355X (meta/train.py:14-130, meta/meta.py:33-52).
+
+``MetaGradStep(spec...)(rng, eta, agents)`` performs, for all N agents at once:
+  forward  K x [fused rollout -> LPG inputs -> MFMA GRU forward -> LPG-agent
+           gradient -> clipped SGD (+lifetime discard) -> entropy metrics],
+           eval rollout, frozen-value-critic GAE + lpg_loss, eval_agent (4 workers)
+  reverse  the explicit adjoint of jax.grad(_train_agent) w.r.t. eta through the
+           K clipped-SGD steps: lpg_loss seed, entropy-regulariser gradients,
+           clip VJPs, Hessian-vector products, then one batched MFMA GRU backward
+           over all K x N x W rows and the weight-gradient GEMMs
+  update   mean over agents (all-reduce across ranks when distributed), Adam.
+
+Everything stays on the GPU; the host only enqueues launches.  Per-agent keys
+follow meta/train.py exactly (split(rng, N); per agent the scan keys of
+train_lpg_agent, then the eval-rollout and eval_agent keys).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib, prng
+from .lpg import LPGGRU, LPGLayout, Y
+from .rollout import RolloutWrapper, Transition
+
+
+@dataclass
+class LpgHyperparams:
+    """util/data.py:7-35 + the agent/meta hyperparameters the step needs."""
+    num_agent_updates: int = 5
+    agent_target_coeff: float = 0.5
+    policy_entropy_coeff: float = 5e-2
+    target_entropy_coeff: float = 1e-3
+    policy_l2_coeff: float = 5e-3
+    target_l2_coeff: float = 1e-3
+    gamma: float = 0.99
+    gae_lambda: float = 0.95
+    actor_lr: float = 40.0
+    critic_lr: float = 4.0
+    max_grad_norm: float = 0.5
+    lpg_lr: float = 1e-4
+    eval_workers: int = 4        # meta/train.py:115
+
+
+class AdamState:
+    """optax.scale_by_adam state for the flat LPG parameters."""
+
+    def __init__(self, P: int, device):
+        self.m = torch.zeros(P, dtype=torch.float32, device=device)
+        self.v = torch.zeros(P, dtype=torch.float32, device=device)
+        self.count = 0
+
+
+class MetaGradStep:
+    def __init__(self, rollout: RolloutWrapper, n_agents: int, hyp: LpgHyperparams, lifetime_conditioning: bool,
+                 device=None, world=None):
+        self.ro = rollout
+        self.N = n_agents
+        self.W = rollout.env_workers
+        self.T = rollout.train_rollout_len
+        self.K = hyp.num_agent_updates
+        self.D = rollout.obs_dim
+        self.hyp = hyp
+        self.F = 7 if lifetime_conditioning else 5
+        self.lay = LPGLayout(self.F)
+        self.world = world
+        dev = torch.device(device) if device is not None else torch.device("cuda")
+        self.dev = dev
+        N, W, T, K, D = self.N, self.W, self.T, self.K, self.D
+        R = N * W
+        if R % 32 or W % 32:
+            raise ValueError(f"env_workers={W} must be a multiple of 32 for the MFMA GRU row blocks")
+        self.R = R
+        f32, i32, u8 = torch.float32, torch.int32, torch.uint8
+        z = lambda *s, dt=f32: torch.zeros(s, dtype=dt, device=dev)
+        self.theta_h = z(K + 1, N, D, 5)
+        self.phi_h = z(K + 1, N, D, Y)
+        self.G_th = z(K, N, D, 5)
+        self.G_ph = z(K, N, D, Y)
+        self.gstat = z(K, N, 4)
+        self.met = z(K, N, 8)
+        self.traj = Transition(z(K + 1, N, T + 1, W, dt=i32), z(K + 1, N, T + 1, W, dt=i32),
+                               z(K + 1, N, T, W, dt=u8), z(K + 1, N, T, W), z(K + 1, N, T, W, dt=u8))
+        self.X = z(self.F, K, T, R)
+        self.pi_hat = z(K, T, R)
+        self.y_hat = z(K, T, Y, R)
+        self.d_pi_hat = z(K, T, R)
+        self.d_y_hat = z(K, T, Y, R)
+        self.adv = z(N, W, T)
+        self.abar = z(N, W)
+        self.loss_out = z(N, 2)
+        self.adj_th = [z(N, D, 5), z(N, D, 5)]
+        self.adj_ph = [z(N, D, Y), z(N, D, Y)]
+        self.coef = z(N, 4)
+        self.keys_roll = z(K, N, 2, dt=i32)
+        self.keys_eval = z(N, 2, dt=i32)
+        self.keys_ea_reset = z(N, 2, dt=i32)
+        self.keys_ea_roll = z(N, 2, dt=i32)
+        self.gru = LPGGRU(self.lay, R, T, K, W, dev)
+        self.grad = z(self.lay.size)
+        self.embed_blocks = 512
+        self.embed_partial = z(self.embed_blocks, 161)
+        self.ea_cum = None
+
+    # ------------------------------------------------------------------ helpers
+    def _t(self, k: int) -> Transition:
+        tr = self.traj
+        return Transition(tr.obs_idx[k], tr.obs_time[k], tr.action[k], tr.reward[k], tr.done[k])
+
+    def _eta(self, eta, name):
+        return self.lay.view(eta, name)
+
+    # ------------------------------------------------------------------ step
+    def __call__(self, rng: torch.Tensor, eta: torch.Tensor, adam: AdamState, agents, rank_slice=None):
+        """One meta-gradient train step (meta/train.py:14-130).
+
+        rng: device key [2]; eta: flat LPG params (updated in place); agents: AgentBatch (updated in place:
+        actor/critic tables, steps, env state).  Returns a dict of per-agent metric tensors.
+        """
+        L = _lib
+        N, W, T, K, D, R = self.N, self.W, self.T, self.K, self.D, self.R
+        hyp = self.hyp
+        st = L.stream_ptr()
+        ptr = L.ptr
+        # meta/train.py:173 rng = split(rng, num_agents); under data parallelism every rank
+        # derives all N keys and keeps its contiguous slice (identical keys at any world size).
+        keys_all = prng.split(rng, agents_total := (self.N if rank_slice is None else rank_slice[2]))
+        agent_keys = keys_all if rank_slice is None else keys_all[rank_slice[0]:rank_slice[1]].contiguous()
+        L.call("toued_meta_keys", ptr(agent_keys), N, K, ptr(self.keys_roll), ptr(self.keys_eval),
+               ptr(self.keys_ea_reset), ptr(self.keys_ea_roll), st)
+        self.gru.pack(eta)
+        self.theta_h[0].copy_(agents.theta)
+        self.phi_h[0].copy_(agents.phi)
+        self.G_th.zero_()
+        self.G_ph.zero_()
+        self.met.zero_()
+        e1w, e1b = self._eta(eta, "e1_w"), self._eta(eta, "e1_b")
+        e2w, e2b = self._eta(eta, "e2_w"), self._eta(eta, "e2_b")
+        state = agents.state
+        # ---------------- forward: K inner updates (agents/lpg_agent.py:88-140)
+        for k in range(K):
+            tk = self._t(k)
+            self.ro.batch_rollout(self.keys_roll[k], self.theta_h[k], agents.levels, state, out=tk,
+                                  inplace_state=True)
+            L.call("toued_lpg_inputs", N, W, T, D, self.F, ptr(self.theta_h[k]), ptr(self.phi_h[k]),
+                   ptr(tk.obs_idx), ptr(tk.obs_time), ptr(tk.action), ptr(tk.reward), ptr(tk.done),
+                   ptr(e1w), ptr(e1b), ptr(e2w), ptr(e2b), ptr(agents.step), ptr(agents.levels),
+                   ptr(self.X) + 4 * k * T * R, self.gru.M, st)
+            self.gru.forward(k, self.X, tk.done, eta, self.pi_hat, self.y_hat)
+            L.call("toued_agent_grad", N, W, T, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(tk.obs_idx),
+                   ptr(tk.obs_time), ptr(tk.action), ptr(tk.reward), ptr(tk.done), ptr(self.pi_hat[k]),
+                   ptr(self.y_hat[k]), hyp.agent_target_coeff, ptr(self.G_th[k]), ptr(self.G_ph[k]),
+                   ptr(self.met[k]), st)
+            L.call("toued_agent_apply", N, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(self.G_th[k]),
+                   ptr(self.G_ph[k]), hyp.actor_lr, hyp.critic_lr, hyp.max_grad_norm, ptr(agents.step),
+                   ptr(agents.levels), ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(self.gstat[k]), st)
+            L.call("toued_entropy", N, W, T, D, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(tk.obs_idx),
+                   ptr(tk.obs_time), ptr(self.met[k]), 0.0, 0.0, None, None, st)
+        # ---------------- eval rollout + lpg loss (meta/train.py:98-145)
+        te = self._t(K)
+        self.ro.batch_rollout(self.keys_eval, self.theta_h[K], agents.levels, state, out=te, inplace_state=True)
+        L.call("toued_eval_loss", N, W, T, D, ptr(self.theta_h[K]), ptr(agents.vcrit), ptr(te.obs_idx),
+               ptr(te.obs_time), ptr(te.action), ptr(te.reward), ptr(te.done), hyp.gamma, hyp.gae_lambda,
+               ptr(self.adv), ptr(self.abar), ptr(self.loss_out), st)
+        # value critic "update" (meta/train.py:113-133): the gradient is identically zero,
+        # so only the TrainState step advances (K train rollouts + 1 eval rollout).
+        agents.vstep.add_(K + 1)
+        # eval_agent (agents/agents.py:98-106): fresh 4-worker reset, eval-length rollout, mean return
+        (_, _), ea_state = self.ro.batch_reset(self.keys_ea_reset, agents.levels, hyp.eval_workers)
+        ea_cum = self._eval_rollout(self.keys_ea_roll, self.theta_h[K], agents.levels, ea_state)
+        # ---------------- reverse: explicit adjoint w.r.t. eta
+        a_in, a_out = 0, 1
+        self.adj_th[a_in].zero_()
+        self.adj_ph[a_in].zero_()
+        L.call("toued_lpgloss_grad", N, W, T, D, ptr(self.theta_h[K]), ptr(te.obs_idx), ptr(te.obs_time),
+               ptr(te.action), ptr(self.abar), ptr(self.adj_th[a_in]), st)
+        for k in range(K - 1, -1, -1):
+            tk = self._t(k)
+            # d(-b0*H_pi - b1*H_y)/K at (theta_{k+1}, phi_{k+1}) on rollout k
+            L.call("toued_entropy", N, W, T, D, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(tk.obs_idx),
+                   ptr(tk.obs_time), None, -hyp.policy_entropy_coeff / K, -hyp.target_entropy_coeff / K,
+                   ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]), st)
+            L.call("toued_clip_dot", N, D, ptr(self.G_th[k]), ptr(self.G_ph[k]), ptr(self.adj_th[a_in]),
+                   ptr(self.adj_ph[a_in]), ptr(self.gstat[k]), hyp.actor_lr, hyp.critic_lr, hyp.max_grad_norm,
+                   ptr(self.coef), st)
+            self.adj_th[a_out].copy_(self.adj_th[a_in])
+            self.adj_ph[a_out].copy_(self.adj_ph[a_in])
+            L.call("toued_hvp", N, W, T, D, K, ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(tk.obs_idx),
+                   ptr(tk.obs_time), ptr(tk.action), ptr(self.pi_hat[k]), ptr(self.y_hat[k]), ptr(self.G_th[k]),
+                   ptr(self.G_ph[k]), ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]), ptr(self.coef), hyp.actor_lr,
+                   hyp.critic_lr, hyp.agent_target_coeff, hyp.policy_l2_coeff, hyp.target_l2_coeff,
+                   ptr(self.adj_th[a_out]), ptr(self.adj_ph[a_out]), ptr(self.d_pi_hat[k]), ptr(self.d_y_hat[k]), st)
+            a_in, a_out = a_out, a_in
+        self.grad.zero_()
+        self.gru.backward(self.traj.done, eta, self.y_hat, self.d_pi_hat, self.d_y_hat, self.X, self.grad)
+        tr = self.traj
+        L.call("toued_embed_bwd", N, W, T, D, K, ptr(self.phi_h), self.phi_h[0].numel(), ptr(tr.obs_idx),
+               tr.obs_idx[0].numel(), ptr(tr.obs_time), ptr(tr.done), tr.done[0].numel(), ptr(self.gru.dX3),
+               ptr(self.gru.dX4), T * R, ptr(e1w), ptr(e1b), ptr(e2w), ptr(self.embed_partial), self.embed_blocks, st)
+        emb = self.embed_partial.sum(dim=0)
+        self._eta(self.grad, "e1_b").add_(emb[0:16])
+        self._eta(self.grad, "e1_w").add_(emb[16:144].view(8, 16))
+        self._eta(self.grad, "e2_b").add_(emb[144:145])
+        self._eta(self.grad, "e2_w").add_(emb[145:161].view(16, 1))
+        # ---------------- mean over agents (+ all-reduce across ranks), Adam (meta/train.py:180-181)
+        n_total = N
+        if self.world is not None and self.world.size > 1:
+            self.world.all_reduce_sum(self.grad)
+            n_total = N * self.world.size
+        adam.count += 1
+        L.call("toued_adam", self.lay.size, ptr(eta), ptr(self.grad), ptr(adam.m), ptr(adam.v), 1.0 / n_total,
+               hyp.lpg_lr, 0.9, 0.999, 1e-8, adam.count, st)
+        # ---------------- agent state out + metrics
+        agents.theta.copy_(self.theta_h[K])
+        agents.phi.copy_(self.phi_h[K])
+        inv_wt = 1.0 / (W * T)
+        m = self.met * inv_wt                                     # [K, N, 8]
+        agent_m = m.mean(dim=0)
+        lpg_loss = self.loss_out[:, 0]
+        reg = (lpg_loss - hyp.policy_entropy_coeff * agent_m[:, 3] + hyp.policy_l2_coeff * agent_m[:, 1]
+               - hyp.target_entropy_coeff * agent_m[:, 4] + hyp.target_l2_coeff * agent_m[:, 2])
+        return {
+            "lpg_loss": lpg_loss, "reg_lpg_loss": reg, "value_loss": self.loss_out[:, 1],
+            "lpg_agent": {"policy_l2": agent_m[:, 1], "policy_entropy": agent_m[:, 3], "critic_loss": agent_m[:, 0],
+                          "critic_l2": agent_m[:, 2], "critic_entropy": agent_m[:, 4]},
+            "lpg_agent_return": ea_cum.mean(dim=1),
+        }
+
+    def _eval_rollout(self, keys, theta, levels, state):
+        """Eval-length rollout that only accumulates returns (no trajectory storage)."""
+        N = keys.shape[0]
+        n = state.shape[1]
+        cum = torch.empty((N, n // N), dtype=torch.float32, device=state.device)
+        L = _lib
+        L.call("toued_rollout", self.ro._c, L.ptr(levels), L.ptr(theta), theta.shape[1], L.ptr(keys), L.ptr(state),
+               N, n // N, self.ro.eval_rollout_len, None, None, None, None, None, L.ptr(cum), L.stream_ptr())
+        return cum
