@@ -1,0 +1,184 @@
+"""Headline benchmark: agent-env-steps/sec of the LPG meta-gradient step (BASELINE.json configs[1]).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--env_mode tabular] [--agents_per_gpu 512]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+        bench.py --gpus N --steps K --warmup W
+
+Workload (C2): env_mode=tabular (the build's defined manual dispatch over the five
+LPG tabular levels), num_agents=512 per GPU (weak scaling: 512*N agents
+in total), num_mini_batches=1, W=64 workers, T=20, K=5 inner LPG updates,
+meta-gradient + Adam, score_function=random level sampling.  A "step" is one
+outer iteration of train.py's _meta_train_loop: lpg_meta_grad_train_step then
+level_sampler.sample.  value = N_agents_total * W * T * K / seconds per step
+(inner-rollout agent-env-steps only; the eval rollout and eval_agent steps are
+extra work inside the timed step and are not counted).
+
+Rank 0 prints ONE JSON line.  The dominant kernel's roofline fraction is measured
+live with HIP events around its launches on the stream they run on.  The CPU
+baseline times the oracle restatement (oracle/, numpy rollout + torch-CPU float32
+autograd meta-gradient) on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "to-ued_amd"))
+sys.path.insert(0, str(ROOT))
+
+import torch  # noqa: E402
+
+MFMA_F32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: dense f32 MFMA (v_mfma_f32_32x32x2_f32)
+HBM_PEAK_GBS = 8000.0
+GRU_FWD_FLOP_PER_ELEM = {5: 406080, 7: 409152}    # per (agent, worker, t)
+GRU_BWD_FLOP_PER_ELEM = 2 * 256 * 768              # dh_prev = dG . W_h^T per (k, agent, worker, t)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--env_mode", default="tabular")
+    ap.add_argument("--agents_per_gpu", type=int, default=512)
+    ap.add_argument("--lifetime_conditioning", action="store_true")
+    ap.add_argument("--no_cpu_baseline", action="store_true")
+    ap.add_argument("--cpu_agents", type=int, default=0, help="agents in the CPU sample (0 = auto-size to ~15 s)")
+    return ap.parse_args()
+
+
+def cpu_baseline(env_mode: str, lifetime_conditioning: bool, n_agents: int = 0):
+    """Oracle restatement on the host: numpy rollouts + torch-CPU float32 autograd meta-gradient.
+
+    One meta-step (K=5 updates of W=64 x T=20, eval rollout, meta-gradient) for a bounded
+    sample of agents; reports agent-env-steps/sec in the same unit as the GPU number."""
+    import numpy as np
+
+    from oracle import jaxrand as jr
+    from oracle import levels as olv
+    from oracle import lpg as olpg
+    from oracle import meta as ometa
+    from oracle import rollout as oro
+    W, T, K = 64, 20, 5
+    spec = olv.env_spec(env_mode)
+    F = 7 if lifetime_conditioning else 5
+    eta = olpg.init_params(0, F).astype(np.float32)
+
+    def run(n):
+        keys = jr.split(jr.PRNGKey(0), n)
+        p, lt = olv.reset_env_params(keys, env_mode)
+        rs = np.random.RandomState(0)
+        D = spec.obs_dim
+        theta = (rs.randn(n, D, 5) * 0.1).astype(np.float32)
+        phi = (rs.randn(n, D, 8) * 0.1).astype(np.float32)
+        vc = (rs.randn(n, D, 1) * 0.1).astype(np.float32)
+        t0 = time.perf_counter()
+        st = oro.batch_reset(spec, jr.split(jr.PRNGKey(1), n), p, W)
+        trajs = [[] for _ in range(n)]
+        for k in range(K + 1):
+            tr, st, _ = oro.batch_rollout(spec, jr.split(jr.PRNGKey(10 + k), n), theta, p, st, T)
+            for a in range(n):
+                trajs[a].append({kk: v[a] for kk, v in tr.items()})
+        agents = [dict(theta=theta[a], phi=phi[a], vcrit=vc[a], step=0, lifetime=int(lt[a]),
+                       trajs=trajs[a][:K], eval=trajs[a][K]) for a in range(n)]
+        ometa.meta_gradient(eta, agents, ometa.Hypers(lifetime_conditioning=lifetime_conditioning), K,
+                            dtype=torch.float32)
+        return time.perf_counter() - t0
+
+    if n_agents <= 0:
+        t1 = run(1)
+        n_agents = int(max(1, min(64, round(15.0 / max(t1, 1e-3)))))
+    dt = run(n_agents)
+    return {"value": round(n_agents * W * T * K / dt, 1), "unit": "agent-env-steps/sec",
+            "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle restatement (numpy rollouts + torch-CPU f32 autograd meta-gradient), one meta-step of "
+                      f"{n_agents} agents x W={W} x T={T} x K={K}, env_mode={env_mode}; {dt:.1f} s"}
+
+
+def main():
+    a = parse()
+    from toued.dist import init_from_env
+    from toued.parse_args import parse_args
+    from toued.train import Trainer
+    world = init_from_env()
+    n_gpus = world.size
+    N_total = a.agents_per_gpu * n_gpus
+    cli = ["--env_mode", a.env_mode, "--num_agents", str(N_total), "--num_mini_batches", "1",
+           "--score_function", "random"]
+    if a.lifetime_conditioning:
+        cli.append("--lifetime_conditioning")
+    args = parse_args(cli)
+    tr = Trainer(args, world)
+    step = tr.step_fn
+    for _ in range(a.warmup):
+        tr.meta_step()
+    torch.cuda.synchronize()
+    world.barrier()
+    step.timers.enabled = True
+    step.timers.reset()
+    torch.cuda.synchronize()
+    world.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        metrics = tr.meta_step()
+    torch.cuda.synchronize()
+    world.barrier()
+    dt = time.perf_counter() - t0
+    tmax = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    if world.active:
+        import torch.distributed as dist
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    dt = float(tmax)
+    ksum = step.timers.summary()
+    W, T, K = args.env_workers, args.train_rollout_len, args.num_agent_updates
+    steps_per_meta = N_total * W * T * K
+    value = steps_per_meta * a.steps / dt
+    F = 7 if a.lifetime_conditioning else 5
+    R = a.agents_per_gpu * W
+    kern = {}
+    for name, (n, mean_ms, tot_ms) in ksum.items():
+        kern[name] = {"launches": n, "mean_ms": round(mean_ms, 4), "total_ms_per_step": round(tot_ms / a.steps, 3)}
+    fwd_flops = R * T * GRU_FWD_FLOP_PER_ELEM[F]
+    bwd_flops = K * R * T * GRU_BWD_FLOP_PER_ELEM
+    cand = []
+    if "gru_fwd" in ksum:
+        cand.append(("gru_fwd", ksum["gru_fwd"][2], fwd_flops / (ksum["gru_fwd"][1] * 1e-3) / 1e12))
+    if "gru_bwd" in ksum:
+        cand.append(("gru_bwd", ksum["gru_bwd"][2], bwd_flops / (ksum["gru_bwd"][1] * 1e-3) / 1e12))
+    dom = max(cand, key=lambda c: c[1])
+    roofline = {"bound": "mfma", "kernel": dom[0], "achieved": round(dom[2], 2), "peak": MFMA_F32_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(dom[2] / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None,
+                "flop_per_launch": fwd_flops if dom[0] == "gru_fwd" else bwd_flops}
+    out = {
+        "metric": "agent-env-steps/sec (inner rollout) at num_agents=512; meta-updates/sec",
+        "value": round(value, 1), "unit": "agent-env-steps/sec", "n_gpus": n_gpus, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (procedurally generated levels)",
+        "meta_updates_per_sec": round(a.steps / dt, 3),
+        "config": {"workload": f"C2 LPG meta-gradient env_mode={a.env_mode} num_agents={N_total} "
+                               f"num_mini_batches=1 W={W} T={T} K={K} score_function=random",
+                   "num_agents": N_total, "agents_per_gpu": a.agents_per_gpu, "env_workers": W,
+                   "train_rollout_len": T, "num_agent_updates": K, "parallelism": f"dp{n_gpus} (agent axis)"},
+        "roofline": roofline, "kernels": kern,
+        "metrics": {"lpg_agent_return": float(metrics["lpg_agent_return"].mean()),
+                    "lpg_loss": float(metrics["lpg_loss"].mean())},
+    }
+    if world.rank == 0:
+        if not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(a.env_mode, a.lifetime_conditioning, a.cpu_agents)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world.active:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

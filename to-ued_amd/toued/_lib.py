@@ -60,6 +60,7 @@ _SIGS = {
     "toued_gru_fwd": [_I, _I, _I, _I, _P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _P],
     "toued_gru_bwd": [_I, _I, _I, _I, _P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _P, _P, _P, _P, _P,
                       _P],
+    "toued_choice_cdf": [_P, _P, _I, _I, _P, _P],
     "toued_last_error": [],
     "toued_abi_version": [],
 }

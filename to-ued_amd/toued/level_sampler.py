@@ -1,0 +1,187 @@
+"""UED level sampler on MI355X (environments/level_sampler.py:30-416).
+
+``LevelSampler(args)`` mirrors the reference: ``initialize_buffer``,
+``initial_sample``, ``sample``, ``rollout_manager``, ``max_lifetime``.
+Score functions: ``random`` (domain randomisation), ``frozen`` (uniform replay
+of a fixed buffer) and ``alg_regret`` (PLR with the A2C antagonist's
+algorithmic regret, GROOVE).  All state is device-resident; per-agent work is
+computed for the whole batch and masked by ``terminated`` exactly like the
+reference's vmapped ``jnp.where`` (the masked-out work has no observable effect).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib, prng
+from .agents import AgentBatch, AgentHyperparams, create_agents, create_value_critics
+from .env import L_BUFID, L_LIFETIME, LevelGenerator, get_env_spec
+from .rollout import RolloutWrapper
+
+SCORE_FUNCTIONS = ["random", "frozen", "alg_regret"]
+SCORE_TRANSFORMS = ["proportional", "rank"]
+
+
+@dataclass
+class LevelBuffer:
+    """level_sampler.py:30-52: packed levels [B,64] (buffer_id packed), score, active, new."""
+    levels: torch.Tensor
+    score: torch.Tensor
+    active: torch.Tensor
+    new: torch.Tensor
+
+    def __len__(self):
+        return self.score.shape[0]
+
+
+def cumsum_assoc_np(p: np.ndarray) -> np.ndarray:
+    """jnp.cumsum as lowered by jax 0.4.13 on CPU (lax.associative_scan order), float32."""
+    p = np.asarray(p, np.float32)
+
+    def scan(e):
+        n = e.shape[-1]
+        if n < 2:
+            return e
+        odd = scan(e[0:-1:2] + e[1::2])
+        even = (odd[:-1] + e[2::2]) if n % 2 == 0 else (odd + e[2::2])
+        even = np.concatenate([e[0:1], even])
+        out = np.empty_like(e)
+        out[0::2] = even
+        out[1::2] = odd
+        return out
+
+    return scan(p)
+
+
+class LevelSampler:
+    def __init__(self, args, device=None, world=None):
+        self.env_name = args.env_name
+        self.env_mode = args.env_mode
+        self.env_workers = args.env_workers
+        self.spec, self.max_rollout_len, self.max_lifetime = get_env_spec(self.env_mode)
+        self.rollout_manager = RolloutWrapper(self.env_mode, args.train_rollout_len, self.max_rollout_len,
+                                              args.env_workers)
+        self.agent_hypers = AgentHyperparams.from_args(args)
+        self.agent_hypers.check_supported()
+        if args.score_function not in SCORE_FUNCTIONS:
+            raise ValueError(f"Level score function {args.score_function} not in known functions: {SCORE_FUNCTIONS}")
+        if args.score_transform not in SCORE_TRANSFORMS:
+            raise ValueError(
+                f"Level score transform {args.score_transform} not in known transforms: {SCORE_TRANSFORMS}")
+        self.score_function = args.score_function
+        self.score_transform = args.score_transform
+        self.score_temperature = args.score_temperature
+        self.buffer_size = args.buffer_size
+        self.p_replay = args.p_replay
+        self.num_mini_batches = args.num_mini_batches
+        self.args = args
+        self.world = world
+        self.dev = torch.device(device) if device is not None else torch.device("cuda")
+        self.gen = LevelGenerator(self.env_mode, self.dev)
+        self.Y = args.lpg_target_width
+        self._cdf = None
+
+    @property
+    def obs_dim(self) -> int:
+        return self.spec.obs_dim
+
+    @property
+    def num_actions(self) -> int:
+        return 5
+
+    # ------------------------------------------------------------------ helpers
+    def _slice(self, x: torch.Tensor, sl):
+        return x if sl is None else x[sl[0]:sl[1]].contiguous()
+
+    def _sample_random_levels(self, rng, n_total, sl):
+        """level_sampler.py:268-271: split(rng, N) -> reset_env_params; buffer_id = 0."""
+        keys = self._slice(prng.split(rng, n_total), sl)
+        return self.gen(keys)
+
+    def _create_agents(self, rng, levels, n_total, sl, create_value_critics_too: bool):
+        """vmap(_create_agent) (level_sampler.py:273-291): worker_rng, agent_rng = split(rng_i)."""
+        keys = self._slice(prng.split(rng, n_total), sl)
+        ks = prng.split(keys, 2)
+        (_, _), state = self.rollout_manager.batch_reset(ks[:, 0].contiguous(), levels)
+        theta, phi = create_agents(ks[:, 1].contiguous(), self.obs_dim, self.Y)
+        return theta, phi, state
+
+    # ------------------------------------------------------------------ API
+    def initialize_buffer(self, rng):
+        """level_sampler.py:90-96 (None for score_function=random)."""
+        if self.score_function == "random":
+            return None
+        keys = prng.split(rng, self.buffer_size)
+        ids = torch.arange(self.buffer_size, dtype=torch.int32, device=self.dev)
+        levels = self.gen(keys, buffer_ids=ids)
+        B = self.buffer_size
+        return LevelBuffer(levels, torch.zeros(B, device=self.dev), torch.zeros(B, dtype=torch.bool, device=self.dev),
+                           torch.ones(B, dtype=torch.bool, device=self.dev))
+
+    def initial_sample(self, rng, level_buffer, batch_size: int, create_value_critics_flag: bool, sl=None):
+        """level_sampler.py:103-132.  ``sl`` = (lo, hi, total) agent slice of this rank."""
+        n_local = batch_size if sl is None else sl[1] - sl[0]
+        rng, sub = self._split2(rng)
+        if self.score_function == "random":
+            levels = self._sample_random_levels(sub, batch_size, sl)
+        else:
+            levels = self._slice(level_buffer.levels[:batch_size], sl)
+            level_buffer.active = torch.arange(self.buffer_size, device=self.dev) < batch_size
+        rng, sub = self._split2(rng)
+        theta, phi, state = self._create_agents(sub, levels, batch_size, sl, False)
+        vcrit = None
+        if create_value_critics_flag:
+            rng, sub = self._split2(rng)
+            vcrit = create_value_critics(self._slice(prng.split(sub, batch_size), sl), self.obs_dim)
+        agents = AgentBatch(levels, theta, phi, torch.zeros(n_local, dtype=torch.int32, device=self.dev), state,
+                            vcrit, torch.zeros(n_local, dtype=torch.int32, device=self.dev) if vcrit is not None
+                            else None)
+        return level_buffer, agents
+
+    @staticmethod
+    def _split2(rng):
+        ks = prng.split(rng, 2)
+        return ks[0].contiguous(), ks[1].contiguous()
+
+    def sample(self, rng, level_buffer, agents: AgentBatch, sl=None):
+        """level_sampler.py:134-266: new levels/agents for agents whose step >= lifetime."""
+        n_total = agents.n if sl is None else sl[2]
+        term = agents.step >= agents.levels[:, L_LIFETIME]
+        if self.score_function == "random":
+            rng, sub = self._split2(rng)
+            new_levels = self._sample_random_levels(sub, n_total, sl)
+        elif self.score_function == "frozen":
+            rng, sub = self._split2(rng)
+            ids = self._frozen_ids(sub, n_total)
+            new_levels = self._slice(level_buffer.levels[ids.long()], sl)
+        else:
+            from .plr import plr_sample
+            rng, level_buffer, new_levels = plr_sample(self, rng, level_buffer, agents, term, sl)
+        new_levels = torch.where(term[:, None], new_levels, agents.levels)
+        rng, sub = self._split2(rng)
+        theta, phi, state = self._create_agents(sub, new_levels, n_total, sl, False)
+        W = self.env_workers
+        tw = term.repeat_interleave(W)
+        agents.levels = new_levels
+        agents.theta = torch.where(term[:, None, None], theta, agents.theta)
+        agents.phi = torch.where(term[:, None, None], phi, agents.phi)
+        agents.step = torch.where(term, torch.zeros_like(agents.step), agents.step)
+        agents.state = torch.where(tw[None, :], state, agents.state)
+        if agents.vcrit is not None:
+            rng, sub = self._split2(rng)
+            vc = create_value_critics(self._slice(prng.split(sub, n_total), sl), self.obs_dim)
+            agents.vcrit = torch.where(term[:, None], vc, agents.vcrit)
+            agents.vstep = torch.where(term, torch.zeros_like(agents.vstep), agents.vstep)
+        return level_buffer, agents
+
+    def _frozen_ids(self, rng, n):
+        """random.choice(arange(B), p=uniform, shape=(N,), replace=True) (level_sampler.py:157-165)."""
+        if self._cdf is None:
+            c = cumsum_assoc_np(np.full(self.buffer_size, np.float32(1.0) / np.float32(self.buffer_size), np.float32))
+            self._cdf = torch.from_numpy(c).to(self.dev)
+        out = torch.empty(n, dtype=torch.int32, device=self.dev)
+        _lib.call("toued_choice_cdf", _lib.ptr(rng.contiguous()), _lib.ptr(self._cdf), self.buffer_size, n,
+                  _lib.ptr(out), _lib.stream_ptr())
+        return out

@@ -15,6 +15,7 @@ kernels are built for.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from collections import OrderedDict
 
@@ -50,8 +51,8 @@ class LPGLayout:
             self.offsets[k] = off
             off += int(np.prod(s))
         self.size = off
-        self.off_array = (ctypes_int_array := np.array([self.offsets[k] for k in _OFF_ORDER], np.int32))
-        self._c_off = (__import__("ctypes").c_int * len(_OFF_ORDER))(*ctypes_int_array.tolist())
+        self.off_array = np.array([self.offsets[k] for k in _OFF_ORDER], np.int32)
+        self._c_off = (ctypes.c_int * len(_OFF_ORDER))(*self.off_array.tolist())
 
     def view(self, flat: torch.Tensor, name: str) -> torch.Tensor:
         o = self.offsets[name]
@@ -128,17 +129,21 @@ class LPGGRU:
         del Xk
 
     def backward(self, done_all: torch.Tensor, eta: torch.Tensor, y_hat: torch.Tensor, d_pi_hat: torch.Tensor,
-                 d_y_hat: torch.Tensor, X: torch.Tensor, grad: torch.Tensor):
+                 d_y_hat: torch.Tensor, X: torch.Tensor, grad: torch.Tensor, timers=None):
         """done_all: u8 [K(+1), N, T, W] (first K slots used).  Accumulates d(loss)/d(eta) into ``grad``
         (all parameters except the embedding MLP, which needs dX3/dX4 -> agent-side kernel)."""
         R, T, K, M = self.R, self.T, self.K, self.M
         S = self.S
         stride_k = done_all[0].numel()
+        tok = timers.start("gru_bwd") if timers is not None else None
         _lib.call("toued_gru_bwd", R, T, self.W, K, _lib.ptr(done_all), stride_k, _lib.ptr(self.bwdA), _lib.ptr(eta),
                   self.lay.c_offsets, _lib.ptr(y_hat), _lib.ptr(d_pi_hat), _lib.ptr(d_y_hat),
                   _lib.ptr(S[0]), _lib.ptr(S[1]), _lib.ptr(S[2]), _lib.ptr(S[3]), _lib.ptr(S[4]), M,
                   _lib.ptr(self.DG), _lib.ptr(self.RH), _lib.ptr(self.DH), _lib.ptr(self.dX3), _lib.ptr(self.dX4),
                   _lib.stream_ptr())
+        if timers is not None:
+            timers.stop(tok)
+            tok = timers.start("wgrad_gemm")
         lay = self.lay
         F = lay.F
         DG = self.DG
@@ -162,3 +167,5 @@ class LPGGRU:
         hb = self.DH.sum(dim=1)
         lay.view(grad, "pi_b").add_(hb[0:1])
         lay.view(grad, "y_b").add_(hb[1:9])
+        if timers is not None:
+            timers.stop(tok)

@@ -52,6 +52,40 @@ class AdamState:
         self.count = 0
 
 
+class KernelTimers:
+    """HIP-event timing of selected launches on the stream they are enqueued on (torch's current stream)."""
+
+    def __init__(self):
+        self.events = {}
+        self.enabled = False
+
+    def start(self, name):
+        if not self.enabled:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return (name, ev)
+
+    def stop(self, tok):
+        if tok is None:
+            return
+        name, ev0 = tok
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev1.record()
+        self.events.setdefault(name, []).append((ev0, ev1))
+
+    def summary(self):
+        """name -> (launches, mean ms); call after synchronize."""
+        out = {}
+        for k, v in self.events.items():
+            ms = [a.elapsed_time(b) for a, b in v]
+            out[k] = (len(ms), sum(ms) / len(ms), sum(ms))
+        return out
+
+    def reset(self):
+        self.events = {}
+
+
 class MetaGradStep:
     def __init__(self, rollout: RolloutWrapper, n_agents: int, hyp: LpgHyperparams, lifetime_conditioning: bool,
                  device=None, world=None):
@@ -102,6 +136,7 @@ class MetaGradStep:
         self.embed_blocks = 512
         self.embed_partial = z(self.embed_blocks, 161)
         self.ea_cum = None
+        self.timers = KernelTimers()
 
     # ------------------------------------------------------------------ helpers
     def _t(self, k: int) -> Transition:
@@ -141,13 +176,17 @@ class MetaGradStep:
         # ---------------- forward: K inner updates (agents/lpg_agent.py:88-140)
         for k in range(K):
             tk = self._t(k)
+            tok = self.timers.start("rollout")
             self.ro.batch_rollout(self.keys_roll[k], self.theta_h[k], agents.levels, state, out=tk,
                                   inplace_state=True)
+            self.timers.stop(tok)
             L.call("toued_lpg_inputs", N, W, T, D, self.F, ptr(self.theta_h[k]), ptr(self.phi_h[k]),
                    ptr(tk.obs_idx), ptr(tk.obs_time), ptr(tk.action), ptr(tk.reward), ptr(tk.done),
                    ptr(e1w), ptr(e1b), ptr(e2w), ptr(e2b), ptr(agents.step), ptr(agents.levels),
                    ptr(self.X) + 4 * k * T * R, self.gru.M, st)
+            tok = self.timers.start("gru_fwd")
             self.gru.forward(k, self.X, tk.done, eta, self.pi_hat, self.y_hat)
+            self.timers.stop(tok)
             L.call("toued_agent_grad", N, W, T, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(tk.obs_idx),
                    ptr(tk.obs_time), ptr(tk.action), ptr(tk.reward), ptr(tk.done), ptr(self.pi_hat[k]),
                    ptr(self.y_hat[k]), hyp.agent_target_coeff, ptr(self.G_th[k]), ptr(self.G_ph[k]),
@@ -193,7 +232,8 @@ class MetaGradStep:
                    ptr(self.adj_th[a_out]), ptr(self.adj_ph[a_out]), ptr(self.d_pi_hat[k]), ptr(self.d_y_hat[k]), st)
             a_in, a_out = a_out, a_in
         self.grad.zero_()
-        self.gru.backward(self.traj.done, eta, self.y_hat, self.d_pi_hat, self.d_y_hat, self.X, self.grad)
+        self.gru.backward(self.traj.done, eta, self.y_hat, self.d_pi_hat, self.d_y_hat, self.X, self.grad,
+                          self.timers)
         tr = self.traj
         L.call("toued_embed_bwd", N, W, T, D, K, ptr(self.phi_h), self.phi_h[0].numel(), ptr(tr.obs_idx),
                tr.obs_idx[0].numel(), ptr(tr.obs_time), ptr(tr.done), tr.done[0].numel(), ptr(self.gru.dX3),

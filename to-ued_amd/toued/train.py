@@ -1,0 +1,125 @@
+"""Meta-training driver (train.py:14-82 of the reference) on MI355X.
+
+    python -m toued.train --env_mode tabular --num_agents 512 --num_mini_batches 1 [--score_function alg_regret]
+                         [--use_es --lifetime_conditioning] [--train_steps N | --ref_quirk_steps10]
+
+One process per GPU (torchrun): agents are sharded over ranks; the LPG
+parameters are replicated and updated identically on every rank after the
+meta-gradient all-reduce.  ``--num_mini_batches`` is accepted and validated
+(the reference's divisibility check) but the whole agent batch runs at once:
+mini-batching is numerically a no-op (util/jax.py:25-41) and 288 GB of HBM
+holds the full batch.
+"""
+from __future__ import annotations
+
+import json
+import sys
+import time
+
+import torch
+
+from . import prng
+from .dist import World, init_from_env
+from .level_sampler import LevelSampler
+from .lpg import init_lpg_params
+from .meta import AdamState, LpgHyperparams, MetaGradStep
+from .parse_args import parse_args
+
+
+def lpg_hypers_from_args(args, sampler: LevelSampler) -> LpgHyperparams:
+    ah = sampler.agent_hypers
+    return LpgHyperparams(
+        num_agent_updates=args.num_agent_updates, agent_target_coeff=args.lpg_agent_target_coeff,
+        policy_entropy_coeff=args.lpg_policy_entropy_coeff, target_entropy_coeff=args.lpg_target_entropy_coeff,
+        policy_l2_coeff=args.lpg_policy_l2_coeff, target_l2_coeff=args.lpg_target_l2_coeff, gamma=args.gamma,
+        gae_lambda=args.gae_lambda, actor_lr=ah.actor_learning_rate, critic_lr=ah.critic_learning_rate,
+        max_grad_norm=ah.max_grad_norm, lpg_lr=args.lpg_learning_rate)
+
+
+def check_supported(args):
+    if args.env_name != "GridWorld-v0":
+        raise NotImplementedError("gymnax environments are out of scope (DESIGN.md); use GridWorld-v0")
+    if (args.lpg_gru_width, args.lpg_target_width, args.lpg_embedding_net_width) != (256, 8, 16):
+        raise NotImplementedError("the MFMA LPG kernels are built for gru_width=256, target_width=8, embedding=16")
+    if args.lpg_opt.lower() != "adam" and not args.use_es:
+        raise NotImplementedError("meta-gradient LPG optimiser: Adam (models/optim.py:12-17)")
+
+
+class Trainer:
+    """make_train(args) (train.py:14-59) as a stateful object with one method per meta-step."""
+
+    def __init__(self, args, world: World | None = None, device=None):
+        check_supported(args)
+        self.args = args
+        self.world = world or World()
+        self.dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        sl = self.world.agent_slice(args.num_agents) if self.world.size > 1 else None
+        self.sl = sl
+        rng = prng.PRNGKey(args.seed, self.dev)
+        ks = prng.split(rng, 3)
+        self.rng, lpg_rng, buffer_rng = ks[0].contiguous(), ks[1].contiguous(), ks[2].contiguous()
+        F = 7 if args.lifetime_conditioning else 5
+        # LPG init: flax init key derivation unpinned -> seeded by the key's low word
+        self.eta = init_lpg_params(int(prng.to_uint32_numpy(lpg_rng)[1]), F, self.dev)
+        self.sampler = LevelSampler(args, self.dev, self.world)
+        self.buffer = self.sampler.initialize_buffer(buffer_rng)
+        ks = prng.split(self.rng, 2)
+        self.rng, sub = ks[0].contiguous(), ks[1].contiguous()
+        n_local = args.num_agents if sl is None else sl[1] - sl[0]
+        self.buffer, self.agents = self.sampler.initial_sample(sub, self.buffer, args.num_agents,
+                                                               not args.use_es, sl)
+        if args.use_es:
+            from .es import ESTrainStep
+            self.step_fn = ESTrainStep(args, self.sampler, n_local, self.eta, self.dev, self.world)
+        else:
+            self.hyp = lpg_hypers_from_args(args, self.sampler)
+            self.step_fn = MetaGradStep(self.sampler.rollout_manager, n_local, self.hyp, args.lifetime_conditioning,
+                                        self.dev, self.world)
+            self.adam = AdamState(self.eta.numel(), self.dev)
+
+    def meta_step(self):
+        """_meta_train_loop (train.py:36-54): LPG update, then level_sampler.sample."""
+        ks = prng.split(self.rng, 2)
+        self.rng, sub = ks[0].contiguous(), ks[1].contiguous()
+        if self.args.use_es:
+            metrics = self.step_fn(sub, self.agents, self.sl)
+        else:
+            metrics = self.step_fn(sub, self.eta, self.adam, self.agents, self.sl)
+        ks = prng.split(self.rng, 2)
+        self.rng, sub = ks[0].contiguous(), ks[1].contiguous()
+        self.buffer, self.agents = self.sampler.sample(sub, self.buffer, self.agents, self.sl)
+        return metrics
+
+
+def reduce_metrics(m, world: World):
+    """Mean over agents (meta/train.py:180), across ranks when distributed."""
+    if isinstance(m, dict):
+        return {k: reduce_metrics(v, world) for k, v in m.items()}
+    if not torch.is_tensor(m):
+        return m
+    if m.dim() == 0:
+        return float(m)
+    s = m.float().sum().reshape(1)
+    n = torch.tensor([m.numel()], dtype=torch.float32, device=m.device)
+    world.all_reduce_sum(s)
+    world.all_reduce_sum(n)
+    return float(s / n)
+
+
+def main(cmd_args=None):
+    args = parse_args(cmd_args)
+    world = init_from_env()
+    tr = Trainer(args, world)
+    steps = 10 if args.ref_quirk_steps10 else args.train_steps
+    history = []
+    t0 = time.time()
+    for i in range(steps):
+        m = reduce_metrics(tr.meta_step(), world)
+        history.append(m)
+        if world.rank == 0:
+            print(json.dumps({"step": i, "elapsed_s": round(time.time() - t0, 3), **m}), flush=True)
+    return history
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
