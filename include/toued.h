@@ -80,7 +80,10 @@ int toued_batch_reset(EnvSpec spec, const int* levels, const uint32_t* agent_key
                       int* obs_idx, int* obs_time, hipStream_t stream);
 /* batch_rollout(rng, actor_state, env_params, obs, state) — T policy steps with the
  * linear softmax actor theta[n_agents][D][5].  Trajectory layout: idx/time [N][T+1][W]
- * (slot T = end obs), action/done u8 [N][T][W], reward f32 [N][T][W]; cum_return [N*W]. */
+ * (slot T = end obs), action/done u8 [N][T][W], reward f32 [N][T][W]; cum_return [N*W].
+ * Returns-only mode (all five trajectory pointers NULL, as eval_agent uses it,
+ * agents/agents.py:98-106): cum_return only; a worker stops once its first episode
+ * ends and `state` is left unmodified. */
 int toued_rollout(EnvSpec spec, const int* levels, const float* theta, int D, const uint32_t* agent_keys,
                   int* state, int n_agents, int W, int T, int* traj_idx, int* traj_time, uint8_t* traj_action,
                   float* traj_reward, uint8_t* traj_done, float* cum_return, hipStream_t stream);

@@ -121,7 +121,8 @@ def test_gru_forward_matches_oracle():
     gru = LPGGRU(lay, R, T, K, W, "cuda")
     gru.pack(eta)
     rs = np.random.RandomState(0)
-    X = torch.from_numpy(rs.randn(5, K, T, R).astype(np.float32)).cuda()
+    X = gru.X
+    X.copy_(torch.from_numpy(rs.randn(5, K, T, R).astype(np.float32)))
     done = (rs.rand(K, N, T, W) < 0.1).astype(np.uint8)
     X[1, 0] = torch.from_numpy(done[0].transpose(1, 0, 2).reshape(T, R).astype(np.float32)).cuda()
     pi_hat = torch.zeros(K, T, R, device="cuda")

@@ -359,6 +359,8 @@ __global__ void __launch_bounds__(256) k_rollout(EnvSpec sp, const int* __restri
     env_step<NMAX, TAB>(sp, lev, sub, s, action, r, d);
     cum = __fadd_rn(cum, __fmul_rn(r, valid));
     valid = __fmul_rn(valid, d ? 0.0f : 1.0f);
+    // returns-only mode (eval_agent): nothing after the first episode can change cum_return
+    if (!traj_idx && valid == 0.0f) break;
     if (traj_idx) {   // eval_agent only needs the return (agents/agents.py:98-106)
       traj_idx[base_o + (size_t)t * W] = idx;
       traj_time[base_o + (size_t)t * W] = tm;
@@ -371,7 +373,7 @@ __global__ void __launch_bounds__(256) k_rollout(EnvSpec sp, const int* __restri
     traj_idx[base_o + (size_t)T * W] = tab_index(sp, s);
     traj_time[base_o + (size_t)T * W] = s.time;
   }
-  store_state<NMAX>(state, n, i, s);
+  if (traj_idx) store_state<NMAX>(state, n, i, s);   // returns-only mode leaves the state untouched
   cum_return[i] = cum;
 }
 

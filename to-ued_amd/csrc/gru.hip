@@ -43,13 +43,19 @@ TOUED_DEV floatx16 mfma32(float a, float b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
-// Streamed [256][M] tensors: uniform (SGPR) base for the register's unit + a 32-bit per-lane
-// byte offset, so every access is a single saddr+voffset global instruction.
-TOUED_DEV float ld_u(const float* base_q, unsigned vbyte) {
-  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base_q) + vbyte);
+// Streamed [256][M] tensors: raw buffer ops with a wave-uniform descriptor built from the
+// array base + the register's (uniform) unit/column offset, and ONE 32-bit per-lane byte
+// offset shared by every array (cdna_hip_programming.md T8/T20) -- no per-array 64-bit
+// VGPR addresses.  The host guarantees 256*M*4 < 2^32 (toued_gru_* check).
+TOUED_DEV __amdgpu_buffer_rsrc_t rsrc_of(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, -1 /* 4 GiB */, 0x00020000);
 }
-TOUED_DEV void st_u(float* base_q, unsigned vbyte, float v) {
-  *reinterpret_cast<float*>(reinterpret_cast<char*>(base_q) + vbyte) = v;
+// element (unit u = lane unit base + qu, column c) at base + u*M + c: lane part in vbyte, uniform part in soff
+TOUED_DEV float ld_u(__amdgpu_buffer_rsrc_t r, unsigned vbyte, unsigned soff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)vbyte, (int)soff, 0));
+}
+TOUED_DEV void st_u(__amdgpu_buffer_rsrc_t r, unsigned vbyte, unsigned soff, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)vbyte, (int)soff, 0);
 }
 TOUED_DEV int qunit(int q) { return (q & 3) + 8 * (q >> 2); }
 
@@ -120,7 +126,7 @@ struct FwdArgs {
 #define NWAVE 8         // 512-thread workgroups: wave w owns units [32w, 32w+32)
 #define NGRP (2 * NWAVE)
 
-__global__ void __launch_bounds__(512, 2) k_gru_fwd(FwdArgs p) {
+__global__ void __launch_bounds__(512, 4) k_gru_fwd(FwdArgs p) {
   __shared__ float hT[(HU + NAUG) * LDH];
   __shared__ float wh[HU * 9];
   __shared__ float hp[NGRP * 9 * RB];
@@ -134,9 +140,6 @@ __global__ void __launch_bounds__(512, 2) k_gru_fwd(FwdArgs p) {
     wh[i] = oo == 0 ? p.eta[p.o.pi_w + u] : p.eta[p.o.y_w + u * 8 + (oo - 1)];
   }
   for (int i = tid; i < (HU + NAUG) * LDH; i += 512) hT[i] = 0.0f;
-  float hreg[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) hreg[q] = 0.0f;
   __syncthreads();
   if (tid < RB) {
     const int t = T - 1;
@@ -146,6 +149,8 @@ __global__ void __launch_bounds__(512, 2) k_gru_fwd(FwdArgs p) {
   __syncthreads();
   const float bpi = p.eta[p.o.pi_b];
   const float4* Ab = p.A + lane;
+  const __amdgpu_buffer_rsrc_t rs_hin = rsrc_of(p.s_hin), rs_r = rsrc_of(p.s_r), rs_z = rsrc_of(p.s_z),
+                               rs_n = rsrc_of(p.s_n), rs_hn = rsrc_of(p.s_hn);
   for (int s = 0; s < T; ++s) {
     const int t = T - 1 - s;
     floatx16 acc[4];
@@ -198,37 +203,36 @@ __global__ void __launch_bounds__(512, 2) k_gru_fwd(FwdArgs p) {
 #pragma unroll
     for (int oo = 0; oo < 9; ++oo) hp_loc[oo] = 0.0f;
     float hnew[16];
+    const float* hTl = hT + (32 * wave + 4 * hi) * LDH + col;
+    const float* whl = wh + (32 * wave + 4 * hi) * 9;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const int u = 32 * wave + (q & 3) + 8 * (q >> 2) + 4 * hi;
       const float rg = sigm(acc[0][q]);
       const float zg = sigm(acc[1][q]);
       const float hn = acc[2][q];
       const float ng = tanh_f(acc[3][q] + rg * hn);
-      const float hin = hreg[q];
+      const float hin = hTl[qunit(q) * LDH];    // h_in(t) (masked carry), rewritten after the barrier
       const float h = (1.0f - zg) * ng + zg * hin;
       hnew[q] = h;
-      const long qo = (long)qunit(q) * p.M + cbase;
-      st_u(p.s_hin + qo, vbyte, hin);
-      st_u(p.s_r + qo, vbyte, rg);
-      st_u(p.s_z + qo, vbyte, zg);
-      st_u(p.s_n + qo, vbyte, ng);
-      st_u(p.s_hn + qo, vbyte, hn);
+      const unsigned so = (unsigned)(((long)qunit(q) * p.M + cbase) * 4);
+      st_u(rs_hin, vbyte, so, hin);
+      st_u(rs_r, vbyte, so, rg);
+      st_u(rs_z, vbyte, so, zg);
+      st_u(rs_n, vbyte, so, ng);
+      st_u(rs_hn, vbyte, so, hn);
       const float rl = fmaxf(h, 0.0f);
 #pragma unroll
-      for (int oo = 0; oo < 9; ++oo) hp_loc[oo] += rl * wh[u * 9 + oo];
+      for (int oo = 0; oo < 9; ++oo) hp_loc[oo] += rl * whl[qunit(q) * 9 + oo];
     }
 #pragma unroll
     for (int oo = 0; oo < 9; ++oo) hp[((2 * wave + hi) * 9 + oo) * RB + col] = hp_loc[oo];
     __syncthreads();   // all MFMA reads of hT done; head partials visible
     // next-step carry: h_in(t-1) = where(d_{t-1}, 0, h_out(t))
     const bool dn = (t >= 1) ? p.done[((size_t)a * T + (t - 1)) * W + w] != 0 : false;
+    float* hTw = hT + (32 * wave + 4 * hi) * LDH + col;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const int u = 32 * wave + (q & 3) + 8 * (q >> 2) + 4 * hi;
-      const float h = dn ? 0.0f : hnew[q];
-      hreg[q] = h;
-      hT[u * LDH + col] = h;
+      hTw[qunit(q) * LDH] = dn ? 0.0f : hnew[q];
     }
     if (t >= 1 && tid < RB) {
       for (int f = 0; f < F; ++f) hT[(HU + f) * LDH + tid] = p.X[f * p.xs_f + (size_t)(t - 1) * R + r0 + tid];
@@ -270,9 +274,8 @@ struct BwdArgs {
   float* dX3; float* dX4;   // [K][T][R]
 };
 
-__global__ void __launch_bounds__(512, 2) k_gru_bwd(BwdArgs p) {
+__global__ void __launch_bounds__(512, 4) k_gru_bwd(BwdArgs p) {
   __shared__ float dgT[HU * LDH];
-  __shared__ float wh[HU * 9];
   __shared__ float wi34[2 * 3 * HU];
   __shared__ float hv[9 * RB];
   __shared__ float dxp[NGRP * 2 * RB];
@@ -282,10 +285,6 @@ __global__ void __launch_bounds__(512, 2) k_gru_bwd(BwdArgs p) {
   const int r0 = (blockIdx.x - k * nb) * RB, row = r0 + col;
   const int R = p.R, T = p.T, W = p.W;
   const int a = r0 / W, w = row - a * W;
-  for (int i = tid; i < HU * 9; i += 512) {
-    const int u = i / 9, oo = i - u * 9;
-    wh[i] = oo == 0 ? p.eta[p.o.pi_w + u] : p.eta[p.o.y_w + u * 8 + (oo - 1)];
-  }
   // W_i rows for the embedding inputs (f = 3: pyt, f = 4: pyt1), per gate kind r, z, n
   for (int i = tid; i < 2 * 3 * HU; i += 512) {
     const int f = 3 + i / (3 * HU), g = (i / HU) % 3, u = i % HU;
@@ -295,8 +294,18 @@ __global__ void __launch_bounds__(512, 2) k_gru_bwd(BwdArgs p) {
   float dh[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) dh[q] = 0.0f;
+  float wA[5];    // A fragments of W_heads^T for this wave's unit tile: A[i=l&31][k=2kk+(l>>5)]
+#pragma unroll
+  for (int kk = 0; kk < 5; ++kk) {
+    const int o = 2 * kk + hi, u = 32 * wave + col;
+    wA[kk] = o < 9 ? (o == 0 ? p.eta[p.o.pi_w + u] : p.eta[p.o.y_w + u * 8 + (o - 1)]) : 0.0f;
+  }
   const uint8_t* done = p.done + (long)k * p.done_stride_k;
   const float4* Ab = p.A + lane;
+  const __amdgpu_buffer_rsrc_t rs_hin = rsrc_of(p.s_hin), rs_r = rsrc_of(p.s_r), rs_z = rsrc_of(p.s_z),
+                               rs_n = rsrc_of(p.s_n), rs_hn = rsrc_of(p.s_hn), rs_rh = rsrc_of(p.RH);
+  const __amdgpu_buffer_rsrc_t rs_dg[4] = {rsrc_of(p.DG), rsrc_of(p.DG + 1L * HU * p.M),
+                                           rsrc_of(p.DG + 2L * HU * p.M), rsrc_of(p.DG + 3L * HU * p.M)};
   __syncthreads();
   for (int t = 0; t < T; ++t) {
     const long ctr = ((long)k * T + t) * R;          // column base in [.][K*T*R]
@@ -318,26 +327,27 @@ __global__ void __launch_bounds__(512, 2) k_gru_bwd(BwdArgs p) {
       }
     }
     __syncthreads();
-    float hvl[9];
+    // head VJP W_heads . hv on MFMA: A[i = unit][k = head output o] (constant per lane, wA),
+    // B[k = o][j = row] from hv; the result has the accumulator layout (lane = row, reg = unit).
+    floatx16 hacc;
 #pragma unroll
-    for (int oo = 0; oo < 9; ++oo) hvl[oo] = hv[oo * RB + col];
+    for (int q = 0; q < 16; ++q) hacc[q] = 0.0f;
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) {
+      const int o = 2 * kk + hi;
+      hacc = mfma32(wA[kk], o < 9 ? hv[o * RB + col] : 0.0f, hacc);
+    }
     const unsigned vbyte = (unsigned)(((long)(32 * wave + 4 * hi) * p.M + row) * 4);
     float dx3 = 0.0f, dx4 = 0.0f;
+    const float* wil = wi34 + 32 * wave + 4 * hi;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const int u = 32 * wave + (q & 3) + 8 * (q >> 2) + 4 * hi;
-      const long qo = (long)qunit(q) * p.M + ctr;
-      const float hin = ld_u(p.s_hin + qo, vbyte), rg = ld_u(p.s_r + qo, vbyte), zg = ld_u(p.s_z + qo, vbyte);
-      const float ng = ld_u(p.s_n + qo, vbyte), hn = ld_u(p.s_hn + qo, vbyte);
+      const unsigned so = (unsigned)(((long)qunit(q) * p.M + ctr) * 4);
+      const float hin = ld_u(rs_hin, vbyte, so), rg = ld_u(rs_r, vbyte, so), zg = ld_u(rs_z, vbyte, so);
+      const float ng = ld_u(rs_n, vbyte, so), hn = ld_u(rs_hn, vbyte, so);
       const float hout = (1.0f - zg) * ng + zg * hin;
-      float d = dh[q];
-      if (hout > 0.0f) {
-        float hs = 0.0f;
-#pragma unroll
-        for (int oo = 0; oo < 9; ++oo) hs += wh[u * 9 + oo] * hvl[oo];
-        d += hs;
-      }
-      st_u(p.RH + qo, vbyte, fmaxf(hout, 0.0f));
+      const float d = dh[q] + (hout > 0.0f ? hacc[q] : 0.0f);
+      st_u(rs_rh, vbyte, so, fmaxf(hout, 0.0f));
       const float dn_ = d * (1.0f - zg);
       const float dz = d * (hin - ng);
       const float dnp = dn_ * (1.0f - ng * ng);
@@ -345,12 +355,13 @@ __global__ void __launch_bounds__(512, 2) k_gru_bwd(BwdArgs p) {
       const float drp = dnp * hn * rg * (1.0f - rg);
       const float dzp = dz * zg * (1.0f - zg);
       dh[q] = d * zg;   // direct path; the W_h^T contraction is added below
-      st_u(p.DG + 0L * HU * p.M + qo, vbyte, drp);
-      st_u(p.DG + 1L * HU * p.M + qo, vbyte, dzp);
-      st_u(p.DG + 2L * HU * p.M + qo, vbyte, dhn);
-      st_u(p.DG + 3L * HU * p.M + qo, vbyte, dnp);
-      dx3 += drp * wi34[0 * HU + u] + dzp * wi34[1 * HU + u] + dnp * wi34[2 * HU + u];
-      dx4 += drp * wi34[3 * HU + u] + dzp * wi34[4 * HU + u] + dnp * wi34[5 * HU + u];
+      st_u(rs_dg[0], vbyte, so, drp);
+      st_u(rs_dg[1], vbyte, so, dzp);
+      st_u(rs_dg[2], vbyte, so, dhn);
+      st_u(rs_dg[3], vbyte, so, dnp);
+      const int qu = qunit(q);
+      dx3 += drp * wil[0 * HU + qu] + dzp * wil[1 * HU + qu] + dnp * wil[2 * HU + qu];
+      dx4 += drp * wil[3 * HU + qu] + dzp * wil[4 * HU + qu] + dnp * wil[5 * HU + qu];
     }
     dxp[((2 * wave + hi) * 2 + 0) * RB + col] = dx3;
     dxp[((2 * wave + hi) * 2 + 1) * RB + col] = dx4;
@@ -359,10 +370,11 @@ __global__ void __launch_bounds__(512, 2) k_gru_bwd(BwdArgs p) {
     for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
 #pragma unroll 1
     for (int g = 0; g < 3; ++g) {
+      float* dgl = dgT + (32 * wave + 4 * hi) * LDH + col;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int u = 32 * wave + (q & 3) + 8 * (q >> 2) + 4 * hi;
-        dgT[u * LDH + col] = ld_u(p.DG + (long)g * HU * p.M + (long)qunit(q) * p.M + ctr, vbyte);  // own store
+        dgl[qunit(q) * LDH] = ld_u(g == 0 ? rs_dg[0] : g == 1 ? rs_dg[1] : rs_dg[2], vbyte,
+                                   (unsigned)(((long)qunit(q) * p.M + ctr) * 4));   // this lane's own store
       }
       __syncthreads();
       float4 an = Ab[((wave * 3 + g) * 32 + 0) * 64];
@@ -417,6 +429,8 @@ int toued_gru_fwd(int R, int T, int W, int F, const float* X, long xs_f, const u
                   float* s_n, float* s_hn, long M, hipStream_t stream) {
   TOUED_REQUIRE(R % RB == 0 && W % RB == 0, "toued_gru_fwd: rows R=%d and workers W=%d must be multiples of 32", R, W);
   TOUED_REQUIRE(F >= 1 && F <= 7 && T >= 1, "toued_gru_fwd: F=%d T=%d", F, T);
+  TOUED_REQUIRE((double)M * 264.0 * 4.0 < 4294967295.0, "toued_gru_fwd: M=%ld columns exceed the 4 GiB buffer range "
+                "(use --num_mini_batches to split the agent batch)", M);
   FwdArgs p;
   p.R = R; p.T = T; p.W = W; p.F = F; p.X = X; p.xs_f = xs_f; p.done = done;
   p.A = reinterpret_cast<const float4*>(fwdA); p.eta = eta;
@@ -432,6 +446,8 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
                   const float* s_hin, const float* s_r, const float* s_z, const float* s_n, const float* s_hn, long M,
                   float* DG, float* RH, float* DH, float* dX3, float* dX4, hipStream_t stream) {
   TOUED_REQUIRE(R % RB == 0 && W % RB == 0, "toued_gru_bwd: rows R=%d and workers W=%d must be multiples of 32", R, W);
+  TOUED_REQUIRE((double)M * 264.0 * 4.0 < 4294967295.0, "toued_gru_bwd: M=%ld columns exceed the 4 GiB buffer range",
+                M);
   BwdArgs p;
   p.R = R; p.T = T; p.W = W; p.K = K; p.done = done; p.done_stride_k = done_stride_k;
   p.A = reinterpret_cast<const float4*>(bwdA); p.eta = eta;

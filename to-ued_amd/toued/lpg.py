@@ -103,9 +103,16 @@ class LPGGRU:
         self.fwdA = torch.empty(int(L.toued_gru_packed_floats(0)), dtype=f32, device=dev)
         self.bwdA = torch.empty(int(L.toued_gru_packed_floats(1)), dtype=f32, device=dev)
         M = self.M
-        self.S = torch.empty((5, H, M), dtype=f32, device=dev)          # h_in, r, z, n, hn
+        # h_in saved as rows 0..255 of an augmented [264, M] operand whose rows 256..256+F-1 hold the
+        # GRU inputs X (written by the LPG-input kernel) and row 256+F is all ones: one GEMM against the
+        # gate cotangents then yields dW_h, dW_i and the biases together.
+        self.A = torch.zeros((H + 8, M), dtype=f32, device=dev)
+        self.A[H + lay.F].fill_(1.0)
+        self.X = self.A[H:H + lay.F].view(lay.F, K, T, R)
+        self.S = torch.empty((4, H, M), dtype=f32, device=dev)          # r, z, n, hn
         self.DG = torch.empty((4, H, M), dtype=f32, device=dev)         # dr_pre, dz_pre, d(hn), dn_pre
-        self.RH = torch.empty((H, M), dtype=f32, device=dev)            # relu(h_out)
+        self.RH = torch.zeros((H + 1, M), dtype=f32, device=dev)        # relu(h_out) + ones row
+        self.RH[H].fill_(1.0)
         self.DH = torch.empty((9, M), dtype=f32, device=dev)            # head cotangents
         self.dX3 = torch.empty((K, T, R), dtype=f32, device=dev)
         self.dX4 = torch.empty((K, T, R), dtype=f32, device=dev)
@@ -123,9 +130,9 @@ class LPGGRU:
         S = self.S
         _lib.call("toued_gru_fwd", R, T, self.W, self.lay.F, _lib.ptr(X) + 4 * col, M, _lib.ptr(done_k),
                   _lib.ptr(self.fwdA), _lib.ptr(eta), self.lay.c_offsets, _lib.ptr(pi_hat[k]), _lib.ptr(y_hat[k]),
-                  _lib.ptr(S) + 4 * (0 * H * M + col), _lib.ptr(S) + 4 * (1 * H * M + col),
-                  _lib.ptr(S) + 4 * (2 * H * M + col), _lib.ptr(S) + 4 * (3 * H * M + col),
-                  _lib.ptr(S) + 4 * (4 * H * M + col), M, _lib.stream_ptr())
+                  _lib.ptr(self.A) + 4 * col, _lib.ptr(S) + 4 * (0 * H * M + col),
+                  _lib.ptr(S) + 4 * (1 * H * M + col), _lib.ptr(S) + 4 * (2 * H * M + col),
+                  _lib.ptr(S) + 4 * (3 * H * M + col), M, _lib.stream_ptr())
         del Xk
 
     def backward(self, done_all: torch.Tensor, eta: torch.Tensor, y_hat: torch.Tensor, d_pi_hat: torch.Tensor,
@@ -138,7 +145,7 @@ class LPGGRU:
         tok = timers.start("gru_bwd") if timers is not None else None
         _lib.call("toued_gru_bwd", R, T, self.W, K, _lib.ptr(done_all), stride_k, _lib.ptr(self.bwdA), _lib.ptr(eta),
                   self.lay.c_offsets, _lib.ptr(y_hat), _lib.ptr(d_pi_hat), _lib.ptr(d_y_hat),
-                  _lib.ptr(S[0]), _lib.ptr(S[1]), _lib.ptr(S[2]), _lib.ptr(S[3]), _lib.ptr(S[4]), M,
+                  _lib.ptr(self.A), _lib.ptr(S[0]), _lib.ptr(S[1]), _lib.ptr(S[2]), _lib.ptr(S[3]), M,
                   _lib.ptr(self.DG), _lib.ptr(self.RH), _lib.ptr(self.DH), _lib.ptr(self.dX3), _lib.ptr(self.dX4),
                   _lib.stream_ptr())
         if timers is not None:
@@ -147,25 +154,25 @@ class LPGGRU:
         lay = self.lay
         F = lay.F
         DG = self.DG
-        # weight-gradient GEMMs (library GEMMs on the saved operands; reduction over M = K*T*R)
-        gh = torch.mm(S[0], DG[0:3].reshape(3 * H, M).t())                 # [256, 768]
-        lay.view(grad, "hr_w").add_(gh[:, 0:H])
-        lay.view(grad, "hz_w").add_(gh[:, H:2 * H])
-        lay.view(grad, "hn_w").add_(gh[:, 2 * H:3 * H])
-        X2 = X.reshape(F, M)
-        lay.view(grad, "ir_w").add_(torch.mm(X2, DG[0].t()))
-        lay.view(grad, "iz_w").add_(torch.mm(X2, DG[1].t()))
-        lay.view(grad, "in_w").add_(torch.mm(X2, DG[3].t()))
-        bsum = DG.sum(dim=2)                                                # [4, 256]
-        lay.view(grad, "ir_b").add_(bsum[0])
-        lay.view(grad, "iz_b").add_(bsum[1])
-        lay.view(grad, "hn_b").add_(bsum[2])
-        lay.view(grad, "in_b").add_(bsum[3])
-        heads = torch.mm(self.RH, self.DH.t())                             # [256, 9]
-        lay.view(grad, "pi_w").add_(heads[:, 0:1])
-        lay.view(grad, "y_w").add_(heads[:, 1:9])
-        hb = self.DH.sum(dim=1)
-        lay.view(grad, "pi_b").add_(hb[0:1])
-        lay.view(grad, "y_b").add_(hb[1:9])
+        # weight-gradient GEMMs (library GEMMs on the saved operands; reduction over M = K*T*R):
+        #   [h_in; X; 1] (264 x M) . [dr; dz; dhn]^T  -> dW_h (rows 0..255), dW_ir/dW_iz (X rows), biases (ones row)
+        #   [X; 1] . dn^T -> dW_in, b_in;   [relu(h_out); 1] . DH^T -> head kernels and biases
+        G = torch.mm(self.A, DG[0:3].reshape(3 * H, M).t())                # [264, 768]
+        lay.view(grad, "hr_w").add_(G[0:H, 0:H])
+        lay.view(grad, "hz_w").add_(G[0:H, H:2 * H])
+        lay.view(grad, "hn_w").add_(G[0:H, 2 * H:3 * H])
+        lay.view(grad, "ir_w").add_(G[H:H + F, 0:H])
+        lay.view(grad, "iz_w").add_(G[H:H + F, H:2 * H])
+        lay.view(grad, "ir_b").add_(G[H + F, 0:H])
+        lay.view(grad, "iz_b").add_(G[H + F, H:2 * H])
+        lay.view(grad, "hn_b").add_(G[H + F, 2 * H:3 * H])
+        Gn = torch.mm(self.A[H:H + F + 1], DG[3].t())                      # [F+1, 256]
+        lay.view(grad, "in_w").add_(Gn[0:F])
+        lay.view(grad, "in_b").add_(Gn[F])
+        heads = torch.mm(self.RH, self.DH.t())                             # [257, 9]
+        lay.view(grad, "pi_w").add_(heads[0:H, 0:1])
+        lay.view(grad, "y_w").add_(heads[0:H, 1:9])
+        lay.view(grad, "pi_b").add_(heads[H, 0:1])
+        lay.view(grad, "y_b").add_(heads[H, 1:9])
         if timers is not None:
             timers.stop(tok)

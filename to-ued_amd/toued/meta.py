@@ -116,7 +116,6 @@ class MetaGradStep:
         self.met = z(K, N, 8)
         self.traj = Transition(z(K + 1, N, T + 1, W, dt=i32), z(K + 1, N, T + 1, W, dt=i32),
                                z(K + 1, N, T, W, dt=u8), z(K + 1, N, T, W), z(K + 1, N, T, W, dt=u8))
-        self.X = z(self.F, K, T, R)
         self.pi_hat = z(K, T, R)
         self.y_hat = z(K, T, Y, R)
         self.d_pi_hat = z(K, T, R)
@@ -132,6 +131,7 @@ class MetaGradStep:
         self.keys_ea_reset = z(N, 2, dt=i32)
         self.keys_ea_roll = z(N, 2, dt=i32)
         self.gru = LPGGRU(self.lay, R, T, K, W, dev)
+        self.X = self.gru.X                      # [F, K, T, R] view into the augmented GEMM operand
         self.grad = z(self.lay.size)
         self.embed_blocks = 512
         self.embed_partial = z(self.embed_blocks, 161)
