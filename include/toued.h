@@ -88,6 +88,106 @@ int toued_rollout(EnvSpec spec, const int* levels, const float* theta, int D, co
                   int* state, int n_agents, int W, int T, int* traj_idx, int* traj_time, uint8_t* traj_action,
                   float* traj_reward, uint8_t* traj_done, float* cum_return, hipStream_t stream);
 
+
+/* ---- Level sampler (environments/level_sampler.py) ---- */
+/* frozen mode: random.choice(key, arange(B), p=uniform, shape=(n,), replace=True) (:157-165);
+ * cdf = jnp.cumsum(p) in jax's associative-scan order (host-computed once). */
+int toued_choice_cdf(const uint32_t* key, const float* cdf, int B, int n, int* out, hipStream_t stream);
+/* _reset_lowest_scoring (:338-341): ids = argsort(where(active, inf, where(new, -inf, score)))[:N],
+ * stable, jax float order.  Flags are bool (uint8) arrays of length B <= 8192. */
+int toued_plr_reset_ids(int B, int N, const float* score, const uint8_t* active, const uint8_t* fresh, int* ids,
+                        hipStream_t stream);
+/* alg_regret selection (:203-227) on the buffer after the terminated-level update.
+ * keys[3][2] = {replay_rng, random_rng, rng} from `rng, replay_rng, random_rng = split(rng, 3)`.
+ * Outputs (int32[N]): chosen = where(use, replay, random), replay (_replay_from_buffer :355-390,
+ * rank if !proportional), random (_sample_random_from_buffer :392-408), use (0/1). */
+int toued_plr_sample(int B, int N, const float* score, const uint8_t* active, const uint8_t* fresh,
+                     const uint32_t* keys, int proportional, float temperature, float p_replay, int* chosen, int* rep,
+                     int* rnd, int* use_out, hipStream_t stream);
+
+/* ---- Agents (agents/agents.py:31-95; models/agent.py:7-45) ---- */
+/* Dense(cols, use_bias=False) lecun_normal kernels [n][D][cols]: truncated_normal(keys[i]) in
+ * [lo, hi] = erf(-+2/sqrt2), times stddev.  keys are the flax per-param keys (toued/agents.py). */
+int toued_init_tables(const uint32_t* keys, int n, int cols, int D, float lo, float hi, float stddev, float* out,
+                      hipStream_t stream);
+
+/* ---- A2C antagonist (agents/a2c.py:19-125) ---- */
+/* out[u][i] = the u-th `_rng` of `rng, _rng = split(rng)` chained from keys[i] (a2c.py:97). */
+int toued_key_chain(const uint32_t* keys, int n, int U, uint32_t* out, hipStream_t stream);
+/* a2c_agent_train_step gradients for N agents (a2c.py:29-68) from a trajectory in the
+ * toued_rollout layout; accumulates into Ga [N][D][5], Gv [N][D] (zeroed by the caller or by
+ * toued_a2c_apply) and loss_out[N][2] += {actor_loss, critic_loss}.  W*T <= ~5400. */
+int toued_a2c_grad(int N, int W, int T, int D, const float* theta, const float* vcrit, const int* tidx,
+                   const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone, float gamma,
+                   float lam, float ent_coef, float* Ga, float* Gv, float* loss_out, hipStream_t stream);
+/* apply_gradients (clip_by_global_norm + SGD, models/optim.py:5-11) for actor and value critic,
+ * kept only while step+1 <= levels[i].lifetime (a2c.py:71-75); zeroes Ga/Gv. */
+int toued_a2c_apply(int N, int D, float* theta, float* vcrit, float* Ga, float* Gv, float lr_a, float lr_c,
+                    float max_norm, int* step, const int* levels, hipStream_t stream);
+
+/* ---- LPG meta-gradient step (meta/train.py:14-130, agents/lpg_agent.py:31-140, models/lpg.py) ----
+ * Sample index s = (a*T + t)*W + w; GRU row r = a*W + w; flat LPG parameters eta in
+ * jax tree_flatten order (toued/lpg.py LPGLayout), offsets `off`. */
+/* per-agent keys of _train_agent (meta/train.py:88-170): K train rollouts, the eval rollout, eval_agent */
+int toued_meta_keys(const uint32_t* agent_keys, int N, int K, uint32_t* roll_keys, uint32_t* eval_keys,
+                    uint32_t* ea_reset, uint32_t* ea_roll, hipStream_t stream);
+/* LPG inputs x = [r, d, pi, e(y_t), e(y_tp1) (, step, lifetime)] (models/lpg.py:48-77) into X (feature stride xs_f) */
+int toued_lpg_inputs(int N, int W, int T, int D, int F, const float* theta, const float* phi, const int* tidx,
+                     const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
+                     const float* eta_e1w, const float* eta_e1b, const float* eta_e2w, const float* eta_e2b,
+                     const int* step, const int* levels, float* X, long xs_f, hipStream_t stream);
+/* lpg_agent_train_step gradients (lpg_agent.py:36-70) given pi_hat [T][R], y_hat [T][8][R] */
+int toued_agent_grad(int N, int W, int T, int D, const float* theta, const float* phi, const int* tidx,
+                     const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
+                     const float* pi_hat, const float* y_hat, float alpha_y, float* Gth, float* Gph, float* met,
+                     hipStream_t stream);
+/* clipped SGD of actor [D][5] and LPG critic [D][8]; discard past the lifetime (lpg_agent.py:71-82) */
+int toued_agent_apply(int N, int D, const float* th0, const float* ph0, const float* Gth, const float* Gph,
+                      float lr_a, float lr_c, float max_norm, int* step, const int* levels, float* th1, float* ph1,
+                      float* gstat, hipStream_t stream);
+/* batch_rollout_entropy (util/metrics.py:5-9) metrics, or its gradient scaled by coef_a/coef_c */
+int toued_entropy(int N, int W, int T, int D, const float* theta, const float* phi, const int* tidx, const int* ttime,
+                  float* met, float coef_a, float coef_c, float* adj_th, float* adj_ph, hipStream_t stream);
+/* meta/train.py:61-100: frozen value critic GAE, normalised advantage, lpg_loss and value_loss */
+int toued_eval_loss(int N, int W, int T, int D, const float* theta, const float* vcrit, const int* tidx,
+                    const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone, float gamma,
+                    float lam, float* adv_scratch, float* abar, float* out, hipStream_t stream);
+/* d lpg_loss / d theta_K */
+int toued_lpgloss_grad(int N, int W, int T, int D, const float* theta, const int* tidx, const int* ttime,
+                       const uint8_t* tact, const float* abar, float* adj_th, hipStream_t stream);
+/* VJP coefficients of clip_by_global_norm (optax) per agent */
+int toued_clip_dot(int N, int D, const float* Gth, const float* Gph, const float* adj_th, const float* adj_ph,
+                   const float* gstat, float lr_a, float lr_c, float max_norm, float* coef, hipStream_t stream);
+/* Hessian-vector products through one LPG agent update + cotangents on pi_hat / y_hat */
+int toued_hvp(int N, int W, int T, int D, int K, const float* theta, const float* phi, const int* tidx,
+              const int* ttime, const uint8_t* tact, const float* pi_hat, const float* y_hat, const float* Gth,
+              const float* Gph, const float* adj_th_in, const float* adj_ph_in, const float* coef, float lr_a,
+              float lr_c, float alpha_y, float b2, float b3, float* adj_th_out, float* adj_ph_out, float* d_pi_hat,
+              float* d_y_hat, hipStream_t stream);
+/* embedding-MLP (models/lpg.py:36-46) parameter gradient from the GRU input cotangents */
+int toued_embed_bwd(int N, int W, int T, int D, int K, const float* phi_hist, long phi_stride, const int* tidx_hist,
+                    long tidx_stride, const int* ttime_hist, const uint8_t* tdone_hist, long tstep_stride,
+                    const float* dX3, const float* dX4, long dx_stride_k, const float* e1w, const float* e1b,
+                    const float* e2w, float* partial, int n_blocks, hipStream_t stream);
+/* optax adam (b1, b2, eps, bias-corrected) + scale(lr) + scale(-1) on the flat eta (meta/meta.py) */
+int toued_adam(int P, float* eta, const float* grad, float* m, float* v, float scale, float lr, float b1, float b2,
+               float eps, int count, hipStream_t stream);
+
+/* ---- LPG reverse-time GRU on MFMA (models/lpg.py:11-35, flax GRUCell) ---- */
+size_t toued_gru_packed_floats(int which);
+/* repack eta's GRU weights into MFMA A-fragment order (fwdA / bwdA) */
+int toued_gru_pack(const float* eta, const int* off, int F, float* fwdA, float* bwdA, hipStream_t stream);
+/* forward over R rows x T steps (t = T-1 .. 0, h reset on done); heads pi_hat [T][R], y_hat [T][8][R];
+ * saves h_in, r, z, n, hn [T][256][R] for the backward (row stride M) */
+int toued_gru_fwd(int R, int T, int W, int F, const float* X, long xs_f, const uint8_t* done, const float* fwdA,
+                  const float* eta, const int* off, float* pi_hat, float* y_hat, float* s_hin, float* s_r, float* s_z,
+                  float* s_n, float* s_hn, long M, hipStream_t stream);
+/* VJP: gate cotangents DG [4][256][M], relu(h) RH, head cotangents DH [9][M], input cotangents dX3/dX4 */
+int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_stride_k, const float* bwdA,
+                  const float* eta, const int* off, const float* y_hat, const float* d_pi_hat, const float* d_y_hat,
+                  const float* s_hin, const float* s_r, const float* s_z, const float* s_n, const float* s_hn, long M,
+                  float* DG, float* RH, float* DH, float* dX3, float* dX4, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,7 +17,7 @@ def test_header_symbols_exported():
     assert len(syms) >= 10
     for s in syms:
         assert hasattr(L, s), f"{s} declared in include/toued.h but not exported"
-    assert set(syms) <= set(_lib.exported_symbols()), set(syms) - set(_lib.exported_symbols())
+    assert set(syms) == set(_lib.exported_symbols()), set(syms) ^ set(_lib.exported_symbols())
 
 
 def test_host_only_entry_points():

@@ -1,0 +1,266 @@
+"""GPU parity of the GROOVE / PLR path: A2C antagonist, algorithmic regret, level buffer.
+
+  * agent tables (flax lecun_normal with flax's param-key derivation): bit-exact vs oracle/agents.py
+  * one A2C update (agents/a2c.py:19-76): the rollout bit-exact, the updated actor/critic within
+    float32-vs-float64 tolerance of the torch autograd oracle (oracle/a2c.py):
+    relative L2 error of the parameter change < 1e-4
+  * key plumbing of _compute_algorithmic_regret with max_lifetime=0 (untrained antagonist):
+    regret within 1e-5 of the oracle (float32 mean over workers vs float64)
+  * buffer logic (level_sampler.py:169-234, 331-408): reset ids, replay ids (rank and
+    proportional), random ids, replay/random selection — bit-exact vs oracle/sampler.py
+  * LevelSampler.sample end to end (alg_regret): buffer flags and chosen levels bit-exact vs the
+    oracle driven by the device's regret scores
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import a2c as oa2c
+from oracle import agents as oag
+from oracle import jaxrand as jr
+from oracle import levels as olv
+from oracle import meta as ometa
+from oracle import rollout as oro
+from oracle import sampler as osp
+
+pytestmark = pytest.mark.gpu
+
+
+def dk(a):
+    from toued.prng import from_uint32_numpy
+    return from_uint32_numpy(a, "cuda")
+
+
+def _ahyp(mode):
+    from toued.agents import AgentHyperparams
+    from toued.env import get_agent_hypers
+    return AgentHyperparams(**get_agent_hypers(mode), critic_dims=1)
+
+
+def _ost(state0, nmax):
+    ex = np.stack([(state0[2] >> i) & 1 for i in range(nmax)], 1).astype(bool)
+    return {"time": state0[0], "pos": state0[1], "obj_existss": ex, "early_term": state0[3].astype(bool),
+            "obj_poss": state0[4:4 + nmax].T.copy()}
+
+
+@pytest.mark.parametrize("mode,cols", [("dense", 5), ("all_shortlife", 1), ("mazes", 8)])
+def test_init_tables_bitexact(mode, cols):
+    from toued.agents import lecun_tables
+    spec = olv.env_spec(mode)
+    D = spec.obs_dim
+    keys = jr.split(jr.PRNGKey(11), 3)
+    got = lecun_tables(dk(keys), D, cols).cpu().numpy()
+    for a in range(3):
+        assert np.array_equal(got[a], oag.lecun_table(keys[a], D, cols)), a
+
+
+def _a2c_setup(mode, N, W, T, seed=0, scale=20.0):
+    from toued.agents import create_agents
+    from toued.env import LevelGenerator
+    from toued.rollout import RolloutWrapper
+    keys = jr.split(jr.PRNGKey(seed), N)
+    levels = LevelGenerator(mode)(dk(keys))
+    p, lt = olv.reset_env_params(keys, mode)
+    ro = RolloutWrapper(mode, T, env_workers=W)
+    D = ro.obs_dim
+    theta, vc = create_agents(dk(jr.split(jr.PRNGKey(seed + 1), N)), D, 1)
+    theta.mul_(scale)
+    vcrit = (vc.reshape(N, D) * scale).contiguous()
+    (_, _), state = ro.batch_reset(dk(jr.split(jr.PRNGKey(seed + 2), N)), levels)
+    return ro, levels, p, lt, theta, vcrit, state, D
+
+
+def test_a2c_update_matches_oracle():
+    from toued.a2c import A2CHyperparams, A2CTrainer
+    mode, N, W, T = "dense", 3, 64, 20
+    ro, levels, p, lt, theta, vcrit, state, D = _a2c_setup(mode, N, W, T)
+    spec = olv.env_spec(mode)
+    th0, vc0, st0 = theta.cpu().numpy(), vcrit.cpu().numpy(), state.cpu().numpy()
+    rng = jr.split(jr.PRNGKey(9), N)
+    tr = A2CTrainer(ro, A2CHyperparams(), _ahyp(mode), use_graph=False)
+    step = torch.zeros(N, dtype=torch.int32, device="cuda")
+    loss = tr.train(dk(rng), theta, vcrit, step, levels, state, 1).cpu().numpy()
+    b = tr._bufs["tr"]
+    idx, tm, act = b.obs_idx.cpu().numpy(), b.obs_time.cpu().numpy(), b.action.cpu().numpy()
+    rew, dn = b.reward.cpu().numpy(), b.done.cpu().numpy()
+    # rollout of update 0 with key split(rng)[1], bit-exact
+    sub = jr.split(rng, 2)[:, 1]
+    otr, _, _ = oro.batch_rollout(spec, sub, th0, p, _ost(st0, spec.max_n_objs), T)
+    assert np.array_equal(act, otr["action"].transpose(0, 2, 1))
+    assert np.array_equal(idx, otr["idx"].transpose(0, 2, 1))
+    assert np.array_equal(rew, otr["reward"].transpose(0, 2, 1))
+    assert step.cpu().numpy().tolist() == [1] * N
+    th1, vc1 = theta.cpu().numpy(), vcrit.cpu().numpy()
+    hyp = ometa.Hypers()
+    for a in range(N):
+        traj = {"idx": idx[a].T.copy(), "time": tm[a].T.copy(), "action": act[a].T.astype(np.int64),
+                "reward": rew[a].T.copy(), "done": dn[a].T.astype(bool)}
+        t_ref, v_ref, s_ref, al, cl = oa2c.a2c_step(
+            torch.from_numpy(th0[a].astype(np.float64)), torch.from_numpy(vc0[a][:, None].astype(np.float64)), 0,
+            int(lt[a]), traj, hyp, 40.0, 4.0, 0.5)
+        dt_ref = t_ref.numpy() - th0[a]
+        dv_ref = v_ref.numpy()[:, 0] - vc0[a]
+        dt = th1[a].astype(np.float64) - th0[a]
+        dv = vc1[a].astype(np.float64) - vc0[a]
+        assert np.linalg.norm(dt - dt_ref) <= 1e-4 * np.linalg.norm(dt_ref) + 1e-6, a
+        assert np.linalg.norm(dv - dv_ref) <= 1e-4 * np.linalg.norm(dv_ref) + 1e-6, a
+        assert abs(loss[a, 0] - al) <= 1e-4 * max(1.0, abs(al))
+        assert abs(loss[a, 1] - cl) <= 1e-4 * max(1.0, abs(cl))
+
+
+def test_a2c_graph_replay_matches_eager_and_lifetime_discard():
+    from toued.a2c import A2CHyperparams, A2CTrainer
+    from toued.env import L_LIFETIME
+    mode, N, W, T, U = "dense", 4, 64, 20, 5
+    ro, levels, p, lt, theta, vcrit, state, D = _a2c_setup(mode, N, W, T, seed=3)
+    levels[:, L_LIFETIME] = torch.tensor([1, 3, 100, 5], dtype=torch.int32, device="cuda")
+    rng = dk(jr.split(jr.PRNGKey(5), N))
+    outs = []
+    for g in (False, True):
+        th, vc, st = theta.clone(), vcrit.clone(), state.clone()
+        step = torch.zeros(N, dtype=torch.int32, device="cuda")
+        tr = A2CTrainer(ro, A2CHyperparams(), _ahyp(mode), use_graph=g)
+        tr.train(rng, th, vc, step, levels, st, U)
+        if g:   # a second replay of the captured graph on fresh inputs gives the same answer
+            th2, vc2, st2 = theta.clone(), vcrit.clone(), state.clone()
+            step2 = torch.zeros(N, dtype=torch.int32, device="cuda")
+            tr.train(rng, th2, vc2, step2, levels, st2, U)
+            torch.testing.assert_close(th2, th, rtol=1e-5, atol=1e-6)
+        outs.append((th, vc, st, step))
+    (th_e, vc_e, st_e, s_e), (th_g, vc_g, st_g, s_g) = outs
+    assert s_e.cpu().tolist() == [1, 3, 5, 5]
+    assert torch.equal(s_e, s_g)
+    torch.testing.assert_close(th_g, th_e, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(vc_g, vc_e, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("mode", ["mazes", "dense"])
+def test_regret_untrained_matches_oracle(mode):
+    """max_lifetime = 0: regret = eval(fresh A2C actor) - eval(LPG actor) — checks the key
+    derivation of _compute_algorithmic_regret, agent creation and eval_agent."""
+    from toued.agents import create_agents
+    from toued.env import LevelGenerator
+    from toued.parse_args import parse_args
+    from toued.level_sampler import LevelSampler
+    from toued.plr import algorithmic_regret
+    N = 3
+    args = parse_args(["--env_mode", mode, "--score_function", "alg_regret", "--num_agents", str(N), "--num_mini_batches", "1"])
+    smp = LevelSampler(args)
+    smp.max_lifetime = 0
+    spec = olv.env_spec(mode)
+    lk = jr.split(jr.PRNGKey(21), N)
+    levels = LevelGenerator(mode)(dk(lk))
+    p, _ = olv.reset_env_params(lk, mode)
+    D = spec.obs_dim
+    lpg_theta, _ = create_agents(dk(jr.split(jr.PRNGKey(22), N)), D, 8)
+    lpg_theta.mul_(10.0)
+    keys = jr.split(jr.PRNGKey(23), N)
+    got = algorithmic_regret(smp, dk(keys), levels, lpg_theta).cpu().numpy()
+    # oracle
+    k = jr.split(keys, 2)
+    rng, c = k[:, 0], k[:, 1]
+    ag = jr.split(c, 2)[:, 1]
+    a2c_theta = np.stack([oag.create_agent(ag[a], D, 1)[0] for a in range(N)])
+    rng = jr.split(rng, 2)[:, 0]
+    ev = jr.split(rng, 2)
+    L = smp.max_rollout_len
+    r_lpg = oag.eval_agent(spec, ev[:, 0], p, lpg_theta.cpu().numpy(), 64, L)
+    r_a2c = oag.eval_agent(spec, ev[:, 1], p, a2c_theta, 64, L)
+    np.testing.assert_allclose(got, r_a2c - r_lpg, atol=1e-5, rtol=0)
+
+
+def _buffer_state(B, N, seed, n_active, frac_new, ties=True):
+    rs = np.random.RandomState(seed)
+    score = rs.randn(B).astype(np.float32)
+    if ties:
+        score = (np.round(score * 4) / 4).astype(np.float32)
+        score[rs.rand(B) < 0.05] = -0.0
+    active = np.zeros(B, bool)
+    active[rs.choice(B, n_active, replace=False)] = True
+    new = (rs.rand(B) < frac_new) & ~active
+    return score, active, new
+
+
+@pytest.mark.parametrize("B,N", [(4000, 512), (64, 8), (1000, 1000), (33, 7)])
+def test_plr_reset_ids_bitexact(B, N):
+    score, active, new = _buffer_state(B, N, B + N, min(N // 2, B), 0.3)
+    ids = torch.empty(N, dtype=torch.int32, device="cuda")
+    from toued import _lib
+    s, a, n = (torch.from_numpy(x).cuda() for x in (score, active, new))
+    _lib.call("toued_plr_reset_ids", B, N, _lib.ptr(s), _lib.ptr(a), _lib.ptr(n), _lib.ptr(ids), _lib.stream_ptr())
+    ref, _, _, _ = osp.reset_lowest_scoring(score, active, new, N)
+    assert np.array_equal(ids.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("transform", ["rank", "proportional"])
+@pytest.mark.parametrize("B,N,n_active,frac_new", [(4000, 512, 512, 0.3), (4000, 512, 512, 0.9),
+                                                    (300, 64, 32, 0.5), (100, 16, 0, 0.0)])
+def test_plr_sample_bitexact(transform, B, N, n_active, frac_new):
+    from toued import _lib
+    score, active, new = _buffer_state(B, N, B * 7 + N, n_active, frac_new)
+    if frac_new == 0.0:   # no new levels at all: the random draw sees p = 0/0
+        new[:] = False
+    keys = jr.split(jr.PRNGKey(B + N), 3)
+    kbuf = np.stack([keys[1], keys[2], keys[0]])
+    s, a, n = (torch.from_numpy(x).cuda() for x in (score, active, new))
+    out = [torch.empty(N, dtype=torch.int32, device="cuda") for _ in range(4)]
+    _lib.call("toued_plr_sample", B, N, _lib.ptr(s), _lib.ptr(a), _lib.ptr(n), _lib.ptr(dk(kbuf)),
+              int(transform == "proportional"), 1.0, 0.5, *[_lib.ptr(o) for o in out], _lib.stream_ptr())
+    chosen, rep, rnd, use = (o.cpu().numpy() for o in out)
+    rep_ref = osp.replay_ids(keys[1], score, active, new, N, transform, 1.0)
+    rnd_ref = osp.random_ids(keys[2], active, new, N)
+    ch_ref, use_ref = osp.select(keys[0], rep_ref, rnd_ref, active, new, N, 0.5)
+    assert np.array_equal(rep, rep_ref)
+    assert np.array_equal(rnd, rnd_ref)
+    assert np.array_equal(use.astype(bool), use_ref)
+    assert np.array_equal(chosen, ch_ref)
+
+
+def test_level_sampler_alg_regret_end_to_end():
+    from toued import prng
+    from toued.env import L_BUFID, L_LIFETIME
+    from toued.level_sampler import LevelSampler
+    from toued.parse_args import parse_args
+    N, B = 8, 64
+    args = parse_args(["--env_mode", "mazes", "--score_function", "alg_regret", "--num_agents", str(N), "--num_mini_batches", "1",
+                       "--buffer_size", str(B)])
+    smp = LevelSampler(args)
+    smp.max_lifetime = 3
+    buf = smp.initialize_buffer(prng.PRNGKey(0, "cuda"))
+    buf, agents = smp.initial_sample(prng.PRNGKey(1, "cuda"), buf, N, False)
+    assert buf.active.sum().item() == N
+    # a first round with all agents terminated fills the buffer with scores
+    agents.step = agents.levels[:, L_LIFETIME].clone()
+    rng = prng.PRNGKey(2, "cuda")
+    for it in range(3):
+        pre = {k: getattr(buf, k).clone() for k in ("score", "active", "new", "levels")}
+        term = (agents.step >= agents.levels[:, L_LIFETIME]).cpu().numpy()
+        old_ids = agents.levels[:, L_BUFID].cpu().numpy()
+        rng_np = prng.to_uint32_numpy(rng)
+        buf, agents = smp.sample(rng, buf, agents)
+        rng = prng.split(rng, 2)[1].contiguous()
+        # oracle replay of the buffer logic with the device's regret scores
+        r, sub = jr.split(rng_np, 2)
+        ids, score, active, new = osp.reset_lowest_scoring(pre["score"].cpu().numpy(), pre["active"].cpu().numpy(),
+                                                           pre["new"].cpu().numpy(), N)
+        r, sub = jr.split(r, 2)
+        sc = smp.last_plr["score"].cpu().numpy()
+        score[old_ids[term]] = sc[term]
+        active[old_ids[term]] = False
+        new[old_ids[term]] = False
+        k3 = jr.split(r, 3)
+        rep = osp.replay_ids(k3[1], score, active, new, N, "rank", 1.0)
+        rnd = osp.random_ids(k3[2], active, new, N)
+        ch, _ = osp.select(k3[0], rep, rnd, active, new, N, 0.5)
+        new_ids = np.where(term, ch, old_ids)
+        active[new_ids] = True
+        assert np.array_equal(buf.levels[torch.from_numpy(ids).long().cuda(), L_BUFID].cpu().numpy(), ids)
+        assert np.array_equal(buf.score.cpu().numpy(), score), it
+        assert np.array_equal(buf.active.cpu().numpy(), active), it
+        assert np.array_equal(buf.new.cpu().numpy(), new), it
+        assert np.array_equal(agents.levels[:, L_BUFID].cpu().numpy(), new_ids), it
+        assert np.array_equal(agents.levels.cpu().numpy(), buf.levels.cpu().numpy()[new_ids]), it
+        assert buf.active.sum().item() >= N
+        # terminate half the agents for the next round
+        agents.step = torch.where(torch.arange(N, device="cuda") % 2 == it % 2, agents.levels[:, L_LIFETIME],
+                                  torch.zeros_like(agents.step))

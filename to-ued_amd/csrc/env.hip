@@ -374,7 +374,7 @@ __global__ void __launch_bounds__(256) k_rollout(EnvSpec sp, const int* __restri
     traj_time[base_o + (size_t)T * W] = s.time;
   }
   if (traj_idx) store_state<NMAX>(state, n, i, s);   // returns-only mode leaves the state untouched
-  cum_return[i] = cum;
+  if (cum_return) cum_return[i] = cum;
 }
 
 }  // namespace
@@ -452,6 +452,7 @@ int toued_rollout(EnvSpec sp, const int* levels, const float* theta, int D, cons
   TOUED_REQUIRE(n_agents >= 0 && W >= 1 && T >= 0, "toued_rollout: bad sizes N=%d W=%d T=%d", n_agents, W, T);
   TOUED_REQUIRE(sp.tabular, "toued_rollout: the linear tabular actor needs a tabular env");
   TOUED_REQUIRE(D == sp.max_grid * sp.max_grid * (1 << sp.n_max) + 1, "toued_rollout: D=%d != obs_dim", D);
+  TOUED_REQUIRE(traj_idx || cum_return, "toued_rollout: returns-only mode needs cum_return");
   const int n = n_agents * W;
   if (n == 0) return 0;
   if (W % 64 == 0) {

@@ -61,6 +61,11 @@ _SIGS = {
     "toued_gru_bwd": [_I, _I, _I, _I, _P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _P, _P, _P, _P, _P,
                       _P],
     "toued_choice_cdf": [_P, _P, _I, _I, _P, _P],
+    "toued_key_chain": [_P, _I, _I, _P, _P],
+    "toued_a2c_grad": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _P, _P, _P, _P],
+    "toued_a2c_apply": [_I, _I, _P, _P, _P, _P, _F, _F, _F, _P, _P, _P],
+    "toued_plr_reset_ids": [_I, _I, _P, _P, _P, _P, _P],
+    "toued_plr_sample": [_I, _I, _P, _P, _P, _P, _I, _F, _F, _P, _P, _P, _P, _P],
     "toued_last_error": [],
     "toued_abi_version": [],
 }

@@ -1,0 +1,117 @@
+"""A2C antagonist on MI355X (agents/a2c.py:12-125).
+
+``A2CTrainer.train`` runs ``train_a2c_agent`` for a batch of antagonists: a chain of
+``num_train_steps`` updates, each = one fused rollout (toued_rollout) + one fused
+gradient kernel (toued_a2c_grad: GAE, advantage normalisation, actor/critic/entropy
+gradients) + one clipped-SGD apply (toued_a2c_apply).  The per-update keys of the
+scan carry (``rng, _rng = split(rng)``, a2c.py:97) are produced up front by
+toued_key_chain.  All buffers are allocated once per batch shape and the update loop
+is replayed from a captured HIP graph (torch.cuda.CUDAGraph on ROCm), so the
+hundreds of small launches per regret evaluation cost one graph launch.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from .agents import AgentHyperparams
+from .rollout import RolloutWrapper, Transition
+
+
+@dataclass
+class A2CHyperparams:
+    """agents/a2c.py:12-16 (level_sampler.py:86-88 builds it from --gamma/--gae_lambda/--entropy_coeff)."""
+    gamma: float = 0.99
+    gae_lambda: float = 0.95
+    entropy_coeff: float = 0.01
+
+
+class A2CTrainer:
+    def __init__(self, ro: RolloutWrapper, hyp: A2CHyperparams, agent_hypers: AgentHyperparams,
+                 use_graph: bool = True):
+        agent_hypers.check_supported()
+        self.ro = ro
+        self.hyp = hyp
+        self.ah = agent_hypers
+        self.use_graph = use_graph
+        self._bufs = None
+        self._graph = None
+        self._graph_key = None
+
+    def _alloc(self, n, D, W, T, U, dev):
+        key = (n, D, W, T, U, str(dev))
+        if self._bufs is not None and self._bufs["key"] == key:
+            return self._bufs
+        z = lambda *s, dt=torch.float32: torch.zeros(s, dtype=dt, device=dev)
+        self._bufs = {
+            "key": key,
+            "tr": Transition(z(n, T + 1, W, dt=torch.int32), z(n, T + 1, W, dt=torch.int32),
+                             z(n, T, W, dt=torch.uint8), z(n, T, W), z(n, T, W, dt=torch.uint8)),
+            "Ga": z(n, D, 5), "Gv": z(n, D), "loss": z(n, 2),
+            "chain": z(U, n, 2, dt=torch.int32),
+            # graph-static inputs
+            "rng": z(n, 2, dt=torch.int32), "theta": z(n, D, 5), "vcrit": z(n, D),
+            "step": z(n, dt=torch.int32), "levels": z(n, 64, dt=torch.int32),
+            "state": z(12, n * W, dt=torch.int32),
+        }
+        self._graph = None
+        return self._bufs
+
+    def _updates(self, b, n, D, W, T, U):
+        L = _lib
+        st = L.stream_ptr()
+        b["loss"].zero_()
+        if U == 0:
+            return
+        L.call("toued_key_chain", L.ptr(b["rng"]), n, U, L.ptr(b["chain"]), st)
+        tr = b["tr"]
+        lr_a, lr_c, mn = self.ah.actor_learning_rate, self.ah.critic_learning_rate, self.ah.max_grad_norm
+        for u in range(U):
+            L.call("toued_rollout", self.ro._c, L.ptr(b["levels"]), L.ptr(b["theta"]), D, L.ptr(b["chain"][u]),
+                   L.ptr(b["state"]), n, W, T, L.ptr(tr.obs_idx), L.ptr(tr.obs_time), L.ptr(tr.action),
+                   L.ptr(tr.reward), L.ptr(tr.done), None, st)
+            L.call("toued_a2c_grad", n, W, T, D, L.ptr(b["theta"]), L.ptr(b["vcrit"]), L.ptr(tr.obs_idx),
+                   L.ptr(tr.obs_time), L.ptr(tr.action), L.ptr(tr.reward), L.ptr(tr.done), self.hyp.gamma,
+                   self.hyp.gae_lambda, self.hyp.entropy_coeff, L.ptr(b["Ga"]), L.ptr(b["Gv"]), L.ptr(b["loss"]), st)
+            L.call("toued_a2c_apply", n, D, L.ptr(b["theta"]), L.ptr(b["vcrit"]), L.ptr(b["Ga"]), L.ptr(b["Gv"]),
+                   lr_a, lr_c, mn, L.ptr(b["step"]), L.ptr(b["levels"]), st)
+
+    def train(self, rng: torch.Tensor, theta: torch.Tensor, vcrit: torch.Tensor, step: torch.Tensor,
+              levels: torch.Tensor, state: torch.Tensor, num_train_steps: int):
+        """train_a2c_agent (a2c.py:79-125) for n agents; updates theta [n,D,5], vcrit [n,D], step [n],
+        state [12, n*W] in place.  Returns mean (actor_loss, critic_loss) over the updates, [n, 2]."""
+        n, D = theta.shape[0], theta.shape[1]
+        if n == 0:
+            return torch.zeros((0, 2), device=theta.device)
+        W = state.shape[1] // n
+        T = self.ro.train_rollout_len
+        U = int(num_train_steps)
+        b = self._alloc(n, D, W, T, U, theta.device)
+        for name, src in (("rng", rng), ("theta", theta), ("vcrit", vcrit.reshape(n, D)), ("step", step),
+                          ("levels", levels), ("state", state)):
+            b[name].copy_(src)
+        if self.use_graph and U > 0:
+            if self._graph is None:
+                # warm the path once outside capture (library load, kernel code objects)
+                s = torch.cuda.Stream(device=theta.device)
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=s):
+                        self._updates(b, n, D, W, T, U)
+                torch.cuda.current_stream().wait_stream(s)
+                self._graph = g
+                # the capture did not execute: restore inputs and run it
+                for name, src in (("rng", rng), ("theta", theta), ("vcrit", vcrit.reshape(n, D)), ("step", step),
+                                  ("levels", levels), ("state", state)):
+                    b[name].copy_(src)
+            self._graph.replay()
+        else:
+            self._updates(b, n, D, W, T, U)
+        theta.copy_(b["theta"])
+        vcrit.copy_(b["vcrit"].reshape(vcrit.shape))
+        step.copy_(b["step"])
+        state.copy_(b["state"])
+        return b["loss"] / max(U, 1)

@@ -10,6 +10,7 @@ and the value critics of the meta-gradient path: vcrit f32 [N, D], vstep int32 [
 """
 from __future__ import annotations
 
+import hashlib
 import math
 from dataclasses import dataclass
 
@@ -19,9 +20,12 @@ import torch
 from . import _lib, prng
 from .env import get_agent_hypers
 
-_SQRT2 = math.sqrt(2.0)
-TN_LO = float(np.float32(math.erf(-2.0 / _SQRT2)))
-TN_HI = float(np.float32(math.erf(2.0 / _SQRT2)))
+# lax.erf(-+2 / sqrt2) in float32 (XLA's f32 erf; equals the correctly rounded value here)
+TN_LO = -0.9544997215270996
+TN_HI = 0.9544997215270996
+# flax 0.6.11 param-key derivation (core/scope.py LazyRng + _legacy_rng_fold_in): the kernel of
+# the module's inline Dense is drawn with fold_in(fold_in(rng, sha1("Dense_0")[:4]), 1).
+DENSE0_HASH = int.from_bytes(hashlib.sha1(b"Dense_0").digest()[:4], "big")
 
 
 @dataclass
@@ -48,11 +52,14 @@ class AgentHyperparams:
 
 
 def lecun_tables(keys: torch.Tensor, D: int, cols: int) -> torch.Tensor:
-    """flax lecun_normal Dense(cols, use_bias=False) kernels [n, D, cols], one per key."""
+    """``model.init(key, obs)`` of Actor/Critic with actor_net=() (models/agent.py:7-45): the
+    Dense(cols, use_bias=False) kernel, flax lecun_normal = truncated_normal(-2, 2) * stddev with
+    stddev = sqrt(1/D) / .87962566103423978 in float32.  Returns [n, D, cols], one per key."""
     n = keys.shape[0]
     out = torch.empty((n, D, cols), dtype=torch.float32, device=keys.device)
-    std = math.sqrt(1.0 / D) / 0.87962566103423978
-    _lib.call("toued_init_tables", _lib.ptr(keys.contiguous()), n, cols, D, TN_LO, TN_HI, std, _lib.ptr(out),
+    pkeys = prng.fold_in(prng.fold_in(keys.contiguous(), DENSE0_HASH), 1)
+    std = float(np.float32(np.sqrt(np.float32(1.0 / D))) / np.float32(0.87962566103423978))
+    _lib.call("toued_init_tables", _lib.ptr(pkeys.contiguous()), n, cols, D, TN_LO, TN_HI, std, _lib.ptr(out),
               _lib.stream_ptr())
     return out
 
@@ -83,3 +90,12 @@ class AgentBatch:
     @property
     def n(self) -> int:
         return self.levels.shape[0]
+
+
+def eval_agent(ro, rng: torch.Tensor, levels: torch.Tensor, theta: torch.Tensor, num_workers: int) -> torch.Tensor:
+    """agents/agents.py:98-106 for n agents: (rng, _rng) = split(rng) -> batch_reset(_rng, W);
+    (rng, _rng) = split(rng) -> eval rollout; mean first-episode return per agent, f32 [n]."""
+    ks = prng.split(rng, 2)
+    (_, _), state = ro.batch_reset(ks[:, 1].contiguous(), levels, num_workers)
+    ks2 = prng.split(ks[:, 0].contiguous(), 2)
+    return ro.eval_returns(ks2[:, 1].contiguous(), theta, levels, state).mean(dim=1)

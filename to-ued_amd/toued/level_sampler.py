@@ -82,6 +82,18 @@ class LevelSampler:
         self.gen = LevelGenerator(self.env_mode, self.dev)
         self.Y = args.lpg_target_width
         self._cdf = None
+        self.regret_all_agents = bool(getattr(args, "regret_all_agents", False))
+        self._a2c = None
+        self.last_plr = None
+
+    def a2c_trainer(self):
+        """The A2C antagonist trainer (level_sampler.py:86-88, 296-310), built on first use."""
+        if self._a2c is None:
+            from .a2c import A2CHyperparams, A2CTrainer
+            self._a2c = A2CTrainer(self.rollout_manager,
+                                   A2CHyperparams(self.args.gamma, self.args.gae_lambda, self.args.entropy_coeff),
+                                   self.agent_hypers)
+        return self._a2c
 
     @property
     def obs_dim(self) -> int:

@@ -137,6 +137,7 @@ class MetaGradStep:
         self.embed_partial = z(self.embed_blocks, 161)
         self.ea_cum = None
         self.timers = KernelTimers()
+        self.side = torch.cuda.Stream(device=dev)
 
     # ------------------------------------------------------------------ helpers
     def _t(self, k: int) -> Transition:
@@ -205,9 +206,14 @@ class MetaGradStep:
         # value critic "update" (meta/train.py:113-133): the gradient is identically zero,
         # so only the TrainState step advances (K train rollouts + 1 eval rollout).
         agents.vstep.add_(K + 1)
-        # eval_agent (agents/agents.py:98-106): fresh 4-worker reset, eval-length rollout, mean return
-        (_, _), ea_state = self.ro.batch_reset(self.keys_ea_reset, agents.levels, hyp.eval_workers)
-        ea_cum = self._eval_rollout(self.keys_ea_roll, self.theta_h[K], agents.levels, ea_state)
+        # eval_agent (agents/agents.py:98-106): fresh 4-worker reset, eval-length rollout, mean return.
+        # It only reads theta_K and the levels, and its long sequential rollout occupies few CUs, so it
+        # runs on a side stream concurrently with the MFMA-bound backward pass.
+        main = torch.cuda.current_stream()
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            (_, _), ea_state = self.ro.batch_reset(self.keys_ea_reset, agents.levels, hyp.eval_workers)
+            ea_cum = self._eval_rollout(self.keys_ea_roll, self.theta_h[K], agents.levels, ea_state)
         # ---------------- reverse: explicit adjoint w.r.t. eta
         a_in, a_out = 0, 1
         self.adj_th[a_in].zero_()
@@ -252,6 +258,9 @@ class MetaGradStep:
         L.call("toued_adam", self.lay.size, ptr(eta), ptr(self.grad), ptr(adam.m), ptr(adam.v), 1.0 / n_total,
                hyp.lpg_lr, 0.9, 0.999, 1e-8, adam.count, st)
         # ---------------- agent state out + metrics
+        main.wait_stream(self.side)
+        ea_cum.record_stream(main)
+        ea_state.record_stream(main)
         agents.theta.copy_(self.theta_h[K])
         agents.phi.copy_(self.phi_h[K])
         inv_wt = 1.0 / (W * T)

@@ -85,3 +85,15 @@ class RolloutWrapper:
                   _lib.ptr(state), N, W, T, _lib.ptr(out.obs_idx), _lib.ptr(out.obs_time), _lib.ptr(out.action),
                   _lib.ptr(out.reward), _lib.ptr(out.done), _lib.ptr(cum), _lib.stream_ptr())
         return out, state, cum
+
+    def eval_returns(self, agent_keys: torch.Tensor, theta: torch.Tensor, levels: torch.Tensor,
+                     state: torch.Tensor) -> torch.Tensor:
+        """batch_rollout(..., eval=True) when only cum_return is consumed (eval_agent): returns-only
+        kernel mode, no trajectory stores; `state` is left unmodified.  Returns f32 [N, W]."""
+        N = agent_keys.shape[0]
+        n = state.shape[1]
+        cum = torch.empty((N, n // N), dtype=torch.float32, device=state.device)
+        _lib.call("toued_rollout", self._c, _lib.ptr(levels), _lib.ptr(theta), theta.shape[1],
+                  _lib.ptr(agent_keys.contiguous()), _lib.ptr(state), N, n // N, self.eval_rollout_len, None, None,
+                  None, None, None, _lib.ptr(cum), _lib.stream_ptr())
+        return cum
