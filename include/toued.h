@@ -131,11 +131,12 @@ int toued_a2c_apply(int N, int D, float* theta, float* vcrit, float* Ga, float* 
 /* per-agent keys of _train_agent (meta/train.py:88-170): K train rollouts, the eval rollout, eval_agent */
 int toued_meta_keys(const uint32_t* agent_keys, int N, int K, uint32_t* roll_keys, uint32_t* eval_keys,
                     uint32_t* ea_reset, uint32_t* ea_roll, hipStream_t stream);
-/* LPG inputs x = [r, d, pi, e(y_t), e(y_tp1) (, step, lifetime)] (models/lpg.py:48-77) into X (feature stride xs_f) */
+/* LPG inputs x = [r, d, pi, e(y_t), e(y_tp1) (, step, lifetime)] (models/lpg.py:48-77) into X (feature stride xs_f);
+ * eta_e* point at the embedding-MLP parameters, advanced by a*eta_stride for agent a (ES candidates; 0 = shared) */
 int toued_lpg_inputs(int N, int W, int T, int D, int F, const float* theta, const float* phi, const int* tidx,
                      const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
                      const float* eta_e1w, const float* eta_e1b, const float* eta_e2w, const float* eta_e2b,
-                     const int* step, const int* levels, float* X, long xs_f, hipStream_t stream);
+                     const int* step, const int* levels, float* X, long xs_f, long eta_stride, hipStream_t stream);
 /* lpg_agent_train_step gradients (lpg_agent.py:36-70) given pi_hat [T][R], y_hat [T][8][R] */
 int toued_agent_grad(int N, int W, int T, int D, const float* theta, const float* phi, const int* tidx,
                      const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
@@ -187,6 +188,27 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
                   const float* eta, const int* off, const float* y_hat, const float* d_pi_hat, const float* d_y_hat,
                   const float* s_hin, const float* s_r, const float* s_z, const float* s_n, const float* s_hn, long M,
                   float* DG, float* RH, float* DH, float* dX3, float* dX4, hipStream_t stream);
+
+/* ES inference path: pack n candidates' forward fragments (candidate c at eta + c*eta_stride) */
+int toued_gru_pack_fwd_multi(const float* eta, long eta_stride, int n, const int* off, int F, float* fwdA,
+                             hipStream_t stream);
+/* forward with per-candidate parameters: rows [c*rows_per_cand, (c+1)*rows_per_cand) use candidate c
+ * (fwdA from toued_gru_pack_fwd_multi); nothing is saved for a backward */
+int toued_gru_fwd_multi(int R, int T, int W, int F, int rows_per_cand, const float* X, long xs_f, const uint8_t* done,
+                        const float* fwdA, const float* eta, long eta_stride, const int* off, float* pi_hat,
+                        float* y_hat, hipStream_t stream);
+
+/* ---- OpenES (evosax 0.1.4 as configured by models/optim.py:21-34; meta/train.py:133-227) ---- */
+/* ask for z rows [row_lo, row_lo+n_rows) of normal(key, (half_pop, nd)): x[2i] = mean + sigma z_i,
+ * x[2i+1] = mean - sigma z_i (the antithetic reorder of meta/train.py:152-158); key is a device key */
+int toued_es_ask(const uint32_t* key, long nd, long half_pop, long row_lo, long n_rows, const float* mean,
+                 float sigma, float* x, hipStream_t stream);
+/* out[j] = sum_c ((x[c][j] - mean[j]) / sigma) * fitness[c] over this rank's C candidates */
+int toued_es_grad(const float* x, const float* mean, float sigma, const float* fitness, int C, long nd, float* out,
+                  hipStream_t stream);
+/* evosax optimiser step on the mean with grad*scale: opt 0 = SGD, 1 = Adam (bias corrections bc1, bc2) */
+int toued_es_opt(long nd, int opt, float* mean, const float* grad, float scale, float* m, float* v, float lrate,
+                 float b1, float b2, float eps, float bc1, float bc2, hipStream_t stream);
 
 #ifdef __cplusplus
 }

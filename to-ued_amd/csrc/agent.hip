@@ -149,11 +149,16 @@ __global__ void __launch_bounds__(256) k_lpg_inputs(int N, int W, int T, int D, 
                                                     const float* __restrict__ e1w, const float* __restrict__ e1b,
                                                     const float* __restrict__ e2w, const float* __restrict__ e2b,
                                                     const int* __restrict__ step, const int* __restrict__ levels,
-                                                    float* __restrict__ X, long xs_f) {
+                                                    float* __restrict__ X, long xs_f, long eta_stride) {
   const long s = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= (long)N * T * W) return;
   const SampleRef q = load_sample(s, T, W, tidx, ttime, tact, trew, tdone, UNIF);
   const int R = N * W;
+  // per-agent LPG parameters (ES candidates) when eta_stride != 0
+  e1w += q.a * eta_stride;
+  e1b += q.a * eta_stride;
+  e2w += q.a * eta_stride;
+  e2b += q.a * eta_stride;
   const float* th = theta + (size_t)q.a * D * 5;
   const float* ph = phi + (size_t)q.a * D * 8;
   float lastA[5], lastC[8];
@@ -689,24 +694,6 @@ __global__ void __launch_bounds__(256) k_adam(int P, float* __restrict__ eta, co
 // lecun_normal (truncated normal in [-2, 2], stddev sqrt(1/fan_in)/0.87962566).  Here the kernel of
 // table i is drawn from keys[i] directly (flax's per-module key derivation is not reproduced: parity
 // unpinned).  u = uniform(lo=erf(-sqrt2), hi=erf(sqrt2)); z = sqrt2*erfinv(u), clipped.
-TOUED_DEV float erfinv_giles(float x) {
-  float w = -plog((1.0f - x) * (1.0f + x));
-  float p;
-  if (w < 5.0f) {
-    w = w - 2.5f;
-    p = 2.81022636e-08f;
-    p = 3.43273939e-07f + p * w; p = -3.5233877e-06f + p * w; p = -4.39150654e-06f + p * w;
-    p = 0.00021858087f + p * w; p = -0.00125372503f + p * w; p = -0.00417768164f + p * w;
-    p = 0.246640727f + p * w; p = 1.50140941f + p * w;
-  } else {
-    w = sqrtf(w) - 3.0f;
-    p = -0.000200214257f;
-    p = 0.000100950558f + p * w; p = 0.00134934322f + p * w; p = -0.00367342844f + p * w;
-    p = 0.00573950773f + p * w; p = -0.0076224613f + p * w; p = 0.00943887047f + p * w;
-    p = 1.00167406f + p * w; p = 2.83297682f + p * w;
-  }
-  return p * x;
-}
 
 __global__ void __launch_bounds__(256) k_init_tables(const uint32_t* __restrict__ keys, int n, int cols, int D,
                                                      float lo, float hi, float stddev, float* __restrict__ out) {
@@ -741,13 +728,13 @@ int toued_meta_keys(const uint32_t* agent_keys, int N, int K, uint32_t* roll_key
 int toued_lpg_inputs(int N, int W, int T, int D, int F, const float* theta, const float* phi, const int* tidx,
                      const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone, const float* eta_e1w,
                      const float* eta_e1b, const float* eta_e2w, const float* eta_e2b, const int* step,
-                     const int* levels, float* X, long xs_f, hipStream_t stream) {
+                     const int* levels, float* X, long xs_f, long eta_stride, hipStream_t stream) {
   TOUED_REQUIRE(F == 5 || F == 7, "toued_lpg_inputs: F=%d", F);
   const long n = (long)N * T * W;
   if (n == 0) return 0;
 #define L_(U, FF) hipLaunchKernelGGL((k_lpg_inputs<U, FF>), dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, theta, \
                                      phi, tidx, ttime, tact, trew, tdone, eta_e1w, eta_e1b, eta_e2w, eta_e2b, step,   \
-                                     levels, X, xs_f)
+                                     levels, X, xs_f, eta_stride)
   if (W % 64 == 0) { if (F == 5) L_(true, 5); else L_(true, 7); }
   else { if (F == 5) L_(false, 5); else L_(false, 7); }
 #undef L_

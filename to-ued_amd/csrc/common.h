@@ -144,6 +144,26 @@ TOUED_DEV float plog(float x) {
   return __fsub_rn(__fmul_rn(dk, 0.693145751953125f), __fsub_rn(__fsub_rn(hfsq, inner), f));
 }
 
+// erf_inv float32 (M. Giles' single-precision approximation, as XLA lowers lax.erf_inv)
+TOUED_DEV float erfinv_giles(float x) {
+  float w = -plog((1.0f - x) * (1.0f + x));
+  float p;
+  if (w < 5.0f) {
+    w = w - 2.5f;
+    p = 2.81022636e-08f;
+    p = 3.43273939e-07f + p * w; p = -3.5233877e-06f + p * w; p = -4.39150654e-06f + p * w;
+    p = 0.00021858087f + p * w; p = -0.00125372503f + p * w; p = -0.00417768164f + p * w;
+    p = 0.246640727f + p * w; p = 1.50140941f + p * w;
+  } else {
+    w = sqrtf(w) - 3.0f;
+    p = -0.000200214257f;
+    p = 0.000100950558f + p * w; p = 0.00134934322f + p * w; p = -0.00367342844f + p * w;
+    p = 0.00573950773f + p * w; p = -0.0076224613f + p * w; p = 0.00943887047f + p * w;
+    p = 1.00167406f + p * w; p = 2.83297682f + p * w;
+  }
+  return p * x;
+}
+
 // ----------------------------------------------------------------------------
 // Error reporting for the C ABI
 namespace toued {

@@ -68,9 +68,12 @@ TOUED_DEV float tanh_f(float x) {
 
 // ------------------------------------------------------------------ packing
 // fwdA[(tile*KQF + kq)*64 + lane] = float4 over kk = 4kq..4kq+3 of A[i=l&31][k=2kk+(l>>5)]
-__global__ void k_pack_fwd(const float* __restrict__ eta, EtaOff o, int F, float4* __restrict__ out) {
+__global__ void k_pack_fwd(const float* __restrict__ eta, EtaOff o, int F, float4* __restrict__ out,
+                           long eta_stride) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= NTILE_F * KQF * 64) return;
+  eta += (long)blockIdx.y * eta_stride;            // candidate blockIdx.y (ES); 0 for the shared eta
+  out += (long)blockIdx.y * NTILE_F * KQF * 64;
   const int lane = gid & 63, kq = (gid >> 6) % KQF, tile = gid / (64 * KQF);
   const int g = tile >> 3, u = 32 * (tile & 7) + (lane & 31);
   float v[4];
@@ -121,6 +124,9 @@ struct FwdArgs {
   float* pi_hat; float* y_hat;         // [T][R], [T][8][R]
   float* s_hin; float* s_r; float* s_z; float* s_n; float* s_hn;  // [256][M] with column base added
   long M;
+  int save;                            // 0: inference only (ES), nothing saved for a backward
+  int rpc;                             // rows per parameter candidate (0: one shared eta)
+  long a_stride4, eta_stride;          // per-candidate strides of A (float4 units) and eta (floats)
 };
 
 #define NWAVE 8         // 512-thread workgroups: wave w owns units [32w, 32w+32)
@@ -135,9 +141,11 @@ __global__ void __launch_bounds__(512, 4) k_gru_fwd(FwdArgs p) {
   const int r0 = blockIdx.x * RB, row = r0 + col;
   const int R = p.R, T = p.T, W = p.W, F = p.F;
   const int a = r0 / W, w = row - a * W;
+  const int cand = p.rpc ? r0 / p.rpc : 0;
+  const float* eta = p.eta + (long)cand * p.eta_stride;
   for (int i = tid; i < HU * 9; i += 512) {
     const int u = i / 9, oo = i - u * 9;
-    wh[i] = oo == 0 ? p.eta[p.o.pi_w + u] : p.eta[p.o.y_w + u * 8 + (oo - 1)];
+    wh[i] = oo == 0 ? eta[p.o.pi_w + u] : eta[p.o.y_w + u * 8 + (oo - 1)];
   }
   for (int i = tid; i < (HU + NAUG) * LDH; i += 512) hT[i] = 0.0f;
   __syncthreads();
@@ -147,8 +155,8 @@ __global__ void __launch_bounds__(512, 4) k_gru_fwd(FwdArgs p) {
       hT[(HU + f) * LDH + tid] = f < F ? p.X[f * p.xs_f + (size_t)t * R + r0 + tid] : (f == F ? 1.0f : 0.0f);
   }
   __syncthreads();
-  const float bpi = p.eta[p.o.pi_b];
-  const float4* Ab = p.A + lane;
+  const float bpi = eta[p.o.pi_b];
+  const float4* Ab = p.A + (long)cand * p.a_stride4 + lane;
   const __amdgpu_buffer_rsrc_t rs_hin = rsrc_of(p.s_hin), rs_r = rsrc_of(p.s_r), rs_z = rsrc_of(p.s_z),
                                rs_n = rsrc_of(p.s_n), rs_hn = rsrc_of(p.s_hn);
   for (int s = 0; s < T; ++s) {
@@ -214,12 +222,14 @@ __global__ void __launch_bounds__(512, 4) k_gru_fwd(FwdArgs p) {
       const float hin = hTl[qunit(q) * LDH];    // h_in(t) (masked carry), rewritten after the barrier
       const float h = (1.0f - zg) * ng + zg * hin;
       hnew[q] = h;
-      const unsigned so = (unsigned)(((long)qunit(q) * p.M + cbase) * 4);
-      st_u(rs_hin, vbyte, so, hin);
-      st_u(rs_r, vbyte, so, rg);
-      st_u(rs_z, vbyte, so, zg);
-      st_u(rs_n, vbyte, so, ng);
-      st_u(rs_hn, vbyte, so, hn);
+      if (p.save) {
+        const unsigned so = (unsigned)(((long)qunit(q) * p.M + cbase) * 4);
+        st_u(rs_hin, vbyte, so, hin);
+        st_u(rs_r, vbyte, so, rg);
+        st_u(rs_z, vbyte, so, zg);
+        st_u(rs_n, vbyte, so, ng);
+        st_u(rs_hn, vbyte, so, hn);
+      }
       const float rl = fmaxf(h, 0.0f);
 #pragma unroll
       for (int oo = 0; oo < 9; ++oo) hp_loc[oo] += rl * whl[qunit(q) * 9 + oo];
@@ -239,7 +249,7 @@ __global__ void __launch_bounds__(512, 4) k_gru_fwd(FwdArgs p) {
     }
     for (int i = tid; i < 9 * RB; i += 512) {
       const int oo = i / RB, c = i - oo * RB;
-      float v = oo == 0 ? bpi : p.eta[p.o.y_b + oo - 1];
+      float v = oo == 0 ? bpi : eta[p.o.y_b + oo - 1];
 #pragma unroll
       for (int gq = 0; gq < NGRP; ++gq) v += hp[(gq * 9 + oo) * RB + c];
       hout[i] = v;
@@ -415,7 +425,7 @@ int toued_gru_pack(const float* eta, const int* off, int F, float* fwdA, float* 
   memcpy(&o, off, sizeof(EtaOff));
   const int n1 = NTILE_F * KQF * 64, n2 = 8 * 3 * 32 * 64;
   hipLaunchKernelGGL(k_pack_fwd, dim3((n1 + 255) / 256), dim3(256), 0, stream, eta, o, F,
-                     reinterpret_cast<float4*>(fwdA));
+                     reinterpret_cast<float4*>(fwdA), 0L);
   hipLaunchKernelGGL(k_pack_bwd, dim3((n2 + 255) / 256), dim3(256), 0, stream, eta, o,
                      reinterpret_cast<float4*>(bwdA));
   TOUED_CHECK_LAUNCH();
@@ -424,6 +434,21 @@ int toued_gru_pack(const float* eta, const int* off, int F, float* fwdA, float* 
 
 size_t toued_gru_packed_floats(int which) { return which == 0 ? (size_t)NTILE_F * KQF * 64 * 4 : (size_t)8 * 3 * 32 * 64 * 4; }
 
+static int gru_fwd_launch(int R, int T, int W, int F, const float* X, long xs_f, const uint8_t* done,
+                          const float* fwdA, const float* eta, const int* off, float* pi_hat, float* y_hat,
+                          float* s_hin, float* s_r, float* s_z, float* s_n, float* s_hn, long M, int save, int rpc,
+                          long eta_stride, hipStream_t stream) {
+  FwdArgs p;
+  p.R = R; p.T = T; p.W = W; p.F = F; p.X = X; p.xs_f = xs_f; p.done = done;
+  p.A = reinterpret_cast<const float4*>(fwdA); p.eta = eta;
+  memcpy(&p.o, off, sizeof(EtaOff));
+  p.pi_hat = pi_hat; p.y_hat = y_hat; p.s_hin = s_hin; p.s_r = s_r; p.s_z = s_z; p.s_n = s_n; p.s_hn = s_hn; p.M = M;
+  p.save = save; p.rpc = rpc; p.a_stride4 = (long)NTILE_F * KQF * 64; p.eta_stride = eta_stride;
+  hipLaunchKernelGGL(k_gru_fwd, dim3(R / RB), dim3(512), 0, stream, p);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
 int toued_gru_fwd(int R, int T, int W, int F, const float* X, long xs_f, const uint8_t* done, const float* fwdA,
                   const float* eta, const int* off, float* pi_hat, float* y_hat, float* s_hin, float* s_r, float* s_z,
                   float* s_n, float* s_hn, long M, hipStream_t stream) {
@@ -431,14 +456,34 @@ int toued_gru_fwd(int R, int T, int W, int F, const float* X, long xs_f, const u
   TOUED_REQUIRE(F >= 1 && F <= 7 && T >= 1, "toued_gru_fwd: F=%d T=%d", F, T);
   TOUED_REQUIRE((double)M * 264.0 * 4.0 < 4294967295.0, "toued_gru_fwd: M=%ld columns exceed the 4 GiB buffer range "
                 "(use --num_mini_batches to split the agent batch)", M);
-  FwdArgs p;
-  p.R = R; p.T = T; p.W = W; p.F = F; p.X = X; p.xs_f = xs_f; p.done = done;
-  p.A = reinterpret_cast<const float4*>(fwdA); p.eta = eta;
-  memcpy(&p.o, off, sizeof(EtaOff));
-  p.pi_hat = pi_hat; p.y_hat = y_hat; p.s_hin = s_hin; p.s_r = s_r; p.s_z = s_z; p.s_n = s_n; p.s_hn = s_hn; p.M = M;
-  hipLaunchKernelGGL(k_gru_fwd, dim3(R / RB), dim3(512), 0, stream, p);
+  TOUED_REQUIRE(s_hin && s_r && s_z && s_n && s_hn, "toued_gru_fwd: saved-activation buffers required");
+  return gru_fwd_launch(R, T, W, F, X, xs_f, done, fwdA, eta, off, pi_hat, y_hat, s_hin, s_r, s_z, s_n, s_hn, M, 1, 0,
+                        0, stream);
+}
+
+int toued_gru_pack_fwd_multi(const float* eta, long eta_stride, int n, const int* off, int F, float* fwdA,
+                             hipStream_t stream) {
+  TOUED_REQUIRE(F >= 1 && F <= 7 && n >= 0, "toued_gru_pack_fwd_multi: F=%d n=%d", F, n);
+  if (n == 0) return 0;
+  EtaOff o;
+  memcpy(&o, off, sizeof(EtaOff));
+  const int n1 = NTILE_F * KQF * 64;
+  hipLaunchKernelGGL(k_pack_fwd, dim3((n1 + 255) / 256, n), dim3(256), 0, stream, eta, o, F,
+                     reinterpret_cast<float4*>(fwdA), eta_stride);
   TOUED_CHECK_LAUNCH();
   return 0;
+}
+
+int toued_gru_fwd_multi(int R, int T, int W, int F, int rows_per_cand, const float* X, long xs_f, const uint8_t* done,
+                        const float* fwdA, const float* eta, long eta_stride, const int* off, float* pi_hat,
+                        float* y_hat, hipStream_t stream) {
+  TOUED_REQUIRE(R % RB == 0 && W % RB == 0, "toued_gru_fwd_multi: rows R=%d and workers W=%d must be multiples of 32",
+                R, W);
+  TOUED_REQUIRE(rows_per_cand > 0 && rows_per_cand % RB == 0 && R % rows_per_cand == 0,
+                "toued_gru_fwd_multi: rows_per_cand=%d must be a multiple of 32 dividing R=%d", rows_per_cand, R);
+  TOUED_REQUIRE(F >= 1 && F <= 7 && T >= 1, "toued_gru_fwd_multi: F=%d T=%d", F, T);
+  return gru_fwd_launch(R, T, W, F, X, xs_f, done, fwdA, eta, off, pi_hat, y_hat, nullptr, nullptr, nullptr, nullptr,
+                        nullptr, 0, 0, rows_per_cand, eta_stride, stream);
 }
 
 int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_stride_k, const float* bwdA,

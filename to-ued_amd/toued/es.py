@@ -1,0 +1,207 @@
+"""TA-LPG: the LPG optimised with OpenES on MI355X (meta/train.py:133-227, meta/meta.py:10-52).
+
+``ESTrainStep(rng, agents, rank_slice)`` = ``lpg_es_train_step``:
+  1. ``rng, _rng = split(rng)``; OpenES ask (toued_es_ask): P = 2 * num_agents candidates,
+     reordered into antithetic pairs (2i: mean + sigma z_i, 2i+1: mean - sigma z_i).
+  2. ``rng, _rng = split(rng)``; ``split(_rng, P)`` per-candidate keys; every agent is repeated
+     for its two candidates; per candidate ``rng_c, _rng_c = split(key_c)``: ``train_lpg_agent``
+     for ``max_lifetime`` updates with that candidate's LPG (per-candidate GRU weights on MFMA,
+     toued_gru_fwd_multi), then ``eval_agent(rng_c)`` over ``env_workers`` workers = fitness.
+  3. rank per antithetic pair, keep the winning agent of each pair, OpenES tell
+     (toued_es_grad + all-reduce + toued_es_opt).
+
+OpenES is evosax 0.1.4 (not vendored) restated from its published algorithm:
+the search mean starts at zero (``initialize`` draws uniform(init_min=0, init_max=0)); the
+fitness shaper negates the rank fitness (maximize=True); Adam uses evosax's defaults
+(b1=0.99, b2=0.999, eps=1e-8); lrate and sigma decay exponentially to their limits after
+every tell.  Multi-GPU: rank r owns agents [lo, hi) -> candidates [2lo, 2hi) and z rows [lo, hi);
+the tell gradient is one all-reduce of a [num_params] vector per ES step.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib, prng
+from .agents import eval_agent
+from .lpg import LPGLayout
+from .rollout import Transition
+
+_Y = 8
+
+
+class OpenES:
+    """evosax.OpenES(popsize, maximize=True, opt_name, lrate_*, sigma_*, mean_decay) state on the device."""
+
+    def __init__(self, popsize: int, num_dims: int, opt_name="adam", lrate_init=0.05, lrate_decay=1.0,
+                 lrate_limit=0.001, sigma_init=0.03, sigma_decay=1.0, sigma_limit=0.01, mean_decay=0.0, device=None):
+        opt_name = opt_name.lower()
+        if opt_name not in ("adam", "sgd"):
+            raise NotImplementedError(f"OpenES optimiser {opt_name}: adam and sgd are implemented")
+        if mean_decay != 0.0:
+            raise NotImplementedError("es_mean_decay != 0 is not implemented (reference default 0.0)")
+        self.popsize = popsize
+        self.nd = num_dims
+        self.opt = 1 if opt_name == "adam" else 0
+        self.lrate_decay, self.lrate_limit = np.float32(lrate_decay), np.float32(lrate_limit)
+        self.sigma_decay, self.sigma_limit = np.float32(sigma_decay), np.float32(sigma_limit)
+        dev = torch.device(device) if device is not None else torch.device("cuda")
+        self.mean = torch.zeros(num_dims, dtype=torch.float32, device=dev)
+        self.m = torch.zeros_like(self.mean)
+        self.v = torch.zeros_like(self.mean)
+        self.grad = torch.zeros_like(self.mean)
+        self.n = 0
+        self.lrate = np.float32(lrate_init)
+        self.sigma = np.float32(sigma_init)
+        self.gen_counter = 0
+
+    def ask(self, rng: torch.Tensor, row_lo: int, n_rows: int, out: torch.Tensor):
+        """Candidates 2*row_lo .. 2*(row_lo+n_rows) of the reordered population into out [2n, nd]."""
+        _lib.call("toued_es_ask", _lib.ptr(rng.contiguous()), self.nd, self.popsize // 2, row_lo, n_rows,
+                  _lib.ptr(self.mean), float(self.sigma), _lib.ptr(out), _lib.stream_ptr())
+        return out
+
+    def tell(self, x_local: torch.Tensor, rank_fitness_local: torch.Tensor, world=None):
+        fit = (-rank_fitness_local).float().contiguous()          # FitnessShaper(maximize=True)
+        _lib.call("toued_es_grad", _lib.ptr(x_local), _lib.ptr(self.mean), float(self.sigma), _lib.ptr(fit),
+                  x_local.shape[0], self.nd, _lib.ptr(self.grad), _lib.stream_ptr())
+        if world is not None:
+            world.all_reduce_sum(self.grad)
+        scale = np.float32(1.0) / (np.float32(self.popsize) * self.sigma)
+        b1, b2, eps = np.float32(0.99), np.float32(0.999), np.float32(1e-8)
+        bc1 = np.float32(1.0) - b1 ** np.float32(self.n + 1)
+        bc2 = np.float32(1.0) - b2 ** np.float32(self.n + 1)
+        _lib.call("toued_es_opt", self.nd, self.opt, _lib.ptr(self.mean), _lib.ptr(self.grad), float(scale),
+                  _lib.ptr(self.m), _lib.ptr(self.v), float(self.lrate), float(b1), float(b2), float(eps), float(bc1),
+                  float(bc2), _lib.stream_ptr())
+        self.n += 1
+        self.lrate = np.maximum(np.float32(self.lrate * self.lrate_decay), self.lrate_limit)
+        self.sigma = np.maximum(np.float32(self.sigma * self.sigma_decay), self.sigma_limit)
+        self.gen_counter += 1
+
+
+class ESTrainStep:
+    def __init__(self, args, sampler, n_local: int, eta: torch.Tensor, device=None, world=None,
+                 num_agent_updates: int | None = None):
+        self.sampler = sampler
+        self.ro = sampler.rollout_manager
+        self.world = world
+        self.dev = torch.device(device) if device is not None else eta.device
+        self.N = n_local
+        self.C = 2 * n_local
+        self.W = self.ro.env_workers
+        self.T = self.ro.train_rollout_len
+        self.D = self.ro.obs_dim
+        # make_lpg_train_step (meta/meta.py:35-37): ES trains each agent for its whole lifetime
+        self.K = sampler.max_lifetime if num_agent_updates is None else num_agent_updates
+        self.F = 7 if args.lifetime_conditioning else 5
+        self.lay = LPGLayout(self.F)
+        if eta.numel() != self.lay.size:
+            raise ValueError("eta does not match the LPG layout")
+        ah = sampler.agent_hypers
+        self.lr_a, self.lr_c, self.mn = ah.actor_learning_rate, ah.critic_learning_rate, ah.max_grad_norm
+        self.alpha_y = args.lpg_agent_target_coeff
+        n_total = args.num_agents
+        self.es = OpenES(2 * n_total, self.lay.size, args.lpg_opt, args.lpg_learning_rate, args.es_lrate_decay,
+                         args.es_lrate_limit, args.es_sigma_init, args.es_sigma_decay, args.es_sigma_limit,
+                         args.es_mean_decay, self.dev)
+        C, W, T, D = self.C, self.W, self.T, self.D
+        R = C * W
+        if W % 32:
+            raise ValueError(f"env_workers={W} must be a multiple of 32 for the MFMA GRU row blocks")
+        self.R = R
+        f32, i32, u8 = torch.float32, torch.int32, torch.uint8
+        z = lambda *s, dt=f32: torch.zeros(s, dtype=dt, device=self.dev)
+        self.x = z(C, self.lay.size)
+        self.fwdA = z(C, _lib.lib().toued_gru_packed_floats(0))
+        self.theta = [z(C, D, 5), z(C, D, 5)]
+        self.phi = [z(C, D, _Y), z(C, D, _Y)]
+        self.G_th, self.G_ph = z(C, D, 5), z(C, D, _Y)
+        self.gstat = z(C, 4)
+        self.met = z(C, 8)
+        self.tr = Transition(z(C, T + 1, W, dt=i32), z(C, T + 1, W, dt=i32), z(C, T, W, dt=u8), z(C, T, W),
+                             z(C, T, W, dt=u8))
+        self.X = z(self.F, T, R)
+        self.pi_hat = z(T, R)
+        self.y_hat = z(T, _Y, R)
+        self.fitness = None
+
+    def _eta(self, name):
+        o = self.lay.offsets[name]
+        return self.x.view(-1)[o:]
+
+    def __call__(self, rng: torch.Tensor, agents, rank_slice=None):
+        L = _lib
+        st = L.stream_ptr()
+        ptr = L.ptr
+        N, C, W, T, D, K, R = self.N, self.C, self.W, self.T, self.D, self.K, self.R
+        lo = 0 if rank_slice is None else rank_slice[0]
+        n_total = N if rank_slice is None else rank_slice[2]
+        nd = self.lay.size
+        # ---- ask (meta/train.py:147-158)
+        ks = prng.split(rng, 2)
+        rng, sub = ks[0].contiguous(), ks[1].contiguous()
+        self.es.ask(sub, lo, N, self.x)
+        L.call("toued_gru_pack_fwd_multi", ptr(self.x), nd, C, self.lay.c_offsets, self.F, ptr(self.fwdA), st)
+        # ---- per-candidate keys (:187-189) and repeated agents (:184-186)
+        ks = prng.split(rng, 2)
+        rng, sub = ks[0].contiguous(), ks[1].contiguous()
+        ck = prng.split(sub, 2 * n_total)[2 * lo:2 * lo + C]
+        ck2 = prng.split(ck.contiguous(), 2)
+        fit_keys, train_keys = ck2[:, 0].contiguous(), ck2[:, 1].contiguous()
+        chain = torch.empty((K, C, 2), dtype=torch.int32, device=self.dev)
+        if K:
+            L.call("toued_key_chain", ptr(train_keys), C, K, ptr(chain), st)
+        levels = agents.levels.repeat_interleave(2, dim=0).contiguous()
+        step = agents.step.repeat_interleave(2).contiguous()
+        state = agents.state.view(12, agents.n, W).repeat_interleave(2, dim=1).reshape(12, C * W).contiguous()
+        cur = 0
+        self.theta[cur].copy_(agents.theta.repeat_interleave(2, dim=0))
+        self.phi[cur].copy_(agents.phi.repeat_interleave(2, dim=0))
+        self.met.zero_()
+        e1w, e1b, e2w, e2b = (self._eta(n) for n in ("e1_w", "e1_b", "e2_w", "e2_b"))
+        tr = self.tr
+        # ---- train_lpg_agent for K = max_lifetime updates (agents/lpg_agent.py:88-140)
+        for k in range(K):
+            th, ph = self.theta[cur], self.phi[cur]
+            self.ro.batch_rollout(chain[k], th, levels, state, out=tr, inplace_state=True)
+            L.call("toued_lpg_inputs", C, W, T, D, self.F, ptr(th), ptr(ph), ptr(tr.obs_idx), ptr(tr.obs_time),
+                   ptr(tr.action), ptr(tr.reward), ptr(tr.done), ptr(e1w), ptr(e1b), ptr(e2w), ptr(e2b), ptr(step),
+                   ptr(levels), ptr(self.X), T * R, nd, st)
+            L.call("toued_gru_fwd_multi", R, T, W, self.F, W, ptr(self.X), T * R, ptr(tr.done), ptr(self.fwdA),
+                   ptr(self.x), nd, self.lay.c_offsets, ptr(self.pi_hat), ptr(self.y_hat), st)
+            self.G_th.zero_()
+            self.G_ph.zero_()
+            L.call("toued_agent_grad", C, W, T, D, ptr(th), ptr(ph), ptr(tr.obs_idx), ptr(tr.obs_time),
+                   ptr(tr.action), ptr(tr.reward), ptr(tr.done), ptr(self.pi_hat), ptr(self.y_hat), self.alpha_y,
+                   ptr(self.G_th), ptr(self.G_ph), ptr(self.met), st)
+            L.call("toued_agent_apply", C, D, ptr(th), ptr(ph), ptr(self.G_th), ptr(self.G_ph), self.lr_a, self.lr_c,
+                   self.mn, ptr(step), ptr(levels), ptr(self.theta[1 - cur]), ptr(self.phi[1 - cur]),
+                   ptr(self.gstat), st)
+            cur = 1 - cur
+            L.call("toued_entropy", C, W, T, D, ptr(self.theta[cur]), ptr(self.phi[cur]), ptr(tr.obs_idx),
+                   ptr(tr.obs_time), ptr(self.met), 0.0, 0.0, None, None, st)
+        # ---- fitness = eval_agent(rng_c) (:178-186)
+        fitness = eval_agent(self.ro, fit_keys, levels, self.theta[cur], W)
+        self.fitness = fitness
+        # ---- rank per antithetic pair, winners (:199-211)
+        first_greater = fitness[0::2] > fitness[1::2]
+        rank = torch.empty_like(fitness)
+        rank[0::2] = first_greater.float()
+        rank[1::2] = 1.0 - first_greater.float()
+        sel = torch.where(first_greater, torch.arange(N, device=self.dev) * 2, torch.arange(N, device=self.dev) * 2 + 1)
+        agents.theta.copy_(self.theta[cur][sel])
+        agents.phi.copy_(self.phi[cur][sel])
+        agents.step.copy_(step[sel])
+        agents.state.copy_(state.view(12, C, W)[:, sel].reshape(12, N * W))
+        # ---- tell (:214-217)
+        self.es.tell(self.x, rank, self.world if (self.world is not None and self.world.size > 1) else None)
+        inv = 1.0 / (W * T * max(K, 1))
+        m = self.met * inv
+        fit_all = fitness if self.world is None or self.world.size == 1 else self.world.all_gather_cat(fitness)
+        return {
+            "fitness": {"mean": fit_all.mean(), "min": fit_all.min(), "max": fit_all.max(),
+                        "var": fit_all.var(unbiased=False)},
+            "lpg_agent": {"critic_loss": m[:, 0], "policy_l2": m[:, 1], "critic_l2": m[:, 2],
+                          "policy_entropy": m[:, 3], "critic_entropy": m[:, 4]},
+        }
