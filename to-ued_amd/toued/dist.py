@@ -20,22 +20,34 @@ class World:
     rank: int = 0
     size: int = 1
     local_rank: int = 0
+    backend: str = ""
 
     @property
     def active(self) -> bool:
         return self.size > 1 and dist.is_available() and dist.is_initialized()
 
+    def _staged(self, t: torch.Tensor) -> bool:
+        # gloo (CPU tests, or several ranks sharing one GPU) moves device tensors through the host
+        return self.backend == "gloo" and t.is_cuda
+
     def all_reduce_sum(self, t: torch.Tensor):
         if self.active:
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            if self._staged(t):
+                h = t.cpu()
+                dist.all_reduce(h, op=dist.ReduceOp.SUM)
+                t.copy_(h)
+            else:
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return t
 
     def all_gather_cat(self, t: torch.Tensor) -> torch.Tensor:
         if not self.active:
             return t
-        parts = [torch.empty_like(t) for _ in range(self.size)]
-        dist.all_gather(parts, t.contiguous())
-        return torch.cat(parts, dim=0)
+        src = t.contiguous().cpu() if self._staged(t) else t.contiguous()
+        parts = [torch.empty_like(src) for _ in range(self.size)]
+        dist.all_gather(parts, src)
+        out = torch.cat(parts, dim=0)
+        return out.to(t.device) if self._staged(t) else out
 
     def barrier(self):
         if self.active:
@@ -56,9 +68,10 @@ def init_from_env(backend: str | None = None) -> World:
     rank = int(os.environ["RANK"])
     local = int(os.environ.get("LOCAL_RANK", rank))
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-    if backend == "nccl":
-        torch.cuda.set_device(local)
+        backend = os.environ.get("TOUED_DIST_BACKEND") or ("nccl" if torch.cuda.device_count() > 0 else "gloo")
+    if torch.cuda.device_count() > 0:
+        # one GPU per rank; ranks beyond the device count share devices (gloo only)
+        torch.cuda.set_device(local % torch.cuda.device_count())
     if not dist.is_initialized():
         dist.init_process_group(backend=backend)
-    return World(rank, ws, local)
+    return World(rank, ws, local, backend)
