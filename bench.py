@@ -39,6 +39,20 @@ GRU_FWD_FLOP_PER_ELEM = {5: 406080, 7: 409152}    # per (agent, w
 GRU_BWD_FLOP_PER_ELEM = 2 * 256 * 768              # dh_prev = dG . W_h^T per (k, agent, worker, t)
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*/pmc_traffic.json,
+    written by tools/profile.sh + tools/prof_summary.py: FETCH_SIZE and WRITE_SIZE passes corrected by the
+    calibration factors).  (None, None) when no summary covers the kernel."""
+    for d in sorted((ROOT / "profiles").glob("*/pmc_traffic.json"), reverse=True):
+        try:
+            k = json.loads(d.read_text())["kernels"].get(kernel)
+        except (OSError, ValueError, KeyError):
+            continue
+        if k:
+            return k["hbm_bytes_per_launch"], str(d.relative_to(ROOT))
+    return None, None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -151,8 +165,10 @@ def main():
     if "gru_bwd" in ksum:
         cand.append(("gru_bwd", ksum["gru_bwd"][2], bwd_flops / (ksum["gru_bwd"][1] * 1e-3) / 1e12))
     dom = max(cand, key=lambda c: c[1])
+    traffic, traffic_src = pmc_traffic("k_" + dom[0])
     roofline = {"bound": "mfma", "kernel": dom[0], "achieved": round(dom[2], 2), "peak": MFMA_F32_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(dom[2] / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(dom[2] / MFMA_F32_PEAK_TFLOPS, 4), "traffic": traffic,
+                "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                 "flop_per_launch": fwd_flops if dom[0] == "gru_fwd" else bwd_flops}
     out = {
         "metric": "agent-env-steps/sec (inner rollout) at num_agents=512; meta-updates/sec",
