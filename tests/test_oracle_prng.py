@@ -9,7 +9,7 @@ import numpy as np
 from oracle import jaxrand as jr
 
 
-def test_threefry_kat():
+def test_threefry_kat():  # (also in tests/golden/prng_kat.json)
     cases = [((0, 0), (0, 0), (0x6B200159, 0x99BA4EFE)),
              ((0xFFFFFFFF, 0xFFFFFFFF), (0xFFFFFFFF, 0xFFFFFFFF), (0x1CB996FC, 0xBB002BE7)),
              ((0x13198A2E, 0x03707344), (0x243F6A88, 0x85A308D3), (0xC4923A9C, 0x483DF7A0))]

@@ -124,14 +124,14 @@ struct FwdArgs {
   float* pi_hat; float* y_hat;         // [T][R], [T][8][R]
   float* s_hin; float* s_r; float* s_z; float* s_n; float* s_hn;  // [256][M] with column base added
   long M;
-  int save;                            // 0: inference only (ES), nothing saved for a backward
-  int rpc;                             // rows per parameter candidate (0: one shared eta)
+  int rpc;                             // rows per parameter candidate (inference mode, ES)
   long a_stride4, eta_stride;          // per-candidate strides of A (float4 units) and eta (floats)
 };
 
 #define NWAVE 8         // 512-thread workgroups: wave w owns units [32w, 32w+32)
 #define NGRP (2 * NWAVE)
 
+template <bool SAVE>
 __global__ void __launch_bounds__(512, 4) k_gru_fwd(FwdArgs p) {
   __shared__ float hT[(HU + NAUG) * LDH];
   __shared__ float wh[HU * 9];
@@ -141,7 +141,7 @@ __global__ void __launch_bounds__(512, 4) k_gru_fwd(FwdArgs p) {
   const int r0 = blockIdx.x * RB, row = r0 + col;
   const int R = p.R, T = p.T, W = p.W, F = p.F;
   const int a = r0 / W, w = row - a * W;
-  const int cand = p.rpc ? r0 / p.rpc : 0;
+  const int cand = SAVE ? 0 : r0 / p.rpc;
   const float* eta = p.eta + (long)cand * p.eta_stride;
   for (int i = tid; i < HU * 9; i += 512) {
     const int u = i / 9, oo = i - u * 9;
@@ -222,7 +222,7 @@ __global__ void __launch_bounds__(512, 4) k_gru_fwd(FwdArgs p) {
       const float hin = hTl[qunit(q) * LDH];    // h_in(t) (masked carry), rewritten after the barrier
       const float h = (1.0f - zg) * ng + zg * hin;
       hnew[q] = h;
-      if (p.save) {
+      if (SAVE) {
         const unsigned so = (unsigned)(((long)qunit(q) * p.M + cbase) * 4);
         st_u(rs_hin, vbyte, so, hin);
         st_u(rs_r, vbyte, so, rg);
@@ -350,11 +350,27 @@ __global__ void __launch_bounds__(512, 4) k_gru_bwd(BwdArgs p) {
     const unsigned vbyte = (unsigned)(((long)(32 * wave + 4 * hi) * p.M + row) * 4);
     float dx3 = 0.0f, dx4 = 0.0f;
     const float* wil = wi34 + 32 * wave + 4 * hi;
+    // Saved activations in batches of QB units, every load of a batch issued before the batch's
+    // stores: raw buffer stores may alias later loads, so the compiler keeps program order and a
+    // load-compute-store per unit would cost one memory round trip per unit.
+    constexpr int QB = 4;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
+    for (int qb = 0; qb < 16; qb += QB) {
+      float v_hin[QB], v_r[QB], v_z[QB], v_n[QB], v_hn[QB];
+#pragma unroll
+      for (int j = 0; j < QB; ++j) {
+        const unsigned so = (unsigned)(((long)qunit(qb + j) * p.M + ctr) * 4);
+        v_hin[j] = ld_u(rs_hin, vbyte, so);
+        v_r[j] = ld_u(rs_r, vbyte, so);
+        v_z[j] = ld_u(rs_z, vbyte, so);
+        v_n[j] = ld_u(rs_n, vbyte, so);
+        v_hn[j] = ld_u(rs_hn, vbyte, so);
+      }
+#pragma unroll
+      for (int j = 0; j < QB; ++j) {
+      const int q = qb + j;
       const unsigned so = (unsigned)(((long)qunit(q) * p.M + ctr) * 4);
-      const float hin = ld_u(rs_hin, vbyte, so), rg = ld_u(rs_r, vbyte, so), zg = ld_u(rs_z, vbyte, so);
-      const float ng = ld_u(rs_n, vbyte, so), hn = ld_u(rs_hn, vbyte, so);
+      const float hin = v_hin[j], rg = v_r[j], zg = v_z[j], ng = v_n[j], hn = v_hn[j];
       const float hout = (1.0f - zg) * ng + zg * hin;
       const float d = dh[q] + (hout > 0.0f ? hacc[q] : 0.0f);
       st_u(rs_rh, vbyte, so, fmaxf(hout, 0.0f));
@@ -372,6 +388,7 @@ __global__ void __launch_bounds__(512, 4) k_gru_bwd(BwdArgs p) {
       const int qu = qunit(q);
       dx3 += drp * wil[0 * HU + qu] + dzp * wil[1 * HU + qu] + dnp * wil[2 * HU + qu];
       dx4 += drp * wil[3 * HU + qu] + dzp * wil[4 * HU + qu] + dnp * wil[5 * HU + qu];
+      }
     }
     dxp[((2 * wave + hi) * 2 + 0) * RB + col] = dx3;
     dxp[((2 * wave + hi) * 2 + 1) * RB + col] = dx4;
@@ -443,8 +460,11 @@ static int gru_fwd_launch(int R, int T, int W, int F, const float* X, long xs_f,
   p.A = reinterpret_cast<const float4*>(fwdA); p.eta = eta;
   memcpy(&p.o, off, sizeof(EtaOff));
   p.pi_hat = pi_hat; p.y_hat = y_hat; p.s_hin = s_hin; p.s_r = s_r; p.s_z = s_z; p.s_n = s_n; p.s_hn = s_hn; p.M = M;
-  p.save = save; p.rpc = rpc; p.a_stride4 = (long)NTILE_F * KQF * 64; p.eta_stride = eta_stride;
-  hipLaunchKernelGGL(k_gru_fwd, dim3(R / RB), dim3(512), 0, stream, p);
+  p.rpc = rpc; p.a_stride4 = (long)NTILE_F * KQF * 64; p.eta_stride = eta_stride;
+  if (save)
+    hipLaunchKernelGGL(k_gru_fwd<true>, dim3(R / RB), dim3(512), 0, stream, p);
+  else
+    hipLaunchKernelGGL(k_gru_fwd<false>, dim3(R / RB), dim3(512), 0, stream, p);
   TOUED_CHECK_LAUNCH();
   return 0;
 }
