@@ -131,12 +131,14 @@ int toued_a2c_apply(int N, int D, float* theta, float* vcrit, float* Ga, float* 
 /* per-agent keys of _train_agent (meta/train.py:88-170): K train rollouts, the eval rollout, eval_agent */
 int toued_meta_keys(const uint32_t* agent_keys, int N, int K, uint32_t* roll_keys, uint32_t* eval_keys,
                     uint32_t* ea_reset, uint32_t* ea_roll, hipStream_t stream);
-/* LPG inputs x = [r, d, pi, e(y_t), e(y_tp1) (, step, lifetime)] (models/lpg.py:48-77) into X (feature stride xs_f);
- * eta_e* point at the embedding-MLP parameters, advanced by a*eta_stride for agent a (ES candidates; 0 = shared) */
+/* LPG inputs x = [r, d, pi, e(y_t), e(y_tp1) (, step, lifetime)] (models/lpg.py:48-77) into
+ * X[f*xs_f + (t*R + r)*xs_col]; eta_e* point at the embedding-MLP parameters, advanced by a*eta_stride for
+ * agent a (ES candidates; 0 = shared) */
 int toued_lpg_inputs(int N, int W, int T, int D, int F, const float* theta, const float* phi, const int* tidx,
                      const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
                      const float* eta_e1w, const float* eta_e1b, const float* eta_e2w, const float* eta_e2b,
-                     const int* step, const int* levels, float* X, long xs_f, long eta_stride, hipStream_t stream);
+                     const int* step, const int* levels, float* X, long xs_f, long xs_col, long eta_stride,
+                     hipStream_t stream);
 /* lpg_agent_train_step gradients (lpg_agent.py:36-70) given pi_hat [T][R], y_hat [T][8][R] */
 int toued_agent_grad(int N, int W, int T, int D, const float* theta, const float* phi, const int* tidx,
                      const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
@@ -178,12 +180,14 @@ int toued_adam(int P, float* eta, const float* grad, float* m, float* v, float s
 size_t toued_gru_packed_floats(int which);
 /* repack eta's GRU weights into MFMA A-fragment order (fwdA / bwdA) */
 int toued_gru_pack(const float* eta, const int* off, int F, float* fwdA, float* bwdA, hipStream_t stream);
-/* forward over R rows x T steps (t = T-1 .. 0, h reset on done); heads pi_hat [T][R], y_hat [T][8][R];
- * saves h_in, r, z, n, hn [T][256][R] for the backward (row stride M) */
-int toued_gru_fwd(int R, int T, int W, int F, const float* X, long xs_f, const uint8_t* done, const float* fwdA,
-                  const float* eta, const int* off, float* pi_hat, float* y_hat, float* s_hin, float* s_r, float* s_z,
-                  float* s_n, float* s_hn, long M, hipStream_t stream);
-/* VJP: gate cotangents DG [4][256][M], relu(h) RH, head cotangents DH [9][M], input cotangents dX3/dX4 */
+/* forward over R rows x T steps (t = T-1 .. 0, h reset on done); X[f*xs_f + (t*R + r)*xs_col];
+ * heads pi_hat [T][R], y_hat [T][8][R]; saves h_in, r, z, n, W_hn h + b_hn as [256][M] row-major
+ * (pointers at this update's first column, row stride M) for the backward */
+int toued_gru_fwd(int R, int T, int W, int F, const float* X, long xs_f, long xs_col, const uint8_t* done,
+                  const float* fwdA, const float* eta, const int* off, float* pi_hat, float* y_hat, float* s_hin,
+                  float* s_r, float* s_z, float* s_n, float* s_hn, long M, hipStream_t stream);
+/* VJP over K updates (M = K*T*R columns): gate cotangents DG [4][256][M] (dr, dz, d(W_hn h + b_hn), dn),
+ * relu(h_out) RH [256][M], head cotangents DH [9][M], input cotangents dX3/dX4 [K][T][R] */
 int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_stride_k, const float* bwdA,
                   const float* eta, const int* off, const float* y_hat, const float* d_pi_hat, const float* d_y_hat,
                   const float* s_hin, const float* s_r, const float* s_z, const float* s_n, const float* s_hn, long M,
@@ -194,9 +198,9 @@ int toued_gru_pack_fwd_multi(const float* eta, long eta_stride, int n, const int
                              hipStream_t stream);
 /* forward with per-candidate parameters: rows [c*rows_per_cand, (c+1)*rows_per_cand) use candidate c
  * (fwdA from toued_gru_pack_fwd_multi); nothing is saved for a backward */
-int toued_gru_fwd_multi(int R, int T, int W, int F, int rows_per_cand, const float* X, long xs_f, const uint8_t* done,
-                        const float* fwdA, const float* eta, long eta_stride, const int* off, float* pi_hat,
-                        float* y_hat, hipStream_t stream);
+int toued_gru_fwd_multi(int R, int T, int W, int F, int rows_per_cand, const float* X, long xs_f, long xs_col,
+                        const uint8_t* done, const float* fwdA, const float* eta, long eta_stride, const int* off,
+                        float* pi_hat, float* y_hat, hipStream_t stream);
 
 /* ---- OpenES (evosax 0.1.4 as configured by models/optim.py:21-34; meta/train.py:133-227) ---- */
 /* ask for z rows [row_lo, row_lo+n_rows) of normal(key, (half_pop, nd)): x[2i] = mean + sigma z_i,

@@ -25,3 +25,23 @@ def test_host_only_entry_points():
     L = _lib.lib()
     assert L.toued_abi_version() == 1
     assert L.toued_mode_program_bytes() == modes.PROGRAM_WORDS * 4
+
+
+def test_ctypes_signatures_match_header():
+    """Every entry point's ctypes argument list has the header's arity and kinds (int / long / float /
+    pointer), so a signature change in include/toued.h cannot silently desynchronise the binding."""
+    import ctypes
+    from toued import _lib
+    text = re.sub(r"/\*.*?\*/", "", (ROOT / "include" / "toued.h").read_text(), flags=re.S)
+    kinds = {ctypes.c_int: "int", ctypes.c_uint32: "int", ctypes.c_long: "long", ctypes.c_float: "float",
+             ctypes.c_void_p: "ptr"}
+    for m in re.finditer(r"\b(?:int|size_t|const char\*)\s+(toued_\w+)\s*\(([^)]*)\)\s*;", text):
+        name, args = m.group(1), m.group(2).strip()
+        params = [] if args in ("", "void") else [a.strip() for a in args.split(",")]
+        sig = _lib._SIGS[name]
+        assert len(sig) == len(params), (name, len(params), len(sig))
+        for a, t in zip(params, sig):
+            want = ("ptr" if "*" in a or a.startswith("hipStream_t") else "long" if a.startswith("long")
+                    else "float" if a.startswith("float") else "int" if a.split()[0] in ("int", "uint32_t") else None)
+            if want is not None and t in kinds:
+                assert kinds[t] == want, (name, a, kinds[t])

@@ -3,7 +3,8 @@ box's GPU (gloo collectives staged through the host) must reproduce a single-pro
 
   * levels / agent steps per agent: bit-exact (every rank derives all N keys and keeps its slice)
   * LPG parameters after the meta-gradient all-reduce + Adam: within 1e-6 (float32 summation
-    order of the gradient differs between one and two partial sums)
+    order of the gradient differs between one and two partial sums); agent actors after the second
+    step (trained under those parameters, lr 40): within 1e-5 absolute
   * alg_regret buffer (replicated, updated from all-gathered scores): flags bit-exact, scores
     within 1e-6 — the regret of an agent depends only on its own key, level and actor
   * OpenES mean after the tell all-reduce: within 1e-6
@@ -59,7 +60,7 @@ def test_two_ranks_match_one(tmp_path, case):
     two = _run(2, tmp_path / "b", flags)
     for k in ("levels", "step"):
         assert np.array_equal(np.concatenate([t[k] for t in two]), one[k]), k
-    np.testing.assert_allclose(np.concatenate([t["theta"] for t in two]), one["theta"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(np.concatenate([t["theta"] for t in two]), one["theta"], rtol=1e-4, atol=1e-5)
     key = "mean" if case == "es" else "eta"
     for t in two:
         np.testing.assert_allclose(t[key], one[key], rtol=0, atol=1e-6)

@@ -79,7 +79,7 @@ def test_gru_fwd_multi_per_candidate():
     X[1] = torch.from_numpy(done.transpose(1, 0, 2).reshape(T, R).astype(np.float32)).cuda()
     pi_hat = torch.zeros(T, R, device="cuda")
     y_hat = torch.zeros(T, 8, R, device="cuda")
-    _lib.call("toued_gru_fwd_multi", R, T, W, F, W, _lib.ptr(X), T * R, _lib.ptr(torch.from_numpy(done).cuda()),
+    _lib.call("toued_gru_fwd_multi", R, T, W, F, W, _lib.ptr(X), T * R, 1, _lib.ptr(torch.from_numpy(done).cuda()),
               _lib.ptr(fwdA), _lib.ptr(etas), lay.size, lay.c_offsets, _lib.ptr(pi_hat), _lib.ptr(y_hat),
               _lib.stream_ptr())
     torch.cuda.synchronize()

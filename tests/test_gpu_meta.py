@@ -135,12 +135,14 @@ def test_gru_forward_matches_oracle():
     d = torch.tensor(done[0].transpose(0, 2, 1).reshape(R, T).astype(bool))
     h = torch.zeros(R, 256, dtype=torch.float64)
     outs = [None] * T
+    saved = {"hin": [None] * T, "r": [None] * T, "z": [None] * T, "n": [None] * T}
     for t in reversed(range(T)):
         h = torch.where(d[:, t, None], torch.zeros_like(h), h)
         xt = x[:, t]
         rg = torch.sigmoid(xt @ P["ir_w"] + P["ir_b"] + h @ P["hr_w"])
         zg = torch.sigmoid(xt @ P["iz_w"] + P["iz_b"] + h @ P["hz_w"])
         ng = torch.tanh(xt @ P["in_w"] + P["in_b"] + rg * (h @ P["hn_w"] + P["hn_b"]))
+        saved["hin"][t], saved["r"][t], saved["z"][t], saved["n"][t] = h, rg, zg, ng
         h = (1 - zg) * ng + zg * h
         outs[t] = h
     hs = torch.relu(torch.stack(outs, 1))
@@ -148,3 +150,78 @@ def test_gru_forward_matches_oracle():
     y_ref = torch.softmax(hs @ P["y_w"] + P["y_b"], -1)
     np.testing.assert_allclose(pi_hat[0].cpu().numpy().T, pi_ref.numpy(), atol=1e-4, rtol=1e-4)
     np.testing.assert_allclose(y_hat[0].cpu().numpy().transpose(2, 0, 1), y_ref.numpy(), atol=1e-5, rtol=1e-4)
+    # the saves the backward reads: [unit][column t*R + r]
+    def tr(a):
+        return a.reshape(256, T, R).transpose(1, 2, 0)
+    for name, arr in (("hin", tr(gru.A[:256].cpu().numpy())), ("r", tr(gru.S[0].cpu().numpy())),
+                      ("z", tr(gru.S[1].cpu().numpy())), ("n", tr(gru.S[2].cpu().numpy()))):
+        ref = np.stack([saved[name][t].numpy() for t in range(T)])
+        np.testing.assert_allclose(arr, ref, atol=1e-4, rtol=1e-4, err_msg=name)
+
+
+def test_gru_backward_matches_autograd():
+    """LPG GRU VJP (toued_gru_bwd + the weight-gradient GEMMs over the saved m-major operands) vs float64
+    torch autograd of the same GRU + heads: every GRU / head parameter gradient and the input cotangents
+    dX3, dX4 within 1e-4 relative L2."""
+    from toued.lpg import LPGGRU, LPGLayout, init_lpg_params
+    N, W, T, K, F = 2, 64, 6, 2, 5
+    R = N * W
+    lay = LPGLayout(F)
+    eta = init_lpg_params(5, F)
+    eta += torch.randn_like(eta) * 0.05
+    gru = LPGGRU(lay, R, T, K, W, "cuda")
+    gru.pack(eta)
+    rs = np.random.RandomState(1)
+    xs = rs.randn(F, K, T, R).astype(np.float32)
+    gru.X.copy_(torch.from_numpy(xs))
+    X = gru.X
+    done = (rs.rand(K, N, T, W) < 0.15).astype(np.uint8)
+    done_t = torch.from_numpy(done).cuda()
+    pi_hat = torch.zeros(K, T, R, device="cuda")
+    y_hat = torch.zeros(K, T, 8, R, device="cuda")
+    for k in range(K):
+        gru.forward(k, X, done_t[k], eta, pi_hat, y_hat)
+    d_pi = torch.from_numpy(rs.randn(K, T, R).astype(np.float32)).cuda()
+    d_y = torch.from_numpy(rs.randn(K, T, 8, R).astype(np.float32)).cuda()
+    grad = torch.zeros(lay.size, device="cuda")
+    gru.backward(done_t, eta, y_hat, d_pi, d_y, X, grad)
+    torch.cuda.synchronize()
+    # float64 autograd oracle
+    flat = torch.tensor(eta.cpu().numpy(), dtype=torch.float64, requires_grad=True)
+    P = olpg.unflatten(flat, F)
+    x = torch.tensor(xs, dtype=torch.float64, requires_grad=True)       # [F, K, T, R]
+    loss = 0.0
+    for k in range(K):
+        xk = x[:, k].permute(2, 1, 0)                                     # [R, T, F]
+        d = torch.tensor(done[k].transpose(0, 2, 1).reshape(R, T).astype(bool))
+        h = torch.zeros(R, 256, dtype=torch.float64)
+        outs = [None] * T
+        for t in reversed(range(T)):
+            h = torch.where(d[:, t, None], torch.zeros_like(h), h)
+            xt = xk[:, t]
+            rg = torch.sigmoid(xt @ P["ir_w"] + P["ir_b"] + h @ P["hr_w"])
+            zg = torch.sigmoid(xt @ P["iz_w"] + P["iz_b"] + h @ P["hz_w"])
+            ng = torch.tanh(xt @ P["in_w"] + P["in_b"] + rg * (h @ P["hn_w"] + P["hn_b"]))
+            h = (1 - zg) * ng + zg * h
+            outs[t] = h
+        hs = torch.relu(torch.stack(outs, 1))                              # [R, T, 256]
+        pi_ref = (hs @ P["pi_w"] + P["pi_b"])[..., 0]                      # [R, T]
+        y_ref = torch.softmax(hs @ P["y_w"] + P["y_b"], -1)                # [R, T, 8]
+        dpi = torch.tensor(d_pi[k].cpu().numpy().T, dtype=torch.float64)
+        dy = torch.tensor(d_y[k].cpu().numpy().transpose(2, 0, 1), dtype=torch.float64)
+        loss = loss + (pi_ref * dpi).sum() + (y_ref * dy).sum()
+    loss.backward()
+    g_ref = flat.grad.numpy()
+    g = grad.cpu().numpy().astype(np.float64)
+    errs = {}
+    for name in ("hr_w", "hz_w", "hn_w", "ir_w", "iz_w", "in_w", "ir_b", "iz_b", "in_b", "hn_b", "pi_w", "pi_b",
+                 "y_w", "y_b"):
+        o = lay.offsets[name]
+        sl = slice(o, o + int(np.prod(lay.shapes[name])))
+        errs[name] = np.linalg.norm(g[sl] - g_ref[sl]) / max(np.linalg.norm(g_ref[sl]), 1e-12)
+    gx = x.grad.numpy()
+    for f, dX in ((3, gru.dX3), (4, gru.dX4)):
+        got = dX.cpu().numpy()
+        errs[f"dX{f}"] = np.linalg.norm(got - gx[f]) / np.linalg.norm(gx[f])
+    bad = {k: v for k, v in errs.items() if not v < 1e-4}
+    assert not bad, errs

@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(256) k_lpg_inputs(int N, int W, int T, int D, 
                                                     const float* __restrict__ e1w, const float* __restrict__ e1b,
                                                     const float* __restrict__ e2w, const float* __restrict__ e2b,
                                                     const int* __restrict__ step, const int* __restrict__ levels,
-                                                    float* __restrict__ X, long xs_f, long eta_stride) {
+                                                    float* __restrict__ X, long xs_f, long xs_col, long eta_stride) {
   const long s = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= (long)N * T * W) return;
   const SampleRef q = load_sample(s, T, W, tidx, ttime, tact, trew, tdone, UNIF);
@@ -187,7 +187,7 @@ __global__ void __launch_bounds__(256) k_lpg_inputs(int N, int W, int T, int D, 
     e1 += fmaxf(h1, 0.0f) * e2w[h];
   }
   if (q.done) e1 = 0.0f;
-  const size_t o = (size_t)q.t * R + q.r;
+  const size_t o = ((size_t)q.t * R + q.r) * xs_col;
   X[0 * xs_f + o] = q.rew;
   X[1 * xs_f + o] = q.done ? 1.0f : 0.0f;
   X[2 * xs_f + o] = pa;
@@ -728,13 +728,13 @@ int toued_meta_keys(const uint32_t* agent_keys, int N, int K, uint32_t* roll_key
 int toued_lpg_inputs(int N, int W, int T, int D, int F, const float* theta, const float* phi, const int* tidx,
                      const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone, const float* eta_e1w,
                      const float* eta_e1b, const float* eta_e2w, const float* eta_e2b, const int* step,
-                     const int* levels, float* X, long xs_f, long eta_stride, hipStream_t stream) {
+                     const int* levels, float* X, long xs_f, long xs_col, long eta_stride, hipStream_t stream) {
   TOUED_REQUIRE(F == 5 || F == 7, "toued_lpg_inputs: F=%d", F);
   const long n = (long)N * T * W;
   if (n == 0) return 0;
 #define L_(U, FF) hipLaunchKernelGGL((k_lpg_inputs<U, FF>), dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, theta, \
                                      phi, tidx, ttime, tact, trew, tdone, eta_e1w, eta_e1b, eta_e2w, eta_e2b, step,   \
-                                     levels, X, xs_f, eta_stride)
+                                     levels, X, xs_f, xs_col, eta_stride)
   if (W % 64 == 0) { if (F == 5) L_(true, 5); else L_(true, 7); }
   else { if (F == 5) L_(false, 5); else L_(false, 7); }
 #undef L_

@@ -10,7 +10,11 @@
 // gate maths happens in the accumulator registers (lane = batch row, registers
 // = 16 gate columns; the r, z, n tiles of a unit line up lane-for-lane).
 // Each wave owns 64 units = 2 unit tiles x {r, z, nh, ni} accumulators.
-// Saved for the backward: h_in (masked carry), r, z, n, W_hn h + b_hn.
+// Saved for the backward: h_in (masked carry), r, z, n, W_hn h + b_hn, row-major [unit][M] (the
+// weight-gradient GEMM layout).  The backward loads them 16 B per lane (4 consecutive rows of one unit,
+// full 128-byte lines per wave instruction) and transposes lane quad (4 rows) x register quad (4 units)
+// blocks in registers (DPP): 4x fewer load instructions than per-dword access.  (Transposed 16-byte
+// stores measured slower at this register budget; the cotangent stores stay per dword.)
 //
 // Backward: one workgroup per (k, 32 rows), t ascending; three LDS phases
 // (dr_pre, dz_pre, d(W_hn h + b_hn)) each contracted with W_h^T on MFMA give
@@ -58,6 +62,40 @@ TOUED_DEV void st_u(__amdgpu_buffer_rsrc_t r, unsigned vbyte, unsigned soff, flo
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)vbyte, (int)soff, 0);
 }
 TOUED_DEV int qunit(int q) { return (q & 3) + 8 * (q >> 2); }
+
+// 16-byte raw buffer ops: the four consecutive units (q & 3) of a register quad in the m-major layout
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+TOUED_DEV void ld4(__amdgpu_buffer_rsrc_t r, unsigned vbyte, unsigned soff, float* v) {
+  const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)vbyte, (int)soff, 0);
+  v[0] = __uint_as_float(x.x); v[1] = __uint_as_float(x.y); v[2] = __uint_as_float(x.z); v[3] = __uint_as_float(x.w);
+}
+// 4x4 transpose between a lane quad (four consecutive rows: lanes 4i..4i+3) and a register quad (four
+// consecutive units): before, lane row j holds units u0..u0+3; after, lane u0+i's data (for rows j0..j0+3)
+// sits in lane j0+i.  Two DPP quad_perm exchange stages; the transpose is its own inverse.
+TOUED_DEV float dpp_swap(float v, int ctrl_sel) {
+  const int x = __float_as_int(v);
+  return __int_as_float(ctrl_sel == 2 ? __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false)     // [2,3,0,1]
+                                      : __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false));   // [1,0,3,2]
+}
+TOUED_DEV void quad_transpose(float* a, int lane) {
+  const bool b1 = (lane & 2) != 0, b0 = (lane & 1) != 0;
+  float r0 = dpp_swap(b1 ? a[0] : a[2], 2), r1 = dpp_swap(b1 ? a[1] : a[3], 2);
+  if (b1) { a[0] = r0; a[1] = r1; } else { a[2] = r0; a[3] = r1; }
+  r0 = dpp_swap(b0 ? a[0] : a[1], 1);
+  r1 = dpp_swap(b0 ? a[2] : a[3], 1);
+  if (b0) { a[0] = r0; a[2] = r1; } else { a[1] = r0; a[3] = r1; }
+}
+
+// A VALU write to the data VGPRs of a preceding >8-byte VMEM store needs wait states that this compiler
+// does not always insert for buffer-store builtins on gfx950 (observed: the first dword of some 16-byte
+// stores replaced by the next value written to its register).  The s_nop after the store provides them
+// and, being volatile asm, keeps the scheduler from moving a write of those registers above it.
+TOUED_DEV void st4(__amdgpu_buffer_rsrc_t r, unsigned vbyte, unsigned soff, const float* v) {
+  u32x4 x;
+  x.x = __float_as_uint(v[0]); x.y = __float_as_uint(v[1]); x.z = __float_as_uint(v[2]); x.w = __float_as_uint(v[3]);
+  __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)vbyte, (int)soff, 0);
+  asm volatile("s_nop 1" ::: "memory");
+}
 
 TOUED_DEV float sigm(float x) { return 1.0f / (1.0f + __expf(-x)); }
 TOUED_DEV float tanh_f(float x) {
@@ -117,7 +155,7 @@ __global__ void k_pack_bwd(const float* __restrict__ eta, EtaOff o, float4* __re
 // ------------------------------------------------------------------ forward
 struct FwdArgs {
   int R, T, W, F;
-  const float* X; long xs_f;           // X[f*xs_f + t*R + r]
+  const float* X; long xs_f, xs_col;   // X[f*xs_f + (t*R + r)*xs_col]
   const uint8_t* done;                 // [N][T][W]
   const float4* A;                     // packed fwd fragments
   const float* eta; EtaOff o;
@@ -152,7 +190,7 @@ __global__ void __launch_bounds__(512, 4) k_gru_fwd(FwdArgs p) {
   if (tid < RB) {
     const int t = T - 1;
     for (int f = 0; f < NAUG; ++f)
-      hT[(HU + f) * LDH + tid] = f < F ? p.X[f * p.xs_f + (size_t)t * R + r0 + tid] : (f == F ? 1.0f : 0.0f);
+      hT[(HU + f) * LDH + tid] = f < F ? p.X[f * p.xs_f + ((size_t)t * R + r0 + tid) * p.xs_col] : (f == F ? 1.0f : 0.0f);
   }
   __syncthreads();
   const float bpi = eta[p.o.pi_b];
@@ -245,7 +283,8 @@ __global__ void __launch_bounds__(512, 4) k_gru_fwd(FwdArgs p) {
       hTw[qunit(q) * LDH] = dn ? 0.0f : hnew[q];
     }
     if (t >= 1 && tid < RB) {
-      for (int f = 0; f < F; ++f) hT[(HU + f) * LDH + tid] = p.X[f * p.xs_f + (size_t)(t - 1) * R + r0 + tid];
+      for (int f = 0; f < F; ++f)
+        hT[(HU + f) * LDH + tid] = p.X[f * p.xs_f + ((size_t)(t - 1) * R + r0 + tid) * p.xs_col];
     }
     for (int i = tid; i < 9 * RB; i += 512) {
       const int oo = i / RB, c = i - oo * RB;
@@ -284,26 +323,39 @@ struct BwdArgs {
   float* dX3; float* dX4;   // [K][T][R]
 };
 
-__global__ void __launch_bounds__(512, 4) k_gru_bwd(BwdArgs p) {
-  __shared__ float dgT[HU * LDH];
+// NT row tiles of 32 rows per workgroup.  NT = 2: one workgroup per CU (150 KB LDS, 256 VGPRs), every
+// packed W_h^T fragment feeds 8 MFMAs instead of 4 (half the L2 fragment stream per FLOP).
+template <int NT>
+__global__ void __launch_bounds__(512, NT == 1 ? 4 : 1) k_gru_bwd(BwdArgs p) {
+  constexpr int RBT = RB * NT;          // rows per workgroup
+  constexpr int LDT = RBT + 1;          // padded LDS row (k-major [unit][row])
+  __shared__ float dgT[2 * HU * LDT];   // [dr | dz], then dhn in slot 0
   __shared__ float wi34[2 * 3 * HU];
-  __shared__ float hv[9 * RB];
-  __shared__ float dxp[NGRP * 2 * RB];
+  __shared__ float hv[9 * RBT];
+  __shared__ float dxp[NGRP * 2 * RBT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hi = lane >> 5, col = lane & 31;
-  const int nb = p.R / RB;
+  const int nb = p.R / RBT;
   const int k = blockIdx.x / nb;
-  const int r0 = (blockIdx.x - k * nb) * RB, row = r0 + col;
+  const int r0 = (blockIdx.x - k * nb) * RBT;
   const int R = p.R, T = p.T, W = p.W;
-  const int a = r0 / W, w = row - a * W;
+  int a_[NT], w_[NT];
+#pragma unroll
+  for (int h = 0; h < NT; ++h) {
+    const int row = r0 + RB * h + col;
+    a_[h] = (r0 + RB * h) / W;
+    w_[h] = row - a_[h] * W;
+  }
   // W_i rows for the embedding inputs (f = 3: pyt, f = 4: pyt1), per gate kind r, z, n
   for (int i = tid; i < 2 * 3 * HU; i += 512) {
     const int f = 3 + i / (3 * HU), g = (i / HU) % 3, u = i % HU;
     const int base = g == 0 ? p.o.ir_w : g == 1 ? p.o.iz_w : p.o.in_w;
     wi34[i] = p.eta[base + f * HU + u];
   }
-  float dh[16];
+  float dh[NT][16];
 #pragma unroll
-  for (int q = 0; q < 16; ++q) dh[q] = 0.0f;
+  for (int h = 0; h < NT; ++h)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dh[h][q] = 0.0f;
   float wA[5];    // A fragments of W_heads^T for this wave's unit tile: A[i=l&31][k=2kk+(l>>5)]
 #pragma unroll
   for (int kk = 0; kk < 5; ++kk) {
@@ -319,8 +371,8 @@ __global__ void __launch_bounds__(512, 4) k_gru_bwd(BwdArgs p) {
   __syncthreads();
   for (int t = 0; t < T; ++t) {
     const long ctr = ((long)k * T + t) * R;          // column base in [.][K*T*R]
-    if (tid < RB) {
-      const long o = ctr + r0 + tid;
+    if (tid < RBT) {
+      const long o = ctr + r0 + tid;       // global column
       float yh[8], dy[8], s = 0.0f;
       for (int j = 0; j < 8; ++j) {
         yh[j] = p.y_hat[((long)k * T * 8 + (long)t * 8 + j) * R + r0 + tid];
@@ -332,78 +384,103 @@ __global__ void __launch_bounds__(512, 4) k_gru_bwd(BwdArgs p) {
       p.DH[o] = dpi;
       for (int j = 0; j < 8; ++j) {
         const float v = yh[j] * (dy[j] - s);
-        hv[(j + 1) * RB + tid] = v;
+        hv[(j + 1) * RBT + tid] = v;
         p.DH[(long)(j + 1) * p.M + o] = v;
       }
     }
     __syncthreads();
-    // head VJP W_heads . hv on MFMA: A[i = unit][k = head output o] (constant per lane, wA),
-    // B[k = o][j = row] from hv; the result has the accumulator layout (lane = row, reg = unit).
-    floatx16 hacc;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) hacc[q] = 0.0f;
-#pragma unroll
-    for (int kk = 0; kk < 5; ++kk) {
-      const int o = 2 * kk + hi;
-      hacc = mfma32(wA[kk], o < 9 ? hv[o * RB + col] : 0.0f, hacc);
-    }
-    const unsigned vbyte = (unsigned)(((long)(32 * wave + 4 * hi) * p.M + row) * 4);
-    float dx3 = 0.0f, dx4 = 0.0f;
+    float dhn_r[NT][16];
     const float* wil = wi34 + 32 * wave + 4 * hi;
-    // Saved activations in batches of QB units, every load of a batch issued before the batch's
-    // stores: raw buffer stores may alias later loads, so the compiler keeps program order and a
-    // load-compute-store per unit would cost one memory round trip per unit.
-    constexpr int QB = 4;
 #pragma unroll
-    for (int qb = 0; qb < 16; qb += QB) {
-      float v_hin[QB], v_r[QB], v_z[QB], v_n[QB], v_hn[QB];
+    for (int h = 0; h < NT; ++h) {
+      // head VJP W_heads . hv on MFMA: A[i = unit][k = head output o] (constant per lane, wA),
+      // B[k = o][j = row] from hv; the result has the accumulator layout (lane = row, reg = unit).
+      floatx16 hacc;
 #pragma unroll
-      for (int j = 0; j < QB; ++j) {
-        const unsigned so = (unsigned)(((long)qunit(qb + j) * p.M + ctr) * 4);
-        v_hin[j] = ld_u(rs_hin, vbyte, so);
-        v_r[j] = ld_u(rs_r, vbyte, so);
-        v_z[j] = ld_u(rs_z, vbyte, so);
-        v_n[j] = ld_u(rs_n, vbyte, so);
-        v_hn[j] = ld_u(rs_hn, vbyte, so);
+      for (int q = 0; q < 16; ++q) hacc[q] = 0.0f;
+#pragma unroll
+      for (int kk = 0; kk < 5; ++kk) {
+        const int o = 2 * kk + hi;
+        hacc = mfma32(wA[kk], o < 9 ? hv[o * RBT + RB * h + col] : 0.0f, hacc);
       }
+      // transposed 16-byte accesses: lane col moves unit (32w + 4hi + 8g4 + (col & 3)) for the four rows
+      // r0 + RB*h + (col & 28) .. +3 of this step's columns
+      const unsigned vq = (unsigned)((((long)(32 * wave + 4 * hi + (col & 3))) * p.M + r0 + RB * h + (col & 28)) * 4);
+      float dx3 = 0.0f, dx4 = 0.0f;
+      // one unit quad (four consecutive units) per iteration: five 16-byte loads + transposes, the gate
+      // maths, five dword stores per unit (+ two LDS writes per unit)
 #pragma unroll
-      for (int j = 0; j < QB; ++j) {
-      const int q = qb + j;
-      const unsigned so = (unsigned)(((long)qunit(q) * p.M + ctr) * 4);
-      const float hin = v_hin[j], rg = v_r[j], zg = v_z[j], ng = v_n[j], hn = v_hn[j];
-      const float hout = (1.0f - zg) * ng + zg * hin;
-      const float d = dh[q] + (hout > 0.0f ? hacc[q] : 0.0f);
-      st_u(rs_rh, vbyte, so, fmaxf(hout, 0.0f));
-      const float dn_ = d * (1.0f - zg);
-      const float dz = d * (hin - ng);
-      const float dnp = dn_ * (1.0f - ng * ng);
-      const float dhn = dnp * rg;
-      const float drp = dnp * hn * rg * (1.0f - rg);
-      const float dzp = dz * zg * (1.0f - zg);
-      dh[q] = d * zg;   // direct path; the W_h^T contraction is added below
-      st_u(rs_dg[0], vbyte, so, drp);
-      st_u(rs_dg[1], vbyte, so, dzp);
-      st_u(rs_dg[2], vbyte, so, dhn);
-      st_u(rs_dg[3], vbyte, so, dnp);
-      const int qu = qunit(q);
-      dx3 += drp * wil[0 * HU + qu] + dzp * wil[1 * HU + qu] + dnp * wil[2 * HU + qu];
-      dx4 += drp * wil[3 * HU + qu] + dzp * wil[4 * HU + qu] + dnp * wil[5 * HU + qu];
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const unsigned so = (unsigned)(((long)8 * g4 * p.M + ctr) * 4);
+        float v_hin[4], v_r[4], v_z[4], v_n[4], v_hn[4];
+        ld4(rs_hin, vq, so, v_hin);
+        ld4(rs_r, vq, so, v_r);
+        ld4(rs_z, vq, so, v_z);
+        ld4(rs_n, vq, so, v_n);
+        ld4(rs_hn, vq, so, v_hn);
+        quad_transpose(v_hin, lane);
+        quad_transpose(v_r, lane);
+        quad_transpose(v_z, lane);
+        quad_transpose(v_n, lane);
+        quad_transpose(v_hn, lane);
+        float* o_rh = v_hin; float* o_dr = v_r; float* o_dz = v_z; float* o_dhn = v_n; float* o_dn = v_hn;  // reused in place
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int q = 4 * g4 + j;
+          const float hin = v_hin[j], rg = v_r[j], zg = v_z[j], ng = v_n[j], hn = v_hn[j];
+          const float hout = (1.0f - zg) * ng + zg * hin;
+          const float d = dh[h][q] + (hout > 0.0f ? hacc[q] : 0.0f);
+          const float dn_ = d * (1.0f - zg);
+          const float dz = d * (hin - ng);
+          const float dnp = dn_ * (1.0f - ng * ng);
+          const float dhn = dnp * rg;
+          const float drp = dnp * hn * rg * (1.0f - rg);
+          const float dzp = dz * zg * (1.0f - zg);
+          dh[h][q] = d * zg;   // direct path; the W_h^T contraction is added below
+          const int lo = (32 * wave + 4 * hi + qunit(q)) * LDT + RB * h + col;   // B operands straight to LDS
+          dgT[lo] = drp;
+          dgT[HU * LDT + lo] = dzp;
+          dhn_r[h][q] = dhn;
+          o_rh[j] = fmaxf(hout, 0.0f); o_dr[j] = drp; o_dz[j] = dzp; o_dhn[j] = dhn; o_dn[j] = dnp;
+          const int qu = qunit(q);
+          dx3 += drp * wil[0 * HU + qu] + dzp * wil[1 * HU + qu] + dnp * wil[2 * HU + qu];
+          dx4 += drp * wil[3 * HU + qu] + dzp * wil[4 * HU + qu] + dnp * wil[5 * HU + qu];
+        }
+        {
+          const unsigned vb = (unsigned)(((long)(32 * wave + 4 * hi) * p.M + r0 + RB * h + col) * 4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const unsigned so1 = (unsigned)(((long)qunit(4 * g4 + j) * p.M + ctr) * 4);
+            st_u(rs_rh, vb, so1, o_rh[j]);
+            st_u(rs_dg[0], vb, so1, o_dr[j]);
+            st_u(rs_dg[1], vb, so1, o_dz[j]);
+            st_u(rs_dg[2], vb, so1, o_dhn[j]);
+            st_u(rs_dg[3], vb, so1, o_dn[j]);
+          }
+        }
       }
+      dxp[((2 * wave + hi) * 2 + 0) * RBT + RB * h + col] = dx3;
+      dxp[((2 * wave + hi) * 2 + 1) * RBT + RB * h + col] = dx4;
     }
-    dxp[((2 * wave + hi) * 2 + 0) * RB + col] = dx3;
-    dxp[((2 * wave + hi) * 2 + 1) * RB + col] = dx4;
-    floatx16 acc;
+    floatx16 acc[NT];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+    for (int h = 0; h < NT; ++h)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[h][q] = 0.0f;
+    // dh_prev = dr . W_hr^T + dz . W_hz^T (both in LDS) then + dhn . W_hn^T (dhn to LDS slot 0)
 #pragma unroll 1
     for (int g = 0; g < 3; ++g) {
-      float* dgl = dgT + (32 * wave + 4 * hi) * LDH + col;
+      if (g == 2) {
+        __syncthreads();     // all waves done reading slot 0 (dr)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        dgl[qunit(q) * LDH] = ld_u(g == 0 ? rs_dg[0] : g == 1 ? rs_dg[1] : rs_dg[2], vbyte,
-                                   (unsigned)(((long)qunit(q) * p.M + ctr) * 4));   // this lane's own store
+        for (int h = 0; h < NT; ++h) {
+          float* dgl = dgT + (32 * wave + 4 * hi) * LDT + RB * h + col;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) dgl[qunit(q) * LDT] = dhn_r[h][q];
+        }
       }
-      __syncthreads();
+      if (g != 1) __syncthreads();
+      const float* dgs = dgT + (g == 1 ? HU * LDT : 0);
       float4 an = Ab[((wave * 3 + g) * 32 + 0) * 64];
 #pragma unroll 2
       for (int kq = 0; kq < 32; ++kq) {
@@ -411,26 +488,33 @@ __global__ void __launch_bounds__(512, 4) k_gru_bwd(BwdArgs p) {
         if (kq + 1 < 32) an = Ab[((wave * 3 + g) * 32 + kq + 1) * 64];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float b = dgT[(2 * (4 * kq + e) + hi) * LDH + col];
           const float x = e == 0 ? av.x : e == 1 ? av.y : e == 2 ? av.z : av.w;
-          acc = mfma32(x, b, acc);
+#pragma unroll
+          for (int h = 0; h < NT; ++h) {
+            const float b = dgs[(2 * (4 * kq + e) + hi) * LDT + RB * h + col];
+            acc[h] = mfma32(x, b, acc[h]);
+          }
         }
       }
-      __syncthreads();
     }
-    if (tid < RB) {
+    __syncthreads();
+    if (tid < RBT) {
       float s3 = 0.0f, s4 = 0.0f;
-      for (int gq = 0; gq < NGRP; ++gq) { s3 += dxp[(gq * 2 + 0) * RB + tid]; s4 += dxp[(gq * 2 + 1) * RB + tid]; }
+      for (int gq = 0; gq < NGRP; ++gq) { s3 += dxp[(gq * 2 + 0) * RBT + tid]; s4 += dxp[(gq * 2 + 1) * RBT + tid]; }
       p.dX3[ctr + r0 + tid] = s3;
       p.dX4[ctr + r0 + tid] = s4;
     }
     // carry to h_out(t+1): h_in(t) = where(d_t, 0, h_out(t+1))
-    const bool dn = done[((size_t)a * T + t) * W + w] != 0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) dh[q] = dn ? 0.0f : dh[q] + acc[q];
+    for (int h = 0; h < NT; ++h) {
+      const bool dn = done[((size_t)a_[h] * T + t) * W + w_[h]] != 0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) dh[h][q] = dn ? 0.0f : dh[h][q] + acc[h][q];
+    }
     __syncthreads();
   }
 }
+
 
 }  // namespace
 
@@ -451,12 +535,12 @@ int toued_gru_pack(const float* eta, const int* off, int F, float* fwdA, float* 
 
 size_t toued_gru_packed_floats(int which) { return which == 0 ? (size_t)NTILE_F * KQF * 64 * 4 : (size_t)8 * 3 * 32 * 64 * 4; }
 
-static int gru_fwd_launch(int R, int T, int W, int F, const float* X, long xs_f, const uint8_t* done,
+static int gru_fwd_launch(int R, int T, int W, int F, const float* X, long xs_f, long xs_col, const uint8_t* done,
                           const float* fwdA, const float* eta, const int* off, float* pi_hat, float* y_hat,
                           float* s_hin, float* s_r, float* s_z, float* s_n, float* s_hn, long M, int save, int rpc,
                           long eta_stride, hipStream_t stream) {
   FwdArgs p;
-  p.R = R; p.T = T; p.W = W; p.F = F; p.X = X; p.xs_f = xs_f; p.done = done;
+  p.R = R; p.T = T; p.W = W; p.F = F; p.X = X; p.xs_f = xs_f; p.xs_col = xs_col; p.done = done;
   p.A = reinterpret_cast<const float4*>(fwdA); p.eta = eta;
   memcpy(&p.o, off, sizeof(EtaOff));
   p.pi_hat = pi_hat; p.y_hat = y_hat; p.s_hin = s_hin; p.s_r = s_r; p.s_z = s_z; p.s_n = s_n; p.s_hn = s_hn; p.M = M;
@@ -469,16 +553,16 @@ static int gru_fwd_launch(int R, int T, int W, int F, const float* X, long xs_f,
   return 0;
 }
 
-int toued_gru_fwd(int R, int T, int W, int F, const float* X, long xs_f, const uint8_t* done, const float* fwdA,
-                  const float* eta, const int* off, float* pi_hat, float* y_hat, float* s_hin, float* s_r, float* s_z,
-                  float* s_n, float* s_hn, long M, hipStream_t stream) {
+int toued_gru_fwd(int R, int T, int W, int F, const float* X, long xs_f, long xs_col, const uint8_t* done,
+                  const float* fwdA, const float* eta, const int* off, float* pi_hat, float* y_hat, float* s_hin,
+                  float* s_r, float* s_z, float* s_n, float* s_hn, long M, hipStream_t stream) {
   TOUED_REQUIRE(R % RB == 0 && W % RB == 0, "toued_gru_fwd: rows R=%d and workers W=%d must be multiples of 32", R, W);
   TOUED_REQUIRE(F >= 1 && F <= 7 && T >= 1, "toued_gru_fwd: F=%d T=%d", F, T);
   TOUED_REQUIRE((double)M * 264.0 * 4.0 < 4294967295.0, "toued_gru_fwd: M=%ld columns exceed the 4 GiB buffer range "
                 "(use --num_mini_batches to split the agent batch)", M);
   TOUED_REQUIRE(s_hin && s_r && s_z && s_n && s_hn, "toued_gru_fwd: saved-activation buffers required");
-  return gru_fwd_launch(R, T, W, F, X, xs_f, done, fwdA, eta, off, pi_hat, y_hat, s_hin, s_r, s_z, s_n, s_hn, M, 1, 0,
-                        0, stream);
+  return gru_fwd_launch(R, T, W, F, X, xs_f, xs_col, done, fwdA, eta, off, pi_hat, y_hat, s_hin, s_r, s_z, s_n, s_hn,
+                        M, 1, 0, 0, stream);
 }
 
 int toued_gru_pack_fwd_multi(const float* eta, long eta_stride, int n, const int* off, int F, float* fwdA,
@@ -494,16 +578,16 @@ int toued_gru_pack_fwd_multi(const float* eta, long eta_stride, int n, const int
   return 0;
 }
 
-int toued_gru_fwd_multi(int R, int T, int W, int F, int rows_per_cand, const float* X, long xs_f, const uint8_t* done,
-                        const float* fwdA, const float* eta, long eta_stride, const int* off, float* pi_hat,
-                        float* y_hat, hipStream_t stream) {
+int toued_gru_fwd_multi(int R, int T, int W, int F, int rows_per_cand, const float* X, long xs_f, long xs_col,
+                        const uint8_t* done, const float* fwdA, const float* eta, long eta_stride, const int* off,
+                        float* pi_hat, float* y_hat, hipStream_t stream) {
   TOUED_REQUIRE(R % RB == 0 && W % RB == 0, "toued_gru_fwd_multi: rows R=%d and workers W=%d must be multiples of 32",
                 R, W);
   TOUED_REQUIRE(rows_per_cand > 0 && rows_per_cand % RB == 0 && R % rows_per_cand == 0,
                 "toued_gru_fwd_multi: rows_per_cand=%d must be a multiple of 32 dividing R=%d", rows_per_cand, R);
   TOUED_REQUIRE(F >= 1 && F <= 7 && T >= 1, "toued_gru_fwd_multi: F=%d T=%d", F, T);
-  return gru_fwd_launch(R, T, W, F, X, xs_f, done, fwdA, eta, off, pi_hat, y_hat, nullptr, nullptr, nullptr, nullptr,
-                        nullptr, 0, 0, rows_per_cand, eta_stride, stream);
+  return gru_fwd_launch(R, T, W, F, X, xs_f, xs_col, done, fwdA, eta, off, pi_hat, y_hat, nullptr, nullptr, nullptr,
+                        nullptr, nullptr, 0, 0, rows_per_cand, eta_stride, stream);
 }
 
 int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_stride_k, const float* bwdA,
@@ -520,7 +604,10 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
   p.y_hat = y_hat; p.d_pi_hat = d_pi_hat; p.d_y_hat = d_y_hat;
   p.s_hin = s_hin; p.s_r = s_r; p.s_z = s_z; p.s_n = s_n; p.s_hn = s_hn; p.M = M;
   p.DG = DG; p.RH = RH; p.DH = DH; p.dX3 = dX3; p.dX4 = dX4;
-  hipLaunchKernelGGL(k_gru_bwd, dim3(K * (R / RB)), dim3(512), 0, stream, p);
+  if (R % (2 * RB) == 0)
+    hipLaunchKernelGGL(k_gru_bwd<2>, dim3(K * (R / (2 * RB))), dim3(512), 0, stream, p);
+  else
+    hipLaunchKernelGGL(k_gru_bwd<1>, dim3(K * (R / RB)), dim3(512), 0, stream, p);
   TOUED_CHECK_LAUNCH();
   return 0;
 }

@@ -43,7 +43,7 @@ _SIGS = {
     "toued_batch_reset": [EnvSpecC, _P, _P, _I, _I, _P, _P, _P, _P],
     "toued_rollout": [EnvSpecC, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "toued_meta_keys": [_P, _I, _I, _P, _P, _P, _P, _P],
-    "toued_lpg_inputs": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _L, _P],
+    "toued_lpg_inputs": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _L, _L, _P],
     "toued_agent_grad": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P],
     "toued_agent_apply": [_I, _I, _P, _P, _P, _P, _F, _F, _F, _P, _P, _P, _P, _P, _P],
     "toued_entropy": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P],
@@ -57,7 +57,7 @@ _SIGS = {
     "toued_adam": [_I, _P, _P, _P, _P, _F, _F, _F, _F, _F, _I, _P],
     "toued_gru_pack": [_P, _P, _I, _P, _P, _P],
     "toued_gru_packed_floats": [_I],
-    "toued_gru_fwd": [_I, _I, _I, _I, _P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _P],
+    "toued_gru_fwd": [_I, _I, _I, _I, _P, _L, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _P],
     "toued_gru_bwd": [_I, _I, _I, _I, _P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _P, _P, _P, _P, _P,
                       _P],
     "toued_choice_cdf": [_P, _P, _I, _I, _P, _P],
@@ -65,7 +65,7 @@ _SIGS = {
     "toued_a2c_grad": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _P, _P, _P, _P],
     "toued_a2c_apply": [_I, _I, _P, _P, _P, _P, _F, _F, _F, _P, _P, _P],
     "toued_gru_pack_fwd_multi": [_P, _L, _I, _P, _I, _P, _P],
-    "toued_gru_fwd_multi": [_I, _I, _I, _I, _I, _P, _L, _P, _P, _P, _L, _P, _P, _P, _P],
+    "toued_gru_fwd_multi": [_I, _I, _I, _I, _I, _P, _L, _L, _P, _P, _P, _L, _P, _P, _P, _P],
     "toued_es_ask": [_P, _L, _L, _L, _L, _P, _F, _P, _P],
     "toued_es_grad": [_P, _P, _F, _P, _I, _L, _P, _P],
     "toued_es_opt": [_L, _I, _P, _P, _F, _P, _P, _F, _F, _F, _F, _F, _F, _P],

@@ -167,8 +167,8 @@ class ESTrainStep:
             self.ro.batch_rollout(chain[k], th, levels, state, out=tr, inplace_state=True)
             L.call("toued_lpg_inputs", C, W, T, D, self.F, ptr(th), ptr(ph), ptr(tr.obs_idx), ptr(tr.obs_time),
                    ptr(tr.action), ptr(tr.reward), ptr(tr.done), ptr(e1w), ptr(e1b), ptr(e2w), ptr(e2b), ptr(step),
-                   ptr(levels), ptr(self.X), T * R, nd, st)
-            L.call("toued_gru_fwd_multi", R, T, W, self.F, W, ptr(self.X), T * R, ptr(tr.done), ptr(self.fwdA),
+                   ptr(levels), ptr(self.X), T * R, 1, nd, st)
+            L.call("toued_gru_fwd_multi", R, T, W, self.F, W, ptr(self.X), T * R, 1, ptr(tr.done), ptr(self.fwdA),
                    ptr(self.x), nd, self.lay.c_offsets, ptr(self.pi_hat), ptr(self.y_hat), st)
             self.G_th.zero_()
             self.G_ph.zero_()

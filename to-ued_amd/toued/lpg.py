@@ -128,7 +128,7 @@ class LPGGRU:
         col = k * T * R
         Xk = X[:, k]
         S = self.S
-        _lib.call("toued_gru_fwd", R, T, self.W, self.lay.F, _lib.ptr(X) + 4 * col, M, _lib.ptr(done_k),
+        _lib.call("toued_gru_fwd", R, T, self.W, self.lay.F, _lib.ptr(X) + 4 * col, M, 1, _lib.ptr(done_k),
                   _lib.ptr(self.fwdA), _lib.ptr(eta), self.lay.c_offsets, _lib.ptr(pi_hat[k]), _lib.ptr(y_hat[k]),
                   _lib.ptr(self.A) + 4 * col, _lib.ptr(S) + 4 * (0 * H * M + col),
                   _lib.ptr(S) + 4 * (1 * H * M + col), _lib.ptr(S) + 4 * (2 * H * M + col),

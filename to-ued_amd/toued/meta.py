@@ -184,7 +184,7 @@ class MetaGradStep:
             L.call("toued_lpg_inputs", N, W, T, D, self.F, ptr(self.theta_h[k]), ptr(self.phi_h[k]),
                    ptr(tk.obs_idx), ptr(tk.obs_time), ptr(tk.action), ptr(tk.reward), ptr(tk.done),
                    ptr(e1w), ptr(e1b), ptr(e2w), ptr(e2b), ptr(agents.step), ptr(agents.levels),
-                   ptr(self.X) + 4 * k * T * R, self.gru.M, 0, st)
+                   ptr(self.X) + 4 * k * T * R, self.gru.M, 1, 0, st)
             tok = self.timers.start("gru_fwd")
             self.gru.forward(k, self.X, tk.done, eta, self.pi_hat, self.y_hat)
             self.timers.stop(tok)
