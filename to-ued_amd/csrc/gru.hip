@@ -152,6 +152,26 @@ __global__ void k_pack_bwd(const float* __restrict__ eta, EtaOff o, float4* __re
   out[gid] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
+// One k-major LDS buffer ([unit][row], pitch RB*NT + 1; h^T in the forward, a gate cotangent in the
+// backward) of NT row tiles out to its row-major
+// [unit][M] array: lane l stores 4 consecutive rows (4*(l & 7) ..) of unit 32*wave + 8i + (l >> 3),
+// so every wave instruction writes 8 units x 128 contiguous bytes; the LDS reads are conflict-free.
+template <int NT>
+TOUED_DEV void store_gate_lds(const float* buf, __amdgpu_buffer_rsrc_t rs, long M, long col0, int wave, int lane) {
+  constexpr int LDT = RB * NT + 1;
+  const unsigned so = (unsigned)(col0 * 4);
+#pragma unroll
+  for (int h = 0; h < NT; ++h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int unit = 32 * wave + 8 * i + (lane >> 3), r = RB * h + 4 * (lane & 7);
+      const float* src = buf + unit * LDT + r;
+      const float v[4] = {src[0], src[1], src[2], src[3]};
+      st4(rs, (unsigned)(((long)unit * M + r) * 4), so, v);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ forward
 struct FwdArgs {
   int R, T, W, F;
@@ -242,6 +262,8 @@ __global__ void __launch_bounds__(512, 4) k_gru_fwd(FwdArgs p) {
         }
       }
     }
+    // ---- h_in(t) leaves from LDS (16-byte row quads) before hT is overwritten with h_in(t-1)
+    if (SAVE) store_gate_lds<1>(hT, rs_hin, p.M, (long)t * R + r0, wave, lane);
     // ---- gate maths (lane = row, register q = unit offset)
     const long cbase = (long)t * R;                              // uniform column base
     const unsigned vbyte = (unsigned)(((long)(32 * wave + 4 * hi) * p.M + row) * 4);
@@ -262,7 +284,6 @@ __global__ void __launch_bounds__(512, 4) k_gru_fwd(FwdArgs p) {
       hnew[q] = h;
       if (SAVE) {
         const unsigned so = (unsigned)(((long)qunit(q) * p.M + cbase) * 4);
-        st_u(rs_hin, vbyte, so, hin);
         st_u(rs_r, vbyte, so, rg);
         st_u(rs_z, vbyte, so, zg);
         st_u(rs_n, vbyte, so, ng);
@@ -452,10 +473,7 @@ __global__ void __launch_bounds__(512, NT == 1 ? 4 : 1) k_gru_bwd(BwdArgs p) {
           for (int j = 0; j < 4; ++j) {
             const unsigned so1 = (unsigned)(((long)qunit(4 * g4 + j) * p.M + ctr) * 4);
             st_u(rs_rh, vb, so1, o_rh[j]);
-            st_u(rs_dg[0], vb, so1, o_dr[j]);
-            st_u(rs_dg[1], vb, so1, o_dz[j]);
-            st_u(rs_dg[2], vb, so1, o_dhn[j]);
-            st_u(rs_dg[3], vb, so1, o_dn[j]);
+            st_u(rs_dg[3], vb, so1, o_dn[j]);          // dr, dz, dhn leave from LDS (store_gate_lds)
           }
         }
       }
@@ -480,6 +498,14 @@ __global__ void __launch_bounds__(512, NT == 1 ? 4 : 1) k_gru_bwd(BwdArgs p) {
         }
       }
       if (g != 1) __syncthreads();
+      // the gate cotangents just completed in LDS go out as 16-byte row-quad stores (LDS does the
+      // transpose): dr and dz before the first contraction, dhn before the third
+      if (g == 0) {
+        store_gate_lds<NT>(dgT, rs_dg[0], p.M, ctr + r0, wave, lane);
+        store_gate_lds<NT>(dgT + HU * LDT, rs_dg[1], p.M, ctr + r0, wave, lane);
+      } else if (g == 2) {
+        store_gate_lds<NT>(dgT, rs_dg[2], p.M, ctr + r0, wave, lane);
+      }
       const float* dgs = dgT + (g == 1 ? HU * LDT : 0);
       float4 an = Ab[((wave * 3 + g) * 32 + 0) * 64];
 #pragma unroll 2
