@@ -189,28 +189,39 @@ struct FwdArgs {
 #define NWAVE 8         // 512-thread workgroups: wave w owns units [32w, 32w+32)
 #define NGRP (2 * NWAVE)
 
-template <bool SAVE>
-__global__ void __launch_bounds__(512, 4) k_gru_fwd(FwdArgs p) {
-  __shared__ float hT[(HU + NAUG) * LDH];
+// NT row tiles of 32 rows per workgroup.  NT = 2 (one workgroup per CU, 256 VGPRs): every packed weight
+// fragment feeds 8 MFMAs instead of 4, halving the L2 fragment stream and the per-step fixed costs.  A
+// barrier after the contraction lets each lane overwrite its own h_in slot with the next carry in place, so
+// h_out never sits in registers across the barrier (no spills at 256 VGPRs).
+template <bool SAVE, int NT>
+__global__ void __launch_bounds__(512, NT == 1 ? 4 : 1) k_gru_fwd(FwdArgs p) {
+  constexpr int RBT = RB * NT;          // rows per workgroup
+  constexpr int LDT = RBT + 1;          // padded LDS row (k-major [unit][row])
+  __shared__ float hT[(HU + NAUG) * LDT];
   __shared__ float wh[HU * 9];
-  __shared__ float hp[NGRP * 9 * RB];
-  __shared__ float hout[9 * RB];
+  __shared__ float hp[NGRP * 9 * RBT];
+  __shared__ float hout[9 * RBT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hi = lane >> 5, col = lane & 31;
-  const int r0 = blockIdx.x * RB, row = r0 + col;
+  const int r0 = blockIdx.x * RBT;
   const int R = p.R, T = p.T, W = p.W, F = p.F;
-  const int a = r0 / W, w = row - a * W;
+  int a_[NT], w_[NT];
+#pragma unroll
+  for (int h = 0; h < NT; ++h) {
+    a_[h] = (r0 + RB * h) / W;
+    w_[h] = r0 + RB * h + col - a_[h] * W;
+  }
   const int cand = SAVE ? 0 : r0 / p.rpc;
   const float* eta = p.eta + (long)cand * p.eta_stride;
   for (int i = tid; i < HU * 9; i += 512) {
     const int u = i / 9, oo = i - u * 9;
     wh[i] = oo == 0 ? eta[p.o.pi_w + u] : eta[p.o.y_w + u * 8 + (oo - 1)];
   }
-  for (int i = tid; i < (HU + NAUG) * LDH; i += 512) hT[i] = 0.0f;
+  for (int i = tid; i < (HU + NAUG) * LDT; i += 512) hT[i] = 0.0f;
   __syncthreads();
-  if (tid < RB) {
+  if (tid < RBT) {
     const int t = T - 1;
     for (int f = 0; f < NAUG; ++f)
-      hT[(HU + f) * LDH + tid] = f < F ? p.X[f * p.xs_f + ((size_t)t * R + r0 + tid) * p.xs_col] : (f == F ? 1.0f : 0.0f);
+      hT[(HU + f) * LDT + tid] = f < F ? p.X[f * p.xs_f + ((size_t)t * R + r0 + tid) * p.xs_col] : (f == F ? 1.0f : 0.0f);
   }
   __syncthreads();
   const float bpi = eta[p.o.pi_b];
@@ -219,11 +230,13 @@ __global__ void __launch_bounds__(512, 4) k_gru_fwd(FwdArgs p) {
                                rs_n = rsrc_of(p.s_n), rs_hn = rsrc_of(p.s_hn);
   for (int s = 0; s < T; ++s) {
     const int t = T - 1 - s;
-    floatx16 acc[4];
+    floatx16 acc[4][NT];
 #pragma unroll
     for (int g = 0; g < 4; ++g)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) acc[g][q] = 0.0f;
+      for (int h = 0; h < NT; ++h)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[g][h][q] = 0.0f;
     // ---- recurrent contraction over the 256 h rows (kq 0..31): r, z, nh tiles of unit tile `wave`
     float4 an[3];
 #pragma unroll
@@ -239,11 +252,14 @@ __global__ void __launch_bounds__(512, 4) k_gru_fwd(FwdArgs p) {
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float b = hT[(2 * (4 * kq + e) + hi) * LDH + col];
 #pragma unroll
-        for (int g = 0; g < 3; ++g) {
-          const float av = e == 0 ? ac[g].x : e == 1 ? ac[g].y : e == 2 ? ac[g].z : ac[g].w;
-          acc[g] = mfma32(av, b, acc[g]);
+        for (int h = 0; h < NT; ++h) {
+          const float b = hT[(2 * (4 * kq + e) + hi) * LDT + RB * h + col];
+#pragma unroll
+          for (int g = 0; g < 3; ++g) {
+            const float av = e == 0 ? ac[g].x : e == 1 ? ac[g].y : e == 2 ? ac[g].z : ac[g].w;
+            acc[g][h] = mfma32(av, b, acc[g][h]);
+          }
         }
       }
     }
@@ -254,74 +270,74 @@ __global__ void __launch_bounds__(512, 4) k_gru_fwd(FwdArgs p) {
       for (int g = 0; g < 4; ++g) ag[g] = Ab[((8 * g + wave) * KQF + 32) * 64];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float b = hT[(HU + 2 * e + hi) * LDH + col];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float av = e == 0 ? ag[g].x : e == 1 ? ag[g].y : e == 2 ? ag[g].z : ag[g].w;
-          acc[g] = mfma32(av, b, acc[g]);
+        for (int h = 0; h < NT; ++h) {
+          const float b = hT[(HU + 2 * e + hi) * LDT + RB * h + col];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const float av = e == 0 ? ag[g].x : e == 1 ? ag[g].y : e == 2 ? ag[g].z : ag[g].w;
+            acc[g][h] = mfma32(av, b, acc[g][h]);
+          }
         }
       }
     }
     // ---- h_in(t) leaves from LDS (16-byte row quads) before hT is overwritten with h_in(t-1)
-    if (SAVE) store_gate_lds<1>(hT, rs_hin, p.M, (long)t * R + r0, wave, lane);
+    if (SAVE) store_gate_lds<NT>(hT, rs_hin, p.M, (long)t * R + r0, wave, lane);
+    __syncthreads();   // all MFMA and h_in reads of hT done: the carry can overwrite it in place
+    if (t >= 1 && tid < RBT) {
+      for (int f = 0; f < F; ++f)
+        hT[(HU + f) * LDT + tid] = p.X[f * p.xs_f + ((size_t)(t - 1) * R + r0 + tid) * p.xs_col];
+    }
     // ---- gate maths (lane = row, register q = unit offset)
     const long cbase = (long)t * R;                              // uniform column base
-    const unsigned vbyte = (unsigned)(((long)(32 * wave + 4 * hi) * p.M + row) * 4);
-    float hp_loc[9];
-#pragma unroll
-    for (int oo = 0; oo < 9; ++oo) hp_loc[oo] = 0.0f;
-    float hnew[16];
-    const float* hTl = hT + (32 * wave + 4 * hi) * LDH + col;
     const float* whl = wh + (32 * wave + 4 * hi) * 9;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const float rg = sigm(acc[0][q]);
-      const float zg = sigm(acc[1][q]);
-      const float hn = acc[2][q];
-      const float ng = tanh_f(acc[3][q] + rg * hn);
-      const float hin = hTl[qunit(q) * LDH];    // h_in(t) (masked carry), rewritten after the barrier
-      const float h = (1.0f - zg) * ng + zg * hin;
-      hnew[q] = h;
-      if (SAVE) {
-        const unsigned so = (unsigned)(((long)qunit(q) * p.M + cbase) * 4);
-        st_u(rs_r, vbyte, so, rg);
-        st_u(rs_z, vbyte, so, zg);
-        st_u(rs_n, vbyte, so, ng);
-        st_u(rs_hn, vbyte, so, hn);
+    for (int h = 0; h < NT; ++h) {
+      const unsigned vbyte = (unsigned)(((long)(32 * wave + 4 * hi) * p.M + r0 + RB * h + col) * 4);
+      float* hTl = hT + (32 * wave + 4 * hi) * LDT + RB * h + col;
+      const bool dn = (t >= 1) ? p.done[((size_t)a_[h] * T + (t - 1)) * W + w_[h]] != 0 : false;
+      float hp_loc[9];
+#pragma unroll
+      for (int oo = 0; oo < 9; ++oo) hp_loc[oo] = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float rg = sigm(acc[0][h][q]);
+        const float zg = sigm(acc[1][h][q]);
+        const float hn = acc[2][h][q];
+        const float ng = tanh_f(acc[3][h][q] + rg * hn);
+        const float hin = hTl[qunit(q) * LDT];    // h_in(t) (masked carry)
+        const float hh = (1.0f - zg) * ng + zg * hin;
+        hTl[qunit(q) * LDT] = dn ? 0.0f : hh;    // next-step carry h_in(t-1) = where(d_{t-1}, 0, h_out(t))
+        if (SAVE) {
+          const unsigned so = (unsigned)(((long)qunit(q) * p.M + cbase) * 4);
+          st_u(rs_r, vbyte, so, rg);
+          st_u(rs_z, vbyte, so, zg);
+          st_u(rs_n, vbyte, so, ng);
+          st_u(rs_hn, vbyte, so, hn);
+        }
+        const float rl = fmaxf(hh, 0.0f);
+#pragma unroll
+        for (int oo = 0; oo < 9; ++oo) hp_loc[oo] += rl * whl[qunit(q) * 9 + oo];
       }
-      const float rl = fmaxf(h, 0.0f);
 #pragma unroll
-      for (int oo = 0; oo < 9; ++oo) hp_loc[oo] += rl * whl[qunit(q) * 9 + oo];
+      for (int oo = 0; oo < 9; ++oo) hp[((2 * wave + hi) * 9 + oo) * RBT + RB * h + col] = hp_loc[oo];
     }
-#pragma unroll
-    for (int oo = 0; oo < 9; ++oo) hp[((2 * wave + hi) * 9 + oo) * RB + col] = hp_loc[oo];
-    __syncthreads();   // all MFMA reads of hT done; head partials visible
-    // next-step carry: h_in(t-1) = where(d_{t-1}, 0, h_out(t))
-    const bool dn = (t >= 1) ? p.done[((size_t)a * T + (t - 1)) * W + w] != 0 : false;
-    float* hTw = hT + (32 * wave + 4 * hi) * LDH + col;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      hTw[qunit(q) * LDH] = dn ? 0.0f : hnew[q];
-    }
-    if (t >= 1 && tid < RB) {
-      for (int f = 0; f < F; ++f)
-        hT[(HU + f) * LDH + tid] = p.X[f * p.xs_f + ((size_t)(t - 1) * R + r0 + tid) * p.xs_col];
-    }
-    for (int i = tid; i < 9 * RB; i += 512) {
-      const int oo = i / RB, c = i - oo * RB;
+    __syncthreads();   // head partials and the carry visible
+    for (int i = tid; i < 9 * RBT; i += 512) {
+      const int oo = i / RBT, c = i - oo * RBT;
       float v = oo == 0 ? bpi : eta[p.o.y_b + oo - 1];
 #pragma unroll
-      for (int gq = 0; gq < NGRP; ++gq) v += hp[(gq * 9 + oo) * RB + c];
+      for (int gq = 0; gq < NGRP; ++gq) v += hp[(gq * 9 + oo) * RBT + c];
       hout[i] = v;
     }
     __syncthreads();
-    if (tid < RB) {
+    if (tid < RBT) {
       const long ob = (long)t * R + r0 + tid;
       p.pi_hat[ob] = hout[tid];
       float m = -__builtin_inff();
-      for (int j = 0; j < 8; ++j) m = fmaxf(m, hout[(j + 1) * RB + tid]);
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, hout[(j + 1) * RBT + tid]);
       float e[8], ssum = 0.0f;
-      for (int j = 0; j < 8; ++j) { e[j] = __expf(hout[(j + 1) * RB + tid] - m); ssum += e[j]; }
+      for (int j = 0; j < 8; ++j) { e[j] = __expf(hout[(j + 1) * RBT + tid] - m); ssum += e[j]; }
       const float inv = 1.0f / ssum;
       for (int j = 0; j < 8; ++j) p.y_hat[((long)t * 8 + j) * R + r0 + tid] = e[j] * inv;
     }
@@ -571,10 +587,16 @@ static int gru_fwd_launch(int R, int T, int W, int F, const float* X, long xs_f,
   memcpy(&p.o, off, sizeof(EtaOff));
   p.pi_hat = pi_hat; p.y_hat = y_hat; p.s_hin = s_hin; p.s_r = s_r; p.s_z = s_z; p.s_n = s_n; p.s_hn = s_hn; p.M = M;
   p.rpc = rpc; p.a_stride4 = (long)NTILE_F * KQF * 64; p.eta_stride = eta_stride;
-  if (save)
-    hipLaunchKernelGGL(k_gru_fwd<true>, dim3(R / RB), dim3(512), 0, stream, p);
-  else
-    hipLaunchKernelGGL(k_gru_fwd<false>, dim3(R / RB), dim3(512), 0, stream, p);
+  // two row tiles per workgroup when the rows (and, for per-candidate parameters, each candidate's rows)
+  // split into 64-row blocks
+  const bool nt2 = R % (2 * RB) == 0 && (rpc == 0 || rpc % (2 * RB) == 0);
+  if (save) {
+    if (nt2) hipLaunchKernelGGL((k_gru_fwd<true, 2>), dim3(R / (2 * RB)), dim3(512), 0, stream, p);
+    else hipLaunchKernelGGL((k_gru_fwd<true, 1>), dim3(R / RB), dim3(512), 0, stream, p);
+  } else {
+    if (nt2) hipLaunchKernelGGL((k_gru_fwd<false, 2>), dim3(R / (2 * RB)), dim3(512), 0, stream, p);
+    else hipLaunchKernelGGL((k_gru_fwd<false, 1>), dim3(R / RB), dim3(512), 0, stream, p);
+  }
   TOUED_CHECK_LAUNCH();
   return 0;
 }
