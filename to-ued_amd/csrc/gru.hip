@@ -16,11 +16,12 @@
 // blocks in registers (DPP): 4x fewer load instructions than per-dword access.  (Transposed 16-byte
 // stores measured slower at this register budget; the cotangent stores stay per dword.)
 //
-// Backward: one workgroup per (k, 32 rows), t ascending; three LDS phases
-// (dr_pre, dz_pre, d(W_hn h + b_hn)) each contracted with W_h^T on MFMA give
-// dh_prev; writes the gate-pre-activation cotangents DG[4][256][M], relu(h_out)
-// and the head cotangents for the weight-gradient GEMMs, and dX for the
-// embedding inputs.
+// Backward (k_gru_bwd_g2): one workgroup per (k, 64 rows), t ascending, as two 32-row groups running half
+// a step apart so that one group's saved-activation traffic overlaps the other's MFMA contraction.  Per
+// step: gate maths in registers; the cotangents dr_pre, dz_pre (LDS slots), then d(W_hn h + b_hn) (slot 0
+// again), each contracted with W_h^T on MFMA to give dh_prev; writes the gate-pre-activation cotangents
+// DG[4][256][M], relu(h_out) and the head cotangents for the weight-gradient GEMMs, and dX for the
+// embedding inputs.  (k_gru_bwd<1>, one 32-row tile with both phases in every wave, covers R % 64 != 0.)
 //
 // MFMA f32 32x32x2 operand/result maps (cdna_hip_programming.md §3):
 //   A: lane l holds A[i = l&31][k = l>>5];  B: lane l holds B[k = l>>5][j = l&31]
@@ -557,6 +558,265 @@ __global__ void __launch_bounds__(512, NT == 1 ? 4 : 1) k_gru_bwd(BwdArgs p) {
   }
 }
 
+// Two-group backward: 64 rows per workgroup as two 32-row groups of four waves, run half a time step
+// apart.  Each super-phase one group does the memory/VALU half of a step (saved-activation loads, gate
+// maths, cotangent stores) while the other contracts the previous step's gate cotangents with W_h^T on
+// MFMA, so every SIMD (one wave of each group) overlaps HBM traffic with matrix work instead of
+// alternating between them.  Wave wg of a group owns units [64 wg, 64 wg + 64) (two 32-unit tiles j) for
+// the group's 32 rows; the LDS holds two cotangent slots per group ([dr | dz], then dhn in slot 0).
+__global__ void __launch_bounds__(512, 1) k_gru_bwd_g2(BwdArgs p) {
+  constexpr int LDG = RB + 1;
+  constexpr int SLOT = HU * LDG;
+  __shared__ float dgT[2 * 2 * SLOT];        // [group][slot][unit][row]
+  __shared__ float wi34[2 * 3 * HU];
+  __shared__ float hv[2 * 9 * RB];           // [group][head output][row]
+  __shared__ float dxp[2 * 8 * 2 * RB];      // [group][wave, hi][dx3 | dx4][row]
+  const int tid = threadIdx.x, lane = tid & 63, hi = lane >> 5, col = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: group offsets go to SGPRs
+  // group = wave >> 2: a workgroup's waves go round-robin over the four SIMDs, so every SIMD holds one
+  // wave of each group (grouping by wave & 1 measured 1.8x slower)
+  const int gi = wave >> 2, wg = wave & 3;
+  const int gtid = wg * 64 + lane;           // thread index within the group
+  const int nb = p.R / (2 * RB);
+  const int k = blockIdx.x / nb;
+  const int r0 = (blockIdx.x - k * nb) * (2 * RB) + RB * gi;   // this group's first row
+  const int R = p.R, T = p.T, W = p.W;
+  const int a_ = r0 / W, w_ = r0 + col - a_ * W;
+  float* dg0 = dgT + gi * 2 * SLOT;          // slot 0 of this group (slot 1 at + SLOT)
+  for (int i = tid; i < 2 * 3 * HU; i += 512) {
+    const int f = 3 + i / (3 * HU), g = (i / HU) % 3, u = i % HU;
+    const int base = g == 0 ? p.o.ir_w : g == 1 ? p.o.iz_w : p.o.in_w;
+    wi34[i] = p.eta[base + f * HU + u];
+  }
+  float wA[2][5];   // W_heads^T A fragments of the two unit tiles: A[i = unit][k = head output 2kk + hi]
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) {
+      const int o = 2 * kk + hi, u = 64 * wg + 32 * j + col;
+      wA[j][kk] = o < 9 ? (o == 0 ? p.eta[p.o.pi_w + u] : p.eta[p.o.y_w + u * 8 + (o - 1)]) : 0.0f;
+    }
+  float dh[2][16], dhn_r[2][16];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) { dh[j][q] = 0.0f; dhn_r[j][q] = 0.0f; }
+  const uint8_t* done = p.done + (long)k * p.done_stride_k;
+  const __amdgpu_buffer_rsrc_t rs_hin = rsrc_of(p.s_hin), rs_r = rsrc_of(p.s_r), rs_z = rsrc_of(p.s_z),
+                               rs_n = rsrc_of(p.s_n), rs_hn = rsrc_of(p.s_hn), rs_rh = rsrc_of(p.RH);
+  const __amdgpu_buffer_rsrc_t rs_dg[4] = {rsrc_of(p.DG), rsrc_of(p.DG + 1L * HU * p.M),
+                                           rsrc_of(p.DG + 2L * HU * p.M), rsrc_of(p.DG + 3L * HU * p.M)};
+  // head cotangents of step t (softmax VJP of y_hat, d pi_hat) for the group's rows -> hv, DH
+  auto head_cot = [&](int t) {
+    if (gtid < RB) {
+      const long o = ((long)k * T + t) * R + r0 + gtid;
+      float yh[8], dy[8], s = 0.0f;
+      for (int j = 0; j < 8; ++j) {
+        yh[j] = p.y_hat[((long)k * T * 8 + (long)t * 8 + j) * R + r0 + gtid];
+        dy[j] = p.d_y_hat[((long)k * T * 8 + (long)t * 8 + j) * R + r0 + gtid];
+        s += yh[j] * dy[j];
+      }
+      const float dpi = p.d_pi_hat[o];
+      hv[(gi * 9) * RB + gtid] = dpi;
+      p.DH[o] = dpi;
+      for (int j = 0; j < 8; ++j) {
+        const float v = yh[j] * (dy[j] - s);
+        hv[(gi * 9 + j + 1) * RB + gtid] = v;
+        p.DH[(long)(j + 1) * p.M + o] = v;
+      }
+    }
+  };
+  head_cot(0);
+  __syncthreads();
+  // ---- memory half: unit quad (tile j, quad g4) of step t
+  floatx16 hacc[2];
+  float dx3 = 0.0f, dx4 = 0.0f;
+  // saved activations of unit quad (tile j, quad g4) of step t: 16-byte row-quad loads + quad transposes
+  auto mem_load = [&](int t, int j, int g4, float (&v)[5][4]) {
+    const long ctr = ((long)k * T + t) * R;
+    const int ub = 64 * wg + 32 * j + 4 * hi;
+    const unsigned vq = (unsigned)(((long)(ub + (col & 3)) * p.M + r0 + (col & 28)) * 4);
+    const unsigned so = (unsigned)(((long)8 * g4 * p.M + ctr) * 4);
+    ld4(rs_hin, vq, so, v[0]);
+    ld4(rs_r, vq, so, v[1]);
+    ld4(rs_z, vq, so, v[2]);
+    ld4(rs_n, vq, so, v[3]);
+    ld4(rs_hn, vq, so, v[4]);
+  };
+  auto mem_compute = [&](int t, int j, int g4, float (&v)[5][4]) {
+    const long ctr = ((long)k * T + t) * R;
+    const int ub = 64 * wg + 32 * j + 4 * hi;          // lane's unit base within the tile
+#pragma unroll
+    for (int a = 0; a < 5; ++a) quad_transpose(v[a], lane);
+    float* o_rh = v[0]; float* o_dn = v[4];   // reused in place
+    const float* wil = wi34 + ub;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int q = 4 * g4 + jj;
+      const float hin = v[0][jj], rg = v[1][jj], zg = v[2][jj], ng = v[3][jj], hn = v[4][jj];
+      const float hout = (1.0f - zg) * ng + zg * hin;
+      const float d = dh[j][q] + (hout > 0.0f ? hacc[j][q] : 0.0f);
+      const float dn_ = d * (1.0f - zg);
+      const float dz = d * (hin - ng);
+      const float dnp = dn_ * (1.0f - ng * ng);
+      const float dhn = dnp * rg;
+      const float drp = dnp * hn * rg * (1.0f - rg);
+      const float dzp = dz * zg * (1.0f - zg);
+      dh[j][q] = d * zg;   // direct path; the W_h^T contraction is added in the MFMA half
+      const int lo = (ub + qunit(q)) * LDG + col;
+      dg0[lo] = drp;
+      dg0[SLOT + lo] = dzp;
+      dhn_r[j][q] = dhn;
+      o_rh[jj] = fmaxf(hout, 0.0f); o_dn[jj] = dnp;
+      const int qu = qunit(q);
+      dx3 += drp * wil[0 * HU + qu] + dzp * wil[1 * HU + qu] + dnp * wil[2 * HU + qu];
+      dx4 += drp * wil[3 * HU + qu] + dzp * wil[4 * HU + qu] + dnp * wil[5 * HU + qu];
+    }
+    const unsigned vb = (unsigned)(((long)ub * p.M + r0 + col) * 4);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const unsigned so1 = (unsigned)(((long)qunit(4 * g4 + jj) * p.M + ctr) * 4);
+      st_u(rs_rh, vb, so1, o_rh[jj]);
+      st_u(rs_dg[3], vb, so1, o_dn[jj]);   // dr, dz, dhn leave from LDS in the MFMA half
+    }
+  };
+  // unit quad (tile j, quad g4), written out per quad: the schedule barrier keeps the compiler from
+  // hoisting later quads' loads, and a wrapping lambda (or loop) measured 90-110 VGPR spills
+  float va[5][4], vb[5][4];
+#define G2_QUAD(j, g4, v) { mem_load(t, j, g4, v); __builtin_amdgcn_sched_barrier(0); mem_compute(t, j, g4, v); }
+  auto head_vjp = [&](int j) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) hacc[j][q] = 0.0f;
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) {
+      const int o = 2 * kk + hi;
+      hacc[j] = mfma32(wA[j][kk], o < 9 ? hv[(gi * 9 + o) * RB + col] : 0.0f, hacc[j]);
+    }
+  };
+  // ---- MFMA half: one slot of the group's cotangents out to DG[g] (16-byte row quads from LDS)
+  auto store_slot = [&](const float* buf, __amdgpu_buffer_rsrc_t rs, long col0) {
+    const unsigned so = (unsigned)(col0 * 4);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int unit = 64 * wg + 8 * i + (lane >> 3), r = 4 * (lane & 7);
+      const float* src = buf + unit * LDG + r;
+      const float v[4] = {src[0], src[1], src[2], src[3]};
+      st4(rs, (unsigned)(((long)unit * p.M + r) * 4), so, v);
+    }
+  };
+  floatx16 acc[2];
+  // A fragments stream from L2 through a 4-deep register ring (one wave per SIMD issues these MFMAs, so
+  // the ring, not a second wave, has to cover the L2 latency)
+  float4 ring[4][2];
+  const __amdgpu_buffer_rsrc_t rs_A = rsrc_of(reinterpret_cast<const float*>(p.A));
+  const unsigned vA = (unsigned)lane * 16;
+  // fragment (tile 2 wg + j, gate g, k-quad kq): uniform byte offset into the packed W_h^T stream
+  auto ldA = [&](int j, int g, int kq) {
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(
+        rs_A, (int)vA, (int)((((2 * wg + j) * 3 + g) * 32 + kq) * 64 * 16), 0);
+    return make_float4(__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w));
+  };
+  auto ring_fill = [&](int g) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { ring[i][0] = ldA(0, g, i); ring[i][1] = ldA(1, g, i); }
+  };
+  auto contract = [&](int g, const float* dgs) {
+    // B operands (this lane's cotangent column) one k-quad ahead, so no LDS latency sits between MFMAs
+    const float* bl = dgs + hi * LDG + col;
+    float bq[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bq[e] = bl[2 * e * LDG];
+    auto kstep = [&](int kq, bool reload) {
+      float bn[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bn[e] = kq + 1 < 32 ? bl[2 * (4 * (kq + 1) + e) * LDG] : 0.0f;
+      __builtin_amdgcn_sched_barrier(0);   // next k-quad's B reads in flight during this one's MFMAs
+      const float4 a0 = ring[kq & 3][0], a1 = ring[kq & 3][1];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[0] = mfma32(e == 0 ? a0.x : e == 1 ? a0.y : e == 2 ? a0.z : a0.w, bq[e], acc[0]);
+        acc[1] = mfma32(e == 0 ? a1.x : e == 1 ? a1.y : e == 2 ? a1.z : a1.w, bq[e], acc[1]);
+      }
+      if (reload) { ring[kq & 3][0] = ldA(0, g, kq + 4); ring[kq & 3][1] = ldA(1, g, kq + 4); }
+      __builtin_amdgcn_sched_barrier(0);   // keep each refill right behind its slot's last MFMA
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bq[e] = bn[e];
+    };
+    // main body: every k-quad refills its ring slot (unconditional loads keep the wait counts exact)
+#pragma unroll 4
+    for (int kq = 0; kq < 28; ++kq) kstep(kq, true);
+#pragma unroll
+    for (int kq = 28; kq < 32; ++kq) kstep(kq, false);
+  };
+  for (int s = 0; s <= 2 * T; ++s) {
+    const int u = s - gi;
+    const bool act = u >= 0 && (u >> 1) < T;
+    const bool mem = act && (u & 1) == 0, mm = act && (u & 1) == 1;
+    const int t = u >> 1;
+    const long ctr = ((long)k * T + t) * R;
+    // part X: memory quads of tile 0 | dr, dz out + contraction (the MFMA wave at raised issue priority)
+    if (mem) {
+      dx3 = 0.0f; dx4 = 0.0f;
+      head_vjp(0);
+      G2_QUAD(0, 0, va)
+      G2_QUAD(0, 1, vb)
+      G2_QUAD(0, 2, va)
+      G2_QUAD(0, 3, vb)
+    } else if (mm) {
+      __builtin_amdgcn_s_setprio(2);
+      if (gtid < RB) {
+        float s3 = 0.0f, s4 = 0.0f;
+        for (int gq = 0; gq < 8; ++gq) { s3 += dxp[((gi * 8 + gq) * 2 + 0) * RB + gtid]; s4 += dxp[((gi * 8 + gq) * 2 + 1) * RB + gtid]; }
+        p.dX3[ctr + r0 + gtid] = s3;
+        p.dX4[ctr + r0 + gtid] = s4;
+      }
+      ring_fill(0);
+      store_slot(dg0, rs_dg[0], ctr + r0);
+      store_slot(dg0 + SLOT, rs_dg[1], ctr + r0);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[j][q] = 0.0f;
+      contract(0, dg0);
+      ring_fill(1);
+      contract(1, dg0 + SLOT);
+    }
+    __syncthreads();
+    // part Y: dhn into slot 0 once every wave of the group has read dr
+    if (mm) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        float* dgl = dg0 + (64 * wg + 32 * j + 4 * hi) * LDG + col;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) dgl[qunit(q) * LDG] = dhn_r[j][q];
+      }
+    }
+    __syncthreads();
+    // part Z: memory quads of tile 1 + dx partials | dhn out + contraction, carry, next head cotangents
+    if (mem) {
+      head_vjp(1);
+      G2_QUAD(1, 0, va)
+      G2_QUAD(1, 1, vb)
+      G2_QUAD(1, 2, va)
+      G2_QUAD(1, 3, vb)
+      dxp[((gi * 8 + 2 * wg + hi) * 2 + 0) * RB + col] = dx3;
+      dxp[((gi * 8 + 2 * wg + hi) * 2 + 1) * RB + col] = dx4;
+    } else if (mm) {
+      ring_fill(2);
+      store_slot(dg0, rs_dg[2], ctr + r0);
+      contract(2, dg0);
+      // carry to h_out(t+1): h_in(t) = where(d_t, 0, h_out(t+1))
+      const bool dn = done[((size_t)a_ * T + t) * W + w_] != 0;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) dh[j][q] = dn ? 0.0f : dh[j][q] + acc[j][q];
+      if (t + 1 < T) head_cot(t + 1);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    __syncthreads();
+  }
+}
 
 }  // namespace
 
@@ -653,7 +913,7 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
   p.s_hin = s_hin; p.s_r = s_r; p.s_z = s_z; p.s_n = s_n; p.s_hn = s_hn; p.M = M;
   p.DG = DG; p.RH = RH; p.DH = DH; p.dX3 = dX3; p.dX4 = dX4;
   if (R % (2 * RB) == 0)
-    hipLaunchKernelGGL(k_gru_bwd<2>, dim3(K * (R / (2 * RB))), dim3(512), 0, stream, p);
+    hipLaunchKernelGGL(k_gru_bwd_g2, dim3(K * (R / (2 * RB))), dim3(512), 0, stream, p);
   else
     hipLaunchKernelGGL(k_gru_bwd<1>, dim3(K * (R / RB)), dim3(512), 0, stream, p);
   TOUED_CHECK_LAUNCH();

@@ -34,6 +34,11 @@ def main():
         Ac = A.view(264, ch, M // ch).permute(1, 0, 2)
         Bc = B.view(768, ch, M // ch).permute(1, 0, 2)
         res[f"bmm{ch}_sum"] = timed(lambda: torch.bmm(Ac, Bc.transpose(1, 2)).sum(0))
+    X6 = A[256:262]
+    res["mm_Gn"] = timed(lambda: torch.mm(X6, DG[3].t()))
+    RH = torch.randn(257, M, device="cuda")
+    DH = torch.randn(9, M, device="cuda")
+    res["mm_heads"] = timed(lambda: torch.mm(RH, DH.t()))
     flops = 2 * 264 * 768 * M
     res["tflops_mm_A_Bt"] = round(flops / (res["mm_A_Bt"] * 1e-3) / 1e12, 1)
     print(json.dumps(res), flush=True)
