@@ -193,6 +193,14 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
                   const float* s_hin, const float* s_r, const float* s_z, const float* s_n, const float* s_hn, long M,
                   float* DG, float* RH, float* DH, float* dX3, float* dX4, hipStream_t stream);
 
+/* weight-gradient reduction C[ra][rb] = A[ra x K] . B[rb x K]^T (row strides lda, ldb; K % 32 == 0,
+ * ra <= 272) on f32 MFMA, split over K with per-chunk partials in `work` (toued_wgrad_workspace_floats)
+ * summed in chunk order (deterministic).  Replaces the weight-gradient GEMMs of the LPG backward
+ * (jax.vjp of models/lpg.py:11-35 and :79-85 under meta/meta.py:177-181) */
+size_t toued_wgrad_workspace_floats(int ra, int rb, long K);
+int toued_wgrad(int ra, int rb, long K, const float* A, long lda, const float* B, long ldb, float* C, float* work,
+                size_t work_floats, hipStream_t stream);
+
 /* ES inference path: pack n candidates' forward fragments (candidate c at eta + c*eta_stride) */
 int toued_gru_pack_fwd_multi(const float* eta, long eta_stride, int n, const int* off, int F, float* fwdA,
                              hipStream_t stream);

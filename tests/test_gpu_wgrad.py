@@ -1,0 +1,70 @@
+"""GPU check of the weight-gradient reduction kernel (csrc/wgrad.hip, toued_wgrad).
+
+C[ra][rb] = A[ra x K] . B[rb x K]^T is the f32 reduction behind every LPG weight gradient (the jax.vjp of
+models/lpg.py's GRU and heads, meta/meta.py:177-181).  Checked against a float64 torch product on the
+same f32 operands over the shapes the LPG backward uses, ragged tiles (rb not a multiple of 128, ra not a
+multiple of 16), strided rows, K = 0 and a single 32-k slab.  Tolerance: |C - C64| <= 2e-6 * sqrt(K) *
+(|A| . |B|^T) elementwise (f32 accumulation over K terms), and bit-identical repeat runs (the split-K
+partials are summed in a fixed order).
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def run(ra, rb, K, lda=None, ldb=None, seed=0):
+    from toued import _lib as L
+    lda = K if lda is None else lda
+    ldb = K if ldb is None else ldb
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    Ab = torch.randn(max(ra, 1), max(lda, 4), generator=g, device="cuda")
+    Bb = torch.randn(max(rb, 1), max(ldb, 4), generator=g, device="cuda")
+    C = torch.full((ra, rb), float("nan"), device="cuda")
+    need = int(L.lib().toued_wgrad_workspace_floats(ra, rb, K))
+    work = torch.empty(max(need, 1), device="cuda")
+    L.call("toued_wgrad", ra, rb, K, L.ptr(Ab), lda, L.ptr(Bb), ldb, L.ptr(C), L.ptr(work), work.numel(),
+           L.stream_ptr())
+    torch.cuda.synchronize()
+    A = Ab[:ra, :K].double()
+    B = Bb[:rb, :K].double()
+    return C, A @ B.t(), A.abs() @ B.abs().t(), (Ab, Bb, work)
+
+
+@pytest.mark.parametrize("ra,rb,K", [(262, 768, 32 * 700), (6, 256, 32 * 900), (9, 257, 32 * 640),
+                                     (1, 1, 32), (17, 129, 96), (272, 130, 32 * 37), (16, 128, 32 * 5000),
+                                     (100, 300, 32 * 333)])
+def test_wgrad_matches_float64(ra, rb, K):
+    C, ref, mag, _ = run(ra, rb, K)
+    err = (C.double() - ref).abs()
+    tol = 2e-6 * math.sqrt(K) * mag + 1e-30
+    assert torch.isfinite(C).all()
+    assert (err <= tol).all(), float((err / tol).max())
+
+
+def test_wgrad_strided_rows_and_determinism():
+    from toued import _lib as L
+    ra, rb, K, lda, ldb = 40, 200, 32 * 300, 32 * 300 + 64, 32 * 300 + 12
+    C, ref, mag, (Ab, Bb, work) = run(ra, rb, K, lda, ldb, seed=3)
+    err = (C.double() - ref).abs()
+    assert (err <= 2e-6 * math.sqrt(K) * mag).all()
+    C2 = torch.empty_like(C)
+    L.call("toued_wgrad", ra, rb, K, L.ptr(Ab), lda, L.ptr(Bb), ldb, L.ptr(C2), L.ptr(work), work.numel(),
+           L.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(C, C2)
+
+
+def test_wgrad_empty_k_and_errors():
+    from toued import _lib as L
+    C = torch.full((3, 5), 7.0, device="cuda")
+    A = torch.zeros(3, 4, device="cuda")
+    L.call("toued_wgrad", 3, 5, 0, L.ptr(A), 4, L.ptr(A), 4, L.ptr(C), None, 0, L.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.count_nonzero(C) == 0
+    with pytest.raises(Exception, match="multiple of 32"):
+        L.call("toued_wgrad", 3, 5, 33, L.ptr(A), 36, L.ptr(A), 36, L.ptr(C), L.ptr(A), 12, L.stream_ptr())
+    with pytest.raises(Exception, match="workspace"):
+        L.call("toued_wgrad", 3, 5, 64, L.ptr(A), 64, L.ptr(A), 64, L.ptr(C), L.ptr(A), 1, L.stream_ptr())

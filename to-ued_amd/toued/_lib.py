@@ -71,11 +71,13 @@ _SIGS = {
     "toued_es_opt": [_L, _I, _P, _P, _F, _P, _P, _F, _F, _F, _F, _F, _F, _P],
     "toued_plr_reset_ids": [_I, _I, _P, _P, _P, _P, _P],
     "toued_plr_sample": [_I, _I, _P, _P, _P, _P, _I, _F, _F, _P, _P, _P, _P, _P],
+    "toued_wgrad_workspace_floats": [_I, _I, _L],
+    "toued_wgrad": [_I, _I, _L, _P, _L, _P, _L, _P, _P, ctypes.c_size_t, _P],
     "toued_last_error": [],
     "toued_abi_version": [],
 }
 _RESTYPES = {"toued_last_error": ctypes.c_char_p, "toued_mode_program_bytes": ctypes.c_size_t,
-             "toued_gru_packed_floats": ctypes.c_size_t}
+             "toued_gru_packed_floats": ctypes.c_size_t, "toued_wgrad_workspace_floats": ctypes.c_size_t}
 
 _lib = None
 

@@ -116,6 +116,14 @@ class LPGGRU:
         self.DH = torch.empty((9, M), dtype=f32, device=dev)            # head cotangents
         self.dX3 = torch.empty((K, T, R), dtype=f32, device=dev)
         self.dX4 = torch.empty((K, T, R), dtype=f32, device=dev)
+        # weight-gradient reductions (csrc/wgrad.hip): outputs and the per-K-chunk partial-sum workspace
+        self.G = torch.empty((H + lay.F + 1, 3 * H), dtype=f32, device=dev)
+        self.Gn = torch.empty((lay.F + 1, H), dtype=f32, device=dev)
+        self.Gh = torch.empty((9, H + 1), dtype=f32, device=dev)
+        need = max(int(L.toued_wgrad_workspace_floats(H + lay.F + 1, 3 * H, M)),
+                   int(L.toued_wgrad_workspace_floats(lay.F + 1, H, M)),
+                   int(L.toued_wgrad_workspace_floats(9, H + 1, M)))
+        self.wg_work = torch.empty(max(need, 1), dtype=f32, device=dev)
 
     def pack(self, eta: torch.Tensor):
         _lib.call("toued_gru_pack", _lib.ptr(eta), self.lay.c_offsets, self.lay.F, _lib.ptr(self.fwdA),
@@ -154,10 +162,13 @@ class LPGGRU:
         lay = self.lay
         F = lay.F
         DG = self.DG
-        # weight-gradient GEMMs (library GEMMs on the saved operands; reduction over M = K*T*R):
-        #   [h_in; X; 1] (264 x M) . [dr; dz; dhn]^T  -> dW_h (rows 0..255), dW_ir/dW_iz (X rows), biases (ones row)
-        #   [X; 1] . dn^T -> dW_in, b_in;   [relu(h_out); 1] . DH^T -> head kernels and biases
-        G = torch.mm(self.A, DG[0:3].reshape(3 * H, M).t())                # [264, 768]
+        # weight-gradient reductions over M = K*T*R on MFMA (csrc/wgrad.hip, deterministic split-K):
+        #   [h_in; X; 1] (262 x M) . [dr; dz; dhn]^T  -> dW_h (rows 0..255), dW_ir/dW_iz (X rows), biases (ones row)
+        #   [X; 1] . dn^T -> dW_in, b_in;   DH . [relu(h_out); 1]^T -> head kernels and biases
+        G, Gn, Gh = self.G, self.Gn, self.Gh
+        ws, wn = _lib.ptr(self.wg_work), self.wg_work.numel()
+        st = _lib.stream_ptr()
+        _lib.call("toued_wgrad", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, _lib.ptr(DG), M, _lib.ptr(G), ws, wn, st)
         lay.view(grad, "hr_w").add_(G[0:H, 0:H])
         lay.view(grad, "hz_w").add_(G[0:H, H:2 * H])
         lay.view(grad, "hn_w").add_(G[0:H, 2 * H:3 * H])
@@ -166,10 +177,12 @@ class LPGGRU:
         lay.view(grad, "ir_b").add_(G[H + F, 0:H])
         lay.view(grad, "iz_b").add_(G[H + F, H:2 * H])
         lay.view(grad, "hn_b").add_(G[H + F, 2 * H:3 * H])
-        Gn = torch.mm(self.A[H:H + F + 1], DG[3].t())                      # [F+1, 256]
+        _lib.call("toued_wgrad", F + 1, H, M, _lib.ptr(self.A) + 4 * H * M, M, _lib.ptr(DG[3]), M, _lib.ptr(Gn), ws,
+                  wn, st)
         lay.view(grad, "in_w").add_(Gn[0:F])
         lay.view(grad, "in_b").add_(Gn[F])
-        heads = torch.mm(self.RH, self.DH.t())                             # [257, 9]
+        _lib.call("toued_wgrad", 9, H + 1, M, _lib.ptr(self.DH), M, _lib.ptr(self.RH), M, _lib.ptr(Gh), ws, wn, st)
+        heads = Gh.t()                                                     # [257, 9]
         lay.view(grad, "pi_w").add_(heads[0:H, 0:1])
         lay.view(grad, "y_w").add_(heads[0:H, 1:9])
         lay.view(grad, "pi_b").add_(heads[H, 0:1])

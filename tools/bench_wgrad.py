@@ -25,20 +25,26 @@ def main():
     B = DG[0:3].reshape(768, M)
     res = {"M": M, "blas_pref": os.environ.get("TORCH_BLAS_PREFER_HIPBLASLT", "default")}
     res["mm_A_Bt"] = timed(lambda: torch.mm(A, B.t()))
-    res["mm_B_At_T"] = timed(lambda: torch.mm(B, A.t()))
-    K = 5
-    Ak = A.view(264, K, M // K).permute(1, 0, 2)
-    Bk = B.view(768, K, M // K).permute(1, 0, 2)
-    res["bmm5_sum"] = timed(lambda: torch.bmm(Ak, Bk.transpose(1, 2)).sum(0))
-    for ch in (8, 32):
-        Ac = A.view(264, ch, M // ch).permute(1, 0, 2)
-        Bc = B.view(768, ch, M // ch).permute(1, 0, 2)
-        res[f"bmm{ch}_sum"] = timed(lambda: torch.bmm(Ac, Bc.transpose(1, 2)).sum(0))
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "to-ued_amd"))
+    from toued import _lib as L
+    C = torch.empty(262, 768, device="cuda")
+    work = torch.empty(max(int(L.lib().toued_wgrad_workspace_floats(262, 768, M)),
+                           int(L.lib().toued_wgrad_workspace_floats(6, 256, M)),
+                           int(L.lib().toued_wgrad_workspace_floats(9, 257, M))), device="cuda")
+    res["toued_wgrad"] = timed(lambda: L.call("toued_wgrad", 262, 768, M, L.ptr(A), M, L.ptr(B), M, L.ptr(C), L.ptr(work), work.numel(), L.stream_ptr()))
+    ref = torch.mm(A[:262], B.t())
+    res["max_rel_vs_mm"] = float(((C - ref).abs().max() / ref.abs().max()))
     X6 = A[256:262]
     res["mm_Gn"] = timed(lambda: torch.mm(X6, DG[3].t()))
+    Cn = torch.empty(6, 256, device="cuda")
+    res["toued_Gn"] = timed(lambda: L.call("toued_wgrad", 6, 256, M, L.ptr(A) + 4 * 256 * M, M, L.ptr(DG[3]), M,
+                                           L.ptr(Cn), L.ptr(work), work.numel(), L.stream_ptr()))
     RH = torch.randn(257, M, device="cuda")
     DH = torch.randn(9, M, device="cuda")
     res["mm_heads"] = timed(lambda: torch.mm(RH, DH.t()))
+    Ch = torch.empty(9, 257, device="cuda")
+    res["toued_heads"] = timed(lambda: L.call("toued_wgrad", 9, 257, M, L.ptr(DH), M, L.ptr(RH), M, L.ptr(Ch),
+                                              L.ptr(work), work.numel(), L.stream_ptr()))
     flops = 2 * 264 * 768 * M
     res["tflops_mm_A_Bt"] = round(flops / (res["mm_A_Bt"] * 1e-3) / 1e12, 1)
     print(json.dumps(res), flush=True)
