@@ -39,6 +39,10 @@ GRU_FWD_FLOP_PER_ELEM = {5: 406080, 7: 409152}    # per (agent, w
 GRU_BWD_FLOP_PER_ELEM = 2 * 256 * 768              # dh_prev = dG . W_h^T per (k, agent, worker, t)
 
 
+# device kernel behind each timed region, as rocprofv3 names it (prof_summary.short)
+PROFILED_KERNEL = {"gru_fwd": "k_gru_fwd<true, 2>", "gru_bwd": "k_gru_bwd_g2"}
+
+
 def pmc_traffic(kernel: str):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*/pmc_traffic.json,
     written by tools/profile.sh + tools/prof_summary.py: FETCH_SIZE and WRITE_SIZE passes corrected by the
@@ -165,7 +169,7 @@ def main():
     if "gru_bwd" in ksum:
         cand.append(("gru_bwd", ksum["gru_bwd"][2], bwd_flops / (ksum["gru_bwd"][1] * 1e-3) / 1e12))
     dom = max(cand, key=lambda c: c[1])
-    traffic, traffic_src = pmc_traffic("k_" + dom[0])
+    traffic, traffic_src = pmc_traffic(PROFILED_KERNEL[dom[0]])
     roofline = {"bound": "mfma", "kernel": dom[0], "achieved": round(dom[2], 2), "peak": MFMA_F32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(dom[2] / MFMA_F32_PEAK_TFLOPS, 4), "traffic": traffic,
                 "traffic_unit": "bytes/launch", "traffic_source": traffic_src,

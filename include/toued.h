@@ -139,15 +139,17 @@ int toued_lpg_inputs(int N, int W, int T, int D, int F, const float* theta, cons
                      const float* eta_e1w, const float* eta_e1b, const float* eta_e2w, const float* eta_e2b,
                      const int* step, const int* levels, float* X, long xs_f, long xs_col, long eta_stride,
                      hipStream_t stream);
-/* lpg_agent_train_step gradients (lpg_agent.py:36-70) given pi_hat [T][R], y_hat [T][8][R] */
+/* lpg_agent_train_step gradients (lpg_agent.py:36-70) given pi_hat [T][R], y_hat [T][8][R], added to the
+ * zeroed tables Gth/Gph; also gstat[a] = {|G_theta|, |G_phi|, step + 1 <= lifetime} for toued_agent_apply */
 int toued_agent_grad(int N, int W, int T, int D, const float* theta, const float* phi, const int* tidx,
                      const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
                      const float* pi_hat, const float* y_hat, float alpha_y, float* Gth, float* Gph, float* met,
-                     hipStream_t stream);
-/* clipped SGD of actor [D][5] and LPG critic [D][8]; discard past the lifetime (lpg_agent.py:71-82) */
+                     const int* step, const int* levels, float* gstat, hipStream_t stream);
+/* clipped SGD of actor [D][5] and LPG critic [D][8] (lpg_agent.py:71-82) from the norms and the lifetime
+ * test toued_agent_grad left in gstat; advances step where the update applied */
 int toued_agent_apply(int N, int D, const float* th0, const float* ph0, const float* Gth, const float* Gph,
-                      float lr_a, float lr_c, float max_norm, int* step, const int* levels, float* th1, float* ph1,
-                      float* gstat, hipStream_t stream);
+                      float lr_a, float lr_c, float max_norm, int* step, float* th1, float* ph1, const float* gstat,
+                      hipStream_t stream);
 /* batch_rollout_entropy (util/metrics.py:5-9) metrics, or its gradient scaled by coef_a/coef_c */
 int toued_entropy(int N, int W, int T, int D, const float* theta, const float* phi, const int* tidx, const int* ttime,
                   float* met, float coef_a, float coef_c, float* adj_th, float* adj_ph, hipStream_t stream);

@@ -82,7 +82,7 @@ def test_env_reset_step_bitexact(mode):
     _assert_state(st, ost, spec)
     rs = np.random.RandomState(0)
     key = jr.PRNGKey(8)
-    for t in range(60):
+    for t in range(200):
         key, sk = jr.split(key)
         sk = jr.split(sk, B)
         act = rs.randint(0, 5, B).astype(np.int32)
@@ -97,7 +97,8 @@ def test_env_reset_step_bitexact(mode):
 
 
 @pytest.mark.parametrize("mode,W,T", [("dense", 64, 20), ("tabular", 64, 20), ("all_shortlife", 64, 30),
-                                      ("mazes", 64, 50), ("debug", 7, 13), ("sparse", 32, 25)])
+                                      ("mazes", 64, 50), ("debug", 7, 13), ("sparse", 32, 25),
+                                      ("all_shortlife", 8, 300), ("tabular", 8, 250)])
 def test_rollout_bitexact(mode, W, T):
     from toued.rollout import RolloutWrapper
     N = 12

@@ -80,6 +80,14 @@ TOUED_DEV void add_metric(float* met, int a, int slot, float v) {
   }
 }
 
+// gstat[a] = {|G_theta|, |G_phi|, applied}: applied = step + 1 <= lifetime (lpg_agent.py:71-82)
+TOUED_DEV void grad_stats(int a, float na2, float nc2, const int* step, const int* levels, float* gstat) {
+  gstat[a * 4 + 0] = sqrtf(na2);
+  gstat[a * 4 + 1] = sqrtf(nc2);
+  gstat[a * 4 + 2] = (step[a] + 1) <= levels[(size_t)a * LEVEL_WORDS + L_LIFETIME] ? 1.0f : 0.0f;
+  gstat[a * 4 + 3] = 0.0f;
+}
+
 struct SampleRef {
   int a, t, w, r, idx, idx1, act, done;
   float c, c1, rew;
@@ -257,15 +265,13 @@ __global__ void __launch_bounds__(256) k_agent_grad(int N, int W, int T, int D, 
 }
 
 // ---------------------------------------------------------------------------- apply (clipped SGD)
-// One block per agent.  gstat[a] = {|G_theta|, |G_phi|, applied}.
-__global__ void __launch_bounds__(256) k_agent_apply(int N, int D, const float* __restrict__ th0,
-                                                     const float* __restrict__ ph0, const float* __restrict__ Gth,
-                                                     const float* __restrict__ Gph, float lr_a, float lr_c,
-                                                     float max_norm, int* __restrict__ step,
-                                                     const int* __restrict__ levels, float* __restrict__ th1,
-                                                     float* __restrict__ ph1, float* __restrict__ gstat) {
+// Norms for the atomic gradient path (the sorted path computes them in the gradient kernel): one block per
+// agent, gstat[a] = {|G_theta|, |G_phi|, applied}.
+__global__ void __launch_bounds__(256) k_agent_norms(int N, int D, const float* __restrict__ Gth,
+                                                     const float* __restrict__ Gph, const int* __restrict__ step,
+                                                     const int* __restrict__ levels, float* __restrict__ gstat) {
   const int a = blockIdx.x;
-  __shared__ float red[2][8];
+  __shared__ float red[2][4];
   const size_t na = (size_t)D * 5, nc = (size_t)D * 8;
   const float* ga = Gth + (size_t)a * na;
   const float* gc = Gph + (size_t)a * nc;
@@ -274,33 +280,39 @@ __global__ void __launch_bounds__(256) k_agent_apply(int N, int D, const float* 
   for (size_t i = threadIdx.x; i < nc; i += blockDim.x) sc += gc[i] * gc[i];
   sa = wave_sum(sa);
   sc = wave_sum(sc);
-  const int wv = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { red[0][wv] = sa; red[1][wv] = sc; }
+  if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = sa; red[1][threadIdx.x >> 6] = sc; }
   __syncthreads();
-  float na2 = 0.0f, nc2 = 0.0f;
-  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) { na2 += red[0][i]; nc2 += red[1][i]; }
-  const float gna = sqrtf(na2), gnc = sqrtf(nc2);
-  const int st = step[a];
-  const bool applied = (st + 1) <= levels[(size_t)a * LEVEL_WORDS + L_LIFETIME];
-  const bool clip_a = !(gna < max_norm), clip_c = !(gnc < max_norm);
-  const float* pa0 = th0 + (size_t)a * na;
-  const float* pc0 = ph0 + (size_t)a * nc;
-  float* pa1 = th1 + (size_t)a * na;
-  float* pc1 = ph1 + (size_t)a * nc;
-  for (size_t i = threadIdx.x; i < na; i += blockDim.x) {
-    const float g = clip_a ? (ga[i] / gna) * max_norm : ga[i];
-    pa1[i] = applied ? pa0[i] + (-(lr_a * g)) : pa0[i];
-  }
-  for (size_t i = threadIdx.x; i < nc; i += blockDim.x) {
-    const float g = clip_c ? (gc[i] / gnc) * max_norm : gc[i];
-    pc1[i] = applied ? pc0[i] + (-(lr_c * g)) : pc0[i];
-  }
-  if (threadIdx.x == 0) {
-    gstat[a * 4 + 0] = gna;
-    gstat[a * 4 + 1] = gnc;
-    gstat[a * 4 + 2] = applied ? 1.0f : 0.0f;
-    step[a] = applied ? st + 1 : st;
-  }
+  if (threadIdx.x == 0)
+    grad_stats(a, red[0][0] + red[0][1] + red[0][2] + red[0][3], red[1][0] + red[1][1] + red[1][2] + red[1][3], step,
+               levels, gstat);
+}
+
+// th1 = applied ? th0 - lr * clip(G) : th0 over both tables, one element per thread (a streaming pass:
+// the norms and the lifetime test already sit in gstat).  The first element of an agent's actor table
+// advances its step.
+__global__ void __launch_bounds__(256) k_agent_apply(int N, int D, const float* __restrict__ th0,
+                                                     const float* __restrict__ ph0, const float* __restrict__ Gth,
+                                                     const float* __restrict__ Gph, float lr_a, float lr_c,
+                                                     float max_norm, int* __restrict__ step,
+                                                     float* __restrict__ th1, float* __restrict__ ph1,
+                                                     const float* __restrict__ gstat) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long na = (long)D * 5, nc = (long)D * 8;
+  const long ta = (long)N * na;
+  if (i >= ta + (long)N * nc) return;
+  const bool actor = i < ta;
+  const long j = actor ? i : i - ta;
+  const long per = actor ? na : nc;
+  const int a = (int)(j / per);
+  const float gn = gstat[a * 4 + (actor ? 0 : 1)];
+  const bool applied = gstat[a * 4 + 2] > 0.5f;
+  const float g0 = actor ? Gth[j] : Gph[j];
+  const float p0 = actor ? th0[j] : ph0[j];
+  const float lr = actor ? lr_a : lr_c;
+  const float g = !(gn < max_norm) ? (g0 / gn) * max_norm : g0;
+  const float p1 = applied ? p0 + (-(lr * g)) : p0;
+  if (actor) th1[j] = p1; else ph1[j] = p1;
+  if (actor && j - (long)a * na == 0 && applied) step[a] += 1;
 }
 
 // ---------------------------------------------------------------------------- entropy
@@ -467,23 +479,40 @@ __global__ void __launch_bounds__(256) k_lpgloss_grad(int N, int W, int T, int D
 
 // ---------------------------------------------------------------------------- clip VJP coefficients
 // coef[a] = {alpha_a, beta_a, alpha_c, beta_c}: gbar = alpha*u + beta*G with u = -lr * adjoint.
-__global__ void __launch_bounds__(256) k_clip_dot(int N, int D, const float* __restrict__ Gth,
-                                                  const float* __restrict__ Gph, const float* __restrict__ adj_th,
-                                                  const float* __restrict__ adj_ph, const float* __restrict__ gstat,
-                                                  float lr_a, float lr_c, float max_norm, float* __restrict__ coef) {
+__global__ void __launch_bounds__(1024) k_clip_dot(int N, int D, const float* __restrict__ Gth,
+                                                   const float* __restrict__ Gph, const float* __restrict__ adj_th,
+                                                   const float* __restrict__ adj_ph, const float* __restrict__ gstat,
+                                                   float lr_a, float lr_c, float max_norm, float* __restrict__ coef) {
   const int a = blockIdx.x;
-  __shared__ float red[2][8];
-  const size_t na = (size_t)D * 5, nc = (size_t)D * 8;
-  float da = 0.0f, dc = 0.0f;
-  for (size_t i = threadIdx.x; i < na; i += blockDim.x) da += Gth[(size_t)a * na + i] * adj_th[(size_t)a * na + i];
-  for (size_t i = threadIdx.x; i < nc; i += blockDim.x) dc += Gph[(size_t)a * nc + i] * adj_ph[(size_t)a * nc + i];
-  da = wave_sum(da);
-  dc = wave_sum(dc);
-  if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = da; red[1][threadIdx.x >> 6] = dc; }
+  __shared__ float red[2][16];
+  const long na = (long)D * 5, nc = (long)D * 8;
+  const float* ga = Gth + (long)a * na;
+  const float* ja = adj_th + (long)a * na;
+  const float* gc = Gph + (long)a * nc;
+  const float* jc = adj_ph + (long)a * nc;
+  // four independent partial sums per thread keep several loads in flight
+  float da[4] = {0.0f, 0.0f, 0.0f, 0.0f}, dc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (long i = threadIdx.x; i < na; i += 4 * 1024) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long e = i + u * 1024;
+      if (e < na) da[u] += ga[e] * ja[e];
+    }
+  }
+  for (long i = threadIdx.x; i < nc; i += 4 * 1024) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long e = i + u * 1024;
+      if (e < nc) dc[u] += gc[e] * jc[e];
+    }
+  }
+  float sa_ = wave_sum((da[0] + da[1]) + (da[2] + da[3]));
+  float sc_ = wave_sum((dc[0] + dc[1]) + (dc[2] + dc[3]));
+  if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = sa_; red[1][threadIdx.x >> 6] = sc_; }
   __syncthreads();
   if (threadIdx.x == 0) {
     float sa = 0.0f, sc = 0.0f;
-    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) { sa += red[0][i]; sc += red[1][i]; }
+    for (int i = 0; i < 16; ++i) { sa += red[0][i]; sc += red[1][i]; }
     const float gna = gstat[a * 4 + 0], gnc = gstat[a * 4 + 1];
     const bool applied = gstat[a * 4 + 2] > 0.5f;
     float aa = 0.0f, ba = 0.0f, ac = 0.0f, bc = 0.0f;
@@ -712,6 +741,426 @@ __global__ void __launch_bounds__(256) k_init_tables(const uint32_t* __restrict_
 }  // namespace
 
 // ============================================================================ C ABI
+// ---------------------------------------------------------------------------- sorted per-agent row scatter
+// The table gradients above scatter every sample's 5 + 8 row cotangents with float atomics (8.5M per call at
+// N=512, W=64, T=20).  For T*W <= 2048 the kernels below instead give each agent one workgroup: the
+// samples' row vectors go to LDS, their row indices are sorted (bitonic, key = row << 12 | sample), and one
+// thread per distinct row sums its segment in sample order and adds it to the table with a plain
+// read-modify-write (each row has exactly one writer in the grid).  Same sums, no atomics, and the result is
+// deterministic.  The time row (D-1, every sample contributes c * v) is a block reduction added by its
+// segment's owner (or thread 0).
+#define SORT_MAX_TW 2048
+
+struct GradOp {   // k_agent_grad (+ the global norms and the lifetime test of the update it feeds)
+  static constexpr int NA = 5, NC = 8, NM = 3;
+  static constexpr bool NORMS = true;
+  const float* theta; const float* phi; const int* tidx; const int* ttime; const uint8_t* tact; const float* trew;
+  const uint8_t* tdone; const float* pi_hat; const float* y_hat; float alpha_y; float* Gth; float* Gph; float* met;
+  const int* step; const int* levels; float* gstat;
+  int N, W, T, D;
+  TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* v, float* m) const {
+    const long s = ((long)a * T + t) * W + w;
+    const SampleRef q = load_sample(s, T, W, tidx, ttime, tact, trew, tdone, true);
+    const int R = N * W;
+    const float inv_wt = 1.0f / (float)(W * T);
+    const float* th = theta + (size_t)a * D * 5;
+    const float* ph = phi + (size_t)a * D * 8;
+    float lastA[5], lastC[8];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
+    float p[5], y[8], yh[8];
+    probs_of<5>(th, lastA, q.idx, q.c, p);
+    probs_of<8>(ph, lastC, q.idx, q.c, y);
+    const size_t o = (size_t)q.t * R + q.r;
+    const float pih = pi_hat[o];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) yh[j] = y_hat[((size_t)q.t * 8 + j) * R + q.r];
+    float pa = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) pa = (j == q.act) ? p[j] : pa;
+    const float rho = pa / (pa + EPSF);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) v[j] = pih * inv_wt * rho * ((j == q.act ? 1.0f : 0.0f) - p[j]);
+    float av[8], ya = 0.0f, kl = 0.0f, y2 = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float ly = __logf(y[j] + EPSF), lq = __logf(yh[j] + EPSF);
+      kl += y[j] * (ly - lq);
+      av[j] = ly - lq + y[j] / (y[j] + EPSF);
+      ya += y[j] * av[j];
+      y2 += yh[j] * yh[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[5 + j] = alpha_y * inv_wt * y[j] * (av[j] - ya);
+    m[0] = kl; m[1] = pih * pih; m[2] = y2;
+    idx = q.idx; c = q.c;
+    return true;
+  }
+  TOUED_DEV float* rowA(int a, int r) const { return Gth + ((size_t)a * D + r) * 5; }
+  TOUED_DEV float* rowC(int a, int r) const { return Gph + ((size_t)a * D + r) * 8; }
+  TOUED_DEV void metrics(int a, const float* m) const { for (int j = 0; j < NM; ++j) met[a * 8 + j] += m[j]; }
+  TOUED_DEV void finish(int a, float na2, float nc2) const { grad_stats(a, na2, nc2, step, levels, gstat); }
+};
+
+struct EntropyBwdOp {   // k_entropy, gradient mode
+  static constexpr int NA = 5, NC = 8, NM = 1;
+  static constexpr bool NORMS = false;
+  const float* theta; const float* phi; const int* tidx; const int* ttime; float coef_a, coef_c;
+  float* adj_th; float* adj_ph;
+  int N, W, T, D;
+  TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* v, float* m) const {
+    const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
+    idx = tidx[o0];
+    c = (float)ttime[o0] * 0.001f;
+    const float* th = theta + (size_t)a * D * 5;
+    const float* ph = phi + (size_t)a * D * 8;
+    float lastA[5], lastC[8];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
+    float p[5], y[8];
+    probs_of<5>(th, lastA, idx, c, p);
+    probs_of<8>(ph, lastC, idx, c, y);
+    float ga[5], gc[8];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) ga[j] = -(__logf(p[j] + EPSF) + 1.0f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gc[j] = -(__logf(y[j] + EPSF) + 1.0f);
+    const float inv_wt = 1.0f / (float)(W * T);
+    float pg = 0.0f, yg = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) pg += p[j] * ga[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) yg += y[j] * gc[j];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) v[j] = coef_a * inv_wt * p[j] * (ga[j] - pg);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[5 + j] = coef_c * inv_wt * y[j] * (gc[j] - yg);
+    m[0] = 0.0f;
+    return true;
+  }
+  TOUED_DEV float* rowA(int a, int r) const { return adj_th + ((size_t)a * D + r) * 5; }
+  TOUED_DEV float* rowC(int a, int r) const { return adj_ph + ((size_t)a * D + r) * 8; }
+  TOUED_DEV void metrics(int, const float*) const {}
+  TOUED_DEV void finish(int, float, float) const {}
+};
+
+struct LpgLossOp {   // k_lpgloss_grad
+  static constexpr int NA = 5, NC = 0, NM = 1;
+  static constexpr bool NORMS = false;
+  const float* theta; const int* tidx; const int* ttime; const uint8_t* tact; const float* abar; float* adj_th;
+  int N, W, T, D;
+  TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* v, float* m) const {
+    const long s = ((long)a * T + t) * W + w;
+    const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
+    idx = tidx[o0];
+    c = (float)ttime[o0] * 0.001f;
+    const float* th = theta + (size_t)a * D * 5;
+    float lastA[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
+    float p[5];
+    probs_of<5>(th, lastA, idx, c, p);
+    const int act = tact[s];
+    float pa = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) pa = (j == act) ? p[j] : pa;
+    const float rho = pa / (pa + EPSF);
+    const float kappa = -abar[(size_t)a * W + w] / (float)(W * T);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) v[j] = kappa * rho * ((j == act ? 1.0f : 0.0f) - p[j]);
+    m[0] = 0.0f;
+    return true;
+  }
+  TOUED_DEV float* rowA(int a, int r) const { return adj_th + ((size_t)a * D + r) * 5; }
+  TOUED_DEV float* rowC(int, int) const { return nullptr; }
+  TOUED_DEV void metrics(int, const float*) const {}
+  TOUED_DEV void finish(int, float, float) const {}
+};
+
+struct HvpOp {   // k_hvp
+  static constexpr int NA = 5, NC = 8, NM = 1;
+  static constexpr bool NORMS = false;
+  const float* theta; const float* phi; const int* tidx; const int* ttime; const uint8_t* tact;
+  const float* pi_hat; const float* y_hat; const float* Gth; const float* Gph; const float* adj_th_in;
+  const float* adj_ph_in; const float* coef; float lr_a, lr_c, alpha_y, b2, b3;
+  float* adj_th_out; float* adj_ph_out; float* d_pi_hat; float* d_y_hat;
+  int N, W, T, D, K;
+  TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* vout, float* m) const {
+    m[0] = 0.0f;
+    const long s = ((long)a * T + t) * W + w;
+    const int R = N * W, r = a * W + w;
+    const float inv_wt = 1.0f / (float)(W * T);
+    const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
+    idx = tidx[o0];
+    c = (float)ttime[o0] * 0.001f;
+    const int act = tact[s];
+    const size_t o = (size_t)t * R + r;
+    const float pih = pi_hat[o];
+    float yh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) yh[j] = y_hat[((size_t)t * 8 + j) * R + r];
+    float dpih = (b2 / (float)K) * 2.0f * pih * inv_wt;
+    float dyh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dyh[j] = (b3 / (float)K) * 2.0f * yh[j] * inv_wt;
+    const float aa = coef[a * 4 + 0], ba = coef[a * 4 + 1], ac = coef[a * 4 + 2], bc = coef[a * 4 + 3];
+    const bool applied = aa != 0.0f;
+    if (applied) {
+      const size_t baseA = (size_t)a * D * 5, baseC = (size_t)a * D * 8;
+      const float* th = theta + baseA;
+      const float* ph = phi + baseC;
+      float lastA[5], lastC[8];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
+      float p[5], y[8];
+      probs_of<5>(th, lastA, idx, c, p);
+      probs_of<8>(ph, lastC, idx, c, y);
+      float v[5];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const float adj = adj_th_in[baseA + (size_t)idx * 5 + j] + c * adj_th_in[baseA + (size_t)(D - 1) * 5 + j];
+        const float g = Gth[baseA + (size_t)idx * 5 + j] + c * Gth[baseA + (size_t)(D - 1) * 5 + j];
+        v[j] = -lr_a * aa * adj + ba * g;
+      }
+      float pa = 0.0f, va = 0.0f, pv = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        pa = (j == act) ? p[j] : pa;
+        va = (j == act) ? v[j] : va;
+        pv += p[j] * v[j];
+      }
+      const float rho = pa / (pa + EPSF);
+      dpih += inv_wt * rho * (va - pv);
+      const float ws = pih * inv_wt;
+      const float drs = EPSF * pa / ((pa + EPSF) * (pa + EPSF));
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const float drho = drs * ((k == act ? 1.0f : 0.0f) - p[k]);
+        vout[k] = ws * (drho * (va - pv) - rho * p[k] * (v[k] - pv));
+      }
+      float vc[8], av[8], ay = 0.0f, yv = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float adj = adj_ph_in[baseC + (size_t)idx * 8 + j] + c * adj_ph_in[baseC + (size_t)(D - 1) * 8 + j];
+        const float g = Gph[baseC + (size_t)idx * 8 + j] + c * Gph[baseC + (size_t)(D - 1) * 8 + j];
+        vc[j] = -lr_c * ac * adj + bc * g;
+        av[j] = __logf(y[j] + EPSF) - __logf(yh[j] + EPSF) + y[j] / (y[j] + EPSF);
+        ay += av[j] * y[j];
+        yv += y[j] * vc[j];
+      }
+      const float scale = alpha_y * inv_wt;
+      float sv[8], ys = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float b = vc[j] - yv;
+        dyh[j] += scale * (-y[j] * b / (yh[j] + EPSF));
+        const float ye = y[j] + EPSF;
+        const float adash = 1.0f / ye + EPSF / (ye * ye);
+        sv[j] = y[j] * b * adash + av[j] * b - vc[j] * ay;
+        ys += y[j] * sv[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vout[5 + j] = scale * y[j] * (sv[j] - ys);
+    }
+    d_pi_hat[o] = dpih;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d_y_hat[((size_t)t * 8 + j) * R + r] = dyh[j];
+    return applied;
+  }
+  TOUED_DEV float* rowA(int a, int r) const { return adj_th_out + ((size_t)a * D + r) * 5; }
+  TOUED_DEV float* rowC(int a, int r) const { return adj_ph_out + ((size_t)a * D + r) * 8; }
+  TOUED_DEV void metrics(int, const float*) const {}
+  TOUED_DEV void finish(int, float, float) const {}
+};
+
+// Stable sort of the 2048 keys (row << 12 | sample) in LDS: bitonic network in which every wave owns 256
+// contiguous keys, so the 60 of its 66 stages with partner distance j < 256 need only a wave barrier and
+// only the six with j >= 256 a workgroup barrier.
+TOUED_DEV void cmp_swap(uint32_t* key, int i, int j, int k) {
+  const int ij = i | j;
+  const uint32_t x = key[i], y = key[ij];
+  if ((x > y) == ((i & k) == 0)) { key[i] = y; key[ij] = x; }
+}
+
+TOUED_DEV void sort2048(uint32_t* key, int tid) {
+  const int lane = tid & 63, wv = tid >> 6;
+  for (int k = 2; k <= 2048; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const int lj = 31 - __builtin_clz(j);
+      if (j >= 256) {
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {       // 1024 pairs over 512 threads
+          const int pr = tid + 512 * h;
+          cmp_swap(key, ((pr >> lj) << (lj + 1)) | (pr & (j - 1)), j, k);
+        }
+        __syncthreads();
+      } else {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {       // this wave's 128 pairs
+          const int pr = lane + 64 * h;
+          cmp_swap(key, 256 * wv + (((pr >> lj) << (lj + 1)) | (pr & (j - 1))), j, k);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    }
+  }
+  __syncthreads();
+}
+
+template <class Op>
+__global__ void __launch_bounds__(512) k_rows_sorted(Op op) {
+  constexpr int NA = Op::NA, NC = Op::NC, NV = NA + NC, NM = Op::NM;
+  constexpr int NVP = (NV + 3) & ~3;          // vector stride in floats (16-byte aligned rows)
+  extern __shared__ float lds[];
+  __shared__ float red[8][NV + NM];
+  __shared__ float tot[NV + NM];
+  __shared__ int has_last;
+  uint32_t* key = reinterpret_cast<uint32_t*>(lds);   // [2048]
+  float* vec = lds + 2048;                            // [T*W][NVP]
+  const int a = blockIdx.x, tid = threadIdx.x, W = op.W, T = op.T, D = op.D, TW = T * W;
+  if (tid == 0) has_last = 0;
+  float part[NV + NM];
+#pragma unroll
+  for (int j = 0; j < NV + NM; ++j) part[j] = 0.0f;
+  __syncthreads();
+  // 1) per-sample row vectors -> LDS, sort keys, time-row and metric partial sums
+  for (int sl = tid; sl < 2048; sl += 512) {
+    uint32_t kk = 0xFFFFFFFFu;
+    if (sl < TW) {
+      const int t = sl / W, w = sl - t * W;
+      int idx;
+      float c, v[NV], m[NM];
+      if (op.sample(a, t, w, idx, c, v, m)) {
+        kk = ((uint32_t)idx << 12) | (uint32_t)sl;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) { vec[sl * NVP + j] = v[j]; part[j] += c * v[j]; }
+        if (idx == D - 1) has_last = 1;
+      }
+#pragma unroll
+      for (int j = 0; j < NM; ++j) part[NV + j] += m[j];
+    }
+    key[sl] = kk;
+  }
+#pragma unroll
+  for (int j = 0; j < NV + NM; ++j) {
+    const float r = wave_sum(part[j]);
+    if ((tid & 63) == 0) red[tid >> 6][j] = r;
+  }
+  __syncthreads();
+  if (tid < NV + NM) {
+    float r = 0.0f;
+    for (int w = 0; w < 8; ++w) r += red[w][tid];
+    tot[tid] = r;
+  }
+  // 2) sort by (row, sample)
+  sort2048(key, tid);
+  // 3) one thread per distinct row sums its segment in sample order and updates the table row
+  float na2 = 0.0f, nc2 = 0.0f;
+  for (int i = tid; i < TW; i += 512) {
+    const uint32_t kk = key[i];
+    if (kk == 0xFFFFFFFFu) continue;
+    const uint32_t row = kk >> 12;
+    if (i > 0 && (key[i - 1] >> 12) == row) continue;
+    float4 acc[NVP / 4];
+#pragma unroll
+    for (int j = 0; j < NVP / 4; ++j) acc[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int e = i; e < TW; ++e) {
+      const uint32_t ke = key[e];
+      if ((ke >> 12) != row || ke == 0xFFFFFFFFu) break;
+      const float4* ve = reinterpret_cast<const float4*>(vec + (ke & 4095u) * NVP);
+#pragma unroll
+      for (int j = 0; j < NVP / 4; ++j) {
+        const float4 x = ve[j];
+        acc[j].x += x.x; acc[j].y += x.y; acc[j].z += x.z; acc[j].w += x.w;
+      }
+    }
+    float sum[NVP];
+#pragma unroll
+    for (int j = 0; j < NVP / 4; ++j) {
+      sum[4 * j] = acc[j].x; sum[4 * j + 1] = acc[j].y; sum[4 * j + 2] = acc[j].z; sum[4 * j + 3] = acc[j].w;
+    }
+    if ((int)row == D - 1) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) sum[j] += tot[j];
+    }
+    float* ra = op.rowA(a, (int)row);
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const float g = ra[j] + sum[j];
+      ra[j] = g;
+      if (Op::NORMS) na2 += g * g;
+    }
+    if (NC > 0) {
+      float* rc = op.rowC(a, (int)row);
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        const float g = rc[j] + sum[NA + j];
+        rc[j] = g;
+        if (Op::NORMS) nc2 += g * g;
+      }
+    }
+  }
+  if (tid == 0) {
+    if (!has_last) {
+      float* ra = op.rowA(a, D - 1);
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        const float g = ra[j] + tot[j];
+        ra[j] = g;
+        if (Op::NORMS) na2 += g * g;
+      }
+      if (NC > 0) {
+        float* rc = op.rowC(a, D - 1);
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+          const float g = rc[j] + tot[NA + j];
+          rc[j] = g;
+          if (Op::NORMS) nc2 += g * g;
+        }
+      }
+    }
+    op.metrics(a, tot + NV);
+  }
+  if (Op::NORMS) {   // global norms of the (complete) gradient tables: every nonzero row was written above
+    na2 = wave_sum(na2);
+    nc2 = wave_sum(nc2);
+    __syncthreads();
+    if ((tid & 63) == 0) { red[tid >> 6][0] = na2; red[tid >> 6][1] = nc2; }
+    __syncthreads();
+    if (tid == 0) {
+      float x = 0.0f, y = 0.0f;
+      for (int w = 0; w < 8; ++w) { x += red[w][0]; y += red[w][1]; }
+      op.finish(a, x, y);
+    }
+  }
+}
+
+// launch the sorted variant when one agent's samples fit (T*W <= SORT_MAX_TW, D < 2^19); false otherwise
+template <class Op>
+static bool launch_sorted(const Op& op, int N, hipStream_t stream) {
+  const int TW = op.T * op.W;
+  if (TW > SORT_MAX_TW || TW <= 0 || op.D >= (1 << 20)) return false;
+  const size_t bytes = 2048 * 4 + (size_t)TW * (((Op::NA + Op::NC) + 3) & ~3) * 4;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rows_sorted<Op>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024) != hipSuccess)
+      return false;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k_rows_sorted<Op>, dim3(N), dim3(512), bytes, stream, op);
+  return true;
+}
+
 static inline unsigned nb256(long n) { return (unsigned)((n + 255) / 256); }
 
 extern "C" {
@@ -745,25 +1194,33 @@ int toued_lpg_inputs(int N, int W, int T, int D, int F, const float* theta, cons
 int toued_agent_grad(int N, int W, int T, int D, const float* theta, const float* phi, const int* tidx,
                      const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
                      const float* pi_hat, const float* y_hat, float alpha_y, float* Gth, float* Gph, float* met,
-                     hipStream_t stream) {
+                     const int* step, const int* levels, float* gstat, hipStream_t stream) {
+  TOUED_REQUIRE(step && levels && gstat, "toued_agent_grad: step, levels and gstat are required");
+  if (N == 0) return 0;
   const long n = (long)N * T * W;
-  if (n == 0) return 0;
-  if (W % 64 == 0)
-    hipLaunchKernelGGL(k_agent_grad<true>, dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, theta, phi, tidx, ttime,
-                       tact, trew, tdone, pi_hat, y_hat, alpha_y, Gth, Gph, met);
-  else
-    hipLaunchKernelGGL(k_agent_grad<false>, dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, theta, phi, tidx,
-                       ttime, tact, trew, tdone, pi_hat, y_hat, alpha_y, Gth, Gph, met);
+  if (n > 0) {
+    GradOp op{theta, phi, tidx, ttime, tact, trew, tdone, pi_hat, y_hat, alpha_y, Gth, Gph, met, step, levels, gstat,
+              N, W, T, D};
+    if (launch_sorted(op, N, stream)) { TOUED_CHECK_LAUNCH(); return 0; }
+    if (W % 64 == 0)
+      hipLaunchKernelGGL(k_agent_grad<true>, dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, theta, phi, tidx, ttime,
+                         tact, trew, tdone, pi_hat, y_hat, alpha_y, Gth, Gph, met);
+    else
+      hipLaunchKernelGGL(k_agent_grad<false>, dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, theta, phi, tidx,
+                         ttime, tact, trew, tdone, pi_hat, y_hat, alpha_y, Gth, Gph, met);
+  }
+  hipLaunchKernelGGL(k_agent_norms, dim3(N), dim3(256), 0, stream, N, D, Gth, Gph, step, levels, gstat);
   TOUED_CHECK_LAUNCH();
   return 0;
 }
 
 int toued_agent_apply(int N, int D, const float* th0, const float* ph0, const float* Gth, const float* Gph,
-                      float lr_a, float lr_c, float max_norm, int* step, const int* levels, float* th1, float* ph1,
-                      float* gstat, hipStream_t stream) {
-  if (N == 0) return 0;
-  hipLaunchKernelGGL(k_agent_apply, dim3(N), dim3(256), 0, stream, N, D, th0, ph0, Gth, Gph, lr_a, lr_c, max_norm,
-                     step, levels, th1, ph1, gstat);
+                      float lr_a, float lr_c, float max_norm, int* step, float* th1, float* ph1, const float* gstat,
+                      hipStream_t stream) {
+  if (N == 0 || D == 0) return 0;
+  const long tot = (long)N * D * 13;
+  hipLaunchKernelGGL(k_agent_apply, dim3(nb256(tot)), dim3(256), 0, stream, N, D, th0, ph0, Gth, Gph, lr_a, lr_c,
+                     max_norm, step, th1, ph1, gstat);
   TOUED_CHECK_LAUNCH();
   return 0;
 }
@@ -772,6 +1229,10 @@ int toued_entropy(int N, int W, int T, int D, const float* theta, const float* p
                   float* met, float coef_a, float coef_c, float* adj_th, float* adj_ph, hipStream_t stream) {
   const long n = (long)N * T * W;
   if (n == 0) return 0;
+  if (adj_th && !met) {
+    EntropyBwdOp op{theta, phi, tidx, ttime, coef_a, coef_c, adj_th, adj_ph, N, W, T, D};
+    if (launch_sorted(op, N, stream)) { TOUED_CHECK_LAUNCH(); return 0; }
+  }
   if (W % 64 == 0)
     hipLaunchKernelGGL(k_entropy<true>, dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, theta, phi, tidx, ttime,
                        met, coef_a, coef_c, adj_th, adj_ph);
@@ -796,6 +1257,10 @@ int toued_lpgloss_grad(int N, int W, int T, int D, const float* theta, const int
                        const uint8_t* tact, const float* abar, float* adj_th, hipStream_t stream) {
   const long n = (long)N * T * W;
   if (n == 0) return 0;
+  {
+    LpgLossOp op{theta, tidx, ttime, tact, abar, adj_th, N, W, T, D};
+    if (launch_sorted(op, N, stream)) { TOUED_CHECK_LAUNCH(); return 0; }
+  }
   if (W % 64 == 0)
     hipLaunchKernelGGL(k_lpgloss_grad<true>, dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, theta, tidx, ttime,
                        tact, abar, adj_th);
@@ -809,7 +1274,7 @@ int toued_lpgloss_grad(int N, int W, int T, int D, const float* theta, const int
 int toued_clip_dot(int N, int D, const float* Gth, const float* Gph, const float* adj_th, const float* adj_ph,
                    const float* gstat, float lr_a, float lr_c, float max_norm, float* coef, hipStream_t stream) {
   if (N == 0) return 0;
-  hipLaunchKernelGGL(k_clip_dot, dim3(N), dim3(256), 0, stream, N, D, Gth, Gph, adj_th, adj_ph, gstat, lr_a, lr_c,
+  hipLaunchKernelGGL(k_clip_dot, dim3(N), dim3(1024), 0, stream, N, D, Gth, Gph, adj_th, adj_ph, gstat, lr_a, lr_c,
                      max_norm, coef);
   TOUED_CHECK_LAUNCH();
   return 0;
@@ -822,6 +1287,11 @@ int toued_hvp(int N, int W, int T, int D, int K, const float* theta, const float
               float* d_y_hat, hipStream_t stream) {
   const long n = (long)N * T * W;
   if (n == 0) return 0;
+  {
+    HvpOp op{theta, phi, tidx, ttime, tact, pi_hat, y_hat, Gth, Gph, adj_th_in, adj_ph_in, coef, lr_a, lr_c, alpha_y,
+             b2, b3, adj_th_out, adj_ph_out, d_pi_hat, d_y_hat, N, W, T, D, K};
+    if (launch_sorted(op, N, stream)) { TOUED_CHECK_LAUNCH(); return 0; }
+  }
   if (W % 64 == 0)
     hipLaunchKernelGGL(k_hvp<true>, dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, K, theta, phi, tidx, ttime, tact,
                        pi_hat, y_hat, Gth, Gph, adj_th_in, adj_ph_in, coef, lr_a, lr_c, alpha_y, b2, b3, adj_th_out,

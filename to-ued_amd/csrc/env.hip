@@ -132,16 +132,12 @@ TOUED_DEV void reset_env(const EnvSpec& sp, const int* lev, uint2 key, EnvState&
   for (int i = 0; i < NMAX; ++i) s.obj[i] += lev_i(lev, L_OBJ_IDS + i) * G2;
 }
 
-// gymnax Environment.step -> step_env (gridworld.py:72-136) + auto-reset select.
-template <int NMAX, bool TAB>
+// gymnax Environment.step -> step_env (gridworld.py:72-136) + auto-reset select (RESET = false: the caller
+// discards the state after a done, so the reset and its key are skipped).
+template <int NMAX, bool TAB, bool RESET = true>
 TOUED_DEV void env_step(const EnvSpec& sp, const int* lev, uint2 key, EnvState& s, int action,
                         float& reward, bool& done) {
   const int G2 = sp.max_grid * sp.max_grid;
-  uint2 key_s, key_r;
-  split2(key, key_s, key_r);
-  uint2 term_key, respawn_key, obj_key;
-  split3(key_s, term_key, respawn_key, obj_key);
-
   const int pos = next_pos(lev, s.pos, action);
   int old[NMAX];
   int collected = 0;
@@ -150,13 +146,39 @@ TOUED_DEV void env_step(const EnvSpec& sp, const int* lev, uint2 key, EnvState& 
     old[i] = s.obj[i] - lev_i(lev, L_OBJ_IDS + i) * G2;
     if (((s.exists >> i) & 1) && old[i] == pos) collected |= 1 << i;
   }
-  // respawn = bernoulli(respawn_key, p_respawn[obj_ids]) over NMAX draws
+  const int nobj = lev_i(lev, L_NOBJS);
+  const int used = nobj >= 32 ? -1 : ((1 << nobj) - 1);
+  // The step's keys: (key_s, key_r) = split(key); (term, respawn, obj) = split(key_s, 3).  Only the
+  // threefry blocks whose outcome can change the result are evaluated (identical results, fewer calls):
+  //  * respawn draw i matters only while object i is missing (it is OR-ed into `exists`; with random
+  //    respawn it also picks the missing object's cell);
+  //  * the termination draw matters only when something was collected (p_t = 0 otherwise);
+  //  * key_r only on done.
+  // split(key): blocks d0 = (0,2), d1 = (1,3): key_s = (d0.x, d1.x), key_r = (d0.y, d1.y).
+  // split(key_s, 3): blocks c0 = (0,3), c1 = (1,4), c2 = (2,5): term = (c0.x, c1.x), respawn = (c2.x, c0.y),
+  // obj = (c1.y, c2.y).
+  const int miss = ~s.exists & (TAB ? used : -1) & ((1 << NMAX) - 1);
+  const bool need_term = collected != 0;
+  bool have_d = false, have_c1 = false;
+  uint2 d0 = make_uint2(0u, 0u), d1 = d0, c0 = d0, c1 = d0, c2 = d0;
+  if (need_term || miss != 0) {
+    d0 = threefry(key.x, key.y, 0u, 2u);
+    d1 = threefry(key.x, key.y, 1u, 3u);
+    have_d = true;
+    c0 = threefry(d0.x, d1.x, 0u, 3u);
+    if (miss != 0) c2 = threefry(d0.x, d1.x, 2u, 5u);
+    if (need_term) { c1 = threefry(d0.x, d1.x, 1u, 4u); have_c1 = true; }
+  }
+  // respawn = bernoulli(respawn_key, p_respawn[obj_ids]) over NMAX draws (block b covers draws b, b + nb)
   int respawn = 0;
-  {
+  if (miss != 0) {
+    const uint2 respawn_key = make_uint2(c2.x, c0.y);
     constexpr uint32_t nb = (NMAX + 1) / 2;
 #pragma unroll
     for (uint32_t b = 0; b < nb; ++b) {
       const uint32_t hi = b + nb;
+      const bool want = ((miss >> b) & 1) || (hi < (uint32_t)NMAX && ((miss >> hi) & 1));
+      if (!want) continue;
       const uint2 y = threefry(respawn_key.x, respawn_key.y, b, hi < (uint32_t)NMAX ? hi : 0u);
       const float u0 = bits_to_unit(y.x);
       if (u0 < lev_f(lev, L_PRESP + b)) respawn |= 1 << b;
@@ -173,6 +195,8 @@ TOUED_DEV void env_step(const EnvSpec& sp, const int* lev, uint2 key, EnvState& 
   if (!TAB) {
     const int use_new = (~s.exists) & respawn & ((1 << NMAX) - 1);
     if (lev_i(lev, L_RANDRESP) && use_new) {
+      if (!have_c1) c1 = threefry(d0.x, d1.x, 1u, 4u);
+      const uint2 obj_key = make_uint2(c1.y, c2.y);
       ValidCells vc = make_valid(lev, G2, pos);
 #pragma unroll
       for (int i = 0; i < NMAX; ++i) vc.excl[i] = old[i];
@@ -183,8 +207,6 @@ TOUED_DEV void env_step(const EnvSpec& sp, const int* lev, uint2 key, EnvState& 
       for (int i = 0; i < NMAX; ++i) if ((use_new >> i) & 1) newpos[i] = pick[i];
     }
   }
-  const int nobj = lev_i(lev, L_NOBJS);
-  const int used = nobj >= 32 ? -1 : ((1 << nobj) - 1);
   exists = exists & ~collected & used;
 
   float p_t = 0.0f, rew = 0.0f;
@@ -194,13 +216,19 @@ TOUED_DEV void env_step(const EnvSpec& sp, const int* lev, uint2 key, EnvState& 
     p_t = __fadd_rn(p_t, __fmul_rn(lev_f(lev, L_PTERM + i), ci));
     if ((collected >> i) & 1) rew = __fadd_rn(rew, lev_f(lev, L_REW + i));
   }
-  const float ut = bits_to_unit(bits1(term_key));
-  const int term = (ut < p_t) || s.early_term;
+  bool hit = false;
+  if (need_term) hit = bits_to_unit(threefry(c0.x, c1.x, 0u, 0u).x) < p_t;   // bits1(term_key)
+  const int term = hit || s.early_term;
   const int time = s.time + 1;
   done = (time >= lev_i(lev, L_MAX_STEPS)) || term;
   reward = rew;
   if (done) {
-    reset_env<NMAX, TAB>(sp, lev, key_r, s);
+    if (!RESET) return;
+    if (!have_d) {
+      d0 = threefry(key.x, key.y, 0u, 2u);
+      d1 = threefry(key.x, key.y, 1u, 3u);
+    }
+    reset_env<NMAX, TAB>(sp, lev, make_uint2(d0.y, d1.y), s);
   } else {
     s.time = time;
     s.pos = pos;
@@ -356,7 +384,10 @@ __global__ void __launch_bounds__(256) k_rollout(EnvSpec sp, const int* __restri
     const int action = choice5(sub, p);
     split2(rng, rng, sub);
     float r; bool d;
-    env_step<NMAX, TAB>(sp, lev, sub, s, action, r, d);
+    if (traj_idx)
+      env_step<NMAX, TAB>(sp, lev, sub, s, action, r, d);
+    else
+      env_step<NMAX, TAB, false>(sp, lev, sub, s, action, r, d);   // returns-only: the loop ends on done
     cum = __fadd_rn(cum, __fmul_rn(r, valid));
     valid = __fmul_rn(valid, d ? 0.0f : 1.0f);
     // returns-only mode (eval_agent): nothing after the first episode can change cum_return

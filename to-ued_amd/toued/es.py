@@ -174,10 +174,9 @@ class ESTrainStep:
             self.G_ph.zero_()
             L.call("toued_agent_grad", C, W, T, D, ptr(th), ptr(ph), ptr(tr.obs_idx), ptr(tr.obs_time),
                    ptr(tr.action), ptr(tr.reward), ptr(tr.done), ptr(self.pi_hat), ptr(self.y_hat), self.alpha_y,
-                   ptr(self.G_th), ptr(self.G_ph), ptr(self.met), st)
+                   ptr(self.G_th), ptr(self.G_ph), ptr(self.met), ptr(step), ptr(levels), ptr(self.gstat), st)
             L.call("toued_agent_apply", C, D, ptr(th), ptr(ph), ptr(self.G_th), ptr(self.G_ph), self.lr_a, self.lr_c,
-                   self.mn, ptr(step), ptr(levels), ptr(self.theta[1 - cur]), ptr(self.phi[1 - cur]),
-                   ptr(self.gstat), st)
+                   self.mn, ptr(step), ptr(self.theta[1 - cur]), ptr(self.phi[1 - cur]), ptr(self.gstat), st)
             cur = 1 - cur
             L.call("toued_entropy", C, W, T, D, ptr(self.theta[cur]), ptr(self.phi[cur]), ptr(tr.obs_idx),
                    ptr(tr.obs_time), ptr(self.met), 0.0, 0.0, None, None, st)

@@ -191,10 +191,10 @@ class MetaGradStep:
             L.call("toued_agent_grad", N, W, T, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(tk.obs_idx),
                    ptr(tk.obs_time), ptr(tk.action), ptr(tk.reward), ptr(tk.done), ptr(self.pi_hat[k]),
                    ptr(self.y_hat[k]), hyp.agent_target_coeff, ptr(self.G_th[k]), ptr(self.G_ph[k]),
-                   ptr(self.met[k]), st)
+                   ptr(self.met[k]), ptr(agents.step), ptr(agents.levels), ptr(self.gstat[k]), st)
             L.call("toued_agent_apply", N, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(self.G_th[k]),
                    ptr(self.G_ph[k]), hyp.actor_lr, hyp.critic_lr, hyp.max_grad_norm, ptr(agents.step),
-                   ptr(agents.levels), ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(self.gstat[k]), st)
+                   ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(self.gstat[k]), st)
             L.call("toued_entropy", N, W, T, D, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(tk.obs_idx),
                    ptr(tk.obs_time), ptr(self.met[k]), 0.0, 0.0, None, None, st)
         # ---------------- eval rollout + lpg loss (meta/train.py:98-145)

@@ -23,6 +23,8 @@ GIB = float(1 << 30)
 
 def short(name: str) -> str:
     n = name.replace("(anonymous namespace)::", "")
+    if n.startswith("void "):
+        n = n[5:]
     return n.split("(")[0]
 
 
