@@ -638,6 +638,9 @@ __global__ void __launch_bounds__(256) k_hvp(int N, int W, int T, int D, int K, 
 // ---------------------------------------------------------------------------- embedding MLP backward
 // grad layout (161 floats): e1_b[16], e1_w[8*16], e2_b[1], e2_w[16] (flat-eta order within MLP_0)
 // Inputs: y_t / y_tp1 recomputed from phi_k; cotangents dX3 (pyt), dX4 (pyt1, masked by done).
+// Four lanes per sample, each owning four of the 16 hidden units (41 accumulators per lane instead of 161:
+// occupancy); the quad recomputes the sample's critic output y.  Lane sums are reduced over the 16 samples
+// of a wave with cross-lane adds, then over the block; partial[block][161] in the flat layout below.
 template <bool UNIF>
 __global__ void __launch_bounds__(256) k_embed_bwd(int N, int W, int T, int D, int K, const float* __restrict__ phi_hist,
                                                    long phi_stride, const int* __restrict__ tidx_hist, long tidx_stride,
@@ -646,12 +649,26 @@ __global__ void __launch_bounds__(256) k_embed_bwd(int N, int W, int T, int D, i
                                                    const float* __restrict__ dX4, long dx_stride_k,
                                                    const float* __restrict__ e1w, const float* __restrict__ e1b,
                                                    const float* __restrict__ e2w, float* __restrict__ partial) {
-  float acc[161];
+  const int q = threadIdx.x & 3;                 // hidden units 4q .. 4q+3
+  float w1[8][4], b1[4], w2[4];
 #pragma unroll
-  for (int i = 0; i < 161; ++i) acc[i] = 0.0f;
+  for (int u = 0; u < 4; ++u) {
+    b1[u] = e1b[4 * q + u];
+    w2[u] = e2w[4 * q + u];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w1[i][u] = e1w[i * 16 + 4 * q + u];
+  }
+  float aw[8][4], ab[4], a2[4], ac = 0.0f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    ab[u] = 0.0f; a2[u] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) aw[i][u] = 0.0f;
+  }
   const long total = (long)K * N * T * W;
   const int R = N * W;
-  for (long g = (long)blockIdx.x * blockDim.x + threadIdx.x; g < total; g += (long)gridDim.x * blockDim.x) {
+  const long nthr = (long)gridDim.x * (blockDim.x >> 2);
+  for (long g = (long)blockIdx.x * (blockDim.x >> 2) + (threadIdx.x >> 2); g < total; g += nthr) {
     const int k = (int)(g / ((long)N * T * W));
     const long s = g - (long)k * N * T * W;
     const long at = s / W;
@@ -669,36 +686,53 @@ __global__ void __launch_bounds__(256) k_embed_bwd(int N, int W, int T, int D, i
     for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
     const size_t o = (size_t)k * dx_stride_k + (size_t)t * R + r;
     for (int which = 0; which < 2; ++which) {
-      float cg = which == 0 ? dX3[o] : (tdone[s] ? 0.0f : dX4[o]);
+      const float cg = which == 0 ? dX3[o] : (tdone[s] ? 0.0f : dX4[o]);
       if (cg == 0.0f) continue;
       float y[8];
       probs_of<8>(ph, lastC, which == 0 ? tidx[o0] : tidx[o0 + W],
                   (float)ttime[which == 0 ? o0 : o0 + W] * 0.001f, y);
-      acc[144] += cg;  // e2_b
+      if (q == 0) ac += cg;  // e2_b
 #pragma unroll
-      for (int h = 0; h < 16; ++h) {
-        float pre = e1b[h];
+      for (int u = 0; u < 4; ++u) {
+        float pre = b1[u];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) pre += y[i] * e1w[i * 16 + h];
+        for (int i = 0; i < 8; ++i) pre += y[i] * w1[i][u];
         const float hid = fmaxf(pre, 0.0f);
-        acc[145 + h] += hid * cg;  // e2_w
-        const float dh = pre > 0.0f ? e2w[h] * cg : 0.0f;
-        acc[h] += dh;  // e1_b
+        a2[u] += hid * cg;                               // e2_w
+        const float dh = pre > 0.0f ? w2[u] * cg : 0.0f;
+        ab[u] += dh;                                     // e1_b
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[16 + i * 16 + h] += y[i] * dh;  // e1_w
+        for (int i = 0; i < 8; ++i) aw[i][u] += y[i] * dh;   // e1_w
       }
     }
   }
+  // lanes with the same q: sum over the wave's 16 samples (xor 4, 8, 16, 32), then over the block's waves
+  auto qsum = [](float v) {
+#pragma unroll
+    for (int o = 4; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  };
   __shared__ float red[4][161];
-  const int wv = threadIdx.x >> 6;
-  for (int i = 0; i < 161; ++i) {
-    const float v = wave_sum(acc[i]);
-    if ((threadIdx.x & 63) == 0) red[wv][i] = v;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int h = 4 * q + u;
+    const float vb = qsum(ab[u]), v2 = qsum(a2[u]);
+    if (lane < 4) { red[wv][h] = vb; red[wv][145 + h] = v2; }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float vw = qsum(aw[i][u]);
+      if (lane < 4) red[wv][16 + i * 16 + h] = vw;
+    }
+  }
+  {
+    const float vc = qsum(ac);
+    if (lane == 0) red[wv][144] = vc;
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 161; i += blockDim.x) {
     float v = 0.0f;
-    for (int q = 0; q < (int)(blockDim.x >> 6); ++q) v += red[q][i];
+    for (int qq = 0; qq < (int)(blockDim.x >> 6); ++qq) v += red[qq][i];
     partial[(size_t)blockIdx.x * 161 + i] = v;
   }
 }

@@ -133,7 +133,7 @@ class MetaGradStep:
         self.gru = LPGGRU(self.lay, R, T, K, W, dev)
         self.X = self.gru.X                      # [F, K, T, R] view into the augmented GEMM operand
         self.grad = z(self.lay.size)
-        self.embed_blocks = 512
+        self.embed_blocks = 768
         self.embed_partial = z(self.embed_blocks, 161)
         self.ea_cum = None
         self.timers = KernelTimers()
