@@ -4,15 +4,26 @@
 // gradient [h_in; x; 1] . [dr; dz; dhn]^T, the input-gate gradient [x; 1] . dn^T and the head gradient
 // DH . [relu(h_out); 1]^T).
 //
-// Layout: one workgroup per (128-column tile of B rows, K chunk).  It holds ALL ra rows of A (NRT tiles of
-// 16 rows; ra <= 16 or ra <= 272) against its 128 B rows: every A k-slab is staged once through LDS (by
-// LDS-DMA, double-buffered; two workgroups per CU cover each other's slab waits) and read by the eight
-// waves (one 16-row B tile each), every B row streams from HBM exactly once per chunk.
-// The f32 16x16x4 MFMA (v_mfma_f32_16x16x4_f32, exact f32 fma, 32 cycles/SIMD) runs with the k order
-// permuted per lane: lane l (k-group g = l >> 4) covers k0 + 8g + e of a 32-k slab at step e, for A and B
-// alike, so each lane's B operands are two contiguous 16-byte loads per slab (full 128-byte lines per row).
+// Main reduction (ra <= 272, k_wgrad_x6): f32-accurate products on the bf16 matrix cores.  Every f32
+// operand is split exactly into three bf16 pieces, x = x0 + x1 + x2 (round-to-nearest at each stage; the
+// three 8-bit significands cover f32's 24), and a.b is formed from the six piece products whose weight is
+// at least 2^-16 of a0.b0: a0b0 + a0b1 + a1b0 + a0b2 + a1b1 + a2b0.  Every piece product is exact and the
+// MFMA accumulates in f32; the three dropped products are below 2^-24 relative, so the result carries the
+// error of an f32 GEMM (same test bound as the f32-MFMA kernel) at 6 x 16 = 96 bf16-MFMA cycles per
+// 32x16x16 block instead of the f32 MFMA's 256.
+// One 512-thread workgroup per (256 B rows, K chunk), one per CU: it stages each 32-k slab of ALL ra
+// A rows through LDS once (loaded as f32, split, written as three bf16 images, double-buffered, XOR-swizzled
+// for conflict-free 16-byte fragment reads) and each wave streams its own 32 B rows from HBM (split in
+// registers), so B is read exactly once per chunk.  v_mfma_f32_16x16x32_bf16, 17 A tiles x 2 B tiles of
+// accumulators per wave.
+//
+// Small reductions (ra <= 16, k_wgrad<1>): HBM-bound streams over B on the f32 16x16x4 MFMA, with the k
+// order permuted per lane (lane l, k-group g = l >> 4, covers k0 + 8g + e of a 32-k slab at step e) so each
+// lane's operands are two contiguous 16-byte loads per slab.  (k_wgrad<17> is the former f32 main kernel,
+// kept for comparison: TOUED_WGRAD_F32=1.)
 // Partial sums per K chunk go to a workspace and a second kernel adds them in chunk order: the result is
 // deterministic (no atomics).
+#include <stdlib.h>
 #include "common.h"
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -92,6 +103,188 @@ __global__ void __launch_bounds__(512, 2) k_wgrad(const float* __restrict__ A, l
     for (int r = 0; r < 4; ++r) out[(long)(16 * i + 4 * g + r) * rbp + brow] = acc[i][r];
 }
 
+// ------------------------------------------------------------------ f32-accurate bf16 split kernel
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int X6_RA = 272;          // A rows held (17 tiles of 16, zero-padded past ra)
+constexpr int X6_NW = 4;            // waves per workgroup: one per SIMD (512-register budget)
+constexpr int X6_BT = 3;            // B tiles of 16 rows per wave
+constexpr int X6_CT = 16 * X6_BT * X6_NW;   // B rows per workgroup (192)
+constexpr int X6_AQ = X6_RA * 8;    // float4 per 32-k A slab (2176)
+constexpr int X6_NS = (X6_AQ + 64 * X6_NW - 1) / (64 * X6_NW);   // staging rounds per thread (9)
+
+TOUED_DEV floatx4 mfma_bf(bf16x8 a, bf16x8 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// element e of the three pieces: x = p0 + p1 + p2 exactly (each stage rounds to nearest; the residual
+// subtractions are exact)
+template <typename V>
+TOUED_DEV void split3_bf16(float x, V& p0, V& p1, V& p2, int e) {
+  const __bf16 h = (__bf16)x;
+  const float r1 = x - (float)h;
+  const __bf16 m = (__bf16)r1;
+  p0[e] = h;
+  p1[e] = m;
+  p2[e] = (__bf16)(r1 - (float)m);
+}
+
+// LDS image of one 32-k A slab piece: [row][4 k-octets of 8 bf16], octet o of row r at slot o ^ ((r >> 2) & 3):
+// the 16 lanes of a fragment read (rows 16i + 0..15, one octet) then cover all 64 banks.
+TOUED_DEV int x6_slot(int row, int oct) { return row * 4 + (oct ^ ((row >> 2) & 3)); }
+
+// Software pipeline per 32-k slab s (A image `buf` in LDS, B pieces bp in registers):
+//   slab start: load the raw A slab s+1 (9 float4 per thread);
+//   A tile i (i = 0..16): issue the LDS fragment reads of tile i+1, then the 18 MFMAs of tile i (3 B tiles x 6
+//   piece products), interleaved one-for-one with the side work of that tile:
+//     tiles 0-5:  split half a B tile of slab s+1 (raw loads issued during slab s-1) into bpn;
+//     tile 6:     issue the raw B loads of slab s+2;
+//     tiles 8-16: split one staging round of A slab s+1 into the idle LDS image.
+//   barrier.  Loads run a slab ahead, LDS fragment reads a tile ahead, and every split hides under MFMAs.
+__global__ void __launch_bounds__(64 * X6_NW, 1) k_wgrad_x6(const float* __restrict__ A, long lda, int ra,
+                                                             const float* __restrict__ B, long ldb, int rb, long K,
+                                                             long kchunk, float* __restrict__ part) {
+  constexpr int NT = 64 * X6_NW;
+  // XCD-aware tile order: blocks b and b + 8 share an XCD (round-robin dealing), so block b takes linear slot
+  // L = (first slot of its XCD's contiguous range) + b / 8 and the ncol column tiles of one K chunk (consecutive
+  // L) run on one XCD, where they read each A slab through the same L2.
+  const int G = gridDim.x, ncol = (rb + X6_CT - 1) / X6_CT;
+  const int xcd = blockIdx.x & 7;
+  const int L = xcd * (G >> 3) + (xcd < (G & 7) ? xcd : (G & 7)) + (blockIdx.x >> 3);
+  static_assert(X6_NS == 9 && 2 * X6_BT <= 8, "schedule below: 9 staging rounds at tiles 8-16, B splits before");
+  __shared__ bf16x8 As[2][3][X6_RA * 4];   // [buffer][piece][slot]: 104,448 B
+  const int tid = threadIdx.x, lane = tid & 63, q16 = lane & 15, oct = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ct = L % ncol, sc = L / ncol;
+  const long kb = (long)sc * kchunk;
+  const long ke = kb + kchunk < K ? kb + kchunk : K;
+  const int nslab = (int)((ke - kb) / 32);
+  // this lane's B rows (tiles t): fragment = B[row][k0 + 8 oct .. +7] = two float4
+  const float4* Bp[X6_BT];
+  int brow[X6_BT];
+#pragma unroll
+  for (int t = 0; t < X6_BT; ++t) {
+    brow[t] = ct * X6_CT + 16 * (X6_BT * wave + t) + q16;
+    Bp[t] = reinterpret_cast<const float4*>(B + (long)(brow[t] < rb ? brow[t] : 0) * ldb + kb) + 2 * oct;
+  }
+  // A staging: float4 i = tid + NT j (row i >> 3, k-quad i & 7) of the slab.  The last round covers only part
+  // of the slab: the other threads repeat the element of their previous round (same address, same data) so
+  // that every load and LDS write is unconditional (no exec branch, no vmcnt(0) inside the loop).  Rows past
+  // ra repeat row ra-1: they only feed C rows that are never written out.
+  float4 ast[X6_NS];
+  auto a_index = [&](int j) {
+    const int i = tid + NT * j;
+    return j < X6_NS - 1 || i < X6_AQ ? i : i - NT;
+  };
+  auto load_a = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < X6_NS; ++j) {
+      const int i = a_index(j);
+      const int row = (i >> 3) < ra ? (i >> 3) : ra - 1;
+      ast[j] = *reinterpret_cast<const float4*>(A + (long)row * lda + kb + 32L * s + 4 * (i & 7));
+    }
+  };
+  auto write_a = [&](int buf, int j) {
+    const int i = a_index(j);
+    const int row = i >> 3, kq = i & 7;
+    const int slot = x6_slot(row, kq >> 1);
+    bf16x4 p[3];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split3_bf16(f4(ast[j], e), p[0], p[1], p[2], e);
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) reinterpret_cast<bf16x4*>(&As[buf][pc][slot])[kq & 1] = p[pc];
+  };
+  float4 bq[X6_BT][2];
+  auto issue_b = [&](int s) {
+#pragma unroll
+    for (int t = 0; t < X6_BT; ++t) { bq[t][0] = Bp[t][8 * s]; bq[t][1] = Bp[t][8 * s + 1]; }
+  };
+  auto split_b = [&](bf16x8 (&dst)[X6_BT][3], int t, int half) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split3_bf16(f4(bq[t][half], e), dst[t][0], dst[t][1], dst[t][2], 4 * half + e);
+  };
+  floatx4 acc[17][X6_BT];
+#pragma unroll
+  for (int i = 0; i < 17; ++i)
+#pragma unroll
+    for (int t = 0; t < X6_BT; ++t) acc[i][t] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+
+  auto slab = [&](int s, bf16x8 (&bp)[X6_BT][3], bf16x8 (&bpn)[X6_BT][3]) {
+    const int buf = s & 1;
+    load_a(s + 1 < nslab ? s + 1 : s);
+    const bf16x8* a0p = As[buf][0];
+    const bf16x8* a1p = As[buf][1];
+    const bf16x8* a2p = As[buf][2];
+    bf16x8 a[3];
+    {
+      const int slot = x6_slot(q16, oct);
+      a[0] = a0p[slot]; a[1] = a1p[slot]; a[2] = a2p[slot];
+    }
+#pragma unroll
+    for (int i = 0; i < 17; ++i) {
+      bf16x8 an[3];
+      if (i + 1 < 17) {
+        const int slot = x6_slot(16 * (i + 1) + q16, oct);
+        an[0] = a0p[slot]; an[1] = a1p[slot]; an[2] = a2p[slot];
+      }
+#pragma unroll
+      for (int t = 0; t < X6_BT; ++t) {
+        floatx4 c = acc[i][t];
+        c = mfma_bf(a[2], bp[t][0], c);
+        c = mfma_bf(a[1], bp[t][1], c);
+        c = mfma_bf(a[0], bp[t][2], c);
+        c = mfma_bf(a[1], bp[t][0], c);
+        c = mfma_bf(a[0], bp[t][1], c);
+        c = mfma_bf(a[0], bp[t][0], c);
+        acc[i][t] = c;
+      }
+      if (i < 2 * X6_BT) split_b(bpn, i >> 1, i & 1);
+      if (i == 2 * X6_BT) issue_b(s + 2 < nslab ? s + 2 : nslab - 1);
+      if (i >= 8) write_a(buf ^ 1, i - 8);
+      if (i + 1 < 17) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);   // next tile's fragment reads first
+      }
+#pragma unroll
+      for (int m = 0; m < 6 * X6_BT; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);   // one VALU of the side work
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (i + 1 < 17) { a[0] = an[0]; a[1] = an[1]; a[2] = an[2]; }
+    }
+    __syncthreads();
+  };
+
+  bf16x8 bpa[X6_BT][3], bpb[X6_BT][3];
+  if (nslab > 0) {
+    load_a(0);
+    issue_b(0);
+#pragma unroll
+    for (int j = 0; j < X6_NS; ++j) write_a(0, j);
+#pragma unroll
+    for (int t = 0; t < X6_BT; ++t) { split_b(bpa, t, 0); split_b(bpa, t, 1); }
+    issue_b(nslab > 1 ? 1 : 0);
+  }
+  __syncthreads();
+  for (int s = 0; s < nslab; ++s) {
+    slab(s, bpa, bpb);
+#pragma unroll
+    for (int t = 0; t < X6_BT; ++t)
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc) bpa[t][pc] = bpb[t][pc];   // (a two-slab unrolled swap spills)
+  }
+  // D map: lane l, reg r -> C[16i + 4 oct + r][brow]
+  const int rbp = ncol * X6_CT;
+  float* out = part + (long)sc * X6_RA * rbp;
+#pragma unroll
+  for (int t = 0; t < X6_BT; ++t)
+#pragma unroll
+    for (int i = 0; i < 17; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(long)(16 * i + 4 * oct + r) * rbp + brow[t]] = acc[i][t][r];
+}
+
 // C[i][j] = sum over chunks (in chunk order) of part[s][i][j], i < ra, j < rb
 __global__ void k_wgrad_reduce(const float* __restrict__ part, int S, int RA, int rbp, int ra, int rb,
                                float* __restrict__ C) {
@@ -104,22 +297,34 @@ __global__ void k_wgrad_reduce(const float* __restrict__ part, int S, int RA, in
 }
 
 struct Plan {
-  int nrt, ncol, S;
+  int nrt, ncol, S, ct;   // ct: B rows per workgroup (column-tile width of the partial-sum workspace)
+  bool x6;
   long kchunk;
 };
+
+static bool wgrad_f32_forced() {
+  static const bool f = [] {
+    const char* e = getenv("TOUED_WGRAD_F32");
+    return e && e[0] == '1';
+  }();
+  return f;
+}
 
 static Plan plan(int ra, int rb, long K) {
   Plan p;
   p.nrt = ra <= 16 ? 1 : 17;
-  p.ncol = (rb + 127) / 128;
+  p.x6 = p.nrt == 17 && !wgrad_f32_forced();
+  p.ct = p.x6 ? X6_CT : 128;
+  p.ncol = (rb + p.ct - 1) / p.ct;
   int cus = 256;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
     cus = 256;
-  // NRT = 17: two workgroups per CU (125 VGPRs, 68 KB LDS each), as many K chunks as fill them in one
-  // round.  NRT = 1 is a bandwidth-bound stream over B: four workgroups per CU keep enough loads in flight.
-  int S = (p.nrt == 1 ? 4 : 2) * cus / p.ncol;
+  // x6: one workgroup per CU (104 KB LDS), as many K chunks as fill the CUs in one round.  f32 NRT = 17:
+  // two workgroups per CU (125 VGPRs, 68 KB LDS each).  NRT = 1 is a bandwidth-bound stream over B: four
+  // workgroups per CU keep enough loads in flight.
+  int S = (p.x6 ? 1 : p.nrt == 1 ? 4 : 2) * cus / p.ncol;
   if (S < 1) S = 1;
   long slabs = K / 32;
   if (S > slabs) S = (int)(slabs > 0 ? slabs : 1);
@@ -136,7 +341,7 @@ extern "C" {
 size_t toued_wgrad_workspace_floats(int ra, int rb, long K) {
   if (ra <= 0 || rb <= 0 || K <= 0) return 0;
   const Plan p = plan(ra, rb, K);
-  return (size_t)p.S * p.nrt * 16 * p.ncol * 128;
+  return (size_t)p.S * p.nrt * 16 * p.ncol * p.ct;
 }
 
 int toued_wgrad(int ra, int rb, long K, const float* A, long lda, const float* B, long ldb, float* C, float* work,
@@ -151,16 +356,18 @@ int toued_wgrad(int ra, int rb, long K, const float* A, long lda, const float* B
     return 0;
   }
   const Plan p = plan(ra, rb, K);
-  const size_t need = (size_t)p.S * p.nrt * 16 * p.ncol * 128;
+  const size_t need = (size_t)p.S * p.nrt * 16 * p.ncol * p.ct;
   TOUED_REQUIRE(work && work_floats >= need, "toued_wgrad: workspace of %zu floats needed (got %zu)", need, work_floats);
   const dim3 grid(p.ncol, p.S);
-  if (p.nrt == 1)
+  if (p.x6)
+    hipLaunchKernelGGL(k_wgrad_x6, dim3(p.ncol * p.S), dim3(64 * X6_NW), 0, stream, A, lda, ra, B, ldb, rb, K, p.kchunk, work);
+  else if (p.nrt == 1)
     hipLaunchKernelGGL(k_wgrad<1>, grid, dim3(512), 0, stream, A, lda, ra, B, ldb, rb, K, p.kchunk, work);
   else
     hipLaunchKernelGGL(k_wgrad<17>, grid, dim3(512), 0, stream, A, lda, ra, B, ldb, rb, K, p.kchunk, work);
   const long n = (long)ra * rb;
   hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, work, p.S, p.nrt * 16,
-                     p.ncol * 128, ra, rb, C);
+                     p.ncol * p.ct, ra, rb, C);
   TOUED_CHECK_LAUNCH();
   return 0;
 }
