@@ -70,7 +70,7 @@ def test_gru_fwd_multi_per_candidate():
     lay = LPGLayout(F)
     etas = torch.stack([init_lpg_params(10 + c, F) + torch.randn(lay.size, device="cuda") * 0.05
                         for c in range(C)]).contiguous()
-    fwdA = torch.zeros(C, _lib.lib().toued_gru_packed_floats(0), device="cuda")
+    fwdA = torch.zeros(C, _lib.lib().toued_gru_packed_floats(2), device="cuda")
     _lib.call("toued_gru_pack_fwd_multi", _lib.ptr(etas), lay.size, C, lay.c_offsets, F, _lib.ptr(fwdA),
               _lib.stream_ptr())
     rs = np.random.RandomState(0)

@@ -26,6 +26,7 @@
 // MFMA f32 32x32x2 operand/result maps (cdna_hip_programming.md §3):
 //   A: lane l holds A[i = l&31][k = l>>5];  B: lane l holds B[k = l>>5][j = l&31]
 //   D: reg q of lane l is D[i = (q&3) + 8*(q>>2) + 4*(l>>5)][j = l&31]
+#include <stdlib.h>
 #include <string.h>
 #include "common.h"
 
@@ -99,6 +100,12 @@ TOUED_DEV void st4(__amdgpu_buffer_rsrc_t r, unsigned vbyte, unsigned soff, cons
 }
 
 TOUED_DEV float sigm(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// v_rcp_f32 (1 ulp) instead of the IEEE division sequence: the forward's gate maths is on the critical path
+TOUED_DEV float sigm_r(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+TOUED_DEV float tanh_r(float x) {
+  const float e = __expf(-2.0f * fabsf(x));
+  return copysignf((1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e), x);
+}
 TOUED_DEV float tanh_f(float x) {
   const float e = __expf(-2.0f * fabsf(x));
   const float t = (1.0f - e) / (1.0f + e);
@@ -178,7 +185,8 @@ struct FwdArgs {
   int R, T, W, F;
   const float* X; long xs_f, xs_col;   // X[f*xs_f + (t*R + r)*xs_col]
   const uint8_t* done;                 // [N][T][W]
-  const float4* A;                     // packed fwd fragments
+  const float4* A;                     // packed fwd fragments (f32 MFMA)
+  const void* A6;                      // packed fwd fragments (bf16 split pieces, k_gru_fwd6)
   const float* eta; EtaOff o;
   float* pi_hat; float* y_hat;         // [T][R], [T][8][R]
   float* s_hin; float* s_r; float* s_z; float* s_n; float* s_hn;  // [256][M] with column base added
@@ -343,6 +351,280 @@ __global__ void __launch_bounds__(512, NT == 1 ? 4 : 1) k_gru_fwd(FwdArgs p) {
       for (int j = 0; j < 8; ++j) p.y_hat[((long)t * 8 + j) * R + r0 + tid] = e[j] * inv;
     }
     __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ forward on the bf16 matrix cores
+// f32-accurate split products (as csrc/wgrad.hip): every f32 operand is split exactly into three bf16 pieces
+// x = x0 + x1 + x2, and a.b is formed from the six piece products of weight >= 2^-16 of a0.b0 (a0b0, a0b1,
+// a1b0, a0b2, a1b1, a2b0) on v_mfma_f32_32x32x16_bf16 with f32 accumulation: the three dropped products are
+// below 2^-24 relative, so the pre-activations carry f32 GEMM error at 6 x 32 = 192 cycles per 32x32x16
+// block instead of the f32 MFMA's 512.
+//
+// One 256-thread workgroup (one wave per SIMD, 512 registers) owns 64 rows (two 32-row tiles) for the whole
+// T-step scan; wave w owns units [64w, 64w + 64) (two 32-unit tiles j), so its accumulators are
+// {r, z, W_hn h + b_hn, W_in x + b_in} x 2 unit tiles x 2 row tiles (256 AGPRs).  Per step:
+//   contraction over k = 256 h units (16 k-steps of 16) + one augmented k-step [x (F <= 7); 1; 0...]:
+//     A fragments (weights, pre-split and packed by k_pack_fwd6, 16 B per lane and piece) stream from L2 one
+//     k-step ahead; B fragments (the carry h, three bf16 images [row][unit] in LDS, 528-byte rows: the 16
+//     lanes of a read hit 16 distinct bank quads) are read one k-step ahead; each A fragment feeds both row
+//     tiles;
+//   barrier; gate maths in the accumulator layout (lane = row, register = unit); h_in rebuilt exactly from
+//   its pieces ((h0 + h1) + h2 == h); the new carry split and written back in place (each (row, unit) has
+//   one owner lane); saves r, z, n, W_hn h + b_hn, h_in for the backward; head partials;
+//   barrier; head reduce + softmax.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+#define F6_HP 264        // carry image row pitch (bf16): 528 B
+#define F6_AP 24         // augmented-row image pitch (bf16): 48 B
+#define F6_NFH (16 * 8 * 3 * 3)     // h-part fragments [ks][unit tile][gate r|z|hn][piece], 1 KiB each
+#define F6_NFA (8 * 4 * 3)          // augmented fragments [unit tile][gate r|z|hn|ni][piece]
+#define F6_FLOATS ((F6_NFH + F6_NFA) * 256)   // packed size in floats (1 KiB = 256 floats)
+
+template <typename V>
+TOUED_DEV void split3v(float x, V& p0, V& p1, V& p2, int e) {
+  const __bf16 h = (__bf16)x;
+  const float r1 = x - (float)h;
+  const __bf16 m = (__bf16)r1;
+  p0[e] = h;
+  p1[e] = m;
+  p2[e] = (__bf16)(r1 - (float)m);
+}
+
+// one thread per (fragment group, lane): fragment group = (ks, ut, g) for the h part or (ut, g) for the
+// augmented rows; lane l holds A[i = unit 32 ut + (l & 31)][k = 8 (l >> 5) + e], e = 0..7
+__global__ void k_pack_fwd6(const float* __restrict__ eta, EtaOff o, int F, bf16x8* __restrict__ out) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ngrp_h = 16 * 8 * 3, ngrp = ngrp_h + 8 * 4;
+  if (gid >= ngrp * 64) return;
+  const int lane = gid & 63, grp = gid >> 6;
+  bf16x8 pc[3];
+  int fbase;
+  if (grp < ngrp_h) {
+    const int g = grp % 3, ut = (grp / 3) % 8, ks = grp / 24;
+    const int u = 32 * ut + (lane & 31);
+    const int base = g == 0 ? o.hr_w : g == 1 ? o.hz_w : o.hn_w;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 16 * ks + 8 * (lane >> 5) + e;
+      split3v(eta[base + k * HU + u], pc[0], pc[1], pc[2], e);
+    }
+    fbase = grp * 3;
+  } else {
+    const int ga = grp - ngrp_h, g = ga % 4, ut = ga / 4;
+    const int u = 32 * ut + (lane & 31);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int f = 8 * (lane >> 5) + e;
+      float x = 0.0f;
+      if (f < F) {
+        if (g == 0) x = eta[o.ir_w + f * HU + u];
+        else if (g == 1) x = eta[o.iz_w + f * HU + u];
+        else if (g == 3) x = eta[o.in_w + f * HU + u];
+      } else if (f == F) {
+        x = g == 0 ? eta[o.ir_b + u] : g == 1 ? eta[o.iz_b + u] : g == 2 ? eta[o.hn_b + u] : eta[o.in_b + u];
+      }
+      split3v(x, pc[0], pc[1], pc[2], e);
+    }
+    fbase = F6_NFH + ga * 3;
+  }
+#pragma unroll
+  for (int q = 0; q < 3; ++q) out[(long)(fbase + q) * 64 + lane] = pc[q];
+}
+
+TOUED_DEV floatx16 mfma_bf32(bf16x8 a, bf16x8 b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+// a.b from the pieces, smallest products first
+TOUED_DEV floatx16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx16 c) {
+  c = mfma_bf32(a[2], b[0], c);
+  c = mfma_bf32(a[1], b[1], c);
+  c = mfma_bf32(a[0], b[2], c);
+  c = mfma_bf32(a[1], b[0], c);
+  c = mfma_bf32(a[0], b[1], c);
+  c = mfma_bf32(a[0], b[0], c);
+  return c;
+}
+
+__global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
+  __shared__ __attribute__((aligned(16))) __bf16 hB[3][64 * F6_HP];   // carry h(t) pieces [row][unit]
+  __shared__ __attribute__((aligned(16))) __bf16 xB[3][64 * F6_AP];   // [x(t); 1; 0] pieces [row][16]
+  __shared__ __attribute__((aligned(16))) float wh[HU * 12];          // head weights [unit][pi | y0..y7 | pad]
+  __shared__ float hp[8 * 9 * 64];      // head partials [wave][output][row]
+  __shared__ float hout[9 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, hi = lane >> 5, col = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r0 = blockIdx.x * 64;
+  const int R = p.R, T = p.T, W = p.W, F = p.F;
+  int a_[2], w_[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    a_[h] = (r0 + RB * h) / W;
+    w_[h] = r0 + RB * h + col - a_[h] * W;
+  }
+  const float* eta = p.eta;
+  for (int i = tid; i < HU * 12; i += 512) {
+    const int u = i / 12, oo = i - u * 12;
+    wh[i] = oo == 0 ? eta[p.o.pi_w + u] : oo < 9 ? eta[p.o.y_w + u * 8 + (oo - 1)] : 0.0f;
+  }
+  {
+    uint4* z = reinterpret_cast<uint4*>(&hB[0][0]);
+    for (int i = tid; i < 3 * 64 * F6_HP / 8; i += 512) z[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  // x(t) of row `row` -> the augmented image: [x_0 .. x_{F-1}, 1, 0 ...]
+  auto write_x = [&](int t, int row) {
+    bf16x8 pc[2][3];
+#pragma unroll
+    for (int f = 0; f < 16; ++f) {
+      const float v = f < F ? p.X[f * p.xs_f + ((size_t)t * R + r0 + row) * p.xs_col] : (f == F ? 1.0f : 0.0f);
+      split3v(v, pc[f >> 3][0], pc[f >> 3][1], pc[f >> 3][2], f & 7);
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      bf16x8* d = reinterpret_cast<bf16x8*>(&xB[q][row * F6_AP]);
+      d[0] = pc[0][q];
+      d[1] = pc[1][q];
+    }
+  };
+  if (tid < 64) write_x(T - 1, tid);
+  __syncthreads();
+  const float bpi = eta[p.o.pi_b];
+  const __amdgpu_buffer_rsrc_t rs_A = rsrc_of(reinterpret_cast<const float*>(p.A6));
+  const unsigned vA = (unsigned)lane * 16;
+  auto ldA = [&](int frag) {
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs_A, (int)vA, frag * 1024, 0);
+    return __builtin_bit_cast(bf16x8, x);
+  };
+  const __amdgpu_buffer_rsrc_t rs_hin = rsrc_of(p.s_hin), rs_r = rsrc_of(p.s_r), rs_z = rsrc_of(p.s_z),
+                               rs_n = rsrc_of(p.s_n), rs_hn = rsrc_of(p.s_hn);
+  for (int s = 0; s < T; ++s) {
+    const int t = T - 1 - s;
+    floatx16 acc[4][2];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[g][h][q] = 0.0f;
+    // ---- contraction: 17 k-steps.  Each gate's A fragments (unit tile `wave`) are refilled for the next
+    // k-step right after their last MFMA, each row tile's B fragments right after theirs; the partner wave on
+    // the SIMD covers what latency remains.
+    bf16x8 A[3][3], B[2][3];
+    auto fragA = [&](int ks, int g, int q) {
+      return ks < 16 ? ((ks * 8 + wave) * 3 + g) * 3 + q : F6_NFH + (wave * 4 + g) * 3 + q;
+    };
+    auto load_B = [&](int ks, int h) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        B[h][q] = ks < 16 ? *reinterpret_cast<const bf16x8*>(&hB[q][(RB * h + col) * F6_HP + 16 * ks + 8 * hi])
+                          : *reinterpret_cast<const bf16x8*>(&xB[q][(RB * h + col) * F6_AP + 8 * hi]);
+    };
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) A[g][q] = ldA(fragA(0, g, q));
+    load_B(0, 0);
+    load_B(0, 1);
+    // (a rolled loop: a full unroll hoists ~300 fragment offsets into SGPRs, which spill)
+#pragma nounroll
+    for (int ks = 0; ks < 16; ++ks) {
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          acc[g][h] = mfma6(A[g], B[h], acc[g][h]);
+          if (g == 2) load_B(ks + 1, h);
+        }
+#pragma unroll
+        for (int q = 0; q < 3; ++q) A[g][q] = ldA(fragA(ks + 1, g, q));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // augmented k-step: r, z, hn fragments in A; the ni gate's go into A[0] once r's MFMAs are issued
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) acc[g][h] = mfma6(A[g], B[h], acc[g][h]);
+      if (g == 0) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) A[0][q] = ldA(fragA(16, 3, q));
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) acc[3][h] = mfma6(A[0], B[h], acc[3][h]);
+    __syncthreads();   // every wave done reading hB / xB: the carry and x(t-1) overwrite them in place
+    if (t >= 1 && tid < 64) write_x(t - 1, tid);
+    // ---- gate maths (lane = row 32h + col, register q = unit 32 wave + 4 hi + qunit(q))
+    const long cbase = (long)t * R;
+    const int ub = 32 * wave + 4 * hi;
+    const float4* whl = reinterpret_cast<const float4*>(wh + ub * 12);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = RB * h + col;
+      const bool dn = (t >= 1) ? p.done[((size_t)a_[h] * T + (t - 1)) * W + w_[h]] != 0 : false;
+      const unsigned vbyte = (unsigned)(((long)ub * p.M + r0 + row) * 4);
+      float hp_loc[9];
+#pragma unroll
+      for (int oo = 0; oo < 9; ++oo) hp_loc[oo] = 0.0f;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        // four consecutive units ub + 8 g4 .. +3 of this row: h_in pieces, then the new carry's pieces
+        bf16x4 hq[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) hq[q] = *reinterpret_cast<const bf16x4*>(&hB[q][row * F6_HP + ub + 8 * g4]);
+        bf16x4 nq[3];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int q = 4 * g4 + e;
+          const float rg = sigm_r(acc[0][h][q]);
+          const float zg = sigm_r(acc[1][h][q]);
+          const float hn = acc[2][h][q];
+          const float ng = tanh_r(acc[3][h][q] + rg * hn);
+          const float hin = ((float)hq[0][e] + (float)hq[1][e]) + (float)hq[2][e];   // exact
+          const float hh = (1.0f - zg) * ng + zg * hin;
+          split3v(dn ? 0.0f : hh, nq[0], nq[1], nq[2], e);   // carry h_in(t-1) = where(d_{t-1}, 0, h_out(t))
+          const unsigned so = (unsigned)(((long)qunit(q) * p.M + cbase) * 4);
+          st_u(rs_hin, vbyte, so, hin);
+          st_u(rs_r, vbyte, so, rg);
+          st_u(rs_z, vbyte, so, zg);
+          st_u(rs_n, vbyte, so, ng);
+          st_u(rs_hn, vbyte, so, hn);
+          const float rl = fmaxf(hh, 0.0f);
+          const float4 w0 = whl[qunit(q) * 3], w1 = whl[qunit(q) * 3 + 1], w2 = whl[qunit(q) * 3 + 2];
+          hp_loc[0] += rl * w0.x; hp_loc[1] += rl * w0.y; hp_loc[2] += rl * w0.z;
+          hp_loc[3] += rl * w0.w; hp_loc[4] += rl * w1.x; hp_loc[5] += rl * w1.y;
+          hp_loc[6] += rl * w1.z; hp_loc[7] += rl * w1.w; hp_loc[8] += rl * w2.x;
+        }
+#pragma unroll
+        for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x4*>(&hB[q][row * F6_HP + ub + 8 * g4]) = nq[q];
+      }
+      // lanes l and l + 32 hold the same row: fold the two halves, one lane writes
+#pragma unroll
+      for (int oo = 0; oo < 9; ++oo) {
+        const float o = __shfl_xor(hp_loc[oo], 32);
+        if (hi == 0) hp[(wave * 9 + oo) * 64 + row] = hp_loc[oo] + o;
+      }
+    }
+    __syncthreads();   // head partials, the carry and x(t-1) visible
+    for (int i = tid; i < 9 * 64; i += 512) {
+      const int oo = i >> 6, c = i & 63;
+      float v = oo == 0 ? bpi : eta[p.o.y_b + oo - 1];
+#pragma unroll
+      for (int gq = 0; gq < 8; ++gq) v += hp[(gq * 9 + oo) * 64 + c];
+      hout[i] = v;
+    }
+    __syncthreads();
+    if (tid < 64) {
+      const long ob = (long)t * R + r0 + tid;
+      p.pi_hat[ob] = hout[tid];
+      float m = -__builtin_inff();
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, hout[(j + 1) * 64 + tid]);
+      float e[8], ssum = 0.0f;
+      for (int j = 0; j < 8; ++j) { e[j] = __expf(hout[(j + 1) * 64 + tid] - m); ssum += e[j]; }
+      const float inv = 1.0f / ssum;
+      for (int j = 0; j < 8; ++j) p.y_hat[((long)t * 8 + j) * R + r0 + tid] = e[j] * inv;
+    }
   }
 }
 
@@ -826,16 +1108,31 @@ int toued_gru_pack(const float* eta, const int* off, int F, float* fwdA, float* 
   TOUED_REQUIRE(F >= 1 && F <= 7, "toued_gru_pack: F=%d", F);
   EtaOff o;
   memcpy(&o, off, sizeof(EtaOff));
-  const int n1 = NTILE_F * KQF * 64, n2 = 8 * 3 * 32 * 64;
+  const int n1 = NTILE_F * KQF * 64, n2 = 8 * 3 * 32 * 64, n3 = (16 * 8 * 3 + 8 * 4) * 64;
   hipLaunchKernelGGL(k_pack_fwd, dim3((n1 + 255) / 256), dim3(256), 0, stream, eta, o, F,
                      reinterpret_cast<float4*>(fwdA), 0L);
+  hipLaunchKernelGGL(k_pack_fwd6, dim3((n3 + 255) / 256), dim3(256), 0, stream, eta, o, F,
+                     reinterpret_cast<bf16x8*>(fwdA + (size_t)n1 * 4));
   hipLaunchKernelGGL(k_pack_bwd, dim3((n2 + 255) / 256), dim3(256), 0, stream, eta, o,
                      reinterpret_cast<float4*>(bwdA));
   TOUED_CHECK_LAUNCH();
   return 0;
 }
 
-size_t toued_gru_packed_floats(int which) { return which == 0 ? (size_t)NTILE_F * KQF * 64 * 4 : (size_t)8 * 3 * 32 * 64 * 4; }
+// which: 0 = forward fragments (f32 MFMA, then the bf16-split pieces), 1 = backward, 2 = forward f32 fragments of
+// one candidate (toued_gru_pack_fwd_multi stride)
+size_t toued_gru_packed_floats(int which) {
+  const size_t f32_part = (size_t)NTILE_F * KQF * 64 * 4;
+  return which == 0 ? f32_part + F6_FLOATS : which == 1 ? (size_t)8 * 3 * 32 * 64 * 4 : f32_part;
+}
+
+static bool gru_f32_forced() {
+  static const bool f = [] {
+    const char* e = getenv("TOUED_GRU_F32");
+    return e && e[0] == '1';
+  }();
+  return f;
+}
 
 static int gru_fwd_launch(int R, int T, int W, int F, const float* X, long xs_f, long xs_col, const uint8_t* done,
                           const float* fwdA, const float* eta, const int* off, float* pi_hat, float* y_hat,
@@ -844,13 +1141,16 @@ static int gru_fwd_launch(int R, int T, int W, int F, const float* X, long xs_f,
   FwdArgs p;
   p.R = R; p.T = T; p.W = W; p.F = F; p.X = X; p.xs_f = xs_f; p.xs_col = xs_col; p.done = done;
   p.A = reinterpret_cast<const float4*>(fwdA); p.eta = eta;
+  p.A6 = fwdA + (size_t)NTILE_F * KQF * 64 * 4;
   memcpy(&p.o, off, sizeof(EtaOff));
   p.pi_hat = pi_hat; p.y_hat = y_hat; p.s_hin = s_hin; p.s_r = s_r; p.s_z = s_z; p.s_n = s_n; p.s_hn = s_hn; p.M = M;
   p.rpc = rpc; p.a_stride4 = (long)NTILE_F * KQF * 64; p.eta_stride = eta_stride;
   // two row tiles per workgroup when the rows (and, for per-candidate parameters, each candidate's rows)
   // split into 64-row blocks
   const bool nt2 = R % (2 * RB) == 0 && (rpc == 0 || rpc % (2 * RB) == 0);
-  if (save) {
+  if (save && nt2 && !gru_f32_forced()) {
+    hipLaunchKernelGGL(k_gru_fwd6, dim3(R / (2 * RB)), dim3(512), 0, stream, p);
+  } else if (save) {
     if (nt2) hipLaunchKernelGGL((k_gru_fwd<true, 2>), dim3(R / (2 * RB)), dim3(512), 0, stream, p);
     else hipLaunchKernelGGL((k_gru_fwd<true, 1>), dim3(R / RB), dim3(512), 0, stream, p);
   } else {

@@ -113,7 +113,7 @@ class ESTrainStep:
         f32, i32, u8 = torch.float32, torch.int32, torch.uint8
         z = lambda *s, dt=f32: torch.zeros(s, dtype=dt, device=self.dev)
         self.x = z(C, self.lay.size)
-        self.fwdA = z(C, _lib.lib().toued_gru_packed_floats(0))
+        self.fwdA = z(C, _lib.lib().toued_gru_packed_floats(2))
         self.theta = [z(C, D, 5), z(C, D, 5)]
         self.phi = [z(C, D, _Y), z(C, D, _Y)]
         self.G_th, self.G_ph = z(C, D, 5), z(C, D, _Y)
