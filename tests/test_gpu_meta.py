@@ -225,3 +225,37 @@ def test_gru_backward_matches_autograd():
         errs[f"dX{f}"] = np.linalg.norm(got - gx[f]) / np.linalg.norm(gx[f])
     bad = {k: v for k, v in errs.items() if not v < 1e-4}
     assert not bad, errs
+
+
+def test_gru_backward_repeat_bit_identical():
+    """Two backward passes over the same saved activations give bit-identical outputs: the kernels have no
+    atomics and fixed reduction orders, so any difference is a race (this caught a lane-half LDS hazard in the
+    input-cotangent partials of k_gru_bwd6)."""
+    from toued.lpg import LPGGRU, LPGLayout, init_lpg_params
+    N, W, T, K, F = 2, 64, 6, 2, 5
+    R = N * W
+    lay = LPGLayout(F)
+    eta = init_lpg_params(7, F)
+    gru = LPGGRU(lay, R, T, K, W, "cuda")
+    gru.pack(eta)
+    rs = np.random.RandomState(2)
+    gru.X.copy_(torch.from_numpy(rs.randn(F, K, T, R).astype(np.float32)))
+    done_t = torch.from_numpy((rs.rand(K, N, T, W) < 0.15).astype(np.uint8)).cuda()
+    pi_hat = torch.zeros(K, T, R, device="cuda")
+    y_hat = torch.zeros(K, T, 8, R, device="cuda")
+    for k in range(K):
+        gru.forward(k, gru.X, done_t[k], eta, pi_hat, y_hat)
+    d_pi = torch.from_numpy(rs.randn(K, T, R).astype(np.float32)).cuda()
+    d_y = torch.from_numpy(rs.randn(K, T, 8, R).astype(np.float32)).cuda()
+    outs = []
+    for _ in range(3):
+        gru.dX3.fill_(float("nan"))
+        gru.dX4.fill_(float("nan"))
+        grad = torch.zeros(lay.size, device="cuda")
+        gru.backward(done_t, eta, y_hat, d_pi, d_y, gru.X, grad)
+        torch.cuda.synchronize()
+        outs.append([gru.dX3.clone(), gru.dX4.clone(), gru.DG.clone(), gru.RH.clone(), gru.DH.clone(), grad])
+    for rep in outs[1:]:
+        for a, b in zip(outs[0], rep):
+            assert torch.isfinite(a).all()
+            assert torch.equal(a, b)

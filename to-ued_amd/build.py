@@ -27,7 +27,7 @@ ARCH = os.environ.get("TOUED_ARCH", "gfx950")
 # files allowed to contract a*b+c into fma (tolerance-checked float kernels)
 CONTRACT_OK = {"gru.hip"}
 # per-file extras: packed f32 VALU (SLP-vectorised adds) beside MFMAs costs issue cycles (MI355X_MICROARCH.md)
-EXTRA = {"wgrad.hip": ["-fno-slp-vectorize"]}
+EXTRA = {"wgrad.hip": ["-fno-slp-vectorize"], "gru.hip": ["-fno-slp-vectorize"]}
 
 
 def hipcc() -> str:

@@ -160,6 +160,34 @@ __global__ void k_pack_bwd(const float* __restrict__ eta, EtaOff o, float4* __re
   out[gid] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
+// bwd6 fragments [ks][unit tile ut][gate g][piece] (1 KiB each), appended after the f32 ones: lane l holds
+// A[i = input unit 32 ut + (l & 31)][k = gate unit 16 ks + 8 (l >> 5) + e] = W_g[i][k], split in three bf16
+#define B6_NF (16 * 8 * 3 * 3)
+#define B6_FLOATS (B6_NF * 256)
+__global__ void k_pack_bwd6(const float* __restrict__ eta, EtaOff o, __bf16* __restrict__ out8) {
+  typedef __bf16 v8 __attribute__((ext_vector_type(8)));
+  v8* out = reinterpret_cast<v8*>(out8);
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= 16 * 8 * 3 * 64) return;
+  const int lane = gid & 63, grp = gid >> 6;
+  const int g = grp % 3, ut = (grp / 3) % 8, ks = grp / 24;
+  const int u = 32 * ut + (lane & 31);
+  const int base = g == 0 ? o.hr_w : g == 1 ? o.hz_w : o.hn_w;
+  v8 pc[3];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float x = eta[base + u * HU + 16 * ks + 8 * (lane >> 5) + e];
+    const __bf16 h = (__bf16)x;
+    const float r1 = x - (float)h;
+    const __bf16 m = (__bf16)r1;
+    pc[0][e] = h;
+    pc[1][e] = m;
+    pc[2][e] = (__bf16)(r1 - (float)m);
+  }
+#pragma unroll
+  for (int q = 0; q < 3; ++q) out[(long)(grp * 3 + q) * 64 + lane] = pc[q];
+}
+
 // One k-major LDS buffer ([unit][row], pitch RB*NT + 1; h^T in the forward, a gate cotangent in the
 // backward) of NT row tiles out to its row-major
 // [unit][M] array: lane l stores 4 consecutive rows (4*(l & 7) ..) of unit 32*wave + 8i + (l >> 3),
@@ -377,7 +405,6 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 #define F6_HP 264        // carry image row pitch (bf16): 528 B
-#define F6_AP 24         // augmented-row image pitch (bf16): 48 B
 #define F6_NFH (16 * 8 * 3 * 3)     // h-part fragments [ks][unit tile][gate r|z|hn][piece], 1 KiB each
 #define F6_NFA (8 * 4 * 3)          // augmented fragments [unit tile][gate r|z|hn|ni][piece]
 #define F6_FLOATS ((F6_NFH + F6_NFA) * 256)   // packed size in floats (1 KiB = 256 floats)
@@ -449,7 +476,6 @@ TOUED_DEV floatx16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx16 c)
 
 __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   __shared__ __attribute__((aligned(16))) __bf16 hB[3][64 * F6_HP];   // carry h(t) pieces [row][unit]
-  __shared__ __attribute__((aligned(16))) __bf16 xB[3][64 * F6_AP];   // [x(t); 1; 0] pieces [row][16]
   __shared__ __attribute__((aligned(16))) float wh[HU * 12];          // head weights [unit][pi | y0..y7 | pad]
   __shared__ float hp[8 * 9 * 64];      // head partials [wave][output][row]
   __shared__ float hout[9 * 64];
@@ -473,21 +499,10 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     for (int i = tid; i < 3 * 64 * F6_HP / 8; i += 512) z[i] = make_uint4(0u, 0u, 0u, 0u);
   }
   // x(t) of row `row` -> the augmented image: [x_0 .. x_{F-1}, 1, 0 ...]
-  auto write_x = [&](int t, int row) {
-    bf16x8 pc[2][3];
-#pragma unroll
-    for (int f = 0; f < 16; ++f) {
-      const float v = f < F ? p.X[f * p.xs_f + ((size_t)t * R + r0 + row) * p.xs_col] : (f == F ? 1.0f : 0.0f);
-      split3v(v, pc[f >> 3][0], pc[f >> 3][1], pc[f >> 3][2], f & 7);
-    }
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      bf16x8* d = reinterpret_cast<bf16x8*>(&xB[q][row * F6_AP]);
-      d[0] = pc[0][q];
-      d[1] = pc[1][q];
-    }
-  };
-  if (tid < 64) write_x(T - 1, tid);
+  // per-row global reads through wave-uniform buffer descriptors with 32-bit offsets (64-bit per-lane
+  // addresses kept across the step loop spill)
+  const __amdgpu_buffer_rsrc_t rs_X = rsrc_of(p.X);
+  const __amdgpu_buffer_rsrc_t rs_done = rsrc_of(reinterpret_cast<const float*>(p.done));
   __syncthreads();
   const float bpi = eta[p.o.pi_b];
   const __amdgpu_buffer_rsrc_t rs_A = rsrc_of(reinterpret_cast<const float*>(p.A6));
@@ -510,15 +525,35 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     // ---- contraction: 17 k-steps.  Each gate's A fragments (unit tile `wave`) are refilled for the next
     // k-step right after their last MFMA, each row tile's B fragments right after theirs; the partner wave on
     // the SIMD covers what latency remains.
+    // this lane's row inputs x(t) for the augmented k-step [x_0 .. x_{F-1}, 1, 0 ...] (F <= 7), loaded now
+    // and split into B fragments at the end of the contraction (lanes 32-63 hold k = 8..15: zero)
+    float xv[2][7];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int f = 0; f < 7; ++f) {
+        const int fc = f < F ? f : F - 1;
+        xv[h][f] = ld_u(rs_X, (unsigned)((RB * h + col) * p.xs_col * 4),
+                        (unsigned)((fc * p.xs_f + ((long)t * R + r0) * p.xs_col) * 4));
+      }
     bf16x8 A[3][3], B[2][3];
     auto fragA = [&](int ks, int g, int q) {
       return ks < 16 ? ((ks * 8 + wave) * 3 + g) * 3 + q : F6_NFH + (wave * 4 + g) * 3 + q;
     };
     auto load_B = [&](int ks, int h) {
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
-        B[h][q] = ks < 16 ? *reinterpret_cast<const bf16x8*>(&hB[q][(RB * h + col) * F6_HP + 16 * ks + 8 * hi])
-                          : *reinterpret_cast<const bf16x8*>(&xB[q][(RB * h + col) * F6_AP + 8 * hi]);
+      for (int q = 0; q < 3; ++q) {
+        if (ks < 16) {
+          B[h][q] = *reinterpret_cast<const bf16x8*>(&hB[q][(RB * h + col) * F6_HP + 16 * ks + 8 * hi]);
+        }
+      }
+      if (ks == 16) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = hi ? 0.0f : e < F ? xv[h][e < 7 ? e : 6] : (e == F ? 1.0f : 0.0f);
+          split3v(v, B[h][0], B[h][1], B[h][2], e);
+        }
+      }
     };
 #pragma unroll
     for (int g = 0; g < 3; ++g)
@@ -554,7 +589,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) acc[3][h] = mfma6(A[0], B[h], acc[3][h]);
     __syncthreads();   // every wave done reading hB / xB: the carry and x(t-1) overwrite them in place
-    if (t >= 1 && tid < 64) write_x(t - 1, tid);
     // ---- gate maths (lane = row 32h + col, register q = unit 32 wave + 4 hi + qunit(q))
     const long cbase = (long)t * R;
     const int ub = 32 * wave + 4 * hi;
@@ -562,7 +596,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int row = RB * h + col;
-      const bool dn = (t >= 1) ? p.done[((size_t)a_[h] * T + (t - 1)) * W + w_[h]] != 0 : false;
+      const bool dn = (t >= 1) ? __builtin_amdgcn_raw_buffer_load_b8(rs_done, w_[h],
+                                                                       (int)(((long)a_[h] * T + (t - 1)) * W), 0) != 0
+                               : false;
       const unsigned vbyte = (unsigned)(((long)ub * p.M + r0 + row) * 4);
       float hp_loc[9];
 #pragma unroll
@@ -632,7 +668,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
 struct BwdArgs {
   int R, T, W, K;
   const uint8_t* done; long done_stride_k;     // per k: [N][T][W]
-  const float4* A;                             // packed bwd fragments
+  const float4* A;                             // packed bwd fragments (f32 MFMA, k_gru_bwd<1>)
+  const void* A6;                              // packed bwd fragments (bf16 split pieces, k_gru_bwd6)
   const float* eta; EtaOff o;
   const float* y_hat; const float* d_pi_hat; const float* d_y_hat;   // [K][T][(8)][R]
   const float* s_hin; const float* s_r; const float* s_z; const float* s_n; const float* s_hn;  // [256][M]
@@ -846,13 +883,13 @@ __global__ void __launch_bounds__(512, NT == 1 ? 4 : 1) k_gru_bwd(BwdArgs p) {
 // MFMA, so every SIMD (one wave of each group) overlaps HBM traffic with matrix work instead of
 // alternating between them.  Wave wg of a group owns units [64 wg, 64 wg + 64) (two 32-unit tiles j) for
 // the group's 32 rows; the LDS holds two cotangent slots per group ([dr | dz], then dhn in slot 0).
-__global__ void __launch_bounds__(512, 1) k_gru_bwd_g2(BwdArgs p) {
-  constexpr int LDG = RB + 1;
-  constexpr int SLOT = HU * LDG;
-  __shared__ float dgT[2 * 2 * SLOT];        // [group][slot][unit][row]
+__global__ void __launch_bounds__(512, 1) k_gru_bwd6(BwdArgs p) {
+  constexpr int LDR = HU + 4;                // slot row pitch: 1040 B, conflict-free 16-byte row reads
+  constexpr int SLOT = RB * LDR;
+  __shared__ __attribute__((aligned(16))) float dgT[2 * 2 * SLOT];   // [group][slot][row][unit]
   __shared__ float wi34[2 * 3 * HU];
   __shared__ float hv[2 * 9 * RB];           // [group][head output][row]
-  __shared__ float dxp[2 * 8 * 2 * RB];      // [group][wave, hi][dx3 | dx4][row]
+  __shared__ __attribute__((aligned(8))) float dxp[2 * 4 * RB * 2];   // [group][wave][row][dx3 | dx4]
   const int tid = threadIdx.x, lane = tid & 63, hi = lane >> 5, col = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: group offsets go to SGPRs
   // group = wave >> 2: a workgroup's waves go round-robin over the four SIMDs, so every SIMD holds one
@@ -888,23 +925,30 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd_g2(BwdArgs p) {
                                rs_n = rsrc_of(p.s_n), rs_hn = rsrc_of(p.s_hn), rs_rh = rsrc_of(p.RH);
   const __amdgpu_buffer_rsrc_t rs_dg[4] = {rsrc_of(p.DG), rsrc_of(p.DG + 1L * HU * p.M),
                                            rsrc_of(p.DG + 2L * HU * p.M), rsrc_of(p.DG + 3L * HU * p.M)};
+  // Per-row global accesses go through wave-uniform buffer descriptors with a 32-bit lane offset: 64-bit
+  // per-lane addresses kept live across the phase loop spill, and a spilled store address reloaded into the
+  // same registers right behind the store was observed to drop the store (dX3) on gfx950.
+  const __amdgpu_buffer_rsrc_t rs_yh = rsrc_of(p.y_hat), rs_dyh = rsrc_of(p.d_y_hat), rs_dpi = rsrc_of(p.d_pi_hat),
+                               rs_DH = rsrc_of(p.DH), rs_dx3 = rsrc_of(p.dX3), rs_dx4 = rsrc_of(p.dX4);
+  const unsigned vrow = (unsigned)gtid * 4;   // lane's row offset (gtid < RB)
   // head cotangents of step t (softmax VJP of y_hat, d pi_hat) for the group's rows -> hv, DH
   auto head_cot = [&](int t) {
     if (gtid < RB) {
-      const long o = ((long)k * T + t) * R + r0 + gtid;
+      const long o = ((long)k * T + t) * R + r0;    // uniform column base
       float yh[8], dy[8], s = 0.0f;
       for (int j = 0; j < 8; ++j) {
-        yh[j] = p.y_hat[((long)k * T * 8 + (long)t * 8 + j) * R + r0 + gtid];
-        dy[j] = p.d_y_hat[((long)k * T * 8 + (long)t * 8 + j) * R + r0 + gtid];
+        const unsigned so = (unsigned)((((long)k * T * 8 + (long)t * 8 + j) * R + r0) * 4);
+        yh[j] = ld_u(rs_yh, vrow, so);
+        dy[j] = ld_u(rs_dyh, vrow, so);
         s += yh[j] * dy[j];
       }
-      const float dpi = p.d_pi_hat[o];
+      const float dpi = ld_u(rs_dpi, vrow, (unsigned)(o * 4));
       hv[(gi * 9) * RB + gtid] = dpi;
-      p.DH[o] = dpi;
+      st_u(rs_DH, vrow, (unsigned)(o * 4), dpi);
       for (int j = 0; j < 8; ++j) {
         const float v = yh[j] * (dy[j] - s);
         hv[(gi * 9 + j + 1) * RB + gtid] = v;
-        p.DH[(long)(j + 1) * p.M + o] = v;
+        st_u(rs_DH, vrow, (unsigned)(((long)(j + 1) * p.M + o) * 4), v);
       }
     }
   };
@@ -945,9 +989,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd_g2(BwdArgs p) {
       const float drp = dnp * hn * rg * (1.0f - rg);
       const float dzp = dz * zg * (1.0f - zg);
       dh[j][q] = d * zg;   // direct path; the W_h^T contraction is added in the MFMA half
-      const int lo = (ub + qunit(q)) * LDG + col;
-      dg0[lo] = drp;
-      dg0[SLOT + lo] = dzp;
+      dg0[col * LDR + ub + qunit(q)] = drp;
+      dg0[SLOT + col * LDR + ub + qunit(q)] = dzp;
       dhn_r[j][q] = dhn;
       o_rh[jj] = fmaxf(hout, 0.0f); o_dn[jj] = dnp;
       const int qu = qunit(q);
@@ -981,54 +1024,61 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd_g2(BwdArgs p) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int unit = 64 * wg + 8 * i + (lane >> 3), r = 4 * (lane & 7);
-      const float* src = buf + unit * LDG + r;
-      const float v[4] = {src[0], src[1], src[2], src[3]};
+      const float* src = buf + r * LDR + unit;
+      const float v[4] = {src[0], src[LDR], src[2 * LDR], src[3 * LDR]};
       st4(rs, (unsigned)(((long)unit * p.M + r) * 4), so, v);
     }
   };
   floatx16 acc[2];
-  // A fragments stream from L2 through a 4-deep register ring (one wave per SIMD issues these MFMAs, so
-  // the ring, not a second wave, has to cover the L2 latency)
-  float4 ring[4][2];
-  const __amdgpu_buffer_rsrc_t rs_A = rsrc_of(reinterpret_cast<const float*>(p.A));
+  // dh_prev = W_g . dg on the bf16 matrix cores, f32-accurate split products (k_gru_fwd6): A fragments
+  // (W_g pre-split by k_pack_bwd6) through a 2-deep register ring from L2; B fragments (this lane's row,
+  // 8 consecutive gate units) read from the f32 slot one k-step ahead and split in registers.
+  bf16x8 ring[2][2][3];
+  const __amdgpu_buffer_rsrc_t rs_A = rsrc_of(reinterpret_cast<const float*>(p.A6));
   const unsigned vA = (unsigned)lane * 16;
-  // fragment (tile 2 wg + j, gate g, k-quad kq): uniform byte offset into the packed W_h^T stream
-  auto ldA = [&](int j, int g, int kq) {
+  auto ldA = [&](int ks, int j, int g, int q) {
     const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(
-        rs_A, (int)vA, (int)((((2 * wg + j) * 3 + g) * 32 + kq) * 64 * 16), 0);
-    return make_float4(__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w));
+        rs_A, (int)vA, (int)((((ks * 8 + 2 * wg + j) * 3 + g) * 3 + q) * 1024), 0);
+    return __builtin_bit_cast(bf16x8, x);
   };
   auto ring_fill = [&](int g) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { ring[i][0] = ldA(0, g, i); ring[i][1] = ldA(1, g, i); }
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) ring[i][j][q] = ldA(i, j, g, q);
   };
   auto contract = [&](int g, const float* dgs) {
-    // B operands (this lane's cotangent column) one k-quad ahead, so no LDS latency sits between MFMAs
-    const float* bl = dgs + hi * LDG + col;
-    float bq[4];
+    const float* bl = dgs + col * LDR + 8 * hi;
+    float4 b0 = *reinterpret_cast<const float4*>(bl), b1 = *reinterpret_cast<const float4*>(bl + 4);
+    auto kstep = [&](int ks, bool reload) {
+      bf16x8 bp[3];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) bq[e] = bl[2 * e * LDG];
-    auto kstep = [&](int kq, bool reload) {
-      float bn[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) bn[e] = kq + 1 < 32 ? bl[2 * (4 * (kq + 1) + e) * LDG] : 0.0f;
-      __builtin_amdgcn_sched_barrier(0);   // next k-quad's B reads in flight during this one's MFMAs
-      const float4 a0 = ring[kq & 3][0], a1 = ring[kq & 3][1];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        acc[0] = mfma32(e == 0 ? a0.x : e == 1 ? a0.y : e == 2 ? a0.z : a0.w, bq[e], acc[0]);
-        acc[1] = mfma32(e == 0 ? a1.x : e == 1 ? a1.y : e == 2 ? a1.z : a1.w, bq[e], acc[1]);
+      for (int e = 0; e < 8; ++e) {
+        const float x = e < 4 ? (e == 0 ? b0.x : e == 1 ? b0.y : e == 2 ? b0.z : b0.w)
+                              : (e == 4 ? b1.x : e == 5 ? b1.y : e == 6 ? b1.z : b1.w);
+        split3v(x, bp[0], bp[1], bp[2], e);
       }
-      if (reload) { ring[kq & 3][0] = ldA(0, g, kq + 4); ring[kq & 3][1] = ldA(1, g, kq + 4); }
+      if (ks + 1 < 16) {
+        b0 = *reinterpret_cast<const float4*>(bl + 16 * (ks + 1));
+        b1 = *reinterpret_cast<const float4*>(bl + 16 * (ks + 1) + 4);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[j] = mfma6(ring[ks & 1][j], bp, acc[j]);
+      if (reload) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int q = 0; q < 3; ++q) ring[ks & 1][j][q] = ldA(ks + 2, j, g, q);
+      }
       __builtin_amdgcn_sched_barrier(0);   // keep each refill right behind its slot's last MFMA
-#pragma unroll
-      for (int e = 0; e < 4; ++e) bq[e] = bn[e];
     };
-    // main body: every k-quad refills its ring slot (unconditional loads keep the wait counts exact)
-#pragma unroll 4
-    for (int kq = 0; kq < 28; ++kq) kstep(kq, true);
-#pragma unroll
-    for (int kq = 28; kq < 32; ++kq) kstep(kq, false);
+#pragma unroll 2
+    for (int ks = 0; ks < 14; ++ks) kstep(ks, true);
+    kstep(14, false);
+    kstep(15, false);
   };
   for (int s = 0; s <= 2 * T; ++s) {
     const int u = s - gi;
@@ -1048,9 +1098,13 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd_g2(BwdArgs p) {
       __builtin_amdgcn_s_setprio(2);
       if (gtid < RB) {
         float s3 = 0.0f, s4 = 0.0f;
-        for (int gq = 0; gq < 8; ++gq) { s3 += dxp[((gi * 8 + gq) * 2 + 0) * RB + gtid]; s4 += dxp[((gi * 8 + gq) * 2 + 1) * RB + gtid]; }
-        p.dX3[ctr + r0 + gtid] = s3;
-        p.dX4[ctr + r0 + gtid] = s4;
+        for (int gq = 0; gq < 4; ++gq) {
+          const float2 v = *reinterpret_cast<const float2*>(dxp + ((gi * 4 + gq) * RB + gtid) * 2);
+          s3 += v.x;
+          s4 += v.y;
+        }
+        st_u(rs_dx3, vrow, (unsigned)((ctr + r0) * 4), s3);
+        st_u(rs_dx4, vrow, (unsigned)((ctr + r0) * 4), s4);
       }
       ring_fill(0);
       store_slot(dg0, rs_dg[0], ctr + r0);
@@ -1067,11 +1121,11 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd_g2(BwdArgs p) {
     // part Y: dhn into slot 0 once every wave of the group has read dr
     if (mm) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        float* dgl = dg0 + (64 * wg + 32 * j + 4 * hi) * LDG + col;
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int q = 0; q < 16; ++q) dgl[qunit(q) * LDG] = dhn_r[j][q];
-      }
+        for (int g4 = 0; g4 < 4; ++g4)
+          *reinterpret_cast<float4*>(dg0 + col * LDR + 64 * wg + 32 * j + 4 * hi + 8 * g4) =
+              make_float4(dhn_r[j][4 * g4], dhn_r[j][4 * g4 + 1], dhn_r[j][4 * g4 + 2], dhn_r[j][4 * g4 + 3]);
     }
     __syncthreads();
     // part Z: memory quads of tile 1 + dx partials | dhn out + contraction, carry, next head cotangents
@@ -1081,8 +1135,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd_g2(BwdArgs p) {
       G2_QUAD(1, 1, vb)
       G2_QUAD(1, 2, va)
       G2_QUAD(1, 3, vb)
-      dxp[((gi * 8 + 2 * wg + hi) * 2 + 0) * RB + col] = dx3;
-      dxp[((gi * 8 + 2 * wg + hi) * 2 + 1) * RB + col] = dx4;
+      // lanes l and l + 32 hold the same row: fold the halves, then one float2 per row and wave
+      const float f3 = dx3 + __shfl_xor(dx3, 32), f4 = dx4 + __shfl_xor(dx4, 32);
+      if (hi == 0) *reinterpret_cast<float2*>(dxp + ((gi * 4 + wg) * RB + col) * 2) = make_float2(f3, f4);
     } else if (mm) {
       ring_fill(2);
       store_slot(dg0, rs_dg[2], ctr + r0);
@@ -1115,6 +1170,8 @@ int toued_gru_pack(const float* eta, const int* off, int F, float* fwdA, float* 
                      reinterpret_cast<bf16x8*>(fwdA + (size_t)n1 * 4));
   hipLaunchKernelGGL(k_pack_bwd, dim3((n2 + 255) / 256), dim3(256), 0, stream, eta, o,
                      reinterpret_cast<float4*>(bwdA));
+  hipLaunchKernelGGL(k_pack_bwd6, dim3((16 * 8 * 3 * 64 + 255) / 256), dim3(256), 0, stream, eta, o,
+                     reinterpret_cast<__bf16*>(bwdA + (size_t)n2 * 4));
   TOUED_CHECK_LAUNCH();
   return 0;
 }
@@ -1123,7 +1180,7 @@ int toued_gru_pack(const float* eta, const int* off, int F, float* fwdA, float* 
 // one candidate (toued_gru_pack_fwd_multi stride)
 size_t toued_gru_packed_floats(int which) {
   const size_t f32_part = (size_t)NTILE_F * KQF * 64 * 4;
-  return which == 0 ? f32_part + F6_FLOATS : which == 1 ? (size_t)8 * 3 * 32 * 64 * 4 : f32_part;
+  return which == 0 ? f32_part + F6_FLOATS : which == 1 ? (size_t)8 * 3 * 32 * 64 * 4 + B6_FLOATS : f32_part;
 }
 
 static bool gru_f32_forced() {
@@ -1208,12 +1265,13 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
   BwdArgs p;
   p.R = R; p.T = T; p.W = W; p.K = K; p.done = done; p.done_stride_k = done_stride_k;
   p.A = reinterpret_cast<const float4*>(bwdA); p.eta = eta;
+  p.A6 = bwdA + (size_t)8 * 3 * 32 * 64 * 4;
   memcpy(&p.o, off, sizeof(EtaOff));
   p.y_hat = y_hat; p.d_pi_hat = d_pi_hat; p.d_y_hat = d_y_hat;
   p.s_hin = s_hin; p.s_r = s_r; p.s_z = s_z; p.s_n = s_n; p.s_hn = s_hn; p.M = M;
   p.DG = DG; p.RH = RH; p.DH = DH; p.dX3 = dX3; p.dX4 = dX4;
-  if (R % (2 * RB) == 0)
-    hipLaunchKernelGGL(k_gru_bwd_g2, dim3(K * (R / (2 * RB))), dim3(512), 0, stream, p);
+  if (R % (2 * RB) == 0 && !gru_f32_forced())
+    hipLaunchKernelGGL(k_gru_bwd6, dim3(K * (R / (2 * RB))), dim3(512), 0, stream, p);
   else
     hipLaunchKernelGGL(k_gru_bwd<1>, dim3(K * (R / RB)), dim3(512), 0, stream, p);
   TOUED_CHECK_LAUNCH();
