@@ -1095,7 +1095,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6(BwdArgs p) {
       G2_QUAD(0, 2, va)
       G2_QUAD(0, 3, vb)
     } else if (mm) {
-      __builtin_amdgcn_s_setprio(2);
       if (gtid < RB) {
         float s3 = 0.0f, s4 = 0.0f;
         for (int gq = 0; gq < 4; ++gq) {
@@ -1149,7 +1148,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6(BwdArgs p) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) dh[j][q] = dn ? 0.0f : dh[j][q] + acc[j][q];
       if (t + 1 < T) head_cot(t + 1);
-      __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();
   }
