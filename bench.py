@@ -40,7 +40,7 @@ GRU_BWD_FLOP_PER_ELEM = 2 * 256 * 768              # dh_prev = dG . W_h^T per (k
 
 
 # device kernel behind each timed region, as rocprofv3 names it (prof_summary.short)
-PROFILED_KERNEL = {"gru_fwd": "k_gru_fwd6", "gru_bwd": "k_gru_bwd6"}
+PROFILED_KERNEL = {"gru_fwd": "k_gru_fwd6", "gru_bwd": "k_gru_bwd6n"}
 
 
 def pmc_traffic(kernel: str):

@@ -1153,6 +1153,242 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6(BwdArgs p) {
   }
 }
 
+// Backward in lockstep (k_gru_bwd6n): one 512-thread workgroup per (k, 64 rows), both 32-row tiles in
+// every wave, so each pre-split W_g fragment (L2) feeds both tiles: half the fragment traffic of the two-group
+// kernel, which was the vector-memory bottleneck once the contraction moved to the bf16 matrix cores.  Wave w
+// owns units [32w, 32w + 32).  Per step:
+//   memory part: 16-byte saved-activation loads + quad transposes, gate maths; every cotangent (dr, dz,
+//     d(W_hn h + b_hn), dn) and relu(h_out) leaves as per-unit dword stores (lane = row: 128-byte rows);
+//     dr is split once into three bf16 pieces in the one LDS cotangent image, dz and dhn wait in registers;
+//   contraction: dh_prev = sum_g W_g . dg_g with the pieces as B fragments (no per-wave re-split), the image
+//     refilled with dz, then dhn, between the three gate passes.
+__global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
+  constexpr int RBT = 2 * RB;
+  constexpr int PP = HU + 8;                       // piece image row pitch (bf16): 528 B
+  __shared__ __attribute__((aligned(16))) __bf16 dgB[3][RBT * PP];   // one cotangent, three pieces [row][unit]
+  __shared__ float wi34[2 * 3 * HU];
+  __shared__ float hv[9 * RBT];                    // head cotangents [output][row]
+  __shared__ __attribute__((aligned(8))) float dxp[8 * RBT * 2];   // [wave][row][dx3 | dx4]
+  const int tid = threadIdx.x, lane = tid & 63, hi = lane >> 5, col = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nb = p.R / RBT;
+  const int k = blockIdx.x / nb;
+  const int r0 = (blockIdx.x - k * nb) * RBT;
+  const int R = p.R, T = p.T, W = p.W;
+  int a_[2], w_[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    a_[h] = (r0 + RB * h) / W;
+    w_[h] = r0 + RB * h + col - a_[h] * W;
+  }
+  for (int i = tid; i < 2 * 3 * HU; i += 512) {
+    const int f = 3 + i / (3 * HU), g = (i / HU) % 3, u = i % HU;
+    const int base = g == 0 ? p.o.ir_w : g == 1 ? p.o.iz_w : p.o.in_w;
+    wi34[i] = p.eta[base + f * HU + u];
+  }
+  float wA[5];   // W_heads^T A fragments of unit tile `wave`: A[i = unit][k = head output 2kk + hi]
+#pragma unroll
+  for (int kk = 0; kk < 5; ++kk) {
+    const int o = 2 * kk + hi, u = 32 * wave + col;
+    wA[kk] = o < 9 ? (o == 0 ? p.eta[p.o.pi_w + u] : p.eta[p.o.y_w + u * 8 + (o - 1)]) : 0.0f;
+  }
+  float dh[2][16];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dh[h][q] = 0.0f;
+  const __amdgpu_buffer_rsrc_t rs_hin = rsrc_of(p.s_hin), rs_r = rsrc_of(p.s_r), rs_z = rsrc_of(p.s_z),
+                               rs_n = rsrc_of(p.s_n), rs_hn = rsrc_of(p.s_hn), rs_rh = rsrc_of(p.RH);
+  const __amdgpu_buffer_rsrc_t rs_dg[4] = {rsrc_of(p.DG), rsrc_of(p.DG + 1L * HU * p.M),
+                                           rsrc_of(p.DG + 2L * HU * p.M), rsrc_of(p.DG + 3L * HU * p.M)};
+  const __amdgpu_buffer_rsrc_t rs_yh = rsrc_of(p.y_hat), rs_dyh = rsrc_of(p.d_y_hat), rs_dpi = rsrc_of(p.d_pi_hat),
+                               rs_DH = rsrc_of(p.DH), rs_dx3 = rsrc_of(p.dX3), rs_dx4 = rsrc_of(p.dX4),
+                               rs_done = rsrc_of(reinterpret_cast<const float*>(p.done + (long)k * p.done_stride_k));
+  const unsigned vrow = (unsigned)tid * 4;   // row offset of the per-row work (tid < RBT)
+  // head cotangents of step t (softmax VJP of y_hat, d pi_hat) -> hv, DH
+  auto head_cot = [&](int t) {
+    if (tid < RBT) {
+      const long o = ((long)k * T + t) * R + r0;
+      float yh[8], dy[8], s = 0.0f;
+      for (int j = 0; j < 8; ++j) {
+        const unsigned so = (unsigned)((((long)k * T * 8 + (long)t * 8 + j) * R + r0) * 4);
+        yh[j] = ld_u(rs_yh, vrow, so);
+        dy[j] = ld_u(rs_dyh, vrow, so);
+        s += yh[j] * dy[j];
+      }
+      const float dpi = ld_u(rs_dpi, vrow, (unsigned)(o * 4));
+      hv[tid] = dpi;
+      st_u(rs_DH, vrow, (unsigned)(o * 4), dpi);
+      for (int j = 0; j < 8; ++j) {
+        const float v = yh[j] * (dy[j] - s);
+        hv[(j + 1) * RBT + tid] = v;
+        st_u(rs_DH, vrow, (unsigned)(((long)(j + 1) * p.M + o) * 4), v);
+      }
+    }
+  };
+  // pieces of the four consecutive units ub + 8 g4 .. +3 of row `row` into the cotangent image
+  auto put4 = [&](int row, int u0, const float (&v)[4]) {
+    bf16x4 pc[3];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split3v(v[e], pc[0], pc[1], pc[2], e);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x4*>(&dgB[q][row * PP + u0]) = pc[q];
+  };
+  // contraction of one gate's cotangent image with W_g (bf16 split fragments, 2-deep ring from L2)
+  const __amdgpu_buffer_rsrc_t rs_A = rsrc_of(reinterpret_cast<const float*>(p.A6));
+  const unsigned vA = (unsigned)lane * 16;
+  auto ldA = [&](int ks, int g, int q) {
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs_A, (int)vA,
+                                                          (int)((((ks * 8 + wave) * 3 + g) * 3 + q) * 1024), 0);
+    return __builtin_bit_cast(bf16x8, x);
+  };
+  floatx16 acc[2];
+  auto contract = [&](int g) {
+    bf16x8 ring[2][3], B[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) ring[i][q] = ldA(i, g, q);
+    auto ldB = [&](int ks, int h) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        B[h][q] = *reinterpret_cast<const bf16x8*>(&dgB[q][(RB * h + col) * PP + 16 * ks + 8 * hi]);
+    };
+    ldB(0, 0);
+    ldB(0, 1);
+    auto kstep = [&](int ks, bool reload) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        acc[h] = mfma6(ring[ks & 1], B[h], acc[h]);
+        if (ks + 1 < 16) ldB(ks + 1, h);
+      }
+      if (reload) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) ring[ks & 1][q] = ldA(ks + 2, g, q);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+#pragma unroll 2
+    for (int ks = 0; ks < 14; ++ks) kstep(ks, true);
+    kstep(14, false);
+    kstep(15, false);
+  };
+  for (int t = 0; t < T; ++t) {
+    const long ctr = ((long)k * T + t) * R;
+    head_cot(t);
+    __syncthreads();
+    // ---- memory part
+    float dz_r[2][16], dhn_r[2][16];
+    const int ub = 32 * wave + 4 * hi;               // lane's unit base (register q adds qunit(q))
+    const float* wil = wi34 + ub;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      floatx16 hacc;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) hacc[q] = 0.0f;
+#pragma unroll
+      for (int kk = 0; kk < 5; ++kk) {
+        const int o = 2 * kk + hi;
+        hacc = mfma32(wA[kk], o < 9 ? hv[o * RBT + RB * h + col] : 0.0f, hacc);
+      }
+      const int row = RB * h + col;
+      const unsigned vq = (unsigned)((((long)(ub + (col & 3))) * p.M + r0 + RB * h + (col & 28)) * 4);
+      const unsigned vb = (unsigned)(((long)ub * p.M + r0 + row) * 4);
+      float dx3 = 0.0f, dx4 = 0.0f;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const unsigned so = (unsigned)(((long)8 * g4 * p.M + ctr) * 4);
+        float v[5][4];
+        ld4(rs_hin, vq, so, v[0]);
+        ld4(rs_r, vq, so, v[1]);
+        ld4(rs_z, vq, so, v[2]);
+        ld4(rs_n, vq, so, v[3]);
+        ld4(rs_hn, vq, so, v[4]);
+#pragma unroll
+        for (int a = 0; a < 5; ++a) quad_transpose(v[a], lane);
+        float drq[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int q = 4 * g4 + jj;
+          const float hin = v[0][jj], rg = v[1][jj], zg = v[2][jj], ng = v[3][jj], hn = v[4][jj];
+          const float hout = (1.0f - zg) * ng + zg * hin;
+          const float d = dh[h][q] + (hout > 0.0f ? hacc[q] : 0.0f);
+          const float dn_ = d * (1.0f - zg);
+          const float dz = d * (hin - ng);
+          const float dnp = dn_ * (1.0f - ng * ng);
+          const float dhn = dnp * rg;
+          const float drp = dnp * hn * rg * (1.0f - rg);
+          const float dzp = dz * zg * (1.0f - zg);
+          dh[h][q] = d * zg;   // direct path; the W_h^T contraction is added below
+          drq[jj] = drp;
+          dz_r[h][q] = dzp;
+          dhn_r[h][q] = dhn;
+          const int qu = qunit(q);
+          dx3 += drp * wil[0 * HU + qu] + dzp * wil[1 * HU + qu] + dnp * wil[2 * HU + qu];
+          dx4 += drp * wil[3 * HU + qu] + dzp * wil[4 * HU + qu] + dnp * wil[5 * HU + qu];
+          const unsigned so1 = (unsigned)(((long)qu * p.M + ctr) * 4);
+          st_u(rs_rh, vb, so1, fmaxf(hout, 0.0f));
+          st_u(rs_dg[0], vb, so1, drp);
+          st_u(rs_dg[1], vb, so1, dzp);
+          st_u(rs_dg[2], vb, so1, dhn);
+          st_u(rs_dg[3], vb, so1, dnp);
+        }
+        put4(row, ub + 8 * g4, drq);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // lanes l and l + 32 hold the same row: fold the halves, one float2 per (wave, row)
+      const float f3 = dx3 + __shfl_xor(dx3, 32), f4 = dx4 + __shfl_xor(dx4, 32);
+      if (hi == 0) *reinterpret_cast<float2*>(dxp + (wave * RBT + row) * 2) = make_float2(f3, f4);
+    }
+    __syncthreads();   // dr pieces complete
+    // ---- contraction: dr, then dz, then dhn through the one image
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[h][q] = 0.0f;
+    contract(0);
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float v4[4] = {dz_r[h][4 * g4], dz_r[h][4 * g4 + 1], dz_r[h][4 * g4 + 2], dz_r[h][4 * g4 + 3]};
+        put4(RB * h + col, ub + 8 * g4, v4);
+      }
+    __syncthreads();
+    contract(1);
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float v4[4] = {dhn_r[h][4 * g4], dhn_r[h][4 * g4 + 1], dhn_r[h][4 * g4 + 2], dhn_r[h][4 * g4 + 3]};
+        put4(RB * h + col, ub + 8 * g4, v4);
+      }
+    __syncthreads();
+    contract(2);
+    if (tid < RBT) {
+      float s3 = 0.0f, s4 = 0.0f;
+#pragma unroll
+      for (int w8 = 0; w8 < 8; ++w8) {
+        const float2 v = *reinterpret_cast<const float2*>(dxp + (w8 * RBT + tid) * 2);
+        s3 += v.x;
+        s4 += v.y;
+      }
+      st_u(rs_dx3, vrow, (unsigned)((ctr + r0) * 4), s3);
+      st_u(rs_dx4, vrow, (unsigned)((ctr + r0) * 4), s4);
+    }
+    // carry to h_out(t+1): h_in(t) = where(d_t, 0, h_out(t+1))
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const bool dn = __builtin_amdgcn_raw_buffer_load_b8(rs_done, w_[h], (int)(((long)a_[h] * T + t) * W), 0) != 0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) dh[h][q] = dn ? 0.0f : dh[h][q] + acc[h][q];
+    }
+    __syncthreads();   // hv, dxp and the image are rewritten next step
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1268,8 +1504,12 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
   p.y_hat = y_hat; p.d_pi_hat = d_pi_hat; p.d_y_hat = d_y_hat;
   p.s_hin = s_hin; p.s_r = s_r; p.s_z = s_z; p.s_n = s_n; p.s_hn = s_hn; p.M = M;
   p.DG = DG; p.RH = RH; p.DH = DH; p.dX3 = dX3; p.dX4 = dX4;
-  if (R % (2 * RB) == 0 && !gru_f32_forced())
-    hipLaunchKernelGGL(k_gru_bwd6, dim3(K * (R / (2 * RB))), dim3(512), 0, stream, p);
+  if (R % (2 * RB) == 0 && !gru_f32_forced()) {
+    if (getenv("TOUED_BWD_G2"))
+      hipLaunchKernelGGL(k_gru_bwd6, dim3(K * (R / (2 * RB))), dim3(512), 0, stream, p);
+    else
+      hipLaunchKernelGGL(k_gru_bwd6n, dim3(K * (R / (2 * RB))), dim3(512), 0, stream, p);
+  }
   else
     hipLaunchKernelGGL(k_gru_bwd<1>, dim3(K * (R / RB)), dim3(512), 0, stream, p);
   TOUED_CHECK_LAUNCH();
