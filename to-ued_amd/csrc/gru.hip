@@ -1,31 +1,34 @@
 // LPG reverse-time GRU (models/lpg.py:11-36 LPGGRU + :79-85 heads) on CDNA4 matrix cores.
 //
-// Forward: rows = agents x workers (32,768 at N=512) share the LPG parameters,
-// so every time step is a dense [rows x 264] x [264 x 1024] f32 contraction
-// (h: 256 recurrent units, + x features, + a bias row; columns = r | z | W_hn h + b_hn
-// | W_in x + b_in).  One workgroup owns 32 rows for the whole T-step reverse
-// scan: h^T lives in LDS (k-major, padded to 33 columns: conflict-free
-// ds_read_b32 B-fragments), the weights stream from L2 as pre-packed A-fragment
-// float4s (one dwordx4 per lane feeds four v_mfma_f32_32x32x2_f32), and the
-// gate maths happens in the accumulator registers (lane = batch row, registers
-// = 16 gate columns; the r, z, n tiles of a unit line up lane-for-lane).
-// Each wave owns 64 units = 2 unit tiles x {r, z, nh, ni} accumulators.
-// Saved for the backward: h_in (masked carry), r, z, n, W_hn h + b_hn, row-major [unit][M] (the
-// weight-gradient GEMM layout).  The backward loads them 16 B per lane (4 consecutive rows of one unit,
-// full 128-byte lines per wave instruction) and transposes lane quad (4 rows) x register quad (4 units)
-// blocks in registers (DPP): 4x fewer load instructions than per-dword access.  (Transposed 16-byte
-// stores measured slower at this register budget; the cotangent stores stay per dword.)
+// Rows = agents x workers (32,768 at N=512) share the LPG parameters, so every time step is a dense
+// [rows x 272] x [272 x 1024] contraction (h: 256 recurrent units, + x features and a bias row; columns
+// r | z | W_hn h + b_hn | W_in x + b_in) and the VJP a [rows x 768] x [768 x 256] one.
 //
-// Backward (k_gru_bwd_g2): one workgroup per (k, 64 rows), t ascending, as two 32-row groups running half
-// a step apart so that one group's saved-activation traffic overlaps the other's MFMA contraction.  Per
-// step: gate maths in registers; the cotangents dr_pre, dz_pre (LDS slots), then d(W_hn h + b_hn) (slot 0
-// again), each contracted with W_h^T on MFMA to give dh_prev; writes the gate-pre-activation cotangents
-// DG[4][256][M], relu(h_out) and the head cotangents for the weight-gradient GEMMs, and dX for the
-// embedding inputs.  (k_gru_bwd<1>, one 32-row tile with both phases in every wave, covers R % 64 != 0.)
+// Arithmetic: f32-accurate products on the bf16 matrix cores.  Each f32 operand is split exactly into three
+// bf16 pieces (x = x0 + x1 + x2, round-to-nearest at each stage) and a.b is formed from the six piece
+// products of weight >= 2^-16 (a0b0, a0b1, a1b0, a0b2, a1b1, a2b0) on v_mfma_f32_32x32x16_bf16 with f32
+// accumulation; the dropped products are below 2^-24 relative, so results carry f32-GEMM error
+// (tools/gru_accuracy.py, tests/test_gpu_meta.py) at 6 x 32 = 192 MFMA cycles per 32x32x16 block against
+// 512 for v_mfma_f32_32x32x2_f32.  The weights are split once per eta by the pack kernels.
 //
-// MFMA f32 32x32x2 operand/result maps (cdna_hip_programming.md §3):
-//   A: lane l holds A[i = l&31][k = l>>5];  B: lane l holds B[k = l>>5][j = l&31]
-//   D: reg q of lane l is D[i = (q&3) + 8*(q>>2) + 4*(l>>5)][j = l&31]
+// Forward (k_gru_fwd6): one 512-thread workgroup per 64 rows (two 32-row tiles) for the whole reverse scan;
+// wave w owns units [32w, 32w + 32).  The carry h lives in LDS as three bf16 images [row][unit]; weight
+// fragments stream from L2 one k-step ahead and feed both row tiles; gate maths in the accumulator layout
+// (lane = row, register = unit), h_in rebuilt exactly from its pieces.  Saves h_in, r, z, n, W_hn h + b_hn
+// row-major [unit][M] (the weight-gradient layout) for the backward.
+//
+// Backward (k_gru_bwd6n): one 512-thread workgroup per (k, 64 rows), t ascending, all waves in lockstep:
+// a memory part (16-byte saved-activation loads + DPP quad transposes, gate maths, cotangent stores) and a
+// contraction dh_prev = sum_g W_g . dg_g with the cotangents as bf16-piece B fragments from one LDS image.
+//
+// f32 fallbacks (v_mfma_f32_32x32x2_f32, one 32-row tile per workgroup): k_gru_fwd<SAVE, NT> (also the
+// per-candidate ES forward) and k_gru_bwd<1> for row counts that do not split into 64-row blocks, and every
+// GRU kernel under TOUED_GRU_F32=1 (comparison runs).
+//
+// MFMA operand/result maps (cdna_hip_programming.md §3):
+//   f32 32x32x2:  A: lane l holds A[i = l&31][k = l>>5];  B: lane l holds B[k = l>>5][j = l&31]
+//   bf16 32x32x16: A: lane l holds A[i = l&31][k = 8(l>>5) + e];  B: B[k = 8(l>>5) + e][j = l&31], e = 0..7
+//   D (both): reg q of lane l is D[i = (q&3) + 8*(q>>2) + 4*(l>>5)][j = l&31]
 #include <stdlib.h>
 #include <string.h>
 #include "common.h"
@@ -669,7 +672,7 @@ struct BwdArgs {
   int R, T, W, K;
   const uint8_t* done; long done_stride_k;     // per k: [N][T][W]
   const float4* A;                             // packed bwd fragments (f32 MFMA, k_gru_bwd<1>)
-  const void* A6;                              // packed bwd fragments (bf16 split pieces, k_gru_bwd6)
+  const void* A6;                              // packed bwd fragments (bf16 split pieces, k_gru_bwd6n)
   const float* eta; EtaOff o;
   const float* y_hat; const float* d_pi_hat; const float* d_y_hat;   // [K][T][(8)][R]
   const float* s_hin; const float* s_r; const float* s_z; const float* s_n; const float* s_hn;  // [256][M]
@@ -877,281 +880,6 @@ __global__ void __launch_bounds__(512, NT == 1 ? 4 : 1) k_gru_bwd(BwdArgs p) {
   }
 }
 
-// Two-group backward: 64 rows per workgroup as two 32-row groups of four waves, run half a time step
-// apart.  Each super-phase one group does the memory/VALU half of a step (saved-activation loads, gate
-// maths, cotangent stores) while the other contracts the previous step's gate cotangents with W_h^T on
-// MFMA, so every SIMD (one wave of each group) overlaps HBM traffic with matrix work instead of
-// alternating between them.  Wave wg of a group owns units [64 wg, 64 wg + 64) (two 32-unit tiles j) for
-// the group's 32 rows; the LDS holds two cotangent slots per group ([dr | dz], then dhn in slot 0).
-__global__ void __launch_bounds__(512, 1) k_gru_bwd6(BwdArgs p) {
-  constexpr int LDR = HU + 4;                // slot row pitch: 1040 B, conflict-free 16-byte row reads
-  constexpr int SLOT = RB * LDR;
-  __shared__ __attribute__((aligned(16))) float dgT[2 * 2 * SLOT];   // [group][slot][row][unit]
-  __shared__ float wi34[2 * 3 * HU];
-  __shared__ float hv[2 * 9 * RB];           // [group][head output][row]
-  __shared__ __attribute__((aligned(8))) float dxp[2 * 4 * RB * 2];   // [group][wave][row][dx3 | dx4]
-  const int tid = threadIdx.x, lane = tid & 63, hi = lane >> 5, col = lane & 31;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: group offsets go to SGPRs
-  // group = wave >> 2: a workgroup's waves go round-robin over the four SIMDs, so every SIMD holds one
-  // wave of each group (grouping by wave & 1 measured 1.8x slower)
-  const int gi = wave >> 2, wg = wave & 3;
-  const int gtid = wg * 64 + lane;           // thread index within the group
-  const int nb = p.R / (2 * RB);
-  const int k = blockIdx.x / nb;
-  const int r0 = (blockIdx.x - k * nb) * (2 * RB) + RB * gi;   // this group's first row
-  const int R = p.R, T = p.T, W = p.W;
-  const int a_ = r0 / W, w_ = r0 + col - a_ * W;
-  float* dg0 = dgT + gi * 2 * SLOT;          // slot 0 of this group (slot 1 at + SLOT)
-  for (int i = tid; i < 2 * 3 * HU; i += 512) {
-    const int f = 3 + i / (3 * HU), g = (i / HU) % 3, u = i % HU;
-    const int base = g == 0 ? p.o.ir_w : g == 1 ? p.o.iz_w : p.o.in_w;
-    wi34[i] = p.eta[base + f * HU + u];
-  }
-  float wA[2][5];   // W_heads^T A fragments of the two unit tiles: A[i = unit][k = head output 2kk + hi]
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int kk = 0; kk < 5; ++kk) {
-      const int o = 2 * kk + hi, u = 64 * wg + 32 * j + col;
-      wA[j][kk] = o < 9 ? (o == 0 ? p.eta[p.o.pi_w + u] : p.eta[p.o.y_w + u * 8 + (o - 1)]) : 0.0f;
-    }
-  float dh[2][16], dhn_r[2][16];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) { dh[j][q] = 0.0f; dhn_r[j][q] = 0.0f; }
-  const uint8_t* done = p.done + (long)k * p.done_stride_k;
-  const __amdgpu_buffer_rsrc_t rs_hin = rsrc_of(p.s_hin), rs_r = rsrc_of(p.s_r), rs_z = rsrc_of(p.s_z),
-                               rs_n = rsrc_of(p.s_n), rs_hn = rsrc_of(p.s_hn), rs_rh = rsrc_of(p.RH);
-  const __amdgpu_buffer_rsrc_t rs_dg[4] = {rsrc_of(p.DG), rsrc_of(p.DG + 1L * HU * p.M),
-                                           rsrc_of(p.DG + 2L * HU * p.M), rsrc_of(p.DG + 3L * HU * p.M)};
-  // Per-row global accesses go through wave-uniform buffer descriptors with a 32-bit lane offset: 64-bit
-  // per-lane addresses kept live across the phase loop spill, and a spilled store address reloaded into the
-  // same registers right behind the store was observed to drop the store (dX3) on gfx950.
-  const __amdgpu_buffer_rsrc_t rs_yh = rsrc_of(p.y_hat), rs_dyh = rsrc_of(p.d_y_hat), rs_dpi = rsrc_of(p.d_pi_hat),
-                               rs_DH = rsrc_of(p.DH), rs_dx3 = rsrc_of(p.dX3), rs_dx4 = rsrc_of(p.dX4);
-  const unsigned vrow = (unsigned)gtid * 4;   // lane's row offset (gtid < RB)
-  // head cotangents of step t (softmax VJP of y_hat, d pi_hat) for the group's rows -> hv, DH
-  auto head_cot = [&](int t) {
-    if (gtid < RB) {
-      const long o = ((long)k * T + t) * R + r0;    // uniform column base
-      float yh[8], dy[8], s = 0.0f;
-      for (int j = 0; j < 8; ++j) {
-        const unsigned so = (unsigned)((((long)k * T * 8 + (long)t * 8 + j) * R + r0) * 4);
-        yh[j] = ld_u(rs_yh, vrow, so);
-        dy[j] = ld_u(rs_dyh, vrow, so);
-        s += yh[j] * dy[j];
-      }
-      const float dpi = ld_u(rs_dpi, vrow, (unsigned)(o * 4));
-      hv[(gi * 9) * RB + gtid] = dpi;
-      st_u(rs_DH, vrow, (unsigned)(o * 4), dpi);
-      for (int j = 0; j < 8; ++j) {
-        const float v = yh[j] * (dy[j] - s);
-        hv[(gi * 9 + j + 1) * RB + gtid] = v;
-        st_u(rs_DH, vrow, (unsigned)(((long)(j + 1) * p.M + o) * 4), v);
-      }
-    }
-  };
-  head_cot(0);
-  __syncthreads();
-  // ---- memory half: unit quad (tile j, quad g4) of step t
-  floatx16 hacc[2];
-  float dx3 = 0.0f, dx4 = 0.0f;
-  // saved activations of unit quad (tile j, quad g4) of step t: 16-byte row-quad loads + quad transposes
-  auto mem_load = [&](int t, int j, int g4, float (&v)[5][4]) {
-    const long ctr = ((long)k * T + t) * R;
-    const int ub = 64 * wg + 32 * j + 4 * hi;
-    const unsigned vq = (unsigned)(((long)(ub + (col & 3)) * p.M + r0 + (col & 28)) * 4);
-    const unsigned so = (unsigned)(((long)8 * g4 * p.M + ctr) * 4);
-    ld4(rs_hin, vq, so, v[0]);
-    ld4(rs_r, vq, so, v[1]);
-    ld4(rs_z, vq, so, v[2]);
-    ld4(rs_n, vq, so, v[3]);
-    ld4(rs_hn, vq, so, v[4]);
-  };
-  auto mem_compute = [&](int t, int j, int g4, float (&v)[5][4]) {
-    const long ctr = ((long)k * T + t) * R;
-    const int ub = 64 * wg + 32 * j + 4 * hi;          // lane's unit base within the tile
-#pragma unroll
-    for (int a = 0; a < 5; ++a) quad_transpose(v[a], lane);
-    float* o_rh = v[0]; float* o_dn = v[4];   // reused in place
-    const float* wil = wi34 + ub;
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int q = 4 * g4 + jj;
-      const float hin = v[0][jj], rg = v[1][jj], zg = v[2][jj], ng = v[3][jj], hn = v[4][jj];
-      const float hout = (1.0f - zg) * ng + zg * hin;
-      const float d = dh[j][q] + (hout > 0.0f ? hacc[j][q] : 0.0f);
-      const float dn_ = d * (1.0f - zg);
-      const float dz = d * (hin - ng);
-      const float dnp = dn_ * (1.0f - ng * ng);
-      const float dhn = dnp * rg;
-      const float drp = dnp * hn * rg * (1.0f - rg);
-      const float dzp = dz * zg * (1.0f - zg);
-      dh[j][q] = d * zg;   // direct path; the W_h^T contraction is added in the MFMA half
-      dg0[col * LDR + ub + qunit(q)] = drp;
-      dg0[SLOT + col * LDR + ub + qunit(q)] = dzp;
-      dhn_r[j][q] = dhn;
-      o_rh[jj] = fmaxf(hout, 0.0f); o_dn[jj] = dnp;
-      const int qu = qunit(q);
-      dx3 += drp * wil[0 * HU + qu] + dzp * wil[1 * HU + qu] + dnp * wil[2 * HU + qu];
-      dx4 += drp * wil[3 * HU + qu] + dzp * wil[4 * HU + qu] + dnp * wil[5 * HU + qu];
-    }
-    const unsigned vb = (unsigned)(((long)ub * p.M + r0 + col) * 4);
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const unsigned so1 = (unsigned)(((long)qunit(4 * g4 + jj) * p.M + ctr) * 4);
-      st_u(rs_rh, vb, so1, o_rh[jj]);
-      st_u(rs_dg[3], vb, so1, o_dn[jj]);   // dr, dz, dhn leave from LDS in the MFMA half
-    }
-  };
-  // unit quad (tile j, quad g4), written out per quad: the schedule barrier keeps the compiler from
-  // hoisting later quads' loads, and a wrapping lambda (or loop) measured 90-110 VGPR spills
-  float va[5][4], vb[5][4];
-#define G2_QUAD(j, g4, v) { mem_load(t, j, g4, v); __builtin_amdgcn_sched_barrier(0); mem_compute(t, j, g4, v); }
-  auto head_vjp = [&](int j) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) hacc[j][q] = 0.0f;
-#pragma unroll
-    for (int kk = 0; kk < 5; ++kk) {
-      const int o = 2 * kk + hi;
-      hacc[j] = mfma32(wA[j][kk], o < 9 ? hv[(gi * 9 + o) * RB + col] : 0.0f, hacc[j]);
-    }
-  };
-  // ---- MFMA half: one slot of the group's cotangents out to DG[g] (16-byte row quads from LDS)
-  auto store_slot = [&](const float* buf, __amdgpu_buffer_rsrc_t rs, long col0) {
-    const unsigned so = (unsigned)(col0 * 4);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int unit = 64 * wg + 8 * i + (lane >> 3), r = 4 * (lane & 7);
-      const float* src = buf + r * LDR + unit;
-      const float v[4] = {src[0], src[LDR], src[2 * LDR], src[3 * LDR]};
-      st4(rs, (unsigned)(((long)unit * p.M + r) * 4), so, v);
-    }
-  };
-  floatx16 acc[2];
-  // dh_prev = W_g . dg on the bf16 matrix cores, f32-accurate split products (k_gru_fwd6): A fragments
-  // (W_g pre-split by k_pack_bwd6) through a 2-deep register ring from L2; B fragments (this lane's row,
-  // 8 consecutive gate units) read from the f32 slot one k-step ahead and split in registers.
-  bf16x8 ring[2][2][3];
-  const __amdgpu_buffer_rsrc_t rs_A = rsrc_of(reinterpret_cast<const float*>(p.A6));
-  const unsigned vA = (unsigned)lane * 16;
-  auto ldA = [&](int ks, int j, int g, int q) {
-    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(
-        rs_A, (int)vA, (int)((((ks * 8 + 2 * wg + j) * 3 + g) * 3 + q) * 1024), 0);
-    return __builtin_bit_cast(bf16x8, x);
-  };
-  auto ring_fill = [&](int g) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int q = 0; q < 3; ++q) ring[i][j][q] = ldA(i, j, g, q);
-  };
-  auto contract = [&](int g, const float* dgs) {
-    const float* bl = dgs + col * LDR + 8 * hi;
-    float4 b0 = *reinterpret_cast<const float4*>(bl), b1 = *reinterpret_cast<const float4*>(bl + 4);
-    auto kstep = [&](int ks, bool reload) {
-      bf16x8 bp[3];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float x = e < 4 ? (e == 0 ? b0.x : e == 1 ? b0.y : e == 2 ? b0.z : b0.w)
-                              : (e == 4 ? b1.x : e == 5 ? b1.y : e == 6 ? b1.z : b1.w);
-        split3v(x, bp[0], bp[1], bp[2], e);
-      }
-      if (ks + 1 < 16) {
-        b0 = *reinterpret_cast<const float4*>(bl + 16 * (ks + 1));
-        b1 = *reinterpret_cast<const float4*>(bl + 16 * (ks + 1) + 4);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[j] = mfma6(ring[ks & 1][j], bp, acc[j]);
-      if (reload) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int q = 0; q < 3; ++q) ring[ks & 1][j][q] = ldA(ks + 2, j, g, q);
-      }
-      __builtin_amdgcn_sched_barrier(0);   // keep each refill right behind its slot's last MFMA
-    };
-#pragma unroll 2
-    for (int ks = 0; ks < 14; ++ks) kstep(ks, true);
-    kstep(14, false);
-    kstep(15, false);
-  };
-  for (int s = 0; s <= 2 * T; ++s) {
-    const int u = s - gi;
-    const bool act = u >= 0 && (u >> 1) < T;
-    const bool mem = act && (u & 1) == 0, mm = act && (u & 1) == 1;
-    const int t = u >> 1;
-    const long ctr = ((long)k * T + t) * R;
-    // part X: memory quads of tile 0 | dr, dz out + contraction (the MFMA wave at raised issue priority)
-    if (mem) {
-      dx3 = 0.0f; dx4 = 0.0f;
-      head_vjp(0);
-      G2_QUAD(0, 0, va)
-      G2_QUAD(0, 1, vb)
-      G2_QUAD(0, 2, va)
-      G2_QUAD(0, 3, vb)
-    } else if (mm) {
-      if (gtid < RB) {
-        float s3 = 0.0f, s4 = 0.0f;
-        for (int gq = 0; gq < 4; ++gq) {
-          const float2 v = *reinterpret_cast<const float2*>(dxp + ((gi * 4 + gq) * RB + gtid) * 2);
-          s3 += v.x;
-          s4 += v.y;
-        }
-        st_u(rs_dx3, vrow, (unsigned)((ctr + r0) * 4), s3);
-        st_u(rs_dx4, vrow, (unsigned)((ctr + r0) * 4), s4);
-      }
-      ring_fill(0);
-      store_slot(dg0, rs_dg[0], ctr + r0);
-      store_slot(dg0 + SLOT, rs_dg[1], ctr + r0);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[j][q] = 0.0f;
-      contract(0, dg0);
-      ring_fill(1);
-      contract(1, dg0 + SLOT);
-    }
-    __syncthreads();
-    // part Y: dhn into slot 0 once every wave of the group has read dr
-    if (mm) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4)
-          *reinterpret_cast<float4*>(dg0 + col * LDR + 64 * wg + 32 * j + 4 * hi + 8 * g4) =
-              make_float4(dhn_r[j][4 * g4], dhn_r[j][4 * g4 + 1], dhn_r[j][4 * g4 + 2], dhn_r[j][4 * g4 + 3]);
-    }
-    __syncthreads();
-    // part Z: memory quads of tile 1 + dx partials | dhn out + contraction, carry, next head cotangents
-    if (mem) {
-      head_vjp(1);
-      G2_QUAD(1, 0, va)
-      G2_QUAD(1, 1, vb)
-      G2_QUAD(1, 2, va)
-      G2_QUAD(1, 3, vb)
-      // lanes l and l + 32 hold the same row: fold the halves, then one float2 per row and wave
-      const float f3 = dx3 + __shfl_xor(dx3, 32), f4 = dx4 + __shfl_xor(dx4, 32);
-      if (hi == 0) *reinterpret_cast<float2*>(dxp + ((gi * 4 + wg) * RB + col) * 2) = make_float2(f3, f4);
-    } else if (mm) {
-      ring_fill(2);
-      store_slot(dg0, rs_dg[2], ctr + r0);
-      contract(2, dg0);
-      // carry to h_out(t+1): h_in(t) = where(d_t, 0, h_out(t+1))
-      const bool dn = done[((size_t)a_ * T + t) * W + w_] != 0;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) dh[j][q] = dn ? 0.0f : dh[j][q] + acc[j][q];
-      if (t + 1 < T) head_cot(t + 1);
-    }
-    __syncthreads();
-  }
-}
 
 // Backward in lockstep (k_gru_bwd6n): one 512-thread workgroup per (k, 64 rows), both 32-row tiles in
 // every wave, so each pre-split W_g fragment (L2) feeds both tiles: half the fragment traffic of the two-group
@@ -1504,12 +1232,8 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
   p.y_hat = y_hat; p.d_pi_hat = d_pi_hat; p.d_y_hat = d_y_hat;
   p.s_hin = s_hin; p.s_r = s_r; p.s_z = s_z; p.s_n = s_n; p.s_hn = s_hn; p.M = M;
   p.DG = DG; p.RH = RH; p.DH = DH; p.dX3 = dX3; p.dX4 = dX4;
-  if (R % (2 * RB) == 0 && !gru_f32_forced()) {
-    if (getenv("TOUED_BWD_G2"))
-      hipLaunchKernelGGL(k_gru_bwd6, dim3(K * (R / (2 * RB))), dim3(512), 0, stream, p);
-    else
-      hipLaunchKernelGGL(k_gru_bwd6n, dim3(K * (R / (2 * RB))), dim3(512), 0, stream, p);
-  }
+  if (R % (2 * RB) == 0 && !gru_f32_forced())
+    hipLaunchKernelGGL(k_gru_bwd6n, dim3(K * (R / (2 * RB))), dim3(512), 0, stream, p);
   else
     hipLaunchKernelGGL(k_gru_bwd<1>, dim3(K * (R / RB)), dim3(512), 0, stream, p);
   TOUED_CHECK_LAUNCH();
