@@ -118,11 +118,11 @@ TOUED_DEV float tanh_f(float x) {
 // ------------------------------------------------------------------ packing
 // fwdA[(tile*KQF + kq)*64 + lane] = float4 over kk = 4kq..4kq+3 of A[i=l&31][k=2kk+(l>>5)]
 __global__ void k_pack_fwd(const float* __restrict__ eta, EtaOff o, int F, float4* __restrict__ out,
-                           long eta_stride) {
+                           long eta_stride, long out_stride4) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= NTILE_F * KQF * 64) return;
   eta += (long)blockIdx.y * eta_stride;            // candidate blockIdx.y (ES); 0 for the shared eta
-  out += (long)blockIdx.y * NTILE_F * KQF * 64;
+  out += (long)blockIdx.y * out_stride4;
   const int lane = gid & 63, kq = (gid >> 6) % KQF, tile = gid / (64 * KQF);
   const int g = tile >> 3, u = 32 * (tile & 7) + (lane & 31);
   float v[4];
@@ -424,8 +424,11 @@ TOUED_DEV void split3v(float x, V& p0, V& p1, V& p2, int e) {
 
 // one thread per (fragment group, lane): fragment group = (ks, ut, g) for the h part or (ut, g) for the
 // augmented rows; lane l holds A[i = unit 32 ut + (l & 31)][k = 8 (l >> 5) + e], e = 0..7
-__global__ void k_pack_fwd6(const float* __restrict__ eta, EtaOff o, int F, bf16x8* __restrict__ out) {
+__global__ void k_pack_fwd6(const float* __restrict__ eta, EtaOff o, int F, bf16x8* __restrict__ out,
+                            long eta_stride, long out_stride16) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  eta += (long)blockIdx.y * eta_stride;            // candidate blockIdx.y (ES); 0 for the shared eta
+  out += (long)blockIdx.y * out_stride16;
   const int ngrp_h = 16 * 8 * 3, ngrp = ngrp_h + 8 * 4;
   if (gid >= ngrp * 64) return;
   const int lane = gid & 63, grp = gid >> 6;
@@ -477,6 +480,7 @@ TOUED_DEV floatx16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx16 c)
   return c;
 }
 
+template <bool SAVE>
 __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   __shared__ __attribute__((aligned(16))) __bf16 hB[3][64 * F6_HP];   // carry h(t) pieces [row][unit]
   __shared__ __attribute__((aligned(16))) float wh[HU * 12];          // head weights [unit][pi | y0..y7 | pad]
@@ -492,7 +496,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     a_[h] = (r0 + RB * h) / W;
     w_[h] = r0 + RB * h + col - a_[h] * W;
   }
-  const float* eta = p.eta;
+  // per-candidate parameters in the ES inference mode (rows [c * rpc, (c + 1) * rpc) use candidate c)
+  const int cand = SAVE ? 0 : r0 / p.rpc;
+  const float* eta = p.eta + (long)cand * p.eta_stride;
   for (int i = tid; i < HU * 12; i += 512) {
     const int u = i / 12, oo = i - u * 12;
     wh[i] = oo == 0 ? eta[p.o.pi_w + u] : oo < 9 ? eta[p.o.y_w + u * 8 + (oo - 1)] : 0.0f;
@@ -508,7 +514,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   const __amdgpu_buffer_rsrc_t rs_done = rsrc_of(reinterpret_cast<const float*>(p.done));
   __syncthreads();
   const float bpi = eta[p.o.pi_b];
-  const __amdgpu_buffer_rsrc_t rs_A = rsrc_of(reinterpret_cast<const float*>(p.A6));
+  const __amdgpu_buffer_rsrc_t rs_A =
+      rsrc_of(reinterpret_cast<const float*>(p.A6) + (long)cand * p.a_stride4 * 4);
   const unsigned vA = (unsigned)lane * 16;
   auto ldA = [&](int frag) {
     const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs_A, (int)vA, frag * 1024, 0);
@@ -624,11 +631,13 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
           const float hh = (1.0f - zg) * ng + zg * hin;
           split3v(dn ? 0.0f : hh, nq[0], nq[1], nq[2], e);   // carry h_in(t-1) = where(d_{t-1}, 0, h_out(t))
           const unsigned so = (unsigned)(((long)qunit(q) * p.M + cbase) * 4);
-          st_u(rs_hin, vbyte, so, hin);
-          st_u(rs_r, vbyte, so, rg);
-          st_u(rs_z, vbyte, so, zg);
-          st_u(rs_n, vbyte, so, ng);
-          st_u(rs_hn, vbyte, so, hn);
+          if (SAVE) {
+            st_u(rs_hin, vbyte, so, hin);
+            st_u(rs_r, vbyte, so, rg);
+            st_u(rs_z, vbyte, so, zg);
+            st_u(rs_n, vbyte, so, ng);
+            st_u(rs_hn, vbyte, so, hn);
+          }
           const float rl = fmaxf(hh, 0.0f);
           const float4 w0 = whl[qunit(q) * 3], w1 = whl[qunit(q) * 3 + 1], w2 = whl[qunit(q) * 3 + 2];
           hp_loc[0] += rl * w0.x; hp_loc[1] += rl * w0.y; hp_loc[2] += rl * w0.z;
@@ -1127,9 +1136,9 @@ int toued_gru_pack(const float* eta, const int* off, int F, float* fwdA, float* 
   memcpy(&o, off, sizeof(EtaOff));
   const int n1 = NTILE_F * KQF * 64, n2 = 8 * 3 * 32 * 64, n3 = (16 * 8 * 3 + 8 * 4) * 64;
   hipLaunchKernelGGL(k_pack_fwd, dim3((n1 + 255) / 256), dim3(256), 0, stream, eta, o, F,
-                     reinterpret_cast<float4*>(fwdA), 0L);
+                     reinterpret_cast<float4*>(fwdA), 0L, 0L);
   hipLaunchKernelGGL(k_pack_fwd6, dim3((n3 + 255) / 256), dim3(256), 0, stream, eta, o, F,
-                     reinterpret_cast<bf16x8*>(fwdA + (size_t)n1 * 4));
+                     reinterpret_cast<bf16x8*>(fwdA + (size_t)n1 * 4), 0L, 0L);
   hipLaunchKernelGGL(k_pack_bwd, dim3((n2 + 255) / 256), dim3(256), 0, stream, eta, o,
                      reinterpret_cast<float4*>(bwdA));
   hipLaunchKernelGGL(k_pack_bwd6, dim3((16 * 8 * 3 * 64 + 255) / 256), dim3(256), 0, stream, eta, o,
@@ -1138,11 +1147,11 @@ int toued_gru_pack(const float* eta, const int* off, int F, float* fwdA, float* 
   return 0;
 }
 
-// which: 0 = forward fragments (f32 MFMA, then the bf16-split pieces), 1 = backward, 2 = forward f32 fragments of
-// one candidate (toued_gru_pack_fwd_multi stride)
+// which: 0 = forward fragments (f32 MFMA, then the bf16-split pieces), 1 = backward, 2 = one candidate's forward
+// fragments in a toued_gru_pack_fwd_multi buffer (the same layout as 0)
 size_t toued_gru_packed_floats(int which) {
   const size_t f32_part = (size_t)NTILE_F * KQF * 64 * 4;
-  return which == 0 ? f32_part + F6_FLOATS : which == 1 ? (size_t)8 * 3 * 32 * 64 * 4 + B6_FLOATS : f32_part;
+  return which == 1 ? (size_t)8 * 3 * 32 * 64 * 4 + B6_FLOATS : f32_part + F6_FLOATS;
 }
 
 static bool gru_f32_forced() {
@@ -1163,12 +1172,13 @@ static int gru_fwd_launch(int R, int T, int W, int F, const float* X, long xs_f,
   p.A6 = fwdA + (size_t)NTILE_F * KQF * 64 * 4;
   memcpy(&p.o, off, sizeof(EtaOff));
   p.pi_hat = pi_hat; p.y_hat = y_hat; p.s_hin = s_hin; p.s_r = s_r; p.s_z = s_z; p.s_n = s_n; p.s_hn = s_hn; p.M = M;
-  p.rpc = rpc; p.a_stride4 = (long)NTILE_F * KQF * 64; p.eta_stride = eta_stride;
+  p.rpc = rpc; p.a_stride4 = (long)toued_gru_packed_floats(2) / 4; p.eta_stride = eta_stride;
   // two row tiles per workgroup when the rows (and, for per-candidate parameters, each candidate's rows)
   // split into 64-row blocks
   const bool nt2 = R % (2 * RB) == 0 && (rpc == 0 || rpc % (2 * RB) == 0);
-  if (save && nt2 && !gru_f32_forced()) {
-    hipLaunchKernelGGL(k_gru_fwd6, dim3(R / (2 * RB)), dim3(512), 0, stream, p);
+  if (nt2 && !gru_f32_forced()) {
+    if (save) hipLaunchKernelGGL(k_gru_fwd6<true>, dim3(R / (2 * RB)), dim3(512), 0, stream, p);
+    else hipLaunchKernelGGL(k_gru_fwd6<false>, dim3(R / (2 * RB)), dim3(512), 0, stream, p);
   } else if (save) {
     if (nt2) hipLaunchKernelGGL((k_gru_fwd<true, 2>), dim3(R / (2 * RB)), dim3(512), 0, stream, p);
     else hipLaunchKernelGGL((k_gru_fwd<true, 1>), dim3(R / RB), dim3(512), 0, stream, p);
@@ -1199,8 +1209,12 @@ int toued_gru_pack_fwd_multi(const float* eta, long eta_stride, int n, const int
   EtaOff o;
   memcpy(&o, off, sizeof(EtaOff));
   const int n1 = NTILE_F * KQF * 64;
+  const long cstride = (long)toued_gru_packed_floats(2);   // floats per candidate
   hipLaunchKernelGGL(k_pack_fwd, dim3((n1 + 255) / 256, n), dim3(256), 0, stream, eta, o, F,
-                     reinterpret_cast<float4*>(fwdA), eta_stride);
+                     reinterpret_cast<float4*>(fwdA), eta_stride, cstride / 4);
+  const int n3 = (16 * 8 * 3 + 8 * 4) * 64;
+  hipLaunchKernelGGL(k_pack_fwd6, dim3((n3 + 255) / 256, n), dim3(256), 0, stream, eta, o, F,
+                     reinterpret_cast<bf16x8*>(fwdA + (size_t)n1 * 4), eta_stride, cstride / 4);
   TOUED_CHECK_LAUNCH();
   return 0;
 }
