@@ -123,8 +123,8 @@ class MetaGradStep:
         self.adv = z(N, W, T)
         self.abar = z(N, W)
         self.loss_out = z(N, 2)
-        self.adj_th = [z(N, D, 5), z(N, D, 5)]
-        self.adj_ph = [z(N, D, Y), z(N, D, Y)]
+        self.adj_th = [z(N, D, 5)]       # adjoint tables, accumulated in place over k (toued_hvp)
+        self.adj_ph = [z(N, D, Y)]
         self.coef = z(N, 4)
         self.keys_roll = z(K, N, 2, dt=i32)
         self.keys_eval = z(N, 2, dt=i32)
@@ -215,7 +215,7 @@ class MetaGradStep:
             (_, _), ea_state = self.ro.batch_reset(self.keys_ea_reset, agents.levels, hyp.eval_workers)
             ea_cum = self._eval_rollout(self.keys_ea_roll, self.theta_h[K], agents.levels, ea_state)
         # ---------------- reverse: explicit adjoint w.r.t. eta
-        a_in, a_out = 0, 1
+        a_in = 0
         self.adj_th[a_in].zero_()
         self.adj_ph[a_in].zero_()
         L.call("toued_lpgloss_grad", N, W, T, D, ptr(self.theta_h[K]), ptr(te.obs_idx), ptr(te.obs_time),
@@ -229,14 +229,14 @@ class MetaGradStep:
             L.call("toued_clip_dot", N, D, ptr(self.G_th[k]), ptr(self.G_ph[k]), ptr(self.adj_th[a_in]),
                    ptr(self.adj_ph[a_in]), ptr(self.gstat[k]), hyp.actor_lr, hyp.critic_lr, hyp.max_grad_norm,
                    ptr(self.coef), st)
-            self.adj_th[a_out].copy_(self.adj_th[a_in])
-            self.adj_ph[a_out].copy_(self.adj_ph[a_in])
+            # theta_bar_k = theta_bar_{k+1} + (sparse second-order rows): accumulated in place.  k_rows_sorted reads
+            # every sample's adjoint rows before its first row write (the sort's barriers separate the phases), and
+            # each agent's tables belong to one workgroup, so no copy of the 144 MB adjoint is needed.
             L.call("toued_hvp", N, W, T, D, K, ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(tk.obs_idx),
                    ptr(tk.obs_time), ptr(tk.action), ptr(self.pi_hat[k]), ptr(self.y_hat[k]), ptr(self.G_th[k]),
                    ptr(self.G_ph[k]), ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]), ptr(self.coef), hyp.actor_lr,
                    hyp.critic_lr, hyp.agent_target_coeff, hyp.policy_l2_coeff, hyp.target_l2_coeff,
-                   ptr(self.adj_th[a_out]), ptr(self.adj_ph[a_out]), ptr(self.d_pi_hat[k]), ptr(self.d_y_hat[k]), st)
-            a_in, a_out = a_out, a_in
+                   ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]), ptr(self.d_pi_hat[k]), ptr(self.d_y_hat[k]), st)
         self.grad.zero_()
         self.gru.backward(self.traj.done, eta, self.y_hat, self.d_pi_hat, self.d_y_hat, self.X, self.grad,
                           self.timers)
