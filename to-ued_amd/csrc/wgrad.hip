@@ -296,6 +296,22 @@ __global__ void k_wgrad_reduce(const float* __restrict__ part, int S, int RA, in
   C[idx] = s;
 }
 
+// Many chunks (the small HBM-stream reductions split K ~500 ways): one wave per output element, lane l sums
+// chunks l, l + 64, ... in order, then a fixed xor-butterfly across the wave -- still deterministic, and
+// ~S/64 dependent loads per lane instead of S.
+__global__ void k_wgrad_reduce_wave(const float* __restrict__ part, int S, int RA, int rbp, int ra, int rb,
+                                    float* __restrict__ C) {
+  const long idx = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (idx >= (long)ra * rb) return;
+  const int i = (int)(idx / rb), j = (int)(idx - (long)i * rb);
+  float s = 0.0f;
+  for (int c = lane; c < S; c += 64) s += part[((long)c * RA + i) * rbp + j];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+  if (lane == 0) C[idx] = s;
+}
+
 struct Plan {
   int nrt, ncol, S, ct;   // ct: B rows per workgroup (column-tile width of the partial-sum workspace)
   bool x6;
@@ -366,8 +382,12 @@ int toued_wgrad(int ra, int rb, long K, const float* A, long lda, const float* B
   else
     hipLaunchKernelGGL(k_wgrad<17>, grid, dim3(512), 0, stream, A, lda, ra, B, ldb, rb, K, p.kchunk, work);
   const long n = (long)ra * rb;
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, work, p.S, p.nrt * 16,
-                     p.ncol * p.ct, ra, rb, C);
+  if (p.S > 128)
+    hipLaunchKernelGGL(k_wgrad_reduce_wave, dim3((unsigned)((n * 64 + 255) / 256)), dim3(256), 0, stream, work, p.S,
+                       p.nrt * 16, p.ncol * p.ct, ra, rb, C);
+  else
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, work, p.S,
+                       p.nrt * 16, p.ncol * p.ct, ra, rb, C);
   TOUED_CHECK_LAUNCH();
   return 0;
 }
