@@ -122,6 +122,13 @@ int toued_a2c_grad(int N, int W, int T, int D, const float* theta, const float* 
                    float lam, float ent_coef, float* Ga, float* Gv, float* loss_out, hipStream_t stream);
 /* apply_gradients (clip_by_global_norm + SGD, models/optim.py:5-11) for actor and value critic,
  * kept only while step+1 <= levels[i].lifetime (a2c.py:71-75); zeroes Ga/Gv. */
+/* fused A2C update (toued_a2c_grad + toued_a2c_apply with the gradient tables in LDS), for sizes where
+ * toued_a2c_update_fits(W, T, D) is 1 (D*6 floats plus the agent's staged trajectory fit the LDS) */
+int toued_a2c_update_fits(int W, int T, int D);
+int toued_a2c_update(int N, int W, int T, int D, float* theta, float* vcrit, const int* tidx, const int* ttime,
+                     const uint8_t* tact, const float* trew, const uint8_t* tdone, float gamma, float lam,
+                     float ent_coef, float lr_a, float lr_c, float max_norm, int* step, const int* levels,
+                     float* loss_out, hipStream_t stream);
 int toued_a2c_apply(int N, int D, float* theta, float* vcrit, float* Ga, float* Gv, float lr_a, float lr_c,
                     float max_norm, int* step, const int* levels, hipStream_t stream);
 

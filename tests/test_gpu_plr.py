@@ -70,14 +70,16 @@ def _a2c_setup(mode, N, W, T, seed=0, scale=20.0):
     return ro, levels, p, lt, theta, vcrit, state, D
 
 
-def test_a2c_update_matches_oracle():
+@pytest.mark.parametrize("fused", [True, False])
+def test_a2c_update_matches_oracle(fused):
+    """fused: the LDS-table update kernel (toued_a2c_update); else toued_a2c_grad + toued_a2c_apply."""
     from toued.a2c import A2CHyperparams, A2CTrainer
     mode, N, W, T = "dense", 3, 64, 20
     ro, levels, p, lt, theta, vcrit, state, D = _a2c_setup(mode, N, W, T)
     spec = olv.env_spec(mode)
     th0, vc0, st0 = theta.cpu().numpy(), vcrit.cpu().numpy(), state.cpu().numpy()
     rng = jr.split(jr.PRNGKey(9), N)
-    tr = A2CTrainer(ro, A2CHyperparams(), _ahyp(mode), use_graph=False)
+    tr = A2CTrainer(ro, A2CHyperparams(), _ahyp(mode), use_graph=False, fused=fused)
     step = torch.zeros(N, dtype=torch.int32, device="cuda")
     loss = tr.train(dk(rng), theta, vcrit, step, levels, state, 1).cpu().numpy()
     b = tr._bufs["tr"]

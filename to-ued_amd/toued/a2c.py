@@ -30,12 +30,13 @@ class A2CHyperparams:
 
 class A2CTrainer:
     def __init__(self, ro: RolloutWrapper, hyp: A2CHyperparams, agent_hypers: AgentHyperparams,
-                 use_graph: bool = True):
+                 use_graph: bool = True, fused: bool | None = None):
         agent_hypers.check_supported()
         self.ro = ro
         self.hyp = hyp
         self.ah = agent_hypers
         self.use_graph = use_graph
+        self.fused = fused          # None: the LDS-fused update whenever it fits (toued_a2c_update_fits)
         self._bufs = None
         self._graph = None
         self._graph_key = None
@@ -68,10 +69,18 @@ class A2CTrainer:
         L.call("toued_key_chain", L.ptr(b["rng"]), n, U, L.ptr(b["chain"]), st)
         tr = b["tr"]
         lr_a, lr_c, mn = self.ah.actor_learning_rate, self.ah.critic_learning_rate, self.ah.max_grad_norm
+        fits = bool(L.lib().toued_a2c_update_fits(W, T, D))
+        fused = fits if self.fused is None else (self.fused and fits)
         for u in range(U):
             L.call("toued_rollout", self.ro._c, L.ptr(b["levels"]), L.ptr(b["theta"]), D, L.ptr(b["chain"][u]),
                    L.ptr(b["state"]), n, W, T, L.ptr(tr.obs_idx), L.ptr(tr.obs_time), L.ptr(tr.action),
                    L.ptr(tr.reward), L.ptr(tr.done), None, st)
+            if fused:   # gradient tables in LDS, grad + clip + SGD in one kernel
+                L.call("toued_a2c_update", n, W, T, D, L.ptr(b["theta"]), L.ptr(b["vcrit"]), L.ptr(tr.obs_idx),
+                       L.ptr(tr.obs_time), L.ptr(tr.action), L.ptr(tr.reward), L.ptr(tr.done), self.hyp.gamma,
+                       self.hyp.gae_lambda, self.hyp.entropy_coeff, lr_a, lr_c, mn, L.ptr(b["step"]),
+                       L.ptr(b["levels"]), L.ptr(b["loss"]), st)
+                continue
             L.call("toued_a2c_grad", n, W, T, D, L.ptr(b["theta"]), L.ptr(b["vcrit"]), L.ptr(tr.obs_idx),
                    L.ptr(tr.obs_time), L.ptr(tr.action), L.ptr(tr.reward), L.ptr(tr.done), self.hyp.gamma,
                    self.hyp.gae_lambda, self.hyp.entropy_coeff, L.ptr(b["Ga"]), L.ptr(b["Gv"]), L.ptr(b["loss"]), st)
