@@ -1014,68 +1014,80 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     const long ctr = ((long)k * T + t) * R;
     head_cot(t);
     __syncthreads();
-    // ---- memory part
+    // ---- memory part: the eight unit quads (two row tiles x four) as a software pipeline, quad i+1's five
+    // 16-byte loads in flight while quad i is transposed and processed (twice the bytes in flight per wave)
     float dz_r[2][16], dhn_r[2][16];
     const int ub = 32 * wave + 4 * hi;               // lane's unit base (register q adds qunit(q))
     const float* wil = wi34 + ub;
+    float va[5][4], vb4[5][4];
+    auto load_q = [&](int h, int g4, float (&v)[5][4]) {
+      const unsigned vq = (unsigned)((((long)(ub + (col & 3))) * p.M + r0 + RB * h + (col & 28)) * 4);
+      const unsigned so = (unsigned)(((long)8 * g4 * p.M + ctr) * 4);
+      ld4(rs_hin, vq, so, v[0]);
+      ld4(rs_r, vq, so, v[1]);
+      ld4(rs_z, vq, so, v[2]);
+      ld4(rs_n, vq, so, v[3]);
+      ld4(rs_hn, vq, so, v[4]);
+    };
+    floatx16 hacc;
+    float dx3 = 0.0f, dx4 = 0.0f;
+    load_q(0, 0, va);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      floatx16 hacc;
+    for (int qi = 0; qi < 8; ++qi) {
+      const int h = qi >> 2, g4 = qi & 3;
+      float (&v)[5][4] = (qi & 1) ? vb4 : va;
+      if (qi + 1 < 8) load_q((qi + 1) >> 2, (qi + 1) & 3, (qi & 1) ? va : vb4);
+      __builtin_amdgcn_sched_barrier(0);
+      if (g4 == 0) {
+        // head VJP W_heads . hv on MFMA for this row tile (lane = row, register = unit)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) hacc[q] = 0.0f;
+        for (int q = 0; q < 16; ++q) hacc[q] = 0.0f;
 #pragma unroll
-      for (int kk = 0; kk < 5; ++kk) {
-        const int o = 2 * kk + hi;
-        hacc = mfma32(wA[kk], o < 9 ? hv[o * RBT + RB * h + col] : 0.0f, hacc);
+        for (int kk = 0; kk < 5; ++kk) {
+          const int o = 2 * kk + hi;
+          hacc = mfma32(wA[kk], o < 9 ? hv[o * RBT + RB * h + col] : 0.0f, hacc);
+        }
+        dx3 = 0.0f;
+        dx4 = 0.0f;
       }
       const int row = RB * h + col;
-      const unsigned vq = (unsigned)((((long)(ub + (col & 3))) * p.M + r0 + RB * h + (col & 28)) * 4);
-      const unsigned vb = (unsigned)(((long)ub * p.M + r0 + row) * 4);
-      float dx3 = 0.0f, dx4 = 0.0f;
+      const unsigned vbo = (unsigned)(((long)ub * p.M + r0 + row) * 4);
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const unsigned so = (unsigned)(((long)8 * g4 * p.M + ctr) * 4);
-        float v[5][4];
-        ld4(rs_hin, vq, so, v[0]);
-        ld4(rs_r, vq, so, v[1]);
-        ld4(rs_z, vq, so, v[2]);
-        ld4(rs_n, vq, so, v[3]);
-        ld4(rs_hn, vq, so, v[4]);
+      for (int a = 0; a < 5; ++a) quad_transpose(v[a], lane);
+      float drq[4];
 #pragma unroll
-        for (int a = 0; a < 5; ++a) quad_transpose(v[a], lane);
-        float drq[4];
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int q = 4 * g4 + jj;
-          const float hin = v[0][jj], rg = v[1][jj], zg = v[2][jj], ng = v[3][jj], hn = v[4][jj];
-          const float hout = (1.0f - zg) * ng + zg * hin;
-          const float d = dh[h][q] + (hout > 0.0f ? hacc[q] : 0.0f);
-          const float dn_ = d * (1.0f - zg);
-          const float dz = d * (hin - ng);
-          const float dnp = dn_ * (1.0f - ng * ng);
-          const float dhn = dnp * rg;
-          const float drp = dnp * hn * rg * (1.0f - rg);
-          const float dzp = dz * zg * (1.0f - zg);
-          dh[h][q] = d * zg;   // direct path; the W_h^T contraction is added below
-          drq[jj] = drp;
-          dz_r[h][q] = dzp;
-          dhn_r[h][q] = dhn;
-          const int qu = qunit(q);
-          dx3 += drp * wil[0 * HU + qu] + dzp * wil[1 * HU + qu] + dnp * wil[2 * HU + qu];
-          dx4 += drp * wil[3 * HU + qu] + dzp * wil[4 * HU + qu] + dnp * wil[5 * HU + qu];
-          const unsigned so1 = (unsigned)(((long)qu * p.M + ctr) * 4);
-          st_u(rs_rh, vb, so1, fmaxf(hout, 0.0f));
-          st_u(rs_dg[0], vb, so1, drp);
-          st_u(rs_dg[1], vb, so1, dzp);
-          st_u(rs_dg[2], vb, so1, dhn);
-          st_u(rs_dg[3], vb, so1, dnp);
-        }
-        put4(row, ub + 8 * g4, drq);
-        __builtin_amdgcn_sched_barrier(0);
+      for (int jj = 0; jj < 4; ++jj) {
+        const int q = 4 * g4 + jj;
+        const float hin = v[0][jj], rg = v[1][jj], zg = v[2][jj], ng = v[3][jj], hn = v[4][jj];
+        const float hout = (1.0f - zg) * ng + zg * hin;
+        const float d = dh[h][q] + (hout > 0.0f ? hacc[q] : 0.0f);
+        const float dn_ = d * (1.0f - zg);
+        const float dz = d * (hin - ng);
+        const float dnp = dn_ * (1.0f - ng * ng);
+        const float dhn = dnp * rg;
+        const float drp = dnp * hn * rg * (1.0f - rg);
+        const float dzp = dz * zg * (1.0f - zg);
+        dh[h][q] = d * zg;   // direct path; the W_h^T contraction is added below
+        drq[jj] = drp;
+        dz_r[h][q] = dzp;
+        dhn_r[h][q] = dhn;
+        const int qu = qunit(q);
+        dx3 += drp * wil[0 * HU + qu] + dzp * wil[1 * HU + qu] + dnp * wil[2 * HU + qu];
+        dx4 += drp * wil[3 * HU + qu] + dzp * wil[4 * HU + qu] + dnp * wil[5 * HU + qu];
+        const unsigned so1 = (unsigned)(((long)qu * p.M + ctr) * 4);
+        st_u(rs_rh, vbo, so1, fmaxf(hout, 0.0f));
+        st_u(rs_dg[0], vbo, so1, drp);
+        st_u(rs_dg[1], vbo, so1, dzp);
+        st_u(rs_dg[2], vbo, so1, dhn);
+        st_u(rs_dg[3], vbo, so1, dnp);
       }
-      // lanes l and l + 32 hold the same row: fold the halves, one float2 per (wave, row)
-      const float f3 = dx3 + __shfl_xor(dx3, 32), f4 = dx4 + __shfl_xor(dx4, 32);
-      if (hi == 0) *reinterpret_cast<float2*>(dxp + (wave * RBT + row) * 2) = make_float2(f3, f4);
+      put4(row, ub + 8 * g4, drq);
+      if (g4 == 3) {
+        // lanes l and l + 32 hold the same row: fold the halves, one float2 per (wave, row)
+        const float f3 = dx3 + __shfl_xor(dx3, 32), f4 = dx4 + __shfl_xor(dx4, 32);
+        if (hi == 0) *reinterpret_cast<float2*>(dxp + (wave * RBT + row) * 2) = make_float2(f3, f4);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();   // dr pieces complete
     // ---- contraction: dr, then dz, then dhn through the one image
