@@ -134,9 +134,11 @@ TOUED_DEV void reset_env(const EnvSpec& sp, const int* lev, uint2 key, EnvState&
 
 // gymnax Environment.step -> step_env (gridworld.py:72-136) + auto-reset select (RESET = false: the caller
 // discards the state after a done, so the reset and its key are skipped).
-template <int NMAX, bool TAB, bool RESET = true>
+// PRE: the state-independent blocks d0, d1 (split(key)) and c0 (first block of split(key_s, 3)) come
+// precomputed in pre[0..2] (the rollout computes them a step ahead, beside the actor-row gather).
+template <int NMAX, bool TAB, bool RESET = true, bool PRE = false>
 TOUED_DEV void env_step(const EnvSpec& sp, const int* lev, uint2 key, EnvState& s, int action,
-                        float& reward, bool& done) {
+                        float& reward, bool& done, const uint2* pre = nullptr) {
   const int G2 = sp.max_grid * sp.max_grid;
   const int pos = next_pos(lev, s.pos, action);
   int old[NMAX];
@@ -161,7 +163,14 @@ TOUED_DEV void env_step(const EnvSpec& sp, const int* lev, uint2 key, EnvState& 
   const bool need_term = collected != 0;
   bool have_d = false, have_c1 = false;
   uint2 d0 = make_uint2(0u, 0u), d1 = d0, c0 = d0, c1 = d0, c2 = d0;
-  if (need_term || miss != 0) {
+  if (PRE) {
+    d0 = pre[0];
+    d1 = pre[1];
+    c0 = pre[2];
+    have_d = true;
+    if (miss != 0) c2 = threefry(d0.x, d1.x, 2u, 5u);
+    if (need_term) { c1 = threefry(d0.x, d1.x, 1u, 4u); have_c1 = true; }
+  } else if (need_term || miss != 0) {
     d0 = threefry(key.x, key.y, 0u, 2u);
     d1 = threefry(key.x, key.y, 1u, 3u);
     have_d = true;
@@ -336,6 +345,37 @@ TOUED_DEV void actor_probs5(const float* __restrict__ tab, const float* last, in
   for (int j = 0; j < 5; ++j) p[j] = __fdiv_rn(e[j], s);
 }
 
+// actor_probs5 on an already gathered table row
+TOUED_DEV void actor_probs5_row(const float* row, const float* last, int t, float* p) {
+  const float c = __fmul_rn((float)t, 0.001f);
+  float l[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) l[j] = __fadd_rn(row[j], __fmul_rn(c, last[j]));
+  float m = l[0];
+#pragma unroll
+  for (int j = 1; j < 5; ++j) m = fmaxf(m, l[j]);
+  float e[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) e[j] = pexp(__fsub_rn(l[j], m));
+  float s = e[0];
+#pragma unroll
+  for (int j = 1; j < 5; ++j) s = __fadd_rn(s, e[j]);
+#pragma unroll
+  for (int j = 0; j < 5; ++j) p[j] = __fdiv_rn(e[j], s);
+}
+
+// choice5 with the key's bits1 already drawn
+TOUED_DEV int choice5_bits(uint32_t bits, const float* p) {
+  const float c0 = p[0];
+  const float c1 = __fadd_rn(p[0], p[1]);
+  const float c2 = __fadd_rn(c1, p[2]);
+  const float c3 = __fadd_rn(c1, __fadd_rn(p[2], p[3]));
+  const float c4 = __fadd_rn(c3, p[4]);
+  const float u = bits_to_unit(bits);
+  const float r = __fmul_rn(c4, __fsub_rn(1.0f, u));
+  return (c0 < r) + (c1 < r) + (c2 < r) + (c3 < r) + (c4 < r);
+}
+
 // jax.random.choice(key, 5, p=p): searchsorted(cumsum_assoc(p), c4*(1-u), 'left')
 TOUED_DEV int choice5(uint2 key, const float* p) {
   const float c0 = p[0];
@@ -374,20 +414,39 @@ __global__ void __launch_bounds__(256) k_rollout(EnvSpec sp, const int* __restri
   float cum = 0.0f, valid = 1.0f;
   const size_t base_o = (size_t)a * (T + 1) * W + w;
   const size_t base_t = (size_t)a * T * W + w;
-  for (int t = 0; t < T; ++t) {
+  // Every threefry block that does not depend on the env state is computed one step ahead, between the issue of
+  // the step's actor-row gather and its use: (rng, sub) = split(rng) [action key], the choice bits,
+  // (rng, sub) = split(rng) [env key], and the env key's d0, d1, c0 (env_step<.., PRE>).  The rollout is a
+  // chain of dependent steps per wave, so this independent work fills the gather's latency.
+  struct StepKeys { uint2 rng, sub_env; uint32_t cbits; uint2 pre[3]; };
+  auto keys_of = [&](uint2 r) {
+    StepKeys k;
     uint2 sub;
-    split2(rng, rng, sub);
+    split2(r, r, sub);
+    k.cbits = bits1(sub);
+    split2(r, r, k.sub_env);
+    k.rng = r;
+    k.pre[0] = threefry(k.sub_env.x, k.sub_env.y, 0u, 2u);
+    k.pre[1] = threefry(k.sub_env.x, k.sub_env.y, 1u, 3u);
+    k.pre[2] = threefry(k.pre[0].x, k.pre[1].x, 0u, 3u);
+    return k;
+  };
+  StepKeys kc = keys_of(rng);
+  for (int t = 0; t < T; ++t) {
     const int idx = tab_index(sp, s);
     const int tm = s.time;
+    float row[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) row[j] = tab[(size_t)idx * 5 + j];
+    const StepKeys kn = keys_of(kc.rng);      // next step's keys while the gather is in flight
     float p[5];
-    actor_probs5(tab, last, idx, tm, p);
-    const int action = choice5(sub, p);
-    split2(rng, rng, sub);
+    actor_probs5_row(row, last, tm, p);
+    const int action = choice5_bits(kc.cbits, p);
     float r; bool d;
     if (traj_idx)
-      env_step<NMAX, TAB>(sp, lev, sub, s, action, r, d);
+      env_step<NMAX, TAB, true, true>(sp, lev, kc.sub_env, s, action, r, d, kc.pre);
     else
-      env_step<NMAX, TAB, false>(sp, lev, sub, s, action, r, d);   // returns-only: the loop ends on done
+      env_step<NMAX, TAB, false, true>(sp, lev, kc.sub_env, s, action, r, d, kc.pre);   // returns-only
     cum = __fadd_rn(cum, __fmul_rn(r, valid));
     valid = __fmul_rn(valid, d ? 0.0f : 1.0f);
     // returns-only mode (eval_agent): nothing after the first episode can change cum_return
@@ -399,6 +458,7 @@ __global__ void __launch_bounds__(256) k_rollout(EnvSpec sp, const int* __restri
       traj_reward[base_t + (size_t)t * W] = r;
       traj_done[base_t + (size_t)t * W] = d ? 1 : 0;
     }
+    kc = kn;
   }
   if (traj_idx) {
     traj_idx[base_o + (size_t)T * W] = tab_index(sp, s);
