@@ -18,6 +18,7 @@
 // Sample index s = (a*T + t)*W + w (trajectory layout), GRU row r = a*W + w.
 // A tabular observation (idx, t) contributes logits table[idx] + (0.001 t) * table[D-1].
 #include <string.h>
+#include <algorithm>
 #include "common.h"
 
 #define EPSF 1e-8f
@@ -287,32 +288,59 @@ __global__ void __launch_bounds__(256) k_agent_norms(int N, int D, const float* 
                levels, gstat);
 }
 
-// th1 = applied ? th0 - lr * clip(G) : th0 over both tables, one element per thread (a streaming pass:
-// the norms and the lifetime test already sit in gstat).  The first element of an agent's actor table
-// advances its step.
+// th1 = applied ? th0 - lr * clip(G) : th0 over both tables (a streaming pass: the norms and the lifetime
+// test already sit in gstat).  Grid (chunk, agent, table): the agent's clip scale and learning rate are
+// block-uniform, the table is walked in 16-byte vectors when its rows allow it (no per-element index
+// division).  The first block of an agent's actor table advances its step.
+// CLIP: 0 = not applied (copy), 1 = applied unclipped, 2 = applied and clipped (the per-element division
+// optax's clip_by_global_norm performs, kept for bit parity, only on this block-uniform path)
+template <int CLIP>
+TOUED_DEV float apply_one(float p0, float g0, float gn, float max_norm, float lr) {
+  if (CLIP == 0) return p0;
+  const float g = CLIP == 2 ? (g0 / gn) * max_norm : g0;
+  return p0 + (-(lr * g));
+}
+
+template <int CLIP>
+TOUED_DEV void apply_seg(const float* __restrict__ P0, const float* __restrict__ G, float* __restrict__ P1, long per,
+                         long head, float gn, float max_norm, float lr) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long nv = (per - head) / 4;
+  const float4* p4 = reinterpret_cast<const float4*>(P0 + head);
+  const float4* g4 = reinterpret_cast<const float4*>(G + head);
+  float4* o4 = reinterpret_cast<float4*>(P1 + head);
+  for (long i = i0; i < nv; i += stride) {
+    const float4 p = p4[i], g = g4[i];
+    o4[i] = make_float4(apply_one<CLIP>(p.x, g.x, gn, max_norm, lr), apply_one<CLIP>(p.y, g.y, gn, max_norm, lr),
+                        apply_one<CLIP>(p.z, g.z, gn, max_norm, lr), apply_one<CLIP>(p.w, g.w, gn, max_norm, lr));
+  }
+  for (long i = i0; i < head; i += stride) P1[i] = apply_one<CLIP>(P0[i], G[i], gn, max_norm, lr);
+  for (long i = head + 4 * nv + i0; i < per; i += stride) P1[i] = apply_one<CLIP>(P0[i], G[i], gn, max_norm, lr);
+}
+
 __global__ void __launch_bounds__(256) k_agent_apply(int N, int D, const float* __restrict__ th0,
                                                      const float* __restrict__ ph0, const float* __restrict__ Gth,
                                                      const float* __restrict__ Gph, float lr_a, float lr_c,
                                                      float max_norm, int* __restrict__ step,
                                                      float* __restrict__ th1, float* __restrict__ ph1,
-                                                     const float* __restrict__ gstat) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long na = (long)D * 5, nc = (long)D * 8;
-  const long ta = (long)N * na;
-  if (i >= ta + (long)N * nc) return;
-  const bool actor = i < ta;
-  const long j = actor ? i : i - ta;
-  const long per = actor ? na : nc;
-  const int a = (int)(j / per);
+                                                     const float* __restrict__ gstat, int vec4) {
+  const int a = blockIdx.y;
+  const bool actor = blockIdx.z == 0;
+  const long per = actor ? (long)D * 5 : (long)D * 8;
+  const float* P0 = (actor ? th0 : ph0) + (long)a * per;
+  const float* G = (actor ? Gth : Gph) + (long)a * per;
+  float* P1 = (actor ? th1 : ph1) + (long)a * per;
   const float gn = gstat[a * 4 + (actor ? 0 : 1)];
   const bool applied = gstat[a * 4 + 2] > 0.5f;
-  const float g0 = actor ? Gth[j] : Gph[j];
-  const float p0 = actor ? th0[j] : ph0[j];
   const float lr = actor ? lr_a : lr_c;
-  const float g = !(gn < max_norm) ? (g0 / gn) * max_norm : g0;
-  const float p1 = applied ? p0 + (-(lr * g)) : p0;
-  if (actor) th1[j] = p1; else ph1[j] = p1;
-  if (actor && j - (long)a * na == 0 && applied) step[a] += 1;
+  if (actor && blockIdx.x == 0 && threadIdx.x == 0 && applied) step[a] += 1;
+  // the three arrays are 16-byte aligned at their starts (vec4): the agent's segment has a scalar head up to
+  // the next 16-byte boundary, a float4 body and a scalar tail
+  const long head = vec4 ? std::min(per, (4 - ((long)a * per) % 4) % 4) : per;
+  if (!applied) apply_seg<0>(P0, G, P1, per, head, gn, max_norm, lr);
+  else if (gn < max_norm) apply_seg<1>(P0, G, P1, per, head, gn, max_norm, lr);
+  else apply_seg<2>(P0, G, P1, per, head, gn, max_norm, lr);
 }
 
 // ---------------------------------------------------------------------------- entropy
@@ -479,10 +507,15 @@ __global__ void __launch_bounds__(256) k_lpgloss_grad(int N, int W, int T, int D
 
 // ---------------------------------------------------------------------------- clip VJP coefficients
 // coef[a] = {alpha_a, beta_a, alpha_c, beta_c}: gbar = alpha*u + beta*G with u = -lr * adjoint.
+// <G, adjoint> per table in 16-byte vectors when the tables allow it (vec4), two independent partials per
+// thread and table so four vector loads are in flight per thread.
+TOUED_DEV float dot4(float4 x, float4 y) { return x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w; }
+
 __global__ void __launch_bounds__(1024) k_clip_dot(int N, int D, const float* __restrict__ Gth,
                                                    const float* __restrict__ Gph, const float* __restrict__ adj_th,
                                                    const float* __restrict__ adj_ph, const float* __restrict__ gstat,
-                                                   float lr_a, float lr_c, float max_norm, float* __restrict__ coef) {
+                                                   float lr_a, float lr_c, float max_norm, float* __restrict__ coef,
+                                                   int vec4) {
   const int a = blockIdx.x;
   __shared__ float red[2][16];
   const long na = (long)D * 5, nc = (long)D * 8;
@@ -490,20 +523,37 @@ __global__ void __launch_bounds__(1024) k_clip_dot(int N, int D, const float* __
   const float* ja = adj_th + (long)a * na;
   const float* gc = Gph + (long)a * nc;
   const float* jc = adj_ph + (long)a * nc;
-  // four independent partial sums per thread keep several loads in flight
   float da[4] = {0.0f, 0.0f, 0.0f, 0.0f}, dc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (long i = threadIdx.x; i < na; i += 4 * 1024) {
+  if (vec4) {
+    // the tables start 16-byte aligned: a scalar head to the agent's first 16-byte boundary, a float4 body,
+    // a scalar tail
+    auto seg = [&](const float* g, const float* j, long n, long off, float* acc) {
+      const long head = std::min(n, (4 - off % 4) % 4), nv = (n - head) / 4;
+      const float4 *g4 = reinterpret_cast<const float4*>(g + head), *j4 = reinterpret_cast<const float4*>(j + head);
+      for (long i = threadIdx.x; i < nv; i += 2 * 1024) {
+        acc[0] += dot4(g4[i], j4[i]);
+        if (i + 1024 < nv) acc[1] += dot4(g4[i + 1024], j4[i + 1024]);
+      }
+      // the (at most 3 + 3) scalar elements, one per thread
+      const long t = threadIdx.x < head ? threadIdx.x : head + 4 * nv + (threadIdx.x - head);
+      if (t < n) acc[2] += g[t] * j[t];
+    };
+    seg(ga, ja, na, (long)a * na, da);
+    seg(gc, jc, nc, (long)a * nc, dc);
+  } else {
+    for (long i = threadIdx.x; i < na; i += 4 * 1024) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const long e = i + u * 1024;
-      if (e < na) da[u] += ga[e] * ja[e];
+      for (int u = 0; u < 4; ++u) {
+        const long e = i + u * 1024;
+        if (e < na) da[u] += ga[e] * ja[e];
+      }
     }
-  }
-  for (long i = threadIdx.x; i < nc; i += 4 * 1024) {
+    for (long i = threadIdx.x; i < nc; i += 4 * 1024) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const long e = i + u * 1024;
-      if (e < nc) dc[u] += gc[e] * jc[e];
+      for (int u = 0; u < 4; ++u) {
+        const long e = i + u * 1024;
+        if (e < nc) dc[u] += gc[e] * jc[e];
+      }
     }
   }
   float sa_ = wave_sum((da[0] + da[1]) + (da[2] + da[3]));
@@ -665,16 +715,18 @@ __global__ void __launch_bounds__(256) k_embed_bwd(int N, int W, int T, int D, i
 #pragma unroll
     for (int i = 0; i < 8; ++i) aw[i][u] = 0.0f;
   }
-  const long total = (long)K * N * T * W;
+  // sample indices fit 31 bits (checked by the launcher): 32-bit index maths, no 64-bit divisions
+  const int NTW = N * T * W;
+  const int total = K * NTW;
   const int R = N * W;
-  const long nthr = (long)gridDim.x * (blockDim.x >> 2);
-  for (long g = (long)blockIdx.x * (blockDim.x >> 2) + (threadIdx.x >> 2); g < total; g += nthr) {
-    const int k = (int)(g / ((long)N * T * W));
-    const long s = g - (long)k * N * T * W;
-    const long at = s / W;
-    const int w = (int)(s - at * W);
-    const int a = (int)(at / T);
-    const int t = (int)(at - (long)a * T);
+  const int nthr = gridDim.x * (blockDim.x >> 2);
+  for (int g = blockIdx.x * (blockDim.x >> 2) + (threadIdx.x >> 2); g < total; g += nthr) {
+    const int k = (unsigned)g / (unsigned)NTW;
+    const int s = g - k * NTW;
+    const int at = (unsigned)s / (unsigned)W;
+    const int w = s - at * W;
+    const int a = (unsigned)at / (unsigned)T;
+    const int t = at - a * T;
     const int r = a * W + w;
     const int* tidx = tidx_hist + k * tidx_stride;
     const int* ttime = ttime_hist + k * tidx_stride;
@@ -1051,9 +1103,11 @@ TOUED_DEV void sort2048(uint32_t* key, int tid) {
 }
 
 template <class Op>
-__global__ void __launch_bounds__(512) k_rows_sorted(Op op) {
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k_rows_sorted(Op op) {
   constexpr int NA = Op::NA, NC = Op::NC, NV = NA + NC, NM = Op::NM;
-  constexpr int NVP = (NV + 3) & ~3;          // vector stride in floats (16-byte aligned rows)
+  // unpadded vector stride (odd strides are bank-conflict free): 13-float rows keep a block's LDS at 75 KB,
+  // so two agents' blocks share a CU and all N = 512 blocks are resident in one round
+  constexpr int NVP = NV;
   extern __shared__ float lds[];
   __shared__ float red[8][NV + NM];
   __shared__ float tot[NV + NM];
@@ -1104,23 +1158,15 @@ __global__ void __launch_bounds__(512) k_rows_sorted(Op op) {
     if (kk == 0xFFFFFFFFu) continue;
     const uint32_t row = kk >> 12;
     if (i > 0 && (key[i - 1] >> 12) == row) continue;
-    float4 acc[NVP / 4];
+    float sum[NV];
 #pragma unroll
-    for (int j = 0; j < NVP / 4; ++j) acc[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int j = 0; j < NV; ++j) sum[j] = 0.0f;
     for (int e = i; e < TW; ++e) {
       const uint32_t ke = key[e];
       if ((ke >> 12) != row || ke == 0xFFFFFFFFu) break;
-      const float4* ve = reinterpret_cast<const float4*>(vec + (ke & 4095u) * NVP);
+      const float* ve = vec + (ke & 4095u) * NVP;
 #pragma unroll
-      for (int j = 0; j < NVP / 4; ++j) {
-        const float4 x = ve[j];
-        acc[j].x += x.x; acc[j].y += x.y; acc[j].z += x.z; acc[j].w += x.w;
-      }
-    }
-    float sum[NVP];
-#pragma unroll
-    for (int j = 0; j < NVP / 4; ++j) {
-      sum[4 * j] = acc[j].x; sum[4 * j + 1] = acc[j].y; sum[4 * j + 2] = acc[j].z; sum[4 * j + 3] = acc[j].w;
+      for (int j = 0; j < NV; ++j) sum[j] += ve[j];
     }
     if ((int)row == D - 1) {
 #pragma unroll
@@ -1183,7 +1229,7 @@ template <class Op>
 static bool launch_sorted(const Op& op, int N, hipStream_t stream) {
   const int TW = op.T * op.W;
   if (TW > SORT_MAX_TW || TW <= 0 || op.D >= (1 << 20)) return false;
-  const size_t bytes = 2048 * 4 + (size_t)TW * (((Op::NA + Op::NC) + 3) & ~3) * 4;
+  const size_t bytes = 2048 * 4 + (size_t)TW * (Op::NA + Op::NC) * 4;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rows_sorted<Op>),
@@ -1196,6 +1242,7 @@ static bool launch_sorted(const Op& op, int N, hipStream_t stream) {
 }
 
 static inline unsigned nb256(long n) { return (unsigned)((n + 255) / 256); }
+static inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 extern "C" {
 
@@ -1252,9 +1299,14 @@ int toued_agent_apply(int N, int D, const float* th0, const float* ph0, const fl
                       float lr_a, float lr_c, float max_norm, int* step, float* th1, float* ph1, const float* gstat,
                       hipStream_t stream) {
   if (N == 0 || D == 0) return 0;
-  const long tot = (long)N * D * 13;
-  hipLaunchKernelGGL(k_agent_apply, dim3(nb256(tot)), dim3(256), 0, stream, N, D, th0, ph0, Gth, Gph, lr_a, lr_c,
-                     max_norm, step, th1, ph1, gstat);
+  const bool v4 = aligned16(th0) && aligned16(ph0) && aligned16(Gth) && aligned16(Gph) && aligned16(th1) &&
+                  aligned16(ph1);
+  // critic table (8 D floats): ~2 vectors per thread at the chosen width; the actor table's blocks beyond its
+  // size exit at once
+  const long nvec = v4 ? (long)D * 2 + 1 : (long)D * 8;
+  const unsigned gx = (unsigned)std::max(1L, std::min(64L, (nvec + 511) / 512));
+  hipLaunchKernelGGL(k_agent_apply, dim3(gx, N, 2), dim3(256), 0, stream, N, D, th0, ph0, Gth, Gph, lr_a, lr_c,
+                     max_norm, step, th1, ph1, gstat, v4 ? 1 : 0);
   TOUED_CHECK_LAUNCH();
   return 0;
 }
@@ -1308,8 +1360,9 @@ int toued_lpgloss_grad(int N, int W, int T, int D, const float* theta, const int
 int toued_clip_dot(int N, int D, const float* Gth, const float* Gph, const float* adj_th, const float* adj_ph,
                    const float* gstat, float lr_a, float lr_c, float max_norm, float* coef, hipStream_t stream) {
   if (N == 0) return 0;
+  const bool v4 = aligned16(Gth) && aligned16(Gph) && aligned16(adj_th) && aligned16(adj_ph);
   hipLaunchKernelGGL(k_clip_dot, dim3(N), dim3(1024), 0, stream, N, D, Gth, Gph, adj_th, adj_ph, gstat, lr_a, lr_c,
-                     max_norm, coef);
+                     max_norm, coef, v4 ? 1 : 0);
   TOUED_CHECK_LAUNCH();
   return 0;
 }
@@ -1343,6 +1396,8 @@ int toued_embed_bwd(int N, int W, int T, int D, int K, const float* phi_hist, lo
                     const float* dX3, const float* dX4, long dx_stride_k, const float* e1w, const float* e1b,
                     const float* e2w, float* partial, int n_blocks, hipStream_t stream) {
   if ((long)K * N * T * W == 0) return 0;
+  TOUED_REQUIRE((long)K * N * (T + 1) * W < (1L << 31), "toued_embed_bwd: K*N*(T+1)*W = %ld samples exceed 2^31",
+                (long)K * N * (T + 1) * W);
   if (W % 64 == 0)
     hipLaunchKernelGGL(k_embed_bwd<true>, dim3(n_blocks), dim3(256), 0, stream, N, W, T, D, K, phi_hist, phi_stride,
                        tidx_hist, tidx_stride, ttime_hist, tdone_hist, tstep_stride, dX3, dX4, dx_stride_k, e1w, e1b,
