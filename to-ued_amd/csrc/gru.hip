@@ -407,10 +407,15 @@ __global__ void __launch_bounds__(512, NT == 1 ? 4 : 1) k_gru_fwd(FwdArgs p) {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
-#define F6_HP 264        // carry image row pitch (bf16): 528 B
-#define F6_NFH (16 * 8 * 3 * 3)     // h-part fragments [ks][unit tile][gate r|z|hn][piece], 1 KiB each
-#define F6_NFA (8 * 4 * 3)          // augmented fragments [unit tile][gate r|z|hn|ni][piece]
-#define F6_FLOATS ((F6_NFH + F6_NFA) * 256)   // packed size in floats (1 KiB = 256 floats)
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+#define F6_HP 264        // carry image row pitch (16-bit elements): 528 B
+#define F6_NFH (16 * 8 * 3 * 2)     // h-part fragments [ks][unit tile][gate r|z|hn][fp16 piece], 1 KiB each
+#define F6_NFA (8 * 4 * 3)          // augmented fragments [unit tile][gate r|z|hn|ni][bf16 piece]
+#define F6_SCALES ((F6_NFH + F6_NFA) * 256)   // float offset of the per-(gate, unit) weight scales 2^s [4][256]
+#define F6_FLOATS (F6_SCALES + 4 * HU)        // packed size in floats (1 KiB fragment = 256 floats)
+#define HSCALE 16384.0f  // carry scale 2^14: |h| < 1 -> |2^14 h| < 2^14, inside the fp16 range
 
 template <typename V>
 TOUED_DEV void split3v(float x, V& p0, V& p1, V& p2, int e) {
@@ -422,31 +427,82 @@ TOUED_DEV void split3v(float x, V& p0, V& p1, V& p2, int e) {
   p2[e] = (__bf16)(r1 - (float)m);
 }
 
+// fp16 pair of an f32 value y (|y| < 65504): y ~ x0 + x1 to 2^-22 relative (normal range)
+template <typename V>
+TOUED_DEV void split2h(float y, V& x0, V& x1, int e) {
+  const _Float16 a = (_Float16)y;
+  x0[e] = a;
+  x1[e] = (_Float16)(y - (float)a);
+}
+
+// carry piece triple of h: fp16 x0, x1 of y = 2^14 h (the MFMA operand) and the bf16 residual r = y - x0 - x1,
+// so that (x0 + x1) + r == y exactly for |h| >= 2^-24 (r then has <= 8 significant bits; below, |r| < 2^-25
+// and the reconstruction error is < 2^-47 absolute in h)
+TOUED_DEV void split_carry(float h, f16x4& x0, f16x4& x1, bf16x4& r, int e) {
+  const float y = h * HSCALE;
+  const _Float16 a = (_Float16)y;
+  const float d = y - (float)a;
+  const _Float16 b = (_Float16)d;
+  x0[e] = a;
+  x1[e] = b;
+  r[e] = (__bf16)(d - (float)b);
+}
+
+// per-(gate, output unit) weight scale 2^s: s = 14 - e with max_k |W_g[k][u]| < 2^e (clamped to [-30, 20]), so
+// the scaled row's fp16 pieces stay below 2^14 and its small entries keep their relative precision; the ni gate
+// (no h part) uses s = 0.  One thread per (gate, unit) and candidate (blockIdx.y).
+__global__ void k_fwd6_scales(const float* __restrict__ eta, EtaOff o, float* __restrict__ out, long eta_stride,
+                              long out_stride) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 4 * HU) return;
+  eta += (long)blockIdx.y * eta_stride;
+  out += (long)blockIdx.y * out_stride;
+  const int g = i / HU, u = i - g * HU;
+  int sc = 0;
+  if (g < 3) {
+    const int base = g == 0 ? o.hr_w : g == 1 ? o.hz_w : o.hn_w;
+    float m = 0.0f;
+    for (int k = 0; k < HU; ++k) m = fmaxf(m, fabsf(eta[base + k * HU + u]));
+    if (m > 0.0f && m <= 3.0e38f) {
+      int e;
+      frexpf(m, &e);          // m < 2^e
+      sc = min(20, max(-30, 14 - e));
+    }
+  }
+  out[i] = ldexpf(1.0f, sc);
+}
+
 // one thread per (fragment group, lane): fragment group = (ks, ut, g) for the h part or (ut, g) for the
-// augmented rows; lane l holds A[i = unit 32 ut + (l & 31)][k = 8 (l >> 5) + e], e = 0..7
+// augmented rows; lane l holds A[i = unit 32 ut + (l & 31)][k = 8 (l >> 5) + e], e = 0..7.  Every row is
+// scaled by its 2^s (k_fwd6_scales, at F6_SCALES of the same buffer): the h part as two fp16 pieces, the
+// augmented rows (input weights and biases, multiplied with 2^14 x on the B side) as three bf16 pieces.
 __global__ void k_pack_fwd6(const float* __restrict__ eta, EtaOff o, int F, bf16x8* __restrict__ out,
                             long eta_stride, long out_stride16) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   eta += (long)blockIdx.y * eta_stride;            // candidate blockIdx.y (ES); 0 for the shared eta
   out += (long)blockIdx.y * out_stride16;
+  const float* scl = reinterpret_cast<const float*>(out) + F6_SCALES;
   const int ngrp_h = 16 * 8 * 3, ngrp = ngrp_h + 8 * 4;
   if (gid >= ngrp * 64) return;
   const int lane = gid & 63, grp = gid >> 6;
-  bf16x8 pc[3];
-  int fbase;
   if (grp < ngrp_h) {
     const int g = grp % 3, ut = (grp / 3) % 8, ks = grp / 24;
     const int u = 32 * ut + (lane & 31);
     const int base = g == 0 ? o.hr_w : g == 1 ? o.hz_w : o.hn_w;
+    const float sg = scl[g * HU + u];
+    f16x8 pc[2];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int k = 16 * ks + 8 * (lane >> 5) + e;
-      split3v(eta[base + k * HU + u], pc[0], pc[1], pc[2], e);
+      split2h(eta[base + k * HU + u] * sg, pc[0], pc[1], e);
     }
-    fbase = grp * 3;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) out[(long)(grp * 2 + q) * 64 + lane] = __builtin_bit_cast(bf16x8, pc[q]);
   } else {
     const int ga = grp - ngrp_h, g = ga % 4, ut = ga / 4;
     const int u = 32 * ut + (lane & 31);
+    const float sg = scl[g * HU + u];
+    bf16x8 pc[3];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int f = 8 * (lane >> 5) + e;
@@ -458,16 +514,22 @@ __global__ void k_pack_fwd6(const float* __restrict__ eta, EtaOff o, int F, bf16
       } else if (f == F) {
         x = g == 0 ? eta[o.ir_b + u] : g == 1 ? eta[o.iz_b + u] : g == 2 ? eta[o.hn_b + u] : eta[o.in_b + u];
       }
-      split3v(x, pc[0], pc[1], pc[2], e);
+      split3v(x * sg, pc[0], pc[1], pc[2], e);
     }
-    fbase = F6_NFH + ga * 3;
-  }
 #pragma unroll
-  for (int q = 0; q < 3; ++q) out[(long)(fbase + q) * 64 + lane] = pc[q];
+    for (int q = 0; q < 3; ++q) out[(long)(F6_NFH + ga * 3 + q) * 64 + lane] = pc[q];
+  }
 }
 
 TOUED_DEV floatx16 mfma_bf32(bf16x8 a, bf16x8 b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+// a.b from two fp16 pieces each, a1 b1 (< 2^-22 relative) dropped, smallest products first
+TOUED_DEV floatx16 mfma3h(const f16x8 (&a)[2], const f16x8 (&b)[2], floatx16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], c, 0, 0, 0);
+  return c;
 }
 // a.b from the pieces, smallest products first
 TOUED_DEV floatx16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx16 c) {
@@ -482,8 +544,10 @@ TOUED_DEV floatx16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx16 c)
 
 template <bool SAVE>
 __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
-  __shared__ __attribute__((aligned(16))) __bf16 hB[3][64 * F6_HP];   // carry h(t) pieces [row][unit]
+  // carry image [row][unit]: slots 0, 1 the fp16 pieces of 2^14 h (MFMA B operand), slot 2 the bf16 residual
+  __shared__ __attribute__((aligned(16))) __bf16 hB[3][64 * F6_HP];
   __shared__ __attribute__((aligned(16))) float wh[HU * 12];          // head weights [unit][pi | y0..y7 | pad]
+  __shared__ __attribute__((aligned(16))) float usc[4 * HU];          // accumulator unscale 2^-(s + 14) [gate][unit]
   __shared__ float hp[8 * 9 * 64];      // head partials [wave][output][row]
   __shared__ float hout[9 * 64];
   const int tid = threadIdx.x, lane = tid & 63, hi = lane >> 5, col = lane & 31;
@@ -499,10 +563,12 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   // per-candidate parameters in the ES inference mode (rows [c * rpc, (c + 1) * rpc) use candidate c)
   const int cand = SAVE ? 0 : r0 / p.rpc;
   const float* eta = p.eta + (long)cand * p.eta_stride;
+  const float* A6c = reinterpret_cast<const float*>(p.A6) + (long)cand * p.a_stride4 * 4;
   for (int i = tid; i < HU * 12; i += 512) {
     const int u = i / 12, oo = i - u * 12;
     wh[i] = oo == 0 ? eta[p.o.pi_w + u] : oo < 9 ? eta[p.o.y_w + u * 8 + (oo - 1)] : 0.0f;
   }
+  for (int i = tid; i < 4 * HU; i += 512) usc[i] = 1.0f / (A6c[F6_SCALES + i] * HSCALE);   // powers of two: exact
   {
     uint4* z = reinterpret_cast<uint4*>(&hB[0][0]);
     for (int i = tid; i < 3 * 64 * F6_HP / 8; i += 512) z[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -514,12 +580,15 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   const __amdgpu_buffer_rsrc_t rs_done = rsrc_of(reinterpret_cast<const float*>(p.done));
   __syncthreads();
   const float bpi = eta[p.o.pi_b];
-  const __amdgpu_buffer_rsrc_t rs_A =
-      rsrc_of(reinterpret_cast<const float*>(p.A6) + (long)cand * p.a_stride4 * 4);
+  const __amdgpu_buffer_rsrc_t rs_A = rsrc_of(A6c);
   const unsigned vA = (unsigned)lane * 16;
   auto ldA = [&](int frag) {
     const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs_A, (int)vA, frag * 1024, 0);
     return __builtin_bit_cast(bf16x8, x);
+  };
+  auto ldAh = [&](int frag) {
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs_A, (int)vA, frag * 1024, 0);
+    return __builtin_bit_cast(f16x8, x);
   };
   const __amdgpu_buffer_rsrc_t rs_hin = rsrc_of(p.s_hin), rs_r = rsrc_of(p.s_r), rs_z = rsrc_of(p.s_z),
                                rs_n = rsrc_of(p.s_n), rs_hn = rsrc_of(p.s_hn);
@@ -532,9 +601,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[g][h][q] = 0.0f;
-    // ---- contraction: 17 k-steps.  Each gate's A fragments (unit tile `wave`) are refilled for the next
-    // k-step right after their last MFMA, each row tile's B fragments right after theirs; the partner wave on
-    // the SIMD covers what latency remains.
+    // ---- contraction: 16 fp16 k-steps over the carry + one augmented bf16 k-step.  Each gate's A fragments
+    // (unit tile `wave`) are refilled for the next k-step right after their last MFMA, each row tile's B
+    // fragments right after theirs; the partner wave on the SIMD covers what latency remains.
     // this lane's row inputs x(t) for the augmented k-step [x_0 .. x_{F-1}, 1, 0 ...] (F <= 7), loaded now
     // and split into B fragments at the end of the contraction (lanes 32-63 hold k = 8..15: zero)
     float xv[2][7];
@@ -546,58 +615,65 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
         xv[h][f] = ld_u(rs_X, (unsigned)((RB * h + col) * p.xs_col * 4),
                         (unsigned)((fc * p.xs_f + ((long)t * R + r0) * p.xs_col) * 4));
       }
-    bf16x8 A[3][3], B[2][3];
-    auto fragA = [&](int ks, int g, int q) {
-      return ks < 16 ? ((ks * 8 + wave) * 3 + g) * 3 + q : F6_NFH + (wave * 4 + g) * 3 + q;
-    };
+    f16x8 A[3][2], B[2][2];
+    auto fragA = [&](int ks, int g, int q) { return ((ks * 8 + wave) * 3 + g) * 2 + q; };
+    auto fragAug = [&](int g, int q) { return F6_NFH + (wave * 4 + g) * 3 + q; };
     auto load_B = [&](int ks, int h) {
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        if (ks < 16) {
-          B[h][q] = *reinterpret_cast<const bf16x8*>(&hB[q][(RB * h + col) * F6_HP + 16 * ks + 8 * hi]);
-        }
-      }
-      if (ks == 16) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float v = hi ? 0.0f : e < F ? xv[h][e < 7 ? e : 6] : (e == F ? 1.0f : 0.0f);
-          split3v(v, B[h][0], B[h][1], B[h][2], e);
-        }
-      }
+      for (int q = 0; q < 2; ++q)
+        B[h][q] = *reinterpret_cast<const f16x8*>(&hB[q][(RB * h + col) * F6_HP + 16 * ks + 8 * hi]);
     };
 #pragma unroll
     for (int g = 0; g < 3; ++g)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) A[g][q] = ldA(fragA(0, g, q));
+      for (int q = 0; q < 2; ++q) A[g][q] = ldAh(fragA(0, g, q));
     load_B(0, 0);
     load_B(0, 1);
     // (a rolled loop: a full unroll hoists ~300 fragment offsets into SGPRs, which spill)
 #pragma nounroll
-    for (int ks = 0; ks < 16; ++ks) {
+    for (int ks = 0; ks < 15; ++ks) {
 #pragma unroll
       for (int g = 0; g < 3; ++g) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          acc[g][h] = mfma6(A[g], B[h], acc[g][h]);
+          acc[g][h] = mfma3h(A[g], B[h], acc[g][h]);
           if (g == 2) load_B(ks + 1, h);
         }
 #pragma unroll
-        for (int q = 0; q < 3; ++q) A[g][q] = ldA(fragA(ks + 1, g, q));
+        for (int q = 0; q < 2; ++q) A[g][q] = ldAh(fragA(ks + 1, g, q));
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    // augmented k-step: r, z, hn fragments in A; the ni gate's go into A[0] once r's MFMAs are issued
+    // last carry k-step; each gate's augmented fragments (three bf16 pieces) load behind its MFMAs
+    bf16x8 Aa[3][3], Ba[2][3];
 #pragma unroll
     for (int g = 0; g < 3; ++g) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) acc[g][h] = mfma6(A[g], B[h], acc[g][h]);
+      for (int h = 0; h < 2; ++h) acc[g][h] = mfma3h(A[g], B[h], acc[g][h]);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) Aa[g][q] = ldA(fragAug(g, q));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // augmented k-step: B = bf16 pieces of 2^14 [x, 1, 0 ...]; the ni gate's fragments go into Aa[0] once
+    // r's MFMAs are issued
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = hi ? 0.0f : e < F ? xv[h][e < 7 ? e : 6] : (e == F ? 1.0f : 0.0f);
+        split3v(v * HSCALE, Ba[h][0], Ba[h][1], Ba[h][2], e);
+      }
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) acc[g][h] = mfma6(Aa[g], Ba[h], acc[g][h]);
       if (g == 0) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) A[0][q] = ldA(fragA(16, 3, q));
+        for (int q = 0; q < 3; ++q) Aa[0][q] = ldA(fragAug(3, q));
       }
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) acc[3][h] = mfma6(A[0], B[h], acc[3][h]);
+    for (int h = 0; h < 2; ++h) acc[3][h] = mfma6(Aa[0], Ba[h], acc[3][h]);
     __syncthreads();   // every wave done reading hB / xB: the carry and x(t-1) overwrite them in place
     // ---- gate maths (lane = row 32h + col, register q = unit 32 wave + 4 hi + qunit(q))
     const long cbase = (long)t * R;
@@ -616,20 +692,28 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         // four consecutive units ub + 8 g4 .. +3 of this row: h_in pieces, then the new carry's pieces
-        bf16x4 hq[3];
+        const int ho = row * F6_HP + ub + 8 * g4;
+        const f16x4 h0 = *reinterpret_cast<const f16x4*>(&hB[0][ho]);
+        const f16x4 h1 = *reinterpret_cast<const f16x4*>(&hB[1][ho]);
+        const bf16x4 hr = *reinterpret_cast<const bf16x4*>(&hB[2][ho]);
+        float us[4][4];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) hq[q] = *reinterpret_cast<const bf16x4*>(&hB[q][row * F6_HP + ub + 8 * g4]);
-        bf16x4 nq[3];
+        for (int g = 0; g < 4; ++g) {
+          const float4 v = *reinterpret_cast<const float4*>(&usc[g * HU + ub + 8 * g4]);
+          us[g][0] = v.x; us[g][1] = v.y; us[g][2] = v.z; us[g][3] = v.w;
+        }
+        f16x4 n0, n1;
+        bf16x4 nr;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int q = 4 * g4 + e;
-          const float rg = sigm_r(acc[0][h][q]);
-          const float zg = sigm_r(acc[1][h][q]);
-          const float hn = acc[2][h][q];
-          const float ng = tanh_r(acc[3][h][q] + rg * hn);
-          const float hin = ((float)hq[0][e] + (float)hq[1][e]) + (float)hq[2][e];   // exact
+          const float rg = sigm_r(acc[0][h][q] * us[0][e]);
+          const float zg = sigm_r(acc[1][h][q] * us[1][e]);
+          const float hn = acc[2][h][q] * us[2][e];
+          const float ng = tanh_r(acc[3][h][q] * us[3][e] + rg * hn);
+          const float hin = (((float)h0[e] + (float)h1[e]) + (float)hr[e]) * (1.0f / HSCALE);   // exact
           const float hh = (1.0f - zg) * ng + zg * hin;
-          split3v(dn ? 0.0f : hh, nq[0], nq[1], nq[2], e);   // carry h_in(t-1) = where(d_{t-1}, 0, h_out(t))
+          split_carry(dn ? 0.0f : hh, n0, n1, nr, e);   // carry h_in(t-1) = where(d_{t-1}, 0, h_out(t))
           const unsigned so = (unsigned)(((long)qunit(q) * p.M + cbase) * 4);
           if (SAVE) {
             st_u(rs_hin, vbyte, so, hin);
@@ -644,8 +728,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
           hp_loc[3] += rl * w0.w; hp_loc[4] += rl * w1.x; hp_loc[5] += rl * w1.y;
           hp_loc[6] += rl * w1.z; hp_loc[7] += rl * w1.w; hp_loc[8] += rl * w2.x;
         }
-#pragma unroll
-        for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x4*>(&hB[q][row * F6_HP + ub + 8 * g4]) = nq[q];
+        *reinterpret_cast<f16x4*>(&hB[0][ho]) = n0;
+        *reinterpret_cast<f16x4*>(&hB[1][ho]) = n1;
+        *reinterpret_cast<bf16x4*>(&hB[2][ho]) = nr;
       }
       // lanes l and l + 32 hold the same row: fold the two halves, one lane writes
 #pragma unroll
@@ -1149,6 +1234,7 @@ int toued_gru_pack(const float* eta, const int* off, int F, float* fwdA, float* 
   const int n1 = NTILE_F * KQF * 64, n2 = 8 * 3 * 32 * 64, n3 = (16 * 8 * 3 + 8 * 4) * 64;
   hipLaunchKernelGGL(k_pack_fwd, dim3((n1 + 255) / 256), dim3(256), 0, stream, eta, o, F,
                      reinterpret_cast<float4*>(fwdA), 0L, 0L);
+  hipLaunchKernelGGL(k_fwd6_scales, dim3(4), dim3(256), 0, stream, eta, o, fwdA + (size_t)n1 * 4 + F6_SCALES, 0L, 0L);
   hipLaunchKernelGGL(k_pack_fwd6, dim3((n3 + 255) / 256), dim3(256), 0, stream, eta, o, F,
                      reinterpret_cast<bf16x8*>(fwdA + (size_t)n1 * 4), 0L, 0L);
   hipLaunchKernelGGL(k_pack_bwd, dim3((n2 + 255) / 256), dim3(256), 0, stream, eta, o,
@@ -1225,6 +1311,8 @@ int toued_gru_pack_fwd_multi(const float* eta, long eta_stride, int n, const int
   hipLaunchKernelGGL(k_pack_fwd, dim3((n1 + 255) / 256, n), dim3(256), 0, stream, eta, o, F,
                      reinterpret_cast<float4*>(fwdA), eta_stride, cstride / 4);
   const int n3 = (16 * 8 * 3 + 8 * 4) * 64;
+  hipLaunchKernelGGL(k_fwd6_scales, dim3(4, n), dim3(256), 0, stream, eta, o, fwdA + (size_t)n1 * 4 + F6_SCALES,
+                     eta_stride, cstride);
   hipLaunchKernelGGL(k_pack_fwd6, dim3((n3 + 255) / 256, n), dim3(256), 0, stream, eta, o, F,
                      reinterpret_cast<bf16x8*>(fwdA + (size_t)n1 * 4), eta_stride, cstride / 4);
   TOUED_CHECK_LAUNCH();
