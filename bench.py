@@ -36,7 +36,10 @@ import torch  # noqa: E402
 MFMA_F32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: dense f32 MFMA (v_mfma_f32_32x32x2_f32)
 MFMA_BF16_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: dense bf16 MFMA
 HBM_PEAK_GBS = 8000.0
-SPLIT_PRODUCTS = 6                  # f32-accurate bf16 split: six bf16 MFMA products per f32 product (csrc/gru.hip)
+# 16-bit MFMA products issued per f32 product (csrc/gru.hip): forward = 16 carry k-steps on scaled fp16 pairs
+# (3 products) + 1 input k-step on the exact bf16 triple split (6); backward = the r pass on bf16 triples (6) +
+# the z and hn passes on scaled fp16 pairs (3 each)
+SPLIT_PRODUCTS = {"gru_fwd": (16 * 3 + 6) / 17, "gru_bwd": (6 + 3 + 3) / 3}
 GRU_FWD_FLOP_PER_ELEM = {5: 406080, 7: 409152}    # per (agent, worker, t)
 GRU_BWD_FLOP_PER_ELEM = 2 * 256 * 768              # dh_prev = dG . W_h^T per (k, agent, worker, t)
 # algorithmic HBM bytes per element: forward saves h_in, r, z, n, W_hn h + b_hn (5 x 256 f32) and
@@ -177,15 +180,15 @@ def main():
     dom, _, mean_ms = max(cand, key=lambda c: c[1])
     flop, nbytes = work[dom]
     t_hbm = nbytes / (HBM_PEAK_GBS * 1e9)
-    t_mfma = SPLIT_PRODUCTS * flop / (MFMA_BF16_PEAK_TFLOPS * 1e12)
+    t_mfma = SPLIT_PRODUCTS[dom] * flop / (MFMA_BF16_PEAK_TFLOPS * 1e12)
     traffic, traffic_src = pmc_traffic(PROFILED_KERNEL[dom])
     sec = mean_ms * 1e-3
     if t_hbm >= t_mfma:
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(nbytes / sec / 1e9, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(t_hbm / sec, 4), "bytes_per_launch": nbytes}
     else:
-        roofline = {"bound": "mfma", "kernel": dom, "achieved": round(SPLIT_PRODUCTS * flop / sec / 1e12, 1),
-                    "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s (bf16 issued)", "frac": round(t_mfma / sec, 4)}
+        roofline = {"bound": "mfma", "kernel": dom, "achieved": round(SPLIT_PRODUCTS[dom] * flop / sec / 1e12, 1),
+                    "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s (16-bit issued)", "frac": round(t_mfma / sec, 4)}
     roofline.update({"traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                      "mean_ms": round(mean_ms, 4), "min_ms_hbm": round(t_hbm * 1e3, 3),
                      "min_ms_mfma": round(t_mfma * 1e3, 3), "flop_per_launch_f32": flop,
@@ -195,7 +198,9 @@ def main():
         "value": round(value, 1), "unit": "agent-env-steps/sec", "n_gpus": n_gpus, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "mfma_precision": "f32-accurate: exact 3-piece bf16 split, 6 bf16 MFMA products per f32 product, f32 accumulate",
+        "mfma_precision": "f32-class: GRU carry products (forward, backward z/hn passes) on power-of-two-scaled fp16 "
+                          "pairs (3 fp16 MFMA products, pieces to 2^-22 relative), all other products on the exact "
+                          "3-piece bf16 split (6 products); f32 accumulate",
         "data": "synthetic (procedurally generated levels)",
         "meta_updates_per_sec": round(a.steps / dt, 3),
         "config": {"workload": f"C2 LPG meta-gradient env_mode={a.env_mode} num_agents={N_total} "

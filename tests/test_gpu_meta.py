@@ -223,6 +223,7 @@ def test_gru_backward_matches_autograd():
     for f, dX in ((3, gru.dX3), (4, gru.dX4)):
         got = dX.cpu().numpy()
         errs[f"dX{f}"] = np.linalg.norm(got - gx[f]) / np.linalg.norm(gx[f])
+    print("gru backward relative L2 errors:", {k: f"{v:.2e}" for k, v in errs.items()})
     bad = {k: v for k, v in errs.items() if not v < 1e-4}
     assert not bad, errs
 

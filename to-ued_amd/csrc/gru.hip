@@ -166,31 +166,8 @@ __global__ void k_pack_bwd(const float* __restrict__ eta, EtaOff o, float4* __re
 // bwd6 fragments [ks][unit tile ut][gate g][piece] (1 KiB each), appended after the f32 ones: lane l holds
 // A[i = input unit 32 ut + (l & 31)][k = gate unit 16 ks + 8 (l >> 5) + e] = W_g[i][k], split in three bf16
 #define B6_NF (16 * 8 * 3 * 3)
-#define B6_FLOATS (B6_NF * 256)
-__global__ void k_pack_bwd6(const float* __restrict__ eta, EtaOff o, __bf16* __restrict__ out8) {
-  typedef __bf16 v8 __attribute__((ext_vector_type(8)));
-  v8* out = reinterpret_cast<v8*>(out8);
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= 16 * 8 * 3 * 64) return;
-  const int lane = gid & 63, grp = gid >> 6;
-  const int g = grp % 3, ut = (grp / 3) % 8, ks = grp / 24;
-  const int u = 32 * ut + (lane & 31);
-  const int base = g == 0 ? o.hr_w : g == 1 ? o.hz_w : o.hn_w;
-  v8 pc[3];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float x = eta[base + u * HU + 16 * ks + 8 * (lane >> 5) + e];
-    const __bf16 h = (__bf16)x;
-    const float r1 = x - (float)h;
-    const __bf16 m = (__bf16)r1;
-    pc[0][e] = h;
-    pc[1][e] = m;
-    pc[2][e] = (__bf16)(r1 - (float)m);
-  }
-#pragma unroll
-  for (int q = 0; q < 3; ++q) out[(long)(grp * 3 + q) * 64 + lane] = pc[q];
-}
-
+#define B6_SCALES (B6_NF * 256)            // float offset of the per-input-unit scales 2^s of W_z, W_hn [256]
+#define B6_FLOATS (B6_SCALES + HU)
 // One k-major LDS buffer ([unit][row], pitch RB*NT + 1; h^T in the forward, a gate cotangent in the
 // backward) of NT row tiles out to its row-major
 // [unit][M] array: lane l stores 4 consecutive rows (4*(l & 7) ..) of unit 32*wave + 8i + (l >> 3),
@@ -518,6 +495,52 @@ __global__ void k_pack_fwd6(const float* __restrict__ eta, EtaOff o, int F, bf16
     }
 #pragma unroll
     for (int q = 0; q < 3; ++q) out[(long)(F6_NFH + ga * 3 + q) * 64 + lane] = pc[q];
+  }
+}
+
+// per-input-unit scale 2^s of the backward's fp16 gates (z, hn): s = 14 - e with
+// max_k max(|W_z[i][k]|, |W_hn[i][k]|) < 2^e, clamped to [-30, 20] (the forward's k_fwd6_scales rule)
+__global__ void k_bwd6_scales(const float* __restrict__ eta, EtaOff o, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= HU) return;
+  float m = 0.0f;
+  for (int k = 0; k < HU; ++k)
+    m = fmaxf(m, fmaxf(fabsf(eta[o.hz_w + i * HU + k]), fabsf(eta[o.hn_w + i * HU + k])));
+  int sc = 0;
+  if (m > 0.0f && m <= 3.0e38f) {
+    int e;
+    frexpf(m, &e);
+    sc = min(20, max(-30, 14 - e));
+  }
+  out[i] = ldexpf(1.0f, sc);
+}
+
+// backward A fragments A[i = input unit 32 ut + (l & 31)][k = gate unit 16 ks + 8 (l >> 5) + e] = W_g[i][k]:
+// gate r as three bf16 pieces, gates z and hn (scaled by the row's 2^s from k_bwd6_scales) as two fp16 pieces
+// in piece slots 0, 1 of the same [ks][ut][g][piece] layout
+__global__ void k_pack_bwd6(const float* __restrict__ eta, EtaOff o, __bf16* __restrict__ out8) {
+  typedef __bf16 v8 __attribute__((ext_vector_type(8)));
+  v8* out = reinterpret_cast<v8*>(out8);
+  const float* scl = reinterpret_cast<const float*>(out8) + B6_SCALES;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= 16 * 8 * 3 * 64) return;
+  const int lane = gid & 63, grp = gid >> 6;
+  const int g = grp % 3, ut = (grp / 3) % 8, ks = grp / 24;
+  const int u = 32 * ut + (lane & 31);
+  const int base = g == 0 ? o.hr_w : g == 1 ? o.hz_w : o.hn_w;
+  if (g == 0) {
+    v8 pc[3];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) split3v(eta[base + u * HU + 16 * ks + 8 * (lane >> 5) + e], pc[0], pc[1], pc[2], e);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) out[(long)(grp * 3 + q) * 64 + lane] = pc[q];
+  } else {
+    const float sg = scl[u];
+    f16x8 pc[2];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) split2h(eta[base + u * HU + 16 * ks + 8 * (lane >> 5) + e] * sg, pc[0], pc[1], e);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) out[(long)(grp * 3 + q) * 64 + lane] = __builtin_bit_cast(v8, pc[q]);
   }
 }
 
@@ -991,6 +1014,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   __shared__ float wi34[2 * 3 * HU];
   __shared__ float hv[9 * RBT];                    // head cotangents [output][row]
   __shared__ __attribute__((aligned(8))) float dxp[8 * RBT * 2];   // [wave][row][dx3 | dx4]
+  __shared__ __attribute__((aligned(16))) float wsc[HU];          // 2^s of W_z, W_hn row i (fp16 A scale)
+  __shared__ float rmx[8 * RBT];                   // per-wave row maxima of |dz|, |dhn| (fp16 B scale)
   const int tid = threadIdx.x, lane = tid & 63, hi = lane >> 5, col = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nb = p.R / RBT;
@@ -1008,6 +1033,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     const int base = g == 0 ? p.o.ir_w : g == 1 ? p.o.iz_w : p.o.in_w;
     wi34[i] = p.eta[base + f * HU + u];
   }
+  for (int i = tid; i < HU; i += 512) wsc[i] = reinterpret_cast<const float*>(p.A6)[B6_SCALES + i];
   float wA[5];   // W_heads^T A fragments of unit tile `wave`: A[i = unit][k = head output 2kk + hi]
 #pragma unroll
   for (int kk = 0; kk < 5; ++kk) {
@@ -1095,6 +1121,50 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     kstep(14, false);
     kstep(15, false);
   };
+  // the same for an fp16 gate (z, hn): two scaled fp16 pieces of W_g and of the cotangent, three products
+  auto ldAh = [&](int ks, int g, int q) {
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs_A, (int)vA,
+                                                          (int)((((ks * 8 + wave) * 3 + g) * 3 + q) * 1024), 0);
+    return __builtin_bit_cast(f16x8, x);
+  };
+  auto contract_h = [&](int g) {
+    f16x8 ring[2][2], B[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) ring[i][q] = ldAh(i, g, q);
+    auto ldB = [&](int ks, int h) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        B[h][q] = *reinterpret_cast<const f16x8*>(&dgB[q][(RB * h + col) * PP + 16 * ks + 8 * hi]);
+    };
+    ldB(0, 0);
+    ldB(0, 1);
+    auto kstep = [&](int ks, bool reload) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        acc[h] = mfma3h(ring[ks & 1], B[h], acc[h]);
+        if (ks + 1 < 16) ldB(ks + 1, h);
+      }
+      if (reload) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) ring[ks & 1][q] = ldAh(ks + 2, g, q);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+#pragma unroll 2
+    for (int ks = 0; ks < 14; ++ks) kstep(ks, true);
+    kstep(14, false);
+    kstep(15, false);
+  };
+  // scaled fp16 pieces of the four units u0 .. u0 + 3 of row `row` into image slots 0, 1
+  auto put4h = [&](int row, int u0, const float (&v)[4], float sc) {
+    f16x4 x0, x1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split2h(v[e] * sc, x0, x1, e);
+    *reinterpret_cast<f16x4*>(&dgB[0][row * PP + u0]) = x0;
+    *reinterpret_cast<f16x4*>(&dgB[1][row * PP + u0]) = x1;
+  };
   for (int t = 0; t < T; ++t) {
     const long ctr = ((long)k * T + t) * R;
     head_cot(t);
@@ -1174,33 +1244,76 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    __syncthreads();   // dr pieces complete
-    // ---- contraction: dr, then dz, then dhn through the one image
+    // row maxima of |dz|, |dhn| over this wave's units (the fp16 B scale of the z and hn passes)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float m = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) m = fmaxf(m, fmaxf(fabsf(dz_r[h][q]), fabsf(dhn_r[h][q])));
+      m = fmaxf(m, __shfl_xor(m, 32));
+      if (hi == 0) rmx[wave * RBT + RB * h + col] = m;
+    }
+    __syncthreads();   // dr pieces complete, row maxima visible
+    // ---- contraction: dr (bf16 triples), then dz and dhn (scaled fp16 pairs) through the one image
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[h][q] = 0.0f;
     contract(0);
+    // row scale 2^t (t = 14 - e, max_u max(|dz|, |dhn|) < 2^e, clamped to [-40, 40]); the dr result moves to
+    // the fp16 passes' frame 2^(s_i + t_row) (powers of two: exact), unscaled after the hn pass
+    float bs[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float m = 0.0f;
+#pragma unroll
+      for (int w8 = 0; w8 < 8; ++w8) m = fmaxf(m, rmx[w8 * RBT + RB * h + col]);
+      int sc = 0;
+      if (m > 0.0f && m <= 3.0e38f) {
+        int e;
+        frexpf(m, &e);
+        sc = min(40, max(-40, 14 - e));
+      }
+      bs[h] = ldexpf(1.0f, sc);
+    }
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const float4 w4 = *reinterpret_cast<const float4*>(&wsc[ub + 8 * g4]);
+      const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[h][4 * g4 + e] *= wv[e] * bs[h];
+    }
     __syncthreads();
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const float v4[4] = {dz_r[h][4 * g4], dz_r[h][4 * g4 + 1], dz_r[h][4 * g4 + 2], dz_r[h][4 * g4 + 3]};
-        put4(RB * h + col, ub + 8 * g4, v4);
+        put4h(RB * h + col, ub + 8 * g4, v4, bs[h]);
       }
     __syncthreads();
-    contract(1);
+    contract_h(1);
     __syncthreads();
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const float v4[4] = {dhn_r[h][4 * g4], dhn_r[h][4 * g4 + 1], dhn_r[h][4 * g4 + 2], dhn_r[h][4 * g4 + 3]};
-        put4(RB * h + col, ub + 8 * g4, v4);
+        put4h(RB * h + col, ub + 8 * g4, v4, bs[h]);
       }
     __syncthreads();
-    contract(2);
+    contract_h(2);
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const float4 w4 = *reinterpret_cast<const float4*>(&wsc[ub + 8 * g4]);
+      const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[h][4 * g4 + e] *= 1.0f / (wv[e] * bs[h]);
+    }
     if (tid < RBT) {
       float s3 = 0.0f, s4 = 0.0f;
 #pragma unroll
@@ -1239,6 +1352,7 @@ int toued_gru_pack(const float* eta, const int* off, int F, float* fwdA, float* 
                      reinterpret_cast<bf16x8*>(fwdA + (size_t)n1 * 4), 0L, 0L);
   hipLaunchKernelGGL(k_pack_bwd, dim3((n2 + 255) / 256), dim3(256), 0, stream, eta, o,
                      reinterpret_cast<float4*>(bwdA));
+  hipLaunchKernelGGL(k_bwd6_scales, dim3(1), dim3(256), 0, stream, eta, o, bwdA + (size_t)n2 * 4 + B6_SCALES);
   hipLaunchKernelGGL(k_pack_bwd6, dim3((16 * 8 * 3 * 64 + 255) / 256), dim3(256), 0, stream, eta, o,
                      reinterpret_cast<__bf16*>(bwdA + (size_t)n2 * 4));
   TOUED_CHECK_LAUNCH();
