@@ -159,12 +159,14 @@ def test_gru_forward_matches_oracle():
         np.testing.assert_allclose(arr, ref, atol=1e-4, rtol=1e-4, err_msg=name)
 
 
-def test_gru_backward_matches_autograd():
+@pytest.mark.parametrize("N,W", [(2, 64), (3, 32)])
+def test_gru_backward_matches_autograd(N, W):
     """LPG GRU VJP (toued_gru_bwd + the weight-gradient GEMMs over the saved m-major operands) vs float64
     torch autograd of the same GRU + heads: every GRU / head parameter gradient and the input cotangents
-    dX3, dX4 within 1e-4 relative L2."""
+    dX3, dX4 within 1e-4 relative L2.  R = 128 runs the lockstep kernel with the fused small products; R = 96
+    (not a multiple of 64) the f32 kernel with the small products as separate weight-gradient reductions."""
     from toued.lpg import LPGGRU, LPGLayout, init_lpg_params
-    N, W, T, K, F = 2, 64, 6, 2, 5
+    T, K, F = 6, 2, 5
     R = N * W
     lay = LPGLayout(F)
     eta = init_lpg_params(5, F)
@@ -255,7 +257,7 @@ def test_gru_backward_repeat_bit_identical():
         grad = torch.zeros(lay.size, device="cuda")
         gru.backward(done_t, eta, y_hat, d_pi, d_y, gru.X, grad)
         torch.cuda.synchronize()
-        outs.append([gru.dX3.clone(), gru.dX4.clone(), gru.DG.clone(), gru.RH.clone(), gru.DH.clone(), grad])
+        outs.append([gru.dX3.clone(), gru.dX4.clone(), gru.DG[:3].clone(), gru.GI.clone(), grad])
     for rep in outs[1:]:
         for a, b in zip(outs[0], rep):
             assert torch.isfinite(a).all()

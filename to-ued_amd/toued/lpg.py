@@ -118,11 +118,10 @@ class LPGGRU:
         self.dX4 = torch.empty((K, T, R), dtype=f32, device=dev)
         # weight-gradient reductions (csrc/wgrad.hip): outputs and the per-K-chunk partial-sum workspace
         self.G = torch.empty((H + lay.F + 1, 3 * H), dtype=f32, device=dev)
-        self.Gn = torch.empty((lay.F + 1, H), dtype=f32, device=dev)
-        self.Gh = torch.empty((9, H + 1), dtype=f32, device=dev)
+        # the backward's small products: [8][256] ([X; 1; 0] . dn^T) then [9][257] (DH . [relu(h_out); 1]^T)
+        self.GI = torch.empty(8 * H + 9 * (H + 1), dtype=f32, device=dev)
         need = max(int(L.toued_wgrad_workspace_floats(H + lay.F + 1, 3 * H, M)),
-                   int(L.toued_wgrad_workspace_floats(lay.F + 1, H, M)),
-                   int(L.toued_wgrad_workspace_floats(9, H + 1, M)))
+                   int(L.toued_gru_bwd_work_floats(R, K, M)))
         self.wg_work = torch.empty(max(need, 1), dtype=f32, device=dev)
 
     def pack(self, eta: torch.Tensor):
@@ -155,17 +154,18 @@ class LPGGRU:
                   self.lay.c_offsets, _lib.ptr(y_hat), _lib.ptr(d_pi_hat), _lib.ptr(d_y_hat),
                   _lib.ptr(self.A), _lib.ptr(S[0]), _lib.ptr(S[1]), _lib.ptr(S[2]), _lib.ptr(S[3]), M,
                   _lib.ptr(self.DG), _lib.ptr(self.RH), _lib.ptr(self.DH), _lib.ptr(self.dX3), _lib.ptr(self.dX4),
-                  _lib.stream_ptr())
+                  _lib.ptr(self.GI), _lib.ptr(self.wg_work), self.wg_work.numel(), _lib.stream_ptr())
         if timers is not None:
             timers.stop(tok)
             tok = timers.start("wgrad_gemm")
         lay = self.lay
         F = lay.F
         DG = self.DG
-        # weight-gradient reductions over M = K*T*R on MFMA (csrc/wgrad.hip, deterministic split-K):
+        # weight-gradient reduction over M = K*T*R on MFMA (csrc/wgrad.hip, deterministic split-K):
         #   [h_in; X; 1] (262 x M) . [dr; dz; dhn]^T  -> dW_h (rows 0..255), dW_ir/dW_iz (X rows), biases (ones row)
-        #   [X; 1] . dn^T -> dW_in, b_in;   DH . [relu(h_out); 1]^T -> head kernels and biases
-        G, Gn, Gh = self.G, self.Gn, self.Gh
+        # ([X; 1] . dn^T -> dW_in, b_in and DH . [relu(h_out); 1]^T -> head kernels and biases came with the
+        # backward in GI)
+        G = self.G
         ws, wn = _lib.ptr(self.wg_work), self.wg_work.numel()
         st = _lib.stream_ptr()
         _lib.call("toued_wgrad", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, _lib.ptr(DG), M, _lib.ptr(G), ws, wn, st)
@@ -177,12 +177,10 @@ class LPGGRU:
         lay.view(grad, "ir_b").add_(G[H + F, 0:H])
         lay.view(grad, "iz_b").add_(G[H + F, H:2 * H])
         lay.view(grad, "hn_b").add_(G[H + F, 2 * H:3 * H])
-        _lib.call("toued_wgrad", F + 1, H, M, _lib.ptr(self.A) + 4 * H * M, M, _lib.ptr(DG[3]), M, _lib.ptr(Gn), ws,
-                  wn, st)
+        Gn = self.GI[:8 * H].view(8, H)
         lay.view(grad, "in_w").add_(Gn[0:F])
         lay.view(grad, "in_b").add_(Gn[F])
-        _lib.call("toued_wgrad", 9, H + 1, M, _lib.ptr(self.DH), M, _lib.ptr(self.RH), M, _lib.ptr(Gh), ws, wn, st)
-        heads = Gh.t()                                                     # [257, 9]
+        heads = self.GI[8 * H:].view(9, H + 1).t()                        # [257, 9]
         lay.view(grad, "pi_w").add_(heads[0:H, 0:1])
         lay.view(grad, "y_w").add_(heads[0:H, 1:9])
         lay.view(grad, "pi_b").add_(heads[H, 0:1])
