@@ -195,16 +195,19 @@ int toued_gru_pack(const float* eta, const int* off, int F, float* fwdA, float* 
 int toued_gru_fwd(int R, int T, int W, int F, const float* X, long xs_f, long xs_col, const uint8_t* done,
                   const float* fwdA, const float* eta, const int* off, float* pi_hat, float* y_hat, float* s_hin,
                   float* s_r, float* s_z, float* s_n, float* s_hn, long M, hipStream_t stream);
-/* VJP over K updates (M = K*T*R columns): gate cotangents DG [4][256][M] (dr, dz, d(W_hn h + b_hn), dn), input
- * cotangents dX3/dX4 [K][T][R], and GI = [8][256] ([X; 1; 0] . dn^T: dW_in rows, b_in) followed by [9][257] (head
- * cotangents . [relu(h_out); 1]^T: head kernels and biases).  RH [257][M] (ones row 256) and DH [9][M] are the
- * intermediate relu(h_out) / head-cotangent streams.  `work`: toued_gru_bwd_work_floats(R, K, M) floats. */
-size_t toued_gru_bwd_work_floats(int R, int K, long M);
+/* VJP over K updates (M = K*T*R columns): gate cotangents DG [4][256][M] (dr, dz, d(W_hn h + b_hn), dn),
+ * relu(h_out) RH [256][M] (row 256 of the caller's [257][M] buffer holds ones), head cotangents DH [9][M],
+ * input cotangents dX3/dX4 [K][T][R] */
 int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_stride_k, const float* bwdA,
                   const float* eta, const int* off, const float* y_hat, const float* d_pi_hat, const float* d_y_hat,
                   const float* s_hin, const float* s_r, const float* s_z, const float* s_n, const float* s_hn, long M,
-                  float* DG, float* RH, float* DH, float* dX3, float* dX4, float* GI, float* work, size_t work_floats,
-                  hipStream_t stream);
+                  float* DG, float* RH, float* DH, float* dX3, float* dX4, hipStream_t stream);
+/* the backward's small weight-gradient products: GI = [8][256] ([X; 1; 0] . dn^T: dW_in rows, b_in) followed by
+ * [9][257] (DH . [relu(h_out); 1]^T: head kernels and biases); X rows start at s_hin + 256*M.
+ * `work`: toued_gru_bwd_small_work_floats(M) floats. */
+size_t toued_gru_bwd_small_work_floats(long M);
+int toued_gru_bwd_small(long M, const float* s_hin, const float* DG, const float* RH, const float* DH, float* GI,
+                        float* work, size_t work_floats, hipStream_t stream);
 
 /* weight-gradient reduction C[ra][rb] = A[ra x K] . B[rb x K]^T (row strides lda, ldb; K % 32 == 0,
  * ra <= 272) on f32 MFMA, split over K with per-chunk partials in `work` (toued_wgrad_workspace_floats)

@@ -1450,21 +1450,13 @@ int toued_gru_fwd_multi(int R, int T, int W, int F, int rows_per_cand, const flo
                         nullptr, nullptr, 0, 0, rows_per_cand, eta_stride, stream);
 }
 
-size_t toued_gru_bwd_work_floats(int R, int K, long M) {
-  (void)R; (void)K;
-  return std::max(toued_wgrad_workspace_floats(8, HU, M), toued_wgrad_workspace_floats(9, HU + 1, M));
-}
-
 int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_stride_k, const float* bwdA,
                   const float* eta, const int* off, const float* y_hat, const float* d_pi_hat, const float* d_y_hat,
                   const float* s_hin, const float* s_r, const float* s_z, const float* s_n, const float* s_hn, long M,
-                  float* DG, float* RH, float* DH, float* dX3, float* dX4, float* GI, float* work,
-                  size_t work_floats, hipStream_t stream) {
+                  float* DG, float* RH, float* DH, float* dX3, float* dX4, hipStream_t stream) {
   TOUED_REQUIRE(R % RB == 0 && W % RB == 0, "toued_gru_bwd: rows R=%d and workers W=%d must be multiples of 32", R, W);
   TOUED_REQUIRE((double)M * 264.0 * 4.0 < 4294967295.0, "toued_gru_bwd: M=%ld columns exceed the 4 GiB buffer range",
                 M);
-  TOUED_REQUIRE(work_floats >= toued_gru_bwd_work_floats(R, K, M), "toued_gru_bwd: workspace %zu < %zu floats",
-                work_floats, toued_gru_bwd_work_floats(R, K, M));
   BwdArgs p;
   p.R = R; p.T = T; p.W = W; p.K = K; p.done = done; p.done_stride_k = done_stride_k;
   p.A = reinterpret_cast<const float4*>(bwdA); p.eta = eta;
@@ -1478,12 +1470,23 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
   else
     hipLaunchKernelGGL(k_gru_bwd<1>, dim3(K * (R / RB)), dim3(512), 0, stream, p);
   TOUED_CHECK_LAUNCH();
-  // the small weight-gradient reductions over dn, relu(h_out) and the head cotangents: GI = [8][256]
-  // ([X; 1; 0] . dn^T) | [9][257] (DH . [relu(h_out); 1]^T).  (Folding them into the lockstep kernel was
-  // measured: its register file is full, the spills cost more than the 7 GB of streams saved.)
-  toued_wgrad(8, HU, M, s_hin + (size_t)HU * M, M, DG + (size_t)3 * HU * M, M, GI, work, work_floats, stream);
-  toued_wgrad(9, HU + 1, M, DH, M, RH, M, GI + 8 * HU, work, work_floats, stream);
   return 0;
+}
+
+size_t toued_gru_bwd_small_work_floats(long M) {
+  return std::max(toued_wgrad_workspace_floats(8, HU, M), toued_wgrad_workspace_floats(9, HU + 1, M));
+}
+
+// the backward's small weight-gradient reductions (HBM streams over dn, relu(h_out) and the head cotangents):
+// GI = [8][256] ([X; 1; 0] . dn^T) | [9][257] (DH . [relu(h_out); 1]^T).  (Folding them into the lockstep
+// kernel was measured: its register file is full and the spills cost more than the 7 GB of streams saved.)
+int toued_gru_bwd_small(long M, const float* s_hin, const float* DG, const float* RH, const float* DH, float* GI,
+                        float* work, size_t work_floats, hipStream_t stream) {
+  TOUED_REQUIRE(work_floats >= toued_gru_bwd_small_work_floats(M), "toued_gru_bwd_small: workspace %zu < %zu floats",
+                work_floats, toued_gru_bwd_small_work_floats(M));
+  int rc = toued_wgrad(8, HU, M, s_hin + (size_t)HU * M, M, DG + (size_t)3 * HU * M, M, GI, work, work_floats, stream);
+  if (rc) return rc;
+  return toued_wgrad(9, HU + 1, M, DH, M, RH, M, GI + 8 * HU, work, work_floats, stream);
 }
 
 }  // extern "C"

@@ -121,7 +121,7 @@ class LPGGRU:
         # the backward's small products: [8][256] ([X; 1; 0] . dn^T) then [9][257] (DH . [relu(h_out); 1]^T)
         self.GI = torch.empty(8 * H + 9 * (H + 1), dtype=f32, device=dev)
         need = max(int(L.toued_wgrad_workspace_floats(H + lay.F + 1, 3 * H, M)),
-                   int(L.toued_gru_bwd_work_floats(R, K, M)))
+                   int(L.toued_gru_bwd_small_work_floats(M)))
         self.wg_work = torch.empty(max(need, 1), dtype=f32, device=dev)
 
     def pack(self, eta: torch.Tensor):
@@ -154,20 +154,21 @@ class LPGGRU:
                   self.lay.c_offsets, _lib.ptr(y_hat), _lib.ptr(d_pi_hat), _lib.ptr(d_y_hat),
                   _lib.ptr(self.A), _lib.ptr(S[0]), _lib.ptr(S[1]), _lib.ptr(S[2]), _lib.ptr(S[3]), M,
                   _lib.ptr(self.DG), _lib.ptr(self.RH), _lib.ptr(self.DH), _lib.ptr(self.dX3), _lib.ptr(self.dX4),
-                  _lib.ptr(self.GI), _lib.ptr(self.wg_work), self.wg_work.numel(), _lib.stream_ptr())
+                  _lib.stream_ptr())
         if timers is not None:
             timers.stop(tok)
             tok = timers.start("wgrad_gemm")
         lay = self.lay
         F = lay.F
         DG = self.DG
-        # weight-gradient reduction over M = K*T*R on MFMA (csrc/wgrad.hip, deterministic split-K):
+        # weight-gradient reductions over M = K*T*R on MFMA (csrc/wgrad.hip, deterministic split-K):
         #   [h_in; X; 1] (262 x M) . [dr; dz; dhn]^T  -> dW_h (rows 0..255), dW_ir/dW_iz (X rows), biases (ones row)
-        # ([X; 1] . dn^T -> dW_in, b_in and DH . [relu(h_out); 1]^T -> head kernels and biases came with the
-        # backward in GI)
+        #   GI: [X; 1] . dn^T -> dW_in, b_in;   DH . [relu(h_out); 1]^T -> head kernels and biases
         G = self.G
         ws, wn = _lib.ptr(self.wg_work), self.wg_work.numel()
         st = _lib.stream_ptr()
+        _lib.call("toued_gru_bwd_small", M, _lib.ptr(self.A), _lib.ptr(DG), _lib.ptr(self.RH), _lib.ptr(self.DH),
+                  _lib.ptr(self.GI), ws, wn, st)
         _lib.call("toued_wgrad", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, _lib.ptr(DG), M, _lib.ptr(G), ws, wn, st)
         lay.view(grad, "hr_w").add_(G[0:H, 0:H])
         lay.view(grad, "hz_w").add_(G[0:H, H:2 * H])
