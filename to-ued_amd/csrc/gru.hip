@@ -503,14 +503,15 @@ __global__ void k_pack_fwd6(const float* __restrict__ eta, EtaOff o, int F, bf16
   }
 }
 
-// per-input-unit scale 2^s of the backward's fp16 gates (z, hn): s = 14 - e with
-// max_k max(|W_z[i][k]|, |W_hn[i][k]|) < 2^e, clamped to [-30, 20] (the forward's k_fwd6_scales rule)
+// per-input-unit scale 2^s of the backward's fp16 weight rows: s = 14 - e with
+// max_k max(|W_r[i][k]|, |W_z[i][k]|, |W_hn[i][k]|) < 2^e, clamped to [-30, 20] (the forward's k_fwd6_scales rule)
 __global__ void k_bwd6_scales(const float* __restrict__ eta, EtaOff o, float* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= HU) return;
   float m = 0.0f;
   for (int k = 0; k < HU; ++k)
-    m = fmaxf(m, fmaxf(fabsf(eta[o.hz_w + i * HU + k]), fabsf(eta[o.hn_w + i * HU + k])));
+    m = fmaxf(m, fmaxf(fabsf(eta[o.hr_w + i * HU + k]),
+                       fmaxf(fabsf(eta[o.hz_w + i * HU + k]), fabsf(eta[o.hn_w + i * HU + k]))));
   int sc = 0;
   if (m > 0.0f && m <= 3.0e38f) {
     int e;
@@ -520,9 +521,9 @@ __global__ void k_bwd6_scales(const float* __restrict__ eta, EtaOff o, float* __
   out[i] = ldexpf(1.0f, sc);
 }
 
-// backward A fragments A[i = input unit 32 ut + (l & 31)][k = gate unit 16 ks + 8 (l >> 5) + e] = W_g[i][k]:
-// gate r as three bf16 pieces, gates z and hn (scaled by the row's 2^s from k_bwd6_scales) as two fp16 pieces
-// in piece slots 0, 1 of the same [ks][ut][g][piece] layout
+// backward A fragments A[i = input unit 32 ut + (l & 31)][k = gate unit 16 ks + 8 (l >> 5) + e] = W_g[i][k] of
+// the three gates, row i scaled by its 2^s (k_bwd6_scales), as two fp16 pieces in piece slots 0, 1 of the
+// [ks][ut][g][piece] layout (slot 2 unused)
 __global__ void k_pack_bwd6(const float* __restrict__ eta, EtaOff o, __bf16* __restrict__ out8) {
   typedef __bf16 v8 __attribute__((ext_vector_type(8)));
   v8* out = reinterpret_cast<v8*>(out8);
@@ -533,20 +534,12 @@ __global__ void k_pack_bwd6(const float* __restrict__ eta, EtaOff o, __bf16* __r
   const int g = grp % 3, ut = (grp / 3) % 8, ks = grp / 24;
   const int u = 32 * ut + (lane & 31);
   const int base = g == 0 ? o.hr_w : g == 1 ? o.hz_w : o.hn_w;
-  if (g == 0) {
-    v8 pc[3];
+  const float sg = scl[u];
+  f16x8 pc[2];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) split3v(eta[base + u * HU + 16 * ks + 8 * (lane >> 5) + e], pc[0], pc[1], pc[2], e);
+  for (int e = 0; e < 8; ++e) split2h(eta[base + u * HU + 16 * ks + 8 * (lane >> 5) + e] * sg, pc[0], pc[1], e);
 #pragma unroll
-    for (int q = 0; q < 3; ++q) out[(long)(grp * 3 + q) * 64 + lane] = pc[q];
-  } else {
-    const float sg = scl[u];
-    f16x8 pc[2];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) split2h(eta[base + u * HU + 16 * ks + 8 * (lane >> 5) + e] * sg, pc[0], pc[1], e);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) out[(long)(grp * 3 + q) * 64 + lane] = __builtin_bit_cast(v8, pc[q]);
-  }
+  for (int q = 0; q < 2; ++q) out[(long)(grp * 3 + q) * 64 + lane] = __builtin_bit_cast(v8, pc[q]);
 }
 
 TOUED_DEV floatx16 mfma_bf32(bf16x8 a, bf16x8 b, floatx16 c) {
@@ -1019,8 +1012,12 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   __shared__ float wi34[2 * 3 * HU];
   __shared__ float hv[9 * RBT];                    // head cotangents [output][row]
   __shared__ __attribute__((aligned(8))) float dxp[8 * RBT * 2];   // [wave][row][dx3 | dx4]
-  __shared__ __attribute__((aligned(16))) float wsc[HU];          // 2^s of W_z, W_hn row i (fp16 A scale)
-  __shared__ float rmx[8 * RBT];                   // per-wave row maxima of |dz|, |dhn| (fp16 B scale)
+  __shared__ __attribute__((aligned(16))) float wsc[HU];          // 2^s of W_g row i (fp16 A scale)
+  __shared__ float rmx[8 * RBT];                   // per-wave row maxima of |dr|, |dz|, |dhn| (fp16 B scale)
+  // dr in f32 while the memory part streams ([row][unit], pitch DRP), over image slots 1 and 2
+  constexpr int DRP = HU + 4;
+  static_assert(RBT * DRP * 4 <= 2 * RBT * PP * 2, "dr staging exceeds image slots 1-2");
+  float* drs = reinterpret_cast<float*>(&dgB[1][0]);
   const int tid = threadIdx.x, lane = tid & 63, hi = lane >> 5, col = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nb = p.R / RBT;
@@ -1079,54 +1076,11 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       }
     }
   };
-  // pieces of the four consecutive units ub + 8 g4 .. +3 of row `row` into the cotangent image
-  auto put4 = [&](int row, int u0, const float (&v)[4]) {
-    bf16x4 pc[3];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) split3v(v[e], pc[0], pc[1], pc[2], e);
-#pragma unroll
-    for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x4*>(&dgB[q][row * PP + u0]) = pc[q];
-  };
-  // contraction of one gate's cotangent image with W_g (bf16 split fragments, 2-deep ring from L2)
+  // contraction of one gate's cotangent image with W_g: two scaled fp16 pieces of each operand, three
+  // products, A fragments through a 2-deep ring from L2
   const __amdgpu_buffer_rsrc_t rs_A = rsrc_of(reinterpret_cast<const float*>(p.A6));
   const unsigned vA = (unsigned)lane * 16;
-  auto ldA = [&](int ks, int g, int q) {
-    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs_A, (int)vA,
-                                                          (int)((((ks * 8 + wave) * 3 + g) * 3 + q) * 1024), 0);
-    return __builtin_bit_cast(bf16x8, x);
-  };
   floatx16 acc[2];
-  auto contract = [&](int g) {
-    bf16x8 ring[2][3], B[2][3];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int q = 0; q < 3; ++q) ring[i][q] = ldA(i, g, q);
-    auto ldB = [&](int ks, int h) {
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        B[h][q] = *reinterpret_cast<const bf16x8*>(&dgB[q][(RB * h + col) * PP + 16 * ks + 8 * hi]);
-    };
-    ldB(0, 0);
-    ldB(0, 1);
-    auto kstep = [&](int ks, bool reload) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        acc[h] = mfma6(ring[ks & 1], B[h], acc[h]);
-        if (ks + 1 < 16) ldB(ks + 1, h);
-      }
-      if (reload) {
-#pragma unroll
-        for (int q = 0; q < 3; ++q) ring[ks & 1][q] = ldA(ks + 2, g, q);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    };
-#pragma unroll 2
-    for (int ks = 0; ks < 14; ++ks) kstep(ks, true);
-    kstep(14, false);
-    kstep(15, false);
-  };
-  // the same for an fp16 gate (z, hn): two scaled fp16 pieces of W_g and of the cotangent, three products
   auto ldAh = [&](int ks, int g, int q) {
     const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs_A, (int)vA,
                                                           (int)((((ks * 8 + wave) * 3 + g) * 3 + q) * 1024), 0);
@@ -1191,6 +1145,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     };
     floatx16 hacc;
     float dx3 = 0.0f, dx4 = 0.0f;
+    float rmr[2] = {0.0f, 0.0f};   // running row maxima of |dr|
     load_q(0, 0, va);
 #pragma unroll
     for (int qi = 0; qi < 8; ++qi) {
@@ -1241,7 +1196,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         st_u(rs_dg[2], vbo, so1, dhn);
         st_u(rs_dg[3], vbo, so1, dnp);
       }
-      put4(row, ub + 8 * g4, drq);
+      *reinterpret_cast<float4*>(&drs[row * DRP + ub + 8 * g4]) = make_float4(drq[0], drq[1], drq[2], drq[3]);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) rmr[h] = fmaxf(rmr[h], fabsf(drq[jj]));
       if (g4 == 3) {
         // lanes l and l + 32 hold the same row: fold the halves, one float2 per (wave, row)
         const float f3 = dx3 + __shfl_xor(dx3, 32), f4 = dx4 + __shfl_xor(dx4, 32);
@@ -1249,24 +1206,18 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    // row maxima of |dz|, |dhn| over this wave's units (the fp16 B scale of the z and hn passes)
+    // row maxima of |dr|, |dz|, |dhn| over this wave's units (the fp16 B scale of the three passes)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      float m = 0.0f;
+      float m = rmr[h];
 #pragma unroll
       for (int q = 0; q < 16; ++q) m = fmaxf(m, fmaxf(fabsf(dz_r[h][q]), fabsf(dhn_r[h][q])));
       m = fmaxf(m, __shfl_xor(m, 32));
       if (hi == 0) rmx[wave * RBT + RB * h + col] = m;
     }
-    __syncthreads();   // dr pieces complete, row maxima visible
-    // ---- contraction: dr (bf16 triples), then dz and dhn (scaled fp16 pairs) through the one image
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[h][q] = 0.0f;
-    contract(0);
-    // row scale 2^t (t = 14 - e, max_u max(|dz|, |dhn|) < 2^e, clamped to [-40, 40]); the dr result moves to
-    // the fp16 passes' frame 2^(s_i + t_row) (powers of two: exact), unscaled after the hn pass
+    __syncthreads();   // dr staged, row maxima visible
+    // row scale 2^t (t = 14 - e, max_u max(|dr|, |dz|, |dhn|) < 2^e, clamped to [-40, 40]): the three passes
+    // accumulate in the frame 2^(s_i + t_row), unscaled exactly (powers of two) after the hn pass
     float bs[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1281,15 +1232,34 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       }
       bs[h] = ldexpf(1.0f, sc);
     }
+    // dr -> fp16 pieces: x0 straight into slot 0, x1 held until every lane has read its staged f32 values
+    // (slot 1 overlaps the staging)
+    f16x4 x1h[2][4];
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const float4 w4 = *reinterpret_cast<const float4*>(&wsc[ub + 8 * g4]);
-      const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int row = RB * h + col;
+        const float4 v = *reinterpret_cast<const float4*>(&drs[row * DRP + ub + 8 * g4]);
+        const float v4[4] = {v.x, v.y, v.z, v.w};
+        f16x4 x0;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[h][4 * g4 + e] *= wv[e] * bs[h];
-    }
+        for (int e = 0; e < 4; ++e) split2h(v4[e] * bs[h], x0, x1h[h][g4], e);
+        *reinterpret_cast<f16x4*>(&dgB[0][row * PP + ub + 8 * g4]) = x0;
+      }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+        *reinterpret_cast<f16x4*>(&dgB[1][(RB * h + col) * PP + ub + 8 * g4]) = x1h[h][g4];
+    __syncthreads();
+    // ---- contraction: dr, then dz, then dhn (scaled fp16 pairs) through the one image
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[h][q] = 0.0f;
+    contract_h(0);
     __syncthreads();
 #pragma unroll
     for (int h = 0; h < 2; ++h)
