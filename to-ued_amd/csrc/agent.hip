@@ -1151,23 +1151,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   }
   // 2) sort by (row, sample)
   sort2048(key, tid);
-  // 3) one thread per distinct row sums its segment in sample order and updates the table row
+  // 3) segmented sums over the sorted keys, chunked so that no thread walks a long segment alone: thread t
+  //    sums the runs of its CH entries [CH t, CH t + CH); a run that continues a segment begun in an earlier
+  //    chunk leaves its partial in the vector row of the chunk's first sample (read only by this thread);
+  //    after a barrier each segment's owner (the thread holding its first entry) adds the partials of the
+  //    chunks its segment runs into, in chunk order (deterministic), and updates the table row.
+  constexpr int CH = 4;
   float na2 = 0.0f, nc2 = 0.0f;
-  for (int i = tid; i < TW; i += 512) {
-    const uint32_t kk = key[i];
-    if (kk == 0xFFFFFFFFu) continue;
-    const uint32_t row = kk >> 12;
-    if (i > 0 && (key[i - 1] >> 12) == row) continue;
-    float sum[NV];
-#pragma unroll
-    for (int j = 0; j < NV; ++j) sum[j] = 0.0f;
-    for (int e = i; e < TW; ++e) {
-      const uint32_t ke = key[e];
-      if ((ke >> 12) != row || ke == 0xFFFFFFFFu) break;
-      const float* ve = vec + (ke & 4095u) * NVP;
-#pragma unroll
-      for (int j = 0; j < NV; ++j) sum[j] += ve[j];
-    }
+  auto emit = [&](uint32_t row, float (&sum)[NV]) {
     if ((int)row == D - 1) {
 #pragma unroll
       for (int j = 0; j < NV; ++j) sum[j] += tot[j];
@@ -1188,6 +1179,50 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
         if (Op::NORMS) nc2 += g * g;
       }
     }
+  };
+  const int i0 = CH * tid, i1 = min(i0 + CH, TW);
+  const uint32_t NONE = 0xFFFFFFFFu;
+  float run[NV];
+  uint32_t run_row = NONE;
+  bool run_owned = false;
+  uint32_t pend_row = NONE;          // owned run reaching the chunk end whose segment continues
+  for (int e = i0; e <= i1; ++e) {
+    const uint32_t ke = e < i1 ? key[e] : NONE;
+    const uint32_t row = ke == NONE ? NONE : ke >> 12;
+    if (row != run_row && run_row != NONE) {
+      // the run [.., e) ends here (new row, invalid key or chunk end)
+      const bool cont_next = e == i1 && e < TW && key[e] != NONE && (key[e] >> 12) == run_row;
+      if (!run_owned) {
+        float* slot = vec + (key[i0] & 4095u) * NVP;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) slot[j] = run[j];
+      } else if (cont_next) {
+        pend_row = run_row;
+      } else {
+        emit(run_row, run);
+      }
+    }
+    if (ke == NONE) break;
+    if (row != run_row) {
+      run_row = row;
+      run_owned = e == 0 || (key[e - 1] >> 12) != row;
+#pragma unroll
+      for (int j = 0; j < NV; ++j) run[j] = 0.0f;
+    }
+    const float* ve = vec + (ke & 4095u) * NVP;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) run[j] += ve[j];
+  }
+  __syncthreads();
+  if (pend_row != NONE) {
+    for (int c = tid + 1; CH * c < TW; ++c) {
+      const uint32_t kc = key[CH * c];
+      if (kc == NONE || (kc >> 12) != pend_row) break;
+      const float* slot = vec + (kc & 4095u) * NVP;
+#pragma unroll
+      for (int j = 0; j < NV; ++j) run[j] += slot[j];
+    }
+    emit(pend_row, run);
   }
   if (tid == 0) {
     if (!has_last) {
