@@ -64,6 +64,9 @@ size_t toued_mode_program_bytes(void);
  * buffer_ids may be NULL (0); sub_mode_out may be NULL. */
 int toued_level_gen(const void* program, const uint32_t* keys, const int* buffer_ids, int* levels_out,
                     int* sub_mode_out, int n, hipStream_t stream);
+/* only the levels i with mask[i] != 0 are written (in place: the level sampler's where(terminated, new, old)) */
+int toued_level_gen_masked(const void* program, const uint32_t* keys, const int* buffer_ids, int* levels_out, int n,
+                           const uint8_t* mask, hipStream_t stream);
 
 /* ---- gymnax Environment plugin API (GridWorld, gridworld.py:72-211) ----
  * Worker i uses levels[i / W]; keys are per worker. */
@@ -78,6 +81,9 @@ int toued_gw_step(EnvSpec spec, const int* levels, int W, const uint32_t* keys, 
 /* batch_reset(rng, env_params, W) for n_agents agents: worker keys = split(agent_key, W). */
 int toued_batch_reset(EnvSpec spec, const int* levels, const uint32_t* agent_keys, int n_agents, int W, int* state,
                       int* obs_idx, int* obs_time, hipStream_t stream);
+/* only the workers of the agents a with mask[a] != 0 are reset (in place) */
+int toued_batch_reset_masked(EnvSpec spec, const int* levels, const uint32_t* agent_keys, int n_agents, int W,
+                             int* state, int* obs_idx, int* obs_time, const uint8_t* mask, hipStream_t stream);
 /* batch_rollout(rng, actor_state, env_params, obs, state) — T policy steps with the
  * linear softmax actor theta[n_agents][D][5].  Trajectory layout: idx/time [N][T+1][W]
  * (slot T = end obs), action/done u8 [N][T][W], reward f32 [N][T][W]; cum_return [N*W].
@@ -110,6 +116,9 @@ int toued_plr_sample(int B, int N, const float* score, const uint8_t* active, co
  * [lo, hi] = erf(-+2/sqrt2), times stddev.  keys are the flax per-param keys (toued/agents.py). */
 int toued_init_tables(const uint32_t* keys, int n, int cols, int D, float lo, float hi, float stddev, float* out,
                       hipStream_t stream);
+/* only the tables i with mask[i] != 0 are written (in place) */
+int toued_init_tables_masked(const uint32_t* keys, int n, int cols, int D, float lo, float hi, float stddev,
+                             float* out, const uint8_t* mask, hipStream_t stream);
 
 /* ---- A2C antagonist (agents/a2c.py:19-125) ---- */
 /* out[u][i] = the u-th `_rng` of `rng, _rng = split(rng)` chained from keys[i] (a2c.py:97). */

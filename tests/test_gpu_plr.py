@@ -266,3 +266,40 @@ def test_level_sampler_alg_regret_end_to_end():
         # terminate half the agents for the next round
         agents.step = torch.where(torch.arange(N, device="cuda") % 2 == it % 2, agents.levels[:, L_LIFETIME],
                                   torch.zeros_like(agents.step))
+
+
+def test_masked_generators_match_where():
+    """The level sampler's in-place masked generators (toued_level_gen_masked, toued_batch_reset_masked,
+    toued_init_tables_masked) equal the reference's where(terminated, new, old) over a full new batch."""
+    from toued import prng
+    from toued.agents import create_agents, create_agents_into, lecun_tables, lecun_tables_into
+    from toued.env import LevelGenerator
+    from toued.rollout import RolloutWrapper
+    N, W, mode = 13, 64, "all_shortlife"
+    gen = LevelGenerator(mode)
+    ro = RolloutWrapper(mode, 20, env_workers=W)
+    D = ro.obs_dim
+    keys_old, keys_new = prng.split(prng.PRNGKey(3, "cuda"), N), prng.split(prng.PRNGKey(4, "cuda"), N)
+    mask = (torch.arange(N, device="cuda") % 3 == 1).to(torch.uint8)
+    term = mask.bool()
+    old_lv, new_lv = gen(keys_old), gen(keys_new)
+    lv = old_lv.clone()
+    gen.regenerate(keys_new, lv, mask)
+    assert torch.equal(lv, torch.where(term[:, None], new_lv, old_lv))
+    (_, _), st_old = ro.batch_reset(keys_old, old_lv)
+    (_, _), st_new = ro.batch_reset(keys_new, lv)
+    st = st_old.clone()
+    ro.batch_reset_into(keys_new, lv, st, mask)
+    nf = 4 + ro.spec.max_n_objs     # time, pos, exists, early_term, obj_poss[max_n_objs] (the rest is never written)
+    ref = torch.where(term.repeat_interleave(W)[None, :], st_new, st_old)
+    assert torch.equal(st[:nf], ref[:nf])
+    th_old, ph_old = create_agents(keys_old, D, 8)
+    th_new, ph_new = create_agents(keys_new, D, 8)
+    th, ph = th_old.clone(), ph_old.clone()
+    create_agents_into(keys_new, th, ph, mask)
+    assert torch.equal(th, torch.where(term[:, None, None], th_new, th_old))
+    assert torch.equal(ph, torch.where(term[:, None, None], ph_new, ph_old))
+    vc = lecun_tables(keys_old, D, 1)
+    vc_new = lecun_tables(keys_new, D, 1)
+    lecun_tables_into(keys_new, vc, mask)
+    assert torch.equal(vc, torch.where(term[:, None, None], vc_new, lecun_tables(keys_old, D, 1)))

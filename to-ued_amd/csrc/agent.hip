@@ -811,12 +811,15 @@ __global__ void __launch_bounds__(256) k_adam(int P, float* __restrict__ eta, co
 // unpinned).  u = uniform(lo=erf(-sqrt2), hi=erf(sqrt2)); z = sqrt2*erfinv(u), clipped.
 
 __global__ void __launch_bounds__(256) k_init_tables(const uint32_t* __restrict__ keys, int n, int cols, int D,
-                                                     float lo, float hi, float stddev, float* __restrict__ out) {
-  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+                                                     float lo, float hi, float stddev, float* __restrict__ out,
+                                                     const uint8_t* __restrict__ mask) {
+  // grid (chunk, table i): no per-element index division; masked tables exit at once
+  const int i = blockIdx.y;
+  if (i >= n || (mask && !mask[i])) return;
   const long per = (long)D * cols;
-  if (e >= (long)n * per) return;
-  const int i = (int)(e / per);
-  const long j = e - (long)i * per;
+  const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= per) return;
+  const long e = (long)i * per + j;
   const uint2 key = make_uint2(keys[2 * i], keys[2 * i + 1]);
   const float u = uniform_from_bits(random_bits_at(key, (uint32_t)per, (uint32_t)j), lo, hi);
   float z = 1.41421356237f * erfinv_giles(u);
@@ -1449,7 +1452,20 @@ int toued_init_tables(const uint32_t* keys, int n, int cols, int D, float lo, fl
                       hipStream_t stream) {
   const long tot = (long)n * D * cols;
   if (tot == 0) return 0;
-  hipLaunchKernelGGL(k_init_tables, dim3(nb256(tot)), dim3(256), 0, stream, keys, n, cols, D, lo, hi, stddev, out);
+  hipLaunchKernelGGL(k_init_tables, dim3(nb256((long)D * cols), n), dim3(256), 0, stream, keys, n, cols, D, lo, hi,
+                     stddev, out, nullptr);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+// the same, writing only the tables i with mask[i] != 0 (in place: the level sampler's where(terminated, new, old))
+int toued_init_tables_masked(const uint32_t* keys, int n, int cols, int D, float lo, float hi, float stddev,
+                             float* out, const uint8_t* mask, hipStream_t stream) {
+  TOUED_REQUIRE(mask != nullptr, "toued_init_tables_masked: mask required");
+  const long tot = (long)n * D * cols;
+  if (tot == 0) return 0;
+  hipLaunchKernelGGL(k_init_tables, dim3(nb256((long)D * cols), n), dim3(256), 0, stream, keys, n, cols, D, lo, hi,
+                     stddev, out, mask);
   TOUED_CHECK_LAUNCH();
   return 0;
 }

@@ -313,10 +313,12 @@ template <int NMAX, bool TAB>
 __global__ void __launch_bounds__(256) k_batch_reset(EnvSpec sp, const int* __restrict__ levels,
                                                      const uint32_t* __restrict__ agent_keys, int W,
                                                      int* __restrict__ state, int* __restrict__ obs_idx,
-                                                     int* __restrict__ obs_time, int n) {
+                                                     int* __restrict__ obs_time, int n,
+                                                     const uint8_t* __restrict__ mask) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int a = i / W, w = i - a * W;
+  if (mask && !mask[a]) return;
   const int* lev = levels + (size_t)a * LEVEL_WORDS;
   const uint2 key = split_at(make_uint2(agent_keys[2 * a], agent_keys[2 * a + 1]), (uint32_t)W, (uint32_t)w);
   EnvState s;
@@ -531,7 +533,20 @@ int toued_batch_reset(EnvSpec sp, const int* levels, const uint32_t* agent_keys,
   const int n = n_agents * W;
   if (n == 0) return 0;
   TOUED_DISPATCH(sp, hipLaunchKernelGGL((k_batch_reset<NMAX, TAB>), dim3(nblk(n)), dim3(256), 0, stream, sp, levels,
-                                        agent_keys, W, state, obs_idx, obs_time, n));
+                                        agent_keys, W, state, obs_idx, obs_time, n, nullptr));
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+// the same for the workers of the agents a with mask[a] != 0 only (in place into state / obs_idx / obs_time)
+int toued_batch_reset_masked(EnvSpec sp, const int* levels, const uint32_t* agent_keys, int n_agents, int W, int* state,
+                             int* obs_idx, int* obs_time, const uint8_t* mask, hipStream_t stream) {
+  if (int e = check_spec(sp)) return e;
+  TOUED_REQUIRE(n_agents >= 0 && W >= 1 && mask, "toued_batch_reset_masked: bad sizes N=%d W=%d", n_agents, W);
+  const int n = n_agents * W;
+  if (n == 0) return 0;
+  TOUED_DISPATCH(sp, hipLaunchKernelGGL((k_batch_reset<NMAX, TAB>), dim3(nblk(n)), dim3(256), 0, stream, sp, levels,
+                                        agent_keys, W, state, obs_idx, obs_time, n, mask));
   TOUED_CHECK_LAUNCH();
   return 0;
 }

@@ -190,9 +190,10 @@ TOUED_DEV void gen_level(const ModeSpec& m, const ModeProgram& prog, uint2 rng, 
 __global__ void __launch_bounds__(64) k_level_gen(const ModeProgram* __restrict__ prog_g,
                                                   const uint32_t* __restrict__ keys,
                                                   const int* __restrict__ buffer_ids, int* __restrict__ out,
-                                                  int* __restrict__ sub_mode, int n) {
+                                                  int* __restrict__ sub_mode, int n,
+                                                  const uint8_t* __restrict__ mask) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || (mask && !mask[i])) return;
   const ModeProgram& prog = *prog_g;
   const uint2 key = make_uint2(keys[2 * i], keys[2 * i + 1]);
   uint2 p_rng, l_rng;
@@ -223,7 +224,19 @@ int toued_level_gen(const void* program, const uint32_t* keys, const int* buffer
   TOUED_REQUIRE(n >= 0, "toued_level_gen: n=%d", n);
   if (n == 0) return 0;
   hipLaunchKernelGGL(k_level_gen, dim3((n + 63) / 64), dim3(64), 0, stream,
-                     reinterpret_cast<const ModeProgram*>(program), keys, buffer_ids, levels_out, sub_mode_out, n);
+                     reinterpret_cast<const ModeProgram*>(program), keys, buffer_ids, levels_out, sub_mode_out, n,
+                     nullptr);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+// the same, writing only the levels i with mask[i] != 0 (in place: the level sampler's where(terminated, new, old))
+int toued_level_gen_masked(const void* program, const uint32_t* keys, const int* buffer_ids, int* levels_out, int n,
+                           const uint8_t* mask, hipStream_t stream) {
+  TOUED_REQUIRE(n >= 0 && mask, "toued_level_gen_masked: n=%d mask=%p", n, (const void*)mask);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_level_gen, dim3((n + 63) / 64), dim3(64), 0, stream,
+                     reinterpret_cast<const ModeProgram*>(program), keys, buffer_ids, levels_out, nullptr, n, mask);
   TOUED_CHECK_LAUNCH();
   return 0;
 }

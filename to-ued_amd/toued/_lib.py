@@ -38,9 +38,11 @@ _SIGS = {
     "toued_uniform": [_P, _I, _I, _F, _F, _P, _P],
     "toued_mode_program_bytes": [],
     "toued_level_gen": [_P, _P, _P, _P, _P, _I, _P],
+    "toued_level_gen_masked": [_P, _P, _P, _P, _I, _P, _P],
     "toued_gw_reset": [EnvSpecC, _P, _I, _P, _P, _P, _P, _I, _P],
     "toued_gw_step": [EnvSpecC, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P],
     "toued_batch_reset": [EnvSpecC, _P, _P, _I, _I, _P, _P, _P, _P],
+    "toued_batch_reset_masked": [EnvSpecC, _P, _P, _I, _I, _P, _P, _P, _P, _P],
     "toued_rollout": [EnvSpecC, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "toued_meta_keys": [_P, _I, _I, _P, _P, _P, _P, _P],
     "toued_lpg_inputs": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _L, _L, _P],
@@ -54,6 +56,7 @@ _SIGS = {
                   _P, _P, _P, _P, _P],
     "toued_embed_bwd": [_I, _I, _I, _I, _I, _P, _L, _P, _L, _P, _P, _L, _P, _P, _L, _P, _P, _P, _P, _I, _P],
     "toued_init_tables": [_P, _I, _I, _I, _F, _F, _F, _P, _P],
+    "toued_init_tables_masked": [_P, _I, _I, _I, _F, _F, _F, _P, _P, _P],
     "toued_adam": [_I, _P, _P, _P, _P, _F, _F, _F, _F, _F, _I, _P],
     "toued_gru_pack": [_P, _P, _I, _P, _P, _P],
     "toued_gru_packed_floats": [_I],

@@ -64,6 +64,24 @@ def lecun_tables(keys: torch.Tensor, D: int, cols: int) -> torch.Tensor:
     return out
 
 
+def lecun_tables_into(keys: torch.Tensor, out: torch.Tensor, mask: torch.Tensor):
+    """``lecun_tables(keys, D, cols)`` written in place into ``out`` [n, D, cols] for the tables with
+    ``mask`` (u8 [n]) set; the others keep their values (the level sampler's where(terminated, new, old))."""
+    n, D, cols = out.shape
+    pkeys = prng.fold_in(prng.fold_in(keys.contiguous(), DENSE0_HASH), 1)
+    std = float(np.float32(np.sqrt(np.float32(1.0 / D))) / np.float32(0.87962566103423978))
+    _lib.call("toued_init_tables_masked", _lib.ptr(pkeys.contiguous()), n, cols, D, TN_LO, TN_HI, std, _lib.ptr(out),
+              _lib.ptr(mask), _lib.stream_ptr())
+    return out
+
+
+def create_agents_into(agent_keys: torch.Tensor, theta: torch.Tensor, phi: torch.Tensor, mask: torch.Tensor):
+    """``create_agents`` for the agents with ``mask`` set, in place into theta [n, D, 5] / phi [n, D, Y]."""
+    ks = prng.split(agent_keys, 2)
+    lecun_tables_into(ks[:, 0].contiguous(), theta, mask)
+    lecun_tables_into(ks[:, 1].contiguous(), phi, mask)
+
+
 def create_agents(agent_keys: torch.Tensor, D: int, Y: int):
     """create_agent (agents/agents.py:31-56) for each key: actor_rng, critic_rng = split(agent_rng)."""
     ks = prng.split(agent_keys, 2)

@@ -93,6 +93,12 @@ class LevelGenerator:
                   _lib.ptr(levels), _lib.ptr(sub), n, _lib.stream_ptr())
         return (levels, sub) if with_sub_mode else levels
 
+    def regenerate(self, keys: torch.Tensor, levels: torch.Tensor, mask: torch.Tensor):
+        """``levels[i] = self(keys)[i]`` in place for the i with ``mask[i]`` (u8) set (buffer_id 0)."""
+        _lib.call("toued_level_gen_masked", _lib.ptr(self.program), _lib.ptr(keys.contiguous()), None,
+                  _lib.ptr(levels), keys.shape[0], _lib.ptr(mask), _lib.stream_ptr())
+        return levels
+
 
 class GridWorld:
     """gymnax ``Environment`` API for GridWorld (gridworld.py:38-236), vectorised.

@@ -16,7 +16,8 @@ import numpy as np
 import torch
 
 from . import _lib, prng
-from .agents import AgentBatch, AgentHyperparams, create_agents, create_value_critics
+from .agents import (AgentBatch, AgentHyperparams, create_agents, create_agents_into, create_value_critics,
+                     lecun_tables_into)
 from .env import L_BUFID, L_LIFETIME, LevelGenerator, get_env_spec
 from .rollout import RolloutWrapper
 
@@ -158,33 +159,36 @@ class LevelSampler:
         return ks[0].contiguous(), ks[1].contiguous()
 
     def sample(self, rng, level_buffer, agents: AgentBatch, sl=None):
-        """level_sampler.py:134-266: new levels/agents for agents whose step >= lifetime."""
+        """level_sampler.py:134-266: new levels/agents for agents whose step >= lifetime.
+
+        The reference builds a full batch of new levels/agents/env states and keeps the terminated agents'
+        (``where(term, new, old)``); here the generators write the terminated agents' rows in place (same
+        keys, same values) and leave the others untouched."""
         n_total = agents.n if sl is None else sl[2]
         term = agents.step >= agents.levels[:, L_LIFETIME]
+        mask = term.to(torch.uint8)
         if self.score_function == "random":
             rng, sub = self._split2(rng)
-            new_levels = self._sample_random_levels(sub, n_total, sl)
-        elif self.score_function == "frozen":
-            rng, sub = self._split2(rng)
-            ids = self._frozen_ids(sub, n_total)
-            new_levels = self._slice(level_buffer.levels[ids.long()], sl)
+            self.gen.regenerate(self._slice(prng.split(sub, n_total), sl), agents.levels, mask)
         else:
-            from .plr import plr_sample
-            rng, level_buffer, new_levels = plr_sample(self, rng, level_buffer, agents, term, sl)
-        new_levels = torch.where(term[:, None], new_levels, agents.levels)
+            if self.score_function == "frozen":
+                rng, sub = self._split2(rng)
+                ids = self._frozen_ids(sub, n_total)
+                new_levels = self._slice(level_buffer.levels[ids.long()], sl)
+            else:
+                from .plr import plr_sample
+                rng, level_buffer, new_levels = plr_sample(self, rng, level_buffer, agents, term, sl)
+            agents.levels = torch.where(term[:, None], new_levels, agents.levels)
+        # vmap(_create_agent) (level_sampler.py:273-291): worker_rng, agent_rng = split(rng_i)
         rng, sub = self._split2(rng)
-        theta, phi, state = self._create_agents(sub, new_levels, n_total, sl, False)
-        W = self.env_workers
-        tw = term.repeat_interleave(W)
-        agents.levels = new_levels
-        agents.theta = torch.where(term[:, None, None], theta, agents.theta)
-        agents.phi = torch.where(term[:, None, None], phi, agents.phi)
+        ks = prng.split(self._slice(prng.split(sub, n_total), sl), 2)
+        self.rollout_manager.batch_reset_into(ks[:, 0].contiguous(), agents.levels, agents.state, mask)
+        create_agents_into(ks[:, 1].contiguous(), agents.theta, agents.phi, mask)
         agents.step = torch.where(term, torch.zeros_like(agents.step), agents.step)
-        agents.state = torch.where(tw[None, :], state, agents.state)
         if agents.vcrit is not None:
             rng, sub = self._split2(rng)
-            vc = create_value_critics(self._slice(prng.split(sub, n_total), sl), self.obs_dim)
-            agents.vcrit = torch.where(term[:, None], vc, agents.vcrit)
+            n = agents.vcrit.shape[0]
+            lecun_tables_into(self._slice(prng.split(sub, n_total), sl), agents.vcrit.view(n, self.obs_dim, 1), mask)
             agents.vstep = torch.where(term, torch.zeros_like(agents.vstep), agents.vstep)
         return level_buffer, agents
 

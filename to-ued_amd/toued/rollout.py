@@ -57,6 +57,19 @@ class RolloutWrapper:
                   _lib.ptr(state), _lib.ptr(idx), _lib.ptr(tm), _lib.stream_ptr())
         return (idx, tm), state
 
+    def batch_reset_into(self, agent_keys: torch.Tensor, levels: torch.Tensor, state: torch.Tensor,
+                         mask: torch.Tensor):
+        """``batch_reset`` in place into ``state`` [fields, N*W] for the agents with ``mask`` (u8 [N]) set."""
+        N = agent_keys.shape[0]
+        W = state.shape[1] // N
+        n = N * W
+        if getattr(self, "_obs_scratch", None) is None or self._obs_scratch.shape[1] < n:
+            self._obs_scratch = torch.empty((2, n), dtype=torch.int32, device=state.device)
+        _lib.call("toued_batch_reset_masked", self._c, _lib.ptr(levels), _lib.ptr(agent_keys.contiguous()), N, W,
+                  _lib.ptr(state), _lib.ptr(self._obs_scratch[0]), _lib.ptr(self._obs_scratch[1]), _lib.ptr(mask),
+                  _lib.stream_ptr())
+        return state
+
     def batch_rollout(self, agent_keys: torch.Tensor, theta: torch.Tensor, levels: torch.Tensor,
                       state: torch.Tensor, eval: bool = False, out: Transition | None = None,
                       inplace_state: bool = False):
