@@ -433,25 +433,30 @@ TOUED_DEV void split_carry(float h, f16x4& x0, f16x4& x1, bf16x4& r, int e) {
 // per-(gate, output unit) weight scale 2^s: s = 14 - e with max_k |W_g[k][u]| < 2^e (clamped to [-30, 20]), so
 // the scaled row's fp16 pieces stay below 2^14 and its small entries keep their relative precision; the ni gate
 // (no h part) uses s = 0.  One thread per (gate, unit) and candidate (blockIdx.y).
-__global__ void k_fwd6_scales(const float* __restrict__ eta, EtaOff o, float* __restrict__ out, long eta_stride,
-                              long out_stride) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 4 * HU) return;
+__global__ void __launch_bounds__(256) k_fwd6_scales(const float* __restrict__ eta, EtaOff o, float* __restrict__ out,
+                                                     long eta_stride, long out_stride) {
+  // block (gate, 64-unit group, candidate): thread = (unit, k quarter); coalesced over units
+  __shared__ float red[4][64];
+  const int g = blockIdx.x >> 2, u = 64 * (blockIdx.x & 3) + (threadIdx.x & 63), kq = threadIdx.x >> 6;
   eta += (long)blockIdx.y * eta_stride;
   out += (long)blockIdx.y * out_stride;
-  const int g = i / HU, u = i - g * HU;
-  int sc = 0;
+  float m = 0.0f;
   if (g < 3) {
     const int base = g == 0 ? o.hr_w : g == 1 ? o.hz_w : o.hn_w;
-    float m = 0.0f;
-    for (int k = 0; k < HU; ++k) m = fmaxf(m, fabsf(eta[base + k * HU + u]));
+    for (int k = 64 * kq; k < 64 * kq + 64; ++k) m = fmaxf(m, fabsf(eta[base + k * HU + u]));
+  }
+  red[kq][threadIdx.x & 63] = m;
+  __syncthreads();
+  if (kq == 0) {
+    m = fmaxf(fmaxf(red[0][threadIdx.x], red[1][threadIdx.x]), fmaxf(red[2][threadIdx.x], red[3][threadIdx.x]));
+    int sc = 0;
     if (m > 0.0f && m <= 3.0e38f) {
       int e;
       frexpf(m, &e);          // m < 2^e
       sc = min(20, max(-30, 14 - e));
     }
+    out[g * HU + u] = ldexpf(1.0f, sc);
   }
-  out[i] = ldexpf(1.0f, sc);
 }
 
 // one thread per (fragment group, lane): fragment group = (ks, ut, g) for the h part or (ut, g) for the
@@ -505,20 +510,25 @@ __global__ void k_pack_fwd6(const float* __restrict__ eta, EtaOff o, int F, bf16
 
 // per-input-unit scale 2^s of the backward's fp16 weight rows: s = 14 - e with
 // max_k max(|W_r[i][k]|, |W_z[i][k]|, |W_hn[i][k]|) < 2^e, clamped to [-30, 20] (the forward's k_fwd6_scales rule)
-__global__ void k_bwd6_scales(const float* __restrict__ eta, EtaOff o, float* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(256) k_bwd6_scales(const float* __restrict__ eta, EtaOff o, float* __restrict__ out) {
+  // one wave per input unit i: lane-strided contiguous reads of the three rows, wave max
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (i >= HU) return;
   float m = 0.0f;
-  for (int k = 0; k < HU; ++k)
+  for (int k = lane; k < HU; k += 64)
     m = fmaxf(m, fmaxf(fabsf(eta[o.hr_w + i * HU + k]),
                        fmaxf(fabsf(eta[o.hz_w + i * HU + k]), fabsf(eta[o.hn_w + i * HU + k]))));
-  int sc = 0;
-  if (m > 0.0f && m <= 3.0e38f) {
-    int e;
-    frexpf(m, &e);
-    sc = min(20, max(-30, 14 - e));
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) m = fmaxf(m, __shfl_xor(m, d));
+  if (lane == 0) {
+    int sc = 0;
+    if (m > 0.0f && m <= 3.0e38f) {
+      int e;
+      frexpf(m, &e);
+      sc = min(20, max(-30, 14 - e));
+    }
+    out[i] = ldexpf(1.0f, sc);
   }
-  out[i] = ldexpf(1.0f, sc);
 }
 
 // backward A fragments A[i = input unit 32 ut + (l & 31)][k = gate unit 16 ks + 8 (l >> 5) + e] = W_g[i][k] of
@@ -1322,12 +1332,12 @@ int toued_gru_pack(const float* eta, const int* off, int F, float* fwdA, float* 
   const int n1 = NTILE_F * KQF * 64, n2 = 8 * 3 * 32 * 64, n3 = (16 * 8 * 3 + 8 * 4) * 64;
   hipLaunchKernelGGL(k_pack_fwd, dim3((n1 + 255) / 256), dim3(256), 0, stream, eta, o, F,
                      reinterpret_cast<float4*>(fwdA), 0L, 0L);
-  hipLaunchKernelGGL(k_fwd6_scales, dim3(4), dim3(256), 0, stream, eta, o, fwdA + (size_t)n1 * 4 + F6_SCALES, 0L, 0L);
+  hipLaunchKernelGGL(k_fwd6_scales, dim3(16), dim3(256), 0, stream, eta, o, fwdA + (size_t)n1 * 4 + F6_SCALES, 0L, 0L);
   hipLaunchKernelGGL(k_pack_fwd6, dim3((n3 + 255) / 256), dim3(256), 0, stream, eta, o, F,
                      reinterpret_cast<bf16x8*>(fwdA + (size_t)n1 * 4), 0L, 0L);
   hipLaunchKernelGGL(k_pack_bwd, dim3((n2 + 255) / 256), dim3(256), 0, stream, eta, o,
                      reinterpret_cast<float4*>(bwdA));
-  hipLaunchKernelGGL(k_bwd6_scales, dim3(1), dim3(256), 0, stream, eta, o, bwdA + (size_t)n2 * 4 + B6_SCALES);
+  hipLaunchKernelGGL(k_bwd6_scales, dim3(HU / 4), dim3(256), 0, stream, eta, o, bwdA + (size_t)n2 * 4 + B6_SCALES);
   hipLaunchKernelGGL(k_pack_bwd6, dim3((16 * 8 * 3 * 64 + 255) / 256), dim3(256), 0, stream, eta, o,
                      reinterpret_cast<__bf16*>(bwdA + (size_t)n2 * 4));
   TOUED_CHECK_LAUNCH();
@@ -1400,7 +1410,7 @@ int toued_gru_pack_fwd_multi(const float* eta, long eta_stride, int n, const int
   hipLaunchKernelGGL(k_pack_fwd, dim3((n1 + 255) / 256, n), dim3(256), 0, stream, eta, o, F,
                      reinterpret_cast<float4*>(fwdA), eta_stride, cstride / 4);
   const int n3 = (16 * 8 * 3 + 8 * 4) * 64;
-  hipLaunchKernelGGL(k_fwd6_scales, dim3(4, n), dim3(256), 0, stream, eta, o, fwdA + (size_t)n1 * 4 + F6_SCALES,
+  hipLaunchKernelGGL(k_fwd6_scales, dim3(16, n), dim3(256), 0, stream, eta, o, fwdA + (size_t)n1 * 4 + F6_SCALES,
                      eta_stride, cstride);
   hipLaunchKernelGGL(k_pack_fwd6, dim3((n3 + 255) / 256, n), dim3(256), 0, stream, eta, o, F,
                      reinterpret_cast<bf16x8*>(fwdA + (size_t)n1 * 4), eta_stride, cstride / 4);
