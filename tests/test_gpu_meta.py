@@ -10,6 +10,8 @@ Tolerances (float32 GPU vs float64 oracle): parameters after K updates
 rtol 2e-4; LPG outputs 1e-4 abs; meta-gradient: relative L2 error < 2e-3 and
 cosine > 0.9999.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -268,3 +270,35 @@ def test_gru_backward_repeat_bit_identical():
         for a, b in zip(outs[0], rep):
             assert torch.isfinite(a).all()
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("extra", [[], ["--score_function", "alg_regret", "--env_mode", "all_shortlife"]])
+def test_train_main_writes_checkpoints(tmp_path, extra):
+    """train.py driver end to end (2 meta-steps) with --checkpoint_dir: the restored TrainState holds the
+    trainer's final LPG parameters and Adam state; buffer-based score functions also write buffer_<steps>."""
+    from toued import train
+    from toued.checkpoint import lpg_flat_from_tree, restore_checkpoint
+    from toued.lpg import LPGLayout
+    argv = ["--env_mode", "tabular", "--num_agents", "2", "--num_mini_batches", "1", "--train_steps", "2",
+            "--checkpoint_dir", str(tmp_path)] + extra
+    captured = {}
+    orig = train.save_final_checkpoints
+
+    def spy(ckpt_dir, tr, steps):
+        captured["eta"], captured["m"] = tr.eta.cpu().numpy().copy(), tr.adam.m.cpu().numpy().copy()
+        orig(ckpt_dir, tr, steps)
+    train.save_final_checkpoints = spy
+    try:
+        train.main(argv)
+    finally:
+        train.save_final_checkpoints = orig
+    r = restore_checkpoint(str(tmp_path))
+    lay = LPGLayout(5)
+    assert int(r["step"]) == 2 and int(r["opt_state"]["0"]["count"]) == 2
+    assert np.array_equal(lpg_flat_from_tree(r["params"], lay), captured["eta"])
+    assert np.array_equal(lpg_flat_from_tree(r["opt_state"]["0"]["mu"], lay), captured["m"])
+    files = sorted(os.listdir(tmp_path))
+    assert files == (["buffer_2", "checkpoint_2"] if extra else ["checkpoint_2"])
+    if extra:
+        b = restore_checkpoint(str(tmp_path), prefix="buffer_")
+        assert b["levels"].shape[1] == 64 and b["score"].dtype == np.float32

@@ -16,6 +16,7 @@ import json
 import sys
 import time
 
+import numpy as np
 import torch
 
 from . import prng
@@ -118,7 +119,29 @@ def main(cmd_args=None):
         history.append(m)
         if world.rank == 0:
             print(json.dumps({"step": i, "elapsed_s": round(time.time() - t0, 3), **m}), flush=True)
+    if args.checkpoint_dir and world.rank == 0:
+        save_final_checkpoints(args.checkpoint_dir, tr, steps)
     return history
+
+
+def save_final_checkpoints(ckpt_dir: str, tr: "Trainer", steps: int):
+    """log_results (experiments/logging.py:31-46) without wandb: the LPG train state as checkpoint_<steps>
+    and, for buffer-based score functions, the level buffer as buffer_checkpoint_<steps> (toued/checkpoint.py)."""
+    from .checkpoint import level_buffer_state_dict, lpg_params_tree, lpg_train_state_dict, save_checkpoint
+    from .lpg import LPGLayout
+    lay = LPGLayout(7 if tr.args.lifetime_conditioning else 5)
+    if tr.args.use_es:
+        # ESTrainState (meta/meta.py:29): the search mean as the LPG params, plus the OpenES state (this build's
+        # field names; the evosax state pytree is not reproduced)
+        es = tr.step_fn.es
+        target = {"step": np.asarray(steps, np.int32), "params": lpg_params_tree(es.mean, lay),
+                  "es_state": {"mean": es.mean, "m": es.m, "v": es.v, "lrate": np.float32(es.lrate),
+                               "sigma": np.float32(es.sigma), "gen_counter": np.asarray(es.gen_counter, np.int32)}}
+    else:
+        target = lpg_train_state_dict(tr.eta, lay, steps, tr.adam)
+    save_checkpoint(ckpt_dir, target, steps)
+    if tr.buffer is not None:
+        save_checkpoint(ckpt_dir, level_buffer_state_dict(tr.buffer), steps, prefix="buffer_")
 
 
 if __name__ == "__main__":
