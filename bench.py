@@ -37,9 +37,9 @@ MFMA_F32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: dense f32 MFMA (v_mfma
 MFMA_BF16_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: dense bf16 MFMA
 HBM_PEAK_GBS = 8000.0
 # 16-bit MFMA products issued per f32 product (csrc/gru.hip): forward = 16 carry k-steps on scaled fp16 pairs
-# (3 products) + 1 input k-step on the exact bf16 triple split (6); backward = the r pass on bf16 triples (6) +
-# the z and hn passes on scaled fp16 pairs (3 each)
-SPLIT_PRODUCTS = {"gru_fwd": (16 * 3 + 6) / 17, "gru_bwd": (6 + 3 + 3) / 3}
+# (3 products) + 1 input k-step on the exact bf16 triple split (6); backward = the r, z and hn passes on scaled
+# fp16 pairs (3 each)
+SPLIT_PRODUCTS = {"gru_fwd": (16 * 3 + 6) / 17, "gru_bwd": 3.0}
 GRU_FWD_FLOP_PER_ELEM = {5: 406080, 7: 409152}    # per (agent, worker, t)
 GRU_BWD_FLOP_PER_ELEM = 2 * 256 * 768              # dh_prev = dG . W_h^T per (k, agent, worker, t)
 # algorithmic HBM bytes per element: forward saves h_in, r, z, n, W_hn h + b_hn (5 x 256 f32) and
@@ -198,9 +198,9 @@ def main():
         "value": round(value, 1), "unit": "agent-env-steps/sec", "n_gpus": n_gpus, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "mfma_precision": "f32-class: GRU carry products (forward, backward z/hn passes) on power-of-two-scaled fp16 "
-                          "pairs (3 fp16 MFMA products, pieces to 2^-22 relative), all other products on the exact "
-                          "3-piece bf16 split (6 products); f32 accumulate",
+        "mfma_precision": "f32-class: GRU recurrent products (forward carry, backward gate passes) on power-of-two-"
+                          "scaled fp16 pairs (3 fp16 MFMA products, pieces to 2^-22 relative), the input k-step and the "
+                          "weight-gradient reduction on the exact 3-piece bf16 split (6 products); f32 accumulate",
         "data": "synthetic (procedurally generated levels)",
         "meta_updates_per_sec": round(a.steps / dt, 3),
         "config": {"workload": f"C2 LPG meta-gradient env_mode={a.env_mode} num_agents={N_total} "
