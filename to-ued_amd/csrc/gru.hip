@@ -1201,10 +1201,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         dx4 += drp * wil[3 * HU + qu] + dzp * wil[4 * HU + qu] + dnp * wil[5 * HU + qu];
         const unsigned so1 = (unsigned)(((long)qu * p.M + ctr) * 4);
         st_u(rs_rh, vbo, so1, fmaxf(hout, 0.0f));
-        st_u(rs_dg[0], vbo, so1, drp);
-        st_u(rs_dg[1], vbo, so1, dzp);
-        st_u(rs_dg[2], vbo, so1, dhn);
-        st_u(rs_dg[3], vbo, so1, dnp);
+        st_u(rs_dg[3], vbo, so1, dnp);   // dr, dz, dhn leave during the contraction phase (HBM idle there)
       }
       *reinterpret_cast<float4*>(&drs[row * DRP + ub + 8 * g4]) = make_float4(drq[0], drq[1], drq[2], drq[3]);
 #pragma unroll
@@ -1242,6 +1239,14 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       }
       bs[h] = ldexpf(1.0f, sc);
     }
+    // a lane's four units ub + 8 g4 .. +3 of batch row `row` of gate cotangent g to DG (lane = row: 128-byte
+    // segments), issued beside the contraction's MFMAs where the memory pipe is otherwise idle
+    auto store_dg = [&](int g, int row, int g4, const float (&v)[4]) {
+      const unsigned vb = (unsigned)(((long)ub * p.M + r0 + row) * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        st_u(rs_dg[g], vb, (unsigned)(((long)qunit(4 * g4 + e) * p.M + ctr) * 4), v[e]);
+    };
     // dr -> fp16 pieces: x0 straight into slot 0, x1 held until every lane has read its staged f32 values
     // (slot 1 overlaps the staging)
     f16x4 x1h[2][4];
@@ -1256,6 +1261,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) split2h(v4[e] * bs[h], x0, x1h[h][g4], e);
         *reinterpret_cast<f16x4*>(&dgB[0][row * PP + ub + 8 * g4]) = x0;
+        store_dg(0, row, g4, v4);
       }
     __syncthreads();
 #pragma unroll
@@ -1277,6 +1283,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       for (int g4 = 0; g4 < 4; ++g4) {
         const float v4[4] = {dz_r[h][4 * g4], dz_r[h][4 * g4 + 1], dz_r[h][4 * g4 + 2], dz_r[h][4 * g4 + 3]};
         put4h(RB * h + col, ub + 8 * g4, v4, bs[h]);
+        store_dg(1, RB * h + col, g4, v4);
       }
     __syncthreads();
     contract_h(1);
@@ -1287,6 +1294,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       for (int g4 = 0; g4 < 4; ++g4) {
         const float v4[4] = {dhn_r[h][4 * g4], dhn_r[h][4 * g4 + 1], dhn_r[h][4 * g4 + 2], dhn_r[h][4 * g4 + 3]};
         put4h(RB * h + col, ub + 8 * g4, v4, bs[h]);
+        store_dg(2, RB * h + col, g4, v4);
       }
     __syncthreads();
     contract_h(2);
