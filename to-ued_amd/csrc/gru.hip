@@ -4,22 +4,18 @@
 // [rows x 272] x [272 x 1024] contraction (h: 256 recurrent units, + x features and a bias row; columns
 // r | z | W_hn h + b_hn | W_in x + b_in) and the VJP a [rows x 768] x [768 x 256] one.
 //
-// Arithmetic: f32-accurate products on the bf16 matrix cores.  Each f32 operand is split exactly into three
-// bf16 pieces (x = x0 + x1 + x2, round-to-nearest at each stage) and a.b is formed from the six piece
-// products of weight >= 2^-16 (a0b0, a0b1, a1b0, a0b2, a1b1, a2b0) on v_mfma_f32_32x32x16_bf16 with f32
-// accumulation; the dropped products are below 2^-24 relative, so results carry f32-GEMM error
-// (tools/gru_accuracy.py, tests/test_gpu_meta.py) at 6 x 32 = 192 MFMA cycles per 32x32x16 block against
-// 512 for v_mfma_f32_32x32x2_f32.  The weights are split once per eta by the pack kernels.
+// Arithmetic: f32-class products on the 16-bit matrix cores, f32 accumulation:
+//   * recurrent products (forward carry k-steps, the three backward gate passes): power-of-two-scaled fp16
+//     pairs (y = 2^s x, x0 = fp16(y), x1 = fp16(y - x0)), a0b0 + a0b1 + a1b0 on v_mfma_f32_32x32x16_f16 --
+//     weight rows scaled per unit (k_fwd6_scales / k_bwd6_scales), the carry by 2^14 (|h| < 1), backward
+//     cotangent rows by a per-batch-row 2^t from an LDS row-max exchange; every scale is exact;
+//   * the forward's input k-step [x; 1]: exact three-piece bf16 split, six products of weight >= 2^-16.
+// Accuracy vs float64 equals the all-bf16-triple kernels' (tools/gru_accuracy.py, tests/test_gpu_meta.py).
 //
-// Forward (k_gru_fwd6): one 512-thread workgroup per 64 rows (two 32-row tiles) for the whole reverse scan;
-// wave w owns units [32w, 32w + 32).  The carry h lives in LDS as three bf16 images [row][unit]; weight
-// fragments stream from L2 one k-step ahead and feed both row tiles; gate maths in the accumulator layout
-// (lane = row, register = unit), h_in rebuilt exactly from its pieces.  Saves h_in, r, z, n, W_hn h + b_hn
-// row-major [unit][M] (the weight-gradient layout) for the backward.
-//
-// Backward (k_gru_bwd6n): one 512-thread workgroup per (k, 64 rows), t ascending, all waves in lockstep:
-// a memory part (16-byte saved-activation loads + DPP quad transposes, gate maths, cotangent stores) and a
-// contraction dh_prev = sum_g W_g . dg_g with the cotangents as bf16-piece B fragments from one LDS image.
+// Forward (k_gru_fwd6): one 512-thread workgroup per 64 rows for the whole reverse scan; the carry lives in
+// LDS as two fp16 pieces of 2^14 h + a bf16 residual that keeps h_in exact.  Backward (k_gru_bwd6n): one
+// 512-thread workgroup per (k, 64 rows), t ascending, lockstep memory part then contraction through one LDS
+// cotangent image; dr, dz, dhn are stored to HBM beside the contraction's MFMAs.
 //
 // f32 fallbacks (v_mfma_f32_32x32x2_f32, one 32-row tile per workgroup): k_gru_fwd<SAVE, NT> (also the
 // per-candidate ES forward) and k_gru_bwd<1> for row counts that do not split into 64-row blocks, and every
@@ -367,24 +363,17 @@ __global__ void __launch_bounds__(512, NT == 1 ? 4 : 1) k_gru_fwd(FwdArgs p) {
   }
 }
 
-// ------------------------------------------------------------------ forward on the bf16 matrix cores
-// f32-accurate split products (as csrc/wgrad.hip): every f32 operand is split exactly into three bf16 pieces
-// x = x0 + x1 + x2, and a.b is formed from the six piece products of weight >= 2^-16 of a0.b0 (a0b0, a0b1,
-// a1b0, a0b2, a1b1, a2b0) on v_mfma_f32_32x32x16_bf16 with f32 accumulation: the three dropped products are
-// below 2^-24 relative, so the pre-activations carry f32 GEMM error at 6 x 32 = 192 cycles per 32x32x16
-// block instead of the f32 MFMA's 512.
-//
-// One 256-thread workgroup (one wave per SIMD, 512 registers) owns 64 rows (two 32-row tiles) for the whole
-// T-step scan; wave w owns units [64w, 64w + 64) (two 32-unit tiles j), so its accumulators are
-// {r, z, W_hn h + b_hn, W_in x + b_in} x 2 unit tiles x 2 row tiles (256 AGPRs).  Per step:
-//   contraction over k = 256 h units (16 k-steps of 16) + one augmented k-step [x (F <= 7); 1; 0...]:
-//     A fragments (weights, pre-split and packed by k_pack_fwd6, 16 B per lane and piece) stream from L2 one
-//     k-step ahead; B fragments (the carry h, three bf16 images [row][unit] in LDS, 528-byte rows: the 16
-//     lanes of a read hit 16 distinct bank quads) are read one k-step ahead; each A fragment feeds both row
-//     tiles;
-//   barrier; gate maths in the accumulator layout (lane = row, register = unit); h_in rebuilt exactly from
-//   its pieces ((h0 + h1) + h2 == h); the new carry split and written back in place (each (row, unit) has
-//   one owner lane); saves r, z, n, W_hn h + b_hn, h_in for the backward; head partials;
+// ------------------------------------------------------------------ forward on the 16-bit matrix cores
+// k_gru_fwd6: one 512-thread workgroup owns 64 rows (two 32-row tiles) for the whole T-step scan; wave w owns
+// units [32w, 32w + 32), so its accumulators are {r, z, W_hn h + b_hn, W_in x + b_in} x 2 row tiles.  Per step:
+//   contraction over k = 256 h units (16 k-steps of 16, fp16 pairs) + one augmented k-step [x (F <= 7); 1; 0...]
+//     (bf16 triples): A fragments (weights scaled, split and packed by k_pack_fwd6, 16 B per lane and piece)
+//     stream from L2 one k-step ahead; B fragments (fp16 pieces of 2^14 h in LDS [row][unit], 528-byte rows:
+//     the 16 lanes of a read hit 16 distinct bank quads) are read one k-step ahead; each A fragment feeds both
+//     row tiles;
+//   barrier; exact power-of-two unscale; gate maths in the accumulator layout (lane = row, register = unit);
+//   h_in rebuilt exactly ((x0 + x1) + r == 2^14 h); the new carry split and written back in place (each
+//   (row, unit) has one owner lane); saves r, z, n, W_hn h + b_hn, h_in for the backward; head partials;
 //   barrier; head reduce + softmax.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
