@@ -4,6 +4,10 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
         bench.py --gpus N --steps K --warmup W
 
+With --gpus N > 1 and no torchrun environment (WORLD_SIZE unset) the parent starts the N ranks itself
+(torch.distributed.run as a child process, before any GPU call in the parent) and exits with their status;
+under torchrun WORLD_SIZE must equal --gpus.  Asking for more GPUs than the node has fails loudly.
+
 Workload (C2): env_mode=tabular (the build's defined manual dispatch over the five
 LPG tabular levels), num_agents=512 per GPU (weak scaling: 512*N agents
 in total), num_mini_batches=1, W=64 workers, T=20, K=5 inner LPG updates,
@@ -77,7 +81,57 @@ def parse():
     ap.add_argument("--lifetime_conditioning", action="store_true")
     ap.add_argument("--no_cpu_baseline", action="store_true")
     ap.add_argument("--cpu_agents", type=int, default=0, help="agents in the CPU sample (0 = auto-size to ~15 s)")
+    ap.add_argument("--launcher_selftest", action="store_true",
+                    help="test hook: run the multi-rank launch, barrier and max-over-ranks timing on gloo/CPU with "
+                         "no GPU work, and print the JSON skeleton (tests/test_bench_launch.py)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(a) -> int:
+    """Start --gpus ranks of this script under torch.distributed.run (one process per GPU) and return their exit
+    status.  Runs before anything in this process touches the GPU (device_count() does not initialise HIP)."""
+    import subprocess
+    if not a.launcher_selftest:
+        have = torch.cuda.device_count()
+        if have < a.gpus:
+            raise SystemExit(f"bench.py: --gpus {a.gpus} requested but this node has {have} GPU(s)")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve()), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if a.launcher_selftest:
+        env["TOUED_DIST_BACKEND"] = "gloo"
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launcher_selftest(a):
+    """Multi-rank plumbing without GPU work: world init, barrier-bracketed timing, MAX over ranks, one line."""
+    from toued.dist import init_from_env
+    world = init_from_env("gloo")
+    world.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (world.rank + 1))
+    world.barrier()
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world.active:
+        import torch.distributed as dist
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    if world.rank == 0:
+        print(json.dumps({"metric": "launcher_selftest", "n_gpus": world.size, "ranks_seen": world.size,
+                          "max_dt": float(dt)}), flush=True)
+    if world.active:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def cpu_baseline(env_mode: str, lifetime_conditioning: bool, n_agents: int = 0):
@@ -130,6 +184,13 @@ def cpu_baseline(env_mode: str, lifetime_conditioning: bool, n_agents: int = 0):
 
 def main():
     a = parse()
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
+    if ws != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={ws}")
+    if a.launcher_selftest:
+        return launcher_selftest(a)
     from toued.dist import init_from_env
     from toued.parse_args import parse_args
     from toued.train import Trainer
