@@ -129,15 +129,15 @@ int toued_key_chain(const uint32_t* keys, int n, int U, uint32_t* out, hipStream
 int toued_a2c_grad(int N, int W, int T, int D, const float* theta, const float* vcrit, const int* tidx,
                    const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone, float gamma,
                    float lam, float ent_coef, float* Ga, float* Gv, float* loss_out, hipStream_t stream);
-/* apply_gradients (clip_by_global_norm + SGD, models/optim.py:5-11) for actor and value critic,
- * kept only while step+1 <= levels[i].lifetime (a2c.py:71-75); zeroes Ga/Gv. */
-/* fused A2C update (toued_a2c_grad + toued_a2c_apply with the gradient tables in LDS), for sizes where
- * toued_a2c_update_fits(W, T, D) is 1 (D*6 floats plus the agent's staged trajectory fit the LDS) */
+/* fused, deterministic A2C update (grad + clip + SGD in one block per agent; rows summed in sample order after
+ * an LDS sort by (row, sample), no atomics) for sizes where toued_a2c_update_fits(W, T, D) is 1 (W*T <= 2048) */
 int toued_a2c_update_fits(int W, int T, int D);
 int toued_a2c_update(int N, int W, int T, int D, float* theta, float* vcrit, const int* tidx, const int* ttime,
                      const uint8_t* tact, const float* trew, const uint8_t* tdone, float gamma, float lam,
                      float ent_coef, float lr_a, float lr_c, float max_norm, int* step, const int* levels,
                      float* loss_out, hipStream_t stream);
+/* apply_gradients (clip_by_global_norm + SGD, models/optim.py:5-11) for actor and value critic,
+ * kept only while step+1 <= levels[i].lifetime (a2c.py:71-75); zeroes Ga/Gv. */
 int toued_a2c_apply(int N, int D, float* theta, float* vcrit, float* Ga, float* Gv, float lr_a, float lr_c,
                     float max_norm, int* step, const int* levels, hipStream_t stream);
 
@@ -190,8 +190,10 @@ int toued_embed_bwd(int N, int W, int T, int D, int K, const float* phi_hist, lo
                     long tidx_stride, const int* ttime_hist, const uint8_t* tdone_hist, long tstep_stride,
                     const float* dX3, const float* dX4, long dx_stride_k, const float* e1w, const float* e1b,
                     const float* e2w, float* partial, int n_blocks, hipStream_t stream);
-/* optax adam (b1, b2, eps, bias-corrected) + scale(lr) + scale(-1) on the flat eta (meta/meta.py) */
-int toued_adam(int P, float* eta, const float* grad, float* m, float* v, float scale, float lr, float b1, float b2,
+/* optax 0.1.5 chain(scale_by_adam(b1, b2, eps), scale(lr), scale(-1)) on the flat eta (models/optim.py:12-17),
+   applied to grad / n_mean (the agent mean, meta/train.py:128).  b1, b2 are the python floats (double) so that
+   (1 - b) rounds to f32 once, as jax's weak-typed constants do; count is the post-increment step (>= 1). */
+int toued_adam(int P, float* eta, const float* grad, float* m, float* v, float n_mean, float lr, double b1, double b2,
                float eps, int count, hipStream_t stream);
 
 /* ---- LPG reverse-time GRU on MFMA (models/lpg.py:11-35, flax GRUCell) ---- */

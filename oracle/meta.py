@@ -167,6 +167,43 @@ def meta_gradient(eta_np, agents, hyp: Hypers, K: int, dtype=torch.float64):
     return np.mean(grads, axis=0), auxs, grads
 
 
+_LIBM = None
+
+
+def _powf(b, e) -> np.float32:
+    global _LIBM
+    if _LIBM is None:
+        import ctypes
+        import ctypes.util
+        _LIBM = ctypes.CDLL(ctypes.util.find_library("m") or "libm.so.6")
+        _LIBM.powf.restype = ctypes.c_float
+        _LIBM.powf.argtypes = [ctypes.c_float, ctypes.c_float]
+    return np.float32(_LIBM.powf(float(b), float(e)))
+
+
+def adam_f32(eta, grad_sum, n_mean, m, v, count, lr=1e-4, b1=0.9, b2=0.999, eps=1e-8):
+    """optax 0.1.5 chain(scale_by_adam(), scale(lr), scale(-1.0)) (models/optim.py:12-17) on the agent-mean
+    gradient (meta/train.py:128 ``x.mean(axis=0)`` = sum / N), in the float32 operation order jax traces:
+      update_moment:           (1 - b1) * g + b1 * mu          (python-float constants, weak-typed -> f32 once)
+      update_moment_per_elem_norm: (1 - b2) * g**2 + b2 * nu
+      bias_correction:         t / (1 - b**count)              (count = the incremented int32 step)
+      updates = mu_hat / (sqrt(nu_hat + eps_root=0) + eps); * lr; * -1; params + updates.
+    ``b**count`` is libm powf (what XLA-CPU calls for an f32 pow; unpinned against XLA itself).
+    Returns (eta', m', v', count') as float32 arrays."""
+    F = np.float32
+    g = (np.asarray(grad_sum, F) / F(n_mean)).astype(F)
+    count = int(count) + 1
+    m = (F(1.0 - b1) * g + F(b1) * np.asarray(m, F)).astype(F)
+    v = (F(1.0 - b2) * (g * g) + F(b2) * np.asarray(v, F)).astype(F)
+    # f32 pow: XLA-CPU lowers lax.pow on f32 to the llvm.pow intrinsic, i.e. a call to the C library's powf;
+    # numpy's float32 power and a rounded double power both differ from glibc powf in the last bit at some counts
+    bc1 = F(F(1.0) - _powf(F(b1), count))
+    bc2 = F(F(1.0) - _powf(F(b2), count))
+    upd = ((m / bc1) / (np.sqrt(v / bc2) + F(eps))).astype(F)
+    eta = (np.asarray(eta, F) + (upd * F(lr)) * F(-1.0)).astype(F)
+    return eta, m, v, count
+
+
 def adam_update(eta, grad, m, v, count, lr=1e-4, b1=0.9, b2=0.999, eps=1e-8):
     """optax scale_by_adam + scale(lr) + scale(-1) (models/optim.py:12-17)."""
     m = b1 * m + (1 - b1) * grad

@@ -2,13 +2,18 @@
 
 The HIP step runs K inner LPG updates (fused rollout, MFMA GRU, clipped SGD), the
 eval rollout and the explicit-adjoint meta-gradient.  The oracle replays the
-same trajectories (each one re-generated bit-exactly by the numpy rollout from
-the GPU's theta_k) and differentiates with autograd (create_graph through the
-clipped SGD steps, stop_gradient on the LPG inputs as in lpg_agent.py:170-172).
+same trajectories — every one of the K train rollouts and the eval rollout is
+re-generated bit-exactly by the numpy rollout from the GPU's theta_k, the
+oracle's own key chain (meta/train.py:41,47; lpg_agent.py:107) and the env state
+carried from the previous rollout — and differentiates with autograd
+(create_graph through the clipped SGD steps, stop_gradient on the LPG inputs as
+in agents/lpg_agent.py:47-56).
 
-Tolerances (float32 GPU vs float64 oracle): parameters after K updates
-rtol 2e-4; LPG outputs 1e-4 abs; meta-gradient: relative L2 error < 2e-3 and
-cosine > 0.9999.
+Tolerances (float32 GPU vs float64 oracle), set a few times above the achieved
+error so that a lost split-precision piece (~2^-11 relative) fails them: agent
+parameters after K updates rtol/atol 2e-5; metrics rtol 2e-5; meta-gradient
+relative L2 error < 1e-5; GRU forward outputs and saves 5e-6 abs; GRU backward
+gradients 1e-5 relative L2.
 """
 import os
 
@@ -54,7 +59,7 @@ def _setup(mode, N, W, T, K, lifetime_conditioning=False, seed=0):
     return agents, step, eta, adam, hyp, D
 
 
-@pytest.mark.parametrize("mode,lc", [("dense", False), ("tabular", True)])
+@pytest.mark.parametrize("mode,lc", [("dense", False), ("tabular", True), ("mazes", False), ("all_vrandlife", True)])
 def test_meta_step_matches_oracle(mode, lc):
     N, W, T, K = 3, 64, 20, 3
     agents, step, eta, adam, hyp, D = _setup(mode, N, W, T, K, lc)
@@ -75,19 +80,27 @@ def test_meta_step_matches_oracle(mode, lc):
     rew = tr.reward.cpu().numpy()
     dn = tr.done.cpu().numpy()
     th_h = step.theta_h.cpu().numpy()
-    # ---- trajectories: bit-exact vs the numpy rollout driven by the GPU's theta_k
+    # ---- trajectories: every rollout k = 0..K bit-exact vs the numpy rollout driven by the GPU's theta_k
     spec = olv.env_spec(mode)
     keys = jr.split(jr.PRNGKey(0), N)
     p, lt = olv.reset_env_params(keys, mode)
     from test_gpu_env import _state_np
     ost = _state_np(torch.from_numpy(state0), spec)
-    # meta/train.py keys: rng_a = split(rng, N)[a]; (r0, t) = split(rng_a); (t, roll_0) = split(t)
+    # meta/train.py:41 (r0, t) = split(rng_a); lpg_agent.py:107 (t, roll_k) = split(t) per update k;
+    # meta/train.py:47 (r0, roll_eval) = split(r0)
     ka = jr.split(np.array([0, 77], np.uint32), N)
-    roll0 = jr.split(jr.split(ka, 2)[:, 1], 2)[:, 1]
-    otr, _, _ = oro.batch_rollout(spec, roll0, th_h[0], p, ost, T)
-    np.testing.assert_array_equal(idx[0], otr["idx"].transpose(0, 2, 1))
-    np.testing.assert_array_equal(act[0], otr["action"].transpose(0, 2, 1))
-    np.testing.assert_array_equal(rew[0], otr["reward"].transpose(0, 2, 1))
+    r0t = jr.split(ka, 2)
+    r0, tk = r0t[:, 0], r0t[:, 1]
+    for k in range(K + 1):
+        if k < K:
+            s2 = jr.split(tk, 2)
+            tk, rk = s2[:, 0], s2[:, 1]
+        else:
+            rk = jr.split(r0, 2)[:, 1]
+        otr, ost, _ = oro.batch_rollout(spec, rk, th_h[k], p, ost, T)
+        for name, got in (("idx", idx), ("time", tm), ("action", act), ("reward", rew), ("done", dn)):
+            np.testing.assert_array_equal(got[k], otr[name].transpose(0, 2, 1).astype(got.dtype),
+                                          err_msg=f"rollout {k} {name}")
     # ---- oracle meta-gradient on the same trajectories
     def tr_of(k, a):
         return {"idx": idx[k, a].T.copy(), "time": tm[k, a].T.copy(), "action": act[k, a].T.astype(np.int64),
@@ -100,16 +113,17 @@ def test_meta_step_matches_oracle(mode, lc):
     g_ref, aux, _ = ometa.meta_gradient(eta0.cpu().numpy().astype(np.float64), agents_o, ohyp, K)
     # parameters after K updates
     for a in range(N):
-        np.testing.assert_allclose(agents.theta[a].cpu().numpy(), aux[a]["theta"], rtol=2e-4, atol=2e-4)
-        np.testing.assert_allclose(agents.phi[a].cpu().numpy(), aux[a]["phi"], rtol=2e-4, atol=2e-4)
+        np.testing.assert_allclose(agents.theta[a].cpu().numpy(), aux[a]["theta"], rtol=2e-5, atol=2e-5)
+        np.testing.assert_allclose(agents.phi[a].cpu().numpy(), aux[a]["phi"], rtol=2e-5, atol=2e-5)
     lpg_ref = np.array([x["lpg_loss"] for x in aux])
-    np.testing.assert_allclose(metrics["lpg_loss"].cpu().numpy(), lpg_ref, rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(metrics["lpg_loss"].cpu().numpy(), lpg_ref, rtol=2e-5, atol=1e-7)
     for key in ("policy_entropy", "critic_entropy", "policy_l2", "critic_l2", "critic_loss"):
         ref = np.array([x["lpg_agent"][key] for x in aux])
-        np.testing.assert_allclose(metrics["lpg_agent"][key].cpu().numpy(), ref, rtol=1e-3, atol=1e-6, err_msg=key)
+        np.testing.assert_allclose(metrics["lpg_agent"][key].cpu().numpy(), ref, rtol=2e-5, atol=1e-7, err_msg=key)
     err = np.linalg.norm(g_gpu - g_ref) / np.linalg.norm(g_ref)
     cos = float(g_gpu @ g_ref / (np.linalg.norm(g_gpu) * np.linalg.norm(g_ref)))
-    assert err < 2e-3 and cos > 0.9999, (err, cos)
+    print(f"meta-gradient rel L2 {err:.2e}, cosine {cos:.9f}")
+    assert err < 1e-5 and cos > 1 - 1e-9, (err, cos)
 
 
 def test_gru_forward_matches_oracle():
@@ -150,15 +164,15 @@ def test_gru_forward_matches_oracle():
     hs = torch.relu(torch.stack(outs, 1))
     pi_ref = (hs @ P["pi_w"] + P["pi_b"])[..., 0]
     y_ref = torch.softmax(hs @ P["y_w"] + P["y_b"], -1)
-    np.testing.assert_allclose(pi_hat[0].cpu().numpy().T, pi_ref.numpy(), atol=1e-4, rtol=1e-4)
-    np.testing.assert_allclose(y_hat[0].cpu().numpy().transpose(2, 0, 1), y_ref.numpy(), atol=1e-5, rtol=1e-4)
+    np.testing.assert_allclose(pi_hat[0].cpu().numpy().T, pi_ref.numpy(), atol=5e-6, rtol=0)
+    np.testing.assert_allclose(y_hat[0].cpu().numpy().transpose(2, 0, 1), y_ref.numpy(), atol=5e-6, rtol=0)
     # the saves the backward reads: [unit][column t*R + r]
     def tr(a):
         return a.reshape(256, T, R).transpose(1, 2, 0)
     for name, arr in (("hin", tr(gru.A[:256].cpu().numpy())), ("r", tr(gru.S[0].cpu().numpy())),
                       ("z", tr(gru.S[1].cpu().numpy())), ("n", tr(gru.S[2].cpu().numpy()))):
         ref = np.stack([saved[name][t].numpy() for t in range(T)])
-        np.testing.assert_allclose(arr, ref, atol=1e-4, rtol=1e-4, err_msg=name)
+        np.testing.assert_allclose(arr, ref, atol=5e-6, rtol=0, err_msg=name)
 
 
 @pytest.mark.parametrize("N,W,gscale,wscale", [(2, 64, 1.0, 1.0), (3, 32, 1.0, 1.0), (2, 64, 1e12, 1.0),
@@ -166,7 +180,7 @@ def test_gru_forward_matches_oracle():
 def test_gru_backward_matches_autograd(N, W, gscale, wscale):
     """LPG GRU VJP (toued_gru_bwd + the weight-gradient GEMMs over the saved m-major operands) vs float64
     torch autograd of the same GRU + heads: every GRU / head parameter gradient and the input cotangents
-    dX3, dX4 within 1e-4 relative L2.  R = 128 runs the lockstep split-precision kernel, R = 96 (not a
+    dX3, dX4 within 1e-5 relative L2 (achieved 1e-7..2e-6; one dropped fp16 piece costs ~5e-4).  R = 128 runs the lockstep split-precision kernel, R = 96 (not a
     multiple of 64) the f32 kernel.  gscale multiplies the head cotangents (the backward's per-row fp16
     scales must follow them over 24 decades), wscale the recurrent weights W_hr, W_hz, W_hn (the per-unit
     weight scales of the forward and backward packs).  (At wscale 16 the gates saturate and the f32-MFMA kernel
@@ -234,7 +248,8 @@ def test_gru_backward_matches_autograd(N, W, gscale, wscale):
         got = dX.cpu().numpy()
         errs[f"dX{f}"] = np.linalg.norm(got - gx[f]) / np.linalg.norm(gx[f])
     print("gru backward relative L2 errors:", {k: f"{v:.2e}" for k, v in errs.items()})
-    bad = {k: v for k, v in errs.items() if not v < 1e-4}
+    tol = 1e-5 if R % 64 == 0 else 1e-4     # the f32-MFMA fallback (R % 64 != 0) keeps the f32 bound
+    bad = {k: v for k, v in errs.items() if not v < tol}
     assert not bad, errs
 
 

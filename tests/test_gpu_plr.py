@@ -6,6 +6,9 @@
     relative L2 error of the parameter change < 1e-4
   * key plumbing of _compute_algorithmic_regret with max_lifetime=0 (untrained antagonist):
     regret within 1e-5 of the oracle (float32 mean over workers vs float64)
+  * regret with TRAINED antagonists (all_shortlife / mazes, 3-4 A2C updates, fused and unfused): each
+    update's rollout bit-exact and parameter change within 2e-5 of float64 autograd, regret within 1e-5;
+    and at full C3 size (N=512, 250 updates) batch-invariance plus the oracle eval of 4 agents
   * buffer logic (level_sampler.py:169-234, 331-408): reset ids, replay ids (rank and
     proportional), random ids, replay/random selection — bit-exact vs oracle/sampler.py
   * LevelSampler.sample end to end (alg_regret): buffer flags and chosen levels bit-exact vs the
@@ -169,6 +172,140 @@ def test_regret_untrained_matches_oracle(mode):
     r_lpg = oag.eval_agent(spec, ev[:, 0], p, lpg_theta.cpu().numpy(), 64, L)
     r_a2c = oag.eval_agent(spec, ev[:, 1], p, a2c_theta, 64, L)
     np.testing.assert_allclose(got, r_a2c - r_lpg, atol=1e-5, rtol=0)
+
+
+def _a2c_follow(spec, p, lt, rec, keys_tr, ost, tol=2e-5):
+    """Replays a recorded A2C chain (A2CTrainer.record) on the oracle: every update's rollout bit-exact from
+    the device's starting tables and the oracle's own key chain (a2c.py:97 rng, _rng = split(rng)) and carried
+    env state; every update's parameter change within `tol` relative L2 of the float64 autograd oracle
+    (oracle/a2c.py) applied to the same starting tables.  Returns the oracle end state."""
+    hyp = ometa.Hypers()
+    tr = keys_tr
+    for u, r in enumerate(rec):
+        s2 = jr.split(tr, 2)
+        tr, sub = s2[:, 0], s2[:, 1]
+        th0 = r["theta"].cpu().numpy()
+        otr, ost, _ = oro.batch_rollout(spec, sub, th0, p, ost, 20)
+        b = r["traj"]
+        idx, tm, act = b.obs_idx.cpu().numpy(), b.obs_time.cpu().numpy(), b.action.cpu().numpy()
+        rew, dn = b.reward.cpu().numpy(), b.done.cpu().numpy()
+        for name, got in (("idx", idx), ("time", tm), ("action", act), ("reward", rew), ("done", dn)):
+            np.testing.assert_array_equal(got, otr[name].transpose(0, 2, 1).astype(got.dtype),
+                                          err_msg=f"update {u} {name}")
+        vc0, st0 = r["vcrit"].cpu().numpy(), r["step"].cpu().numpy()
+        th1, vc1, st1 = r["theta_out"].cpu().numpy(), r["vcrit_out"].cpu().numpy(), r["step_out"].cpu().numpy()
+        for a in range(th0.shape[0]):
+            traj = {"idx": idx[a].T.copy(), "time": tm[a].T.copy(), "action": act[a].T.astype(np.int64),
+                    "reward": rew[a].T.copy(), "done": dn[a].T.astype(bool)}
+            t_ref, v_ref, s_ref, _, _ = oa2c.a2c_step(
+                torch.from_numpy(th0[a].astype(np.float64)), torch.from_numpy(vc0[a][:, None].astype(np.float64)),
+                int(st0[a]), int(lt[a]), traj, hyp, 40.0, 4.0, 0.5)
+            assert int(st1[a]) == s_ref, (u, a)
+            dt_ref, dv_ref = t_ref.numpy() - th0[a], v_ref.numpy()[:, 0] - vc0[a]
+            dt, dv = th1[a].astype(np.float64) - th0[a], vc1[a].astype(np.float64) - vc0[a]
+            assert np.linalg.norm(dt - dt_ref) <= tol * np.linalg.norm(dt_ref) + 1e-7, (u, a)
+            assert np.linalg.norm(dv - dv_ref) <= tol * np.linalg.norm(dv_ref) + 1e-7, (u, a)
+    return ost
+
+
+@pytest.mark.parametrize("mode,max_lifetime,fused", [("all_shortlife", 4, None), ("all_shortlife", 3, False),
+                                                     ("mazes", 3, None)])
+def test_regret_trained_antagonist_matches_oracle(mode, max_lifetime, fused):
+    """_compute_algorithmic_regret (level_sampler.py:293-329) with a TRAINED antagonist: train_a2c_agent
+    (a2c.py:79-125) for max_lifetime updates.  Checked against the oracle link by link: the antagonist's
+    initial tables bit-exact (flax lecun init), every A2C update's rollout bit-exact and its parameter change
+    within 2e-5 of float64 autograd, then regret = eval(trained A2C) - eval(LPG) within 1e-5 with both eval
+    rollouts regenerated by the oracle from the oracle's keys."""
+    from toued.agents import create_agents
+    from toued.env import LevelGenerator
+    from toued.level_sampler import LevelSampler
+    from toued.parse_args import parse_args
+    from toued.plr import algorithmic_regret
+    N = 3
+    args = parse_args(["--env_mode", mode, "--score_function", "alg_regret", "--num_agents", str(N),
+                       "--num_mini_batches", "1"])
+    smp = LevelSampler(args)
+    smp.max_lifetime = max_lifetime
+    trn = smp.a2c_trainer()
+    trn.fused = fused
+    trn.record = []
+    spec = olv.env_spec(mode)
+    lk = jr.split(jr.PRNGKey(31), N)
+    levels = LevelGenerator(mode)(dk(lk))
+    p, lt = olv.reset_env_params(lk, mode)
+    D = spec.obs_dim
+    lpg_theta, _ = create_agents(dk(jr.split(jr.PRNGKey(32), N)), D, 8)
+    lpg_theta.mul_(10.0)
+    keys = jr.split(jr.PRNGKey(33), N)
+    got = algorithmic_regret(smp, dk(keys), levels, lpg_theta).cpu().numpy()
+    rec = trn.record
+    assert len(rec) == max_lifetime
+    # oracle key chain of _compute_algorithmic_regret / _create_agent (level_sampler.py:273-329)
+    k = jr.split(keys, 2)
+    rng, c = k[:, 0], k[:, 1]
+    wc = jr.split(c, 2)
+    w_rng, ag_rng = wc[:, 0], wc[:, 1]
+    ost = oro.batch_reset(spec, w_rng, p, smp.env_workers)
+    init = [oag.create_agent(ag_rng[a], D, 1) for a in range(N)]
+    assert np.array_equal(rec[0]["theta"].cpu().numpy(), np.stack([x[0] for x in init]))
+    assert np.array_equal(rec[0]["vcrit"].cpu().numpy(), np.stack([x[1][:, 0] for x in init]))
+    k = jr.split(rng, 2)
+    rng, tr = k[:, 0], k[:, 1]
+    _a2c_follow(spec, p, lt, rec, tr, ost)
+    theta_K = rec[-1]["theta_out"].cpu().numpy()
+    assert not np.array_equal(theta_K, rec[0]["theta"].cpu().numpy())
+    ev = jr.split(rng, 2)
+    L = smp.max_rollout_len
+    r_lpg = oag.eval_agent(spec, ev[:, 0], p, lpg_theta.cpu().numpy(), 64, L)
+    r_a2c = oag.eval_agent(spec, ev[:, 1], p, theta_K, 64, L)
+    np.testing.assert_allclose(got, r_a2c - r_lpg, atol=1e-5, rtol=0)
+
+
+def test_regret_full_size_batch_invariant():
+    """C3 at full size: N=512 all_shortlife antagonists trained for the mode's max_lifetime (250) updates in
+    one batch (graph-replayed fused kernels).  Size-independent properties: every score finite; the regret of
+    an agent depends only on its own key, level and actor — re-scoring 4 of them alone gives bit-identical
+    scores; and the eval part is the oracle's: with the device's trained tables of those 4, the oracle eval
+    rollouts reproduce the regret within 1e-5."""
+    from toued import prng
+    from toued.agents import create_agents
+    from toued.env import LevelGenerator
+    from toued.level_sampler import LevelSampler
+    from toued.parse_args import parse_args
+    from toued.plr import algorithmic_regret
+    mode, N = "all_shortlife", 512
+    args = parse_args(["--env_mode", mode, "--score_function", "alg_regret", "--num_agents", str(N),
+                       "--num_mini_batches", "1"])
+    smp = LevelSampler(args)
+    assert smp.max_lifetime == 250
+    lk = jr.split(jr.PRNGKey(41), N)
+    levels = LevelGenerator(mode)(dk(lk))
+    D = smp.obs_dim
+    lpg_theta, _ = create_agents(dk(jr.split(jr.PRNGKey(42), N)), D, 8)
+    lpg_theta.mul_(10.0)
+    keys = dk(jr.split(jr.PRNGKey(43), N))
+    full = algorithmic_regret(smp, keys, levels, lpg_theta)
+    torch.cuda.synchronize()
+    assert torch.isfinite(full).all()
+    assert (full.abs() > 0).any()
+    sel = torch.tensor([0, 77, 300, 511], device="cuda")
+    part = algorithmic_regret(smp, keys[sel].contiguous(), levels[sel].contiguous(), lpg_theta[sel].contiguous())
+    assert torch.equal(part, full[sel])
+    # oracle eval of the same 4 from the trained tables of an eager re-run (record hook) of the 4-agent batch
+    trn = smp.a2c_trainer()
+    trn.record = []
+    again = algorithmic_regret(smp, keys[sel].contiguous(), levels[sel].contiguous(), lpg_theta[sel].contiguous())
+    assert torch.equal(again, part)
+    theta_K = trn.record[-1]["theta_out"].cpu().numpy()
+    trn.record = None
+    kk = prng.to_uint32_numpy(keys[sel])
+    p, _ = olv.reset_env_params(lk[sel.cpu().numpy()], mode)
+    spec = olv.env_spec(mode)
+    rng = jr.split(jr.split(kk, 2)[:, 0], 2)[:, 0]
+    ev = jr.split(rng, 2)
+    r_lpg = oag.eval_agent(spec, ev[:, 0], p, lpg_theta[sel].cpu().numpy(), 64, smp.max_rollout_len)
+    r_a2c = oag.eval_agent(spec, ev[:, 1], p, theta_K, 64, smp.max_rollout_len)
+    np.testing.assert_allclose(part.cpu().numpy(), r_a2c - r_lpg, atol=1e-5, rtol=0)
 
 
 def _buffer_state(B, N, seed, n_active, frac_new, ties=True):

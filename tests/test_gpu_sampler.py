@@ -1,0 +1,133 @@
+"""GPU parity of the LPG meta-optimiser step and of LevelSampler's non-PLR branches.
+
+  * toued_adam (optax 0.1.5 scale_by_adam + scale(lr) + scale(-1) on the agent-mean gradient,
+    models/optim.py:12-17, meta/train.py:128): bit-exact vs the float32 restatement oracle/meta.adam_f32
+    over several steps, and through a whole MetaGradStep (eta after the step).
+  * LevelSampler.initial_sample / sample for score_function random and frozen
+    (level_sampler.py:90-167, 237-291): levels, env states, actor/critic/value-critic tables and
+    steps bit-exact vs oracle/sampler.py, including which agents are regenerated (terminated mask).
+  * initial_sample for the buffer score functions (alg_regret): the agents' keys (no split before the
+    agents outside the random branch, level_sampler.py:112-119).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import jaxrand as jr
+from oracle import levels as olv
+from oracle import meta as ometa
+from oracle import sampler as osp
+
+pytestmark = pytest.mark.gpu
+
+
+def dk(a):
+    from toued.prng import from_uint32_numpy
+    return from_uint32_numpy(a, "cuda")
+
+
+def test_adam_bitexact_multi_step():
+    from toued import _lib
+    P, n = 100_003, 7
+    rs = np.random.RandomState(0)
+    eta = rs.randn(P).astype(np.float32) * 0.1
+    m = np.zeros(P, np.float32)
+    v = np.zeros(P, np.float32)
+    d_eta, d_m, d_v = (torch.from_numpy(x.copy()).cuda() for x in (eta, m, v))
+    count = 0
+    for it in range(4):
+        g = (rs.randn(P) * 10.0 ** rs.randint(-6, 3, P)).astype(np.float32)
+        g[:5] = [0.0, -0.0, 1e-30, 3e4, -7.5]
+        d_g = torch.from_numpy(g).cuda()
+        _lib.call("toued_adam", P, _lib.ptr(d_eta), _lib.ptr(d_g), _lib.ptr(d_m), _lib.ptr(d_v), float(n), 1e-4, 0.9,
+                  0.999, 1e-8, count + 1, _lib.stream_ptr())
+        eta, m, v, count = ometa.adam_f32(eta, g, n, m, v, count)
+        torch.cuda.synchronize()
+        assert np.array_equal(d_m.cpu().numpy(), m), it
+        assert np.array_equal(d_v.cpu().numpy(), v), it
+        assert np.array_equal(d_eta.cpu().numpy(), eta), it
+
+
+def test_adam_inside_meta_step():
+    """eta after MetaGradStep == adam_f32(eta_before, the step's summed meta-gradient, N): the Adam link of
+    lpg_meta_grad_train_step (meta/train.py:127-129) on the real gradient."""
+    from test_gpu_meta import _setup
+    N = 2
+    agents, step, eta, adam, hyp, D = _setup("dense", N, 64, 20, 2)
+    eta0 = eta.cpu().numpy()
+    step(torch.tensor([0, 9], dtype=torch.int32, device="cuda"), eta, adam, agents)
+    torch.cuda.synchronize()
+    ref, m, v, c = ometa.adam_f32(eta0, step.grad.cpu().numpy(), N, np.zeros_like(eta0), np.zeros_like(eta0), 0)
+    assert adam.count == c == 1
+    assert np.array_equal(eta.cpu().numpy(), ref)
+    assert np.array_equal(adam.m.cpu().numpy(), m)
+    assert np.array_equal(adam.v.cpu().numpy(), v)
+
+
+def _check_agents(spec, agents, lv, th, ph, st, vc, step):
+    from test_gpu_env import _state_np
+    np.testing.assert_array_equal(agents.levels.cpu().numpy(), olv.pack_levels(lv[0], lv[1], spec, lv[2]))
+    np.testing.assert_array_equal(agents.theta.cpu().numpy(), th)
+    np.testing.assert_array_equal(agents.phi.cpu().numpy(), ph)
+    g = _state_np(agents.state, spec)
+    for k in ("time", "pos", "obj_existss", "early_term", "obj_poss"):
+        np.testing.assert_array_equal(g[k], st[k], err_msg=k)
+    if vc is not None:
+        np.testing.assert_array_equal(agents.vcrit.cpu().numpy().reshape(vc.shape), vc)
+    np.testing.assert_array_equal(agents.step.cpu().numpy(), step)
+
+
+@pytest.mark.parametrize("score_function,mode", [("random", "all_shortlife"), ("frozen", "all_shortlife"),
+                                                 ("random", "tabular"), ("frozen", "mazes")])
+def test_sample_nonplr_matches_oracle(score_function, mode):
+    from toued import prng
+    from toued.env import L_LIFETIME
+    from toued.level_sampler import LevelSampler
+    from toued.parse_args import parse_args
+    N, B, W, Y = 6, 40, 64, 8
+    args = parse_args(["--env_mode", mode, "--score_function", score_function, "--num_agents", str(N),
+                       "--num_mini_batches", "1", "--buffer_size", str(B)])
+    smp = LevelSampler(args)
+    spec = olv.env_spec(mode)
+    k_buf, k_init, k_s1, k_s2 = jr.split(jr.PRNGKey(51), 4)
+    buf = smp.initialize_buffer(dk(k_buf))
+    obuf = None
+    if score_function != "random":
+        obuf, _, _, _ = osp.initialize_buffer(k_buf, mode, B)
+        np.testing.assert_array_equal(buf.levels.cpu().numpy(), olv.pack_levels(obuf[0], obuf[1], spec, obuf[2]))
+    buf, agents = smp.initial_sample(dk(k_init), buf, N, True)
+    lv, th, ph, st, vc = osp.initial_sample(spec, mode, score_function, k_init, obuf, N, W, Y, True)
+    step = np.zeros(N, np.int32)
+    _check_agents(spec, agents, lv, th, ph, st, vc, step)
+    # two sample() rounds: first agents 1, 3, 4 terminated, then all but agent 0
+    for key, term_ids in ((k_s1, [1, 3, 4]), (k_s2, [1, 2, 3, 4, 5])):
+        term = np.zeros(N, bool)
+        term[term_ids] = True
+        life = agents.levels[:, L_LIFETIME].cpu().numpy()
+        step = np.where(term, life, np.minimum(life - 1, 3)).astype(np.int32)
+        agents.step = torch.from_numpy(step).cuda()
+        # make the survivors' tables distinguishable from fresh ones
+        agents.theta.add_(0.5)
+        th, ph, vc = agents.theta.cpu().numpy(), agents.phi.cpu().numpy(), agents.vcrit.cpu().numpy().reshape(vc.shape)
+        buf, agents = smp.sample(dk(key), buf, agents)
+        lv, th, ph, st, vc, step = osp.sample_nonplr(spec, mode, score_function, key, obuf, term,
+                                                     (lv, th, ph, st, vc, step), W, Y)
+        torch.cuda.synchronize()
+        _check_agents(spec, agents, lv, th, ph, st, vc, step)
+
+
+def test_initial_sample_buffer_mode_agent_keys():
+    from toued.level_sampler import LevelSampler
+    from toued.parse_args import parse_args
+    mode, N, B = "all_shortlife", 5, 32
+    args = parse_args(["--env_mode", mode, "--score_function", "alg_regret", "--num_agents", str(N),
+                       "--num_mini_batches", "1", "--buffer_size", str(B)])
+    smp = LevelSampler(args)
+    spec = olv.env_spec(mode)
+    k_buf, k_init = jr.split(jr.PRNGKey(61), 2)
+    buf = smp.initialize_buffer(dk(k_buf))
+    buf, agents = smp.initial_sample(dk(k_init), buf, N, False)
+    obuf, _, _, _ = osp.initialize_buffer(k_buf, mode, B)
+    lv, th, ph, st, _ = osp.initial_sample(spec, mode, "alg_regret", k_init, obuf, N, 64, 8, False)
+    _check_agents(spec, agents, lv, th, ph, st, None, np.zeros(N, np.int32))
+    assert buf.active.cpu().numpy().tolist() == [True] * N + [False] * (B - N)

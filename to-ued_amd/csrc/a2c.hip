@@ -8,6 +8,9 @@
 //                mean_t adv per worker) - entropy_coeff * H(pi + 1e-8)   (a2c.py:29-63)
 //   k_a2c_apply  optax clip_by_global_norm + SGD per TrainState (models/optim.py:5-11), discard when
 //                the new step exceeds the lifetime (a2c.py:71-75); clears the gradient tables
+//   k_a2c_update the whole update in one block per agent, deterministic: per-sample row vectors in LDS,
+//                sorted by (row, sample), segment sums in sample order, norms, clip and SGD on the touched rows
+//                (W*T <= 2048; grad + apply, which scatter with float atomics, are the fallback above that)
 //
 // Trajectory layout as the rollout kernel writes it: idx/time [N][T+1][W], act/done/rew [N][T][W].
 #include "common.h"
@@ -34,6 +37,129 @@ TOUED_DEV float block_sum(float v, float* red) {
   return s;
 }
 
+// Staged trajectory of one agent in LDS and the quantities every sample's gradient needs.
+struct A2CStage {
+  float* vt;    // [T+1][W] V(obs)
+  float* cc;    // [T+1][W] 0.001 * time
+  int* ix;      // [T+1][W] obs row
+  float* rw;    // [T][W] reward
+  float* nd;    // [T][W] 1 - done
+  float* adv;   // [W*T] GAE advantages, worker-major
+  float* dv;    // [W*T] target - V
+  float* abar;  // [W] mean_t normalised advantage
+  __host__ __device__ static size_t floats(int W, int T) { return 3 * (size_t)(T + 1) * W + 4 * (size_t)W * T + W; }
+  TOUED_DEV void carve(float* base, int W, int T) {
+    const int NO = (T + 1) * W, NS = T * W;
+    vt = base;
+    cc = vt + NO;
+    ix = reinterpret_cast<int*>(cc + NO);
+    rw = reinterpret_cast<float*>(ix + NO);
+    nd = rw + NS;
+    adv = nd + NS;
+    dv = adv + NS;
+    abar = dv + NS;
+  }
+};
+
+// Latency structure: the agent's whole trajectory (obs rows and times, rewards, dones) is staged into LDS with
+// coalesced loads, V(obs) gathered for every observation at once, and only then the per-worker GAE scans run
+// out of LDS -- a handful of dependent memory round trips per update instead of two per time step.  Returns the
+// critic loss mean((target - V)^2) (a2c.py:29-37); fills adv/dv/abar (a2c.py:43 normalisation, the [T,T]
+// broadcast's mean_t factor).  Ends with a barrier.
+TOUED_DEV float a2c_stage(const A2CStage& S, int a, int W, int T, int D, const float* __restrict__ v,
+                          const int* __restrict__ tidx, const int* __restrict__ ttime,
+                          const float* __restrict__ trew, const uint8_t* __restrict__ tdone, float gamma, float lam,
+                          float* red) {
+  const int NO = (T + 1) * W, NS = T * W, tid = threadIdx.x;
+  const float vlast = v[D - 1];
+  const size_t tb = (size_t)a * (T + 1) * W;
+  const size_t sb = (size_t)a * T * W;
+  for (int i = tid; i < NO; i += blockDim.x) {
+    const int idx = tidx[tb + i];
+    const float c = (float)ttime[tb + i] * 0.001f;
+    S.ix[i] = idx;
+    S.cc[i] = c;
+    S.vt[i] = v[idx] + c * vlast;
+  }
+  for (int i = tid; i < NS; i += blockDim.x) {
+    S.rw[i] = trew[sb + i];
+    S.nd[i] = tdone[sb + i] ? 0.0f : 1.0f;
+  }
+  __syncthreads();
+  // per-worker GAE (reverse scan over T, util/metrics.py:17-38)
+  float s_adv = 0.0f, s_cl = 0.0f;
+  for (int w = tid; w < W; w += blockDim.x) {
+    float vn = S.vt[T * W + w];
+    float g = 0.0f, cl = 0.0f;
+    for (int t = T - 1; t >= 0; --t) {
+      const float vv = S.vt[t * W + w];
+      const float ndt = S.nd[t * W + w];
+      const float delta = S.rw[t * W + w] + (gamma * vn * ndt - vv);
+      g = delta + gamma * lam * ndt * g;
+      const float e = (g + vv) - vv;
+      S.adv[w * T + t] = g;
+      S.dv[w * T + t] = e;
+      cl += e * e;
+      s_adv += g;
+      vn = vv;
+    }
+    s_cl += cl / (float)T;
+  }
+  const float n = (float)(W * T);
+  const float mean = block_sum(s_adv, red) / n;
+  const float closs = block_sum(s_cl, red) / (float)W;
+  float s_var = 0.0f;
+  for (int i = tid; i < W * T; i += blockDim.x) {
+    const float d = S.adv[i] - mean;
+    s_var += d * d;
+  }
+  const float inv_sd = 1.0f / (sqrtf(block_sum(s_var, red) / n) + EPSF);
+  for (int w = tid; w < W; w += blockDim.x) {
+    float ab = 0.0f;
+    for (int t = 0; t < T; ++t) ab += (S.adv[w * T + t] - mean) * inv_sd;
+    S.abar[w] = ab / (float)T;
+  }
+  __syncthreads();
+  return closs;
+}
+
+// Sample i = t*W + w of the staged agent: actor row cotangent d[5] (policy term through the [T,T] broadcast plus
+// the entropy bonus of pi + 1e-8, a2c.py:52-63), critic row cotangent (returned), the row, the time coefficient
+// and this sample's actor-loss term.
+TOUED_DEV float a2c_sample(const A2CStage& S, int i, int W, int T, const float* __restrict__ th,
+                           const float* lastA, const uint8_t* __restrict__ tact, size_t sb, float ent_coef,
+                           float inv_n, float* d, int& idx, float& c, float& al) {
+  const int t = i / W, w = i - t * W;
+  idx = S.ix[i];
+  c = S.cc[i];
+  const int act = tact[sb + (size_t)t * W + w];
+  float l[5], p[5], m = -__builtin_inff();
+#pragma unroll
+  for (int j = 0; j < 5; ++j) { l[j] = th[(size_t)idx * 5 + j] + c * lastA[j]; m = fmaxf(m, l[j]); }
+  float z = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) { p[j] = __expf(l[j] - m); z += p[j]; }
+  const float iz = 1.0f / z;
+  float pa = 0.0f, h = 0.0f, gl[5], pg = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    p[j] *= iz;
+    pa = (j == act) ? p[j] : pa;
+    const float lg = __logf(p[j] + EPSF);
+    h -= (p[j] + EPSF) * lg;
+    gl[j] = -(lg + 1.0f);
+    pg += p[j] * gl[j];
+  }
+  const float ab = S.abar[w];
+  const float rho = pa / (pa + EPSF);
+  const float kap = -ab * inv_n;
+  const float ke = -ent_coef * inv_n;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) d[j] = kap * rho * ((j == act ? 1.0f : 0.0f) - p[j]) + ke * p[j] * (gl[j] - pg);
+  al = -__logf(pa + EPSF) * ab - ent_coef * h;
+  return -2.0f * S.dv[w * T + t] * inv_n;
+}
+
 }  // namespace
 
 __global__ void k_key_chain(const uint32_t* __restrict__ keys, int n, int U, uint32_t* __restrict__ out) {
@@ -49,10 +175,8 @@ __global__ void k_key_chain(const uint32_t* __restrict__ keys, int n, int U, uin
   }
 }
 
-// loss_out[a] += {actor_loss, critic_loss} (accumulated over updates; the caller zeroes it)
-// Latency structure: the agent's whole trajectory (obs rows and times, rewards, dones) is staged into LDS with
-// coalesced loads, V(obs) gathered for every observation at once, and only then the per-worker GAE scans run
-// out of LDS -- a handful of dependent memory round trips per update instead of two per time step.
+// loss_out[a] += {actor_loss, critic_loss} (accumulated over updates; the caller zeroes it).  Fallback for
+// W*T > 2048: the per-sample rows are scattered with float atomics (summation order not fixed).
 __global__ void __launch_bounds__(256) k_a2c_grad(int W, int T, int D, const float* __restrict__ theta,
                                                   const float* __restrict__ vcrit, const int* __restrict__ tidx,
                                                   const int* __restrict__ ttime, const uint8_t* __restrict__ tact,
@@ -60,115 +184,32 @@ __global__ void __launch_bounds__(256) k_a2c_grad(int W, int T, int D, const flo
                                                   float gamma, float lam, float ent_coef, float* __restrict__ Ga,
                                                   float* __restrict__ Gv, float* __restrict__ loss_out) {
   extern __shared__ float lds[];
-  const int NO = (T + 1) * W, NS = T * W;
-  float* vt = lds;                                     // [T+1][W] V(obs)
-  float* cc = vt + NO;                                 // [T+1][W] 0.001 * time
-  int* ix = reinterpret_cast<int*>(cc + NO);           // [T+1][W] obs row
-  float* rw = reinterpret_cast<float*>(ix + NO);       // [T][W] reward
-  float* nd = rw + NS;                                 // [T][W] 1 - done
-  float* adv = nd + NS;                                // [W*T] GAE advantages, worker-major
-  float* dv = adv + NS;                                // [W*T] target - V
-  float* abar = dv + NS;                               // [W] mean_t normalised advantage
   __shared__ float red[8];
-  const int a = blockIdx.x;
-  const int tid = threadIdx.x;
-  const float* v = vcrit + (size_t)a * D;
-  const float vlast = v[D - 1];
-  const size_t tb = (size_t)a * (T + 1) * W;  // trajectory obs base
-  const size_t sb = (size_t)a * T * W;        // trajectory step base
-  // ---- stage the trajectory; V at every observation (all gathers in flight together)
-  for (int i = tid; i < NO; i += blockDim.x) {
-    const int idx = tidx[tb + i];
-    const float c = (float)ttime[tb + i] * 0.001f;
-    ix[i] = idx;
-    cc[i] = c;
-    vt[i] = v[idx] + c * vlast;
-  }
-  for (int i = tid; i < NS; i += blockDim.x) {
-    rw[i] = trew[sb + i];
-    nd[i] = tdone[sb + i] ? 0.0f : 1.0f;
-  }
-  __syncthreads();
-  // ---- per-worker GAE (reverse scan over T, util/metrics.py:17-38)
-  float s_adv = 0.0f, s_cl = 0.0f;
-  for (int w = tid; w < W; w += blockDim.x) {
-    float vn = vt[T * W + w];
-    float g = 0.0f, cl = 0.0f;
-    for (int t = T - 1; t >= 0; --t) {
-      const float vv = vt[t * W + w];
-      const float ndt = nd[t * W + w];
-      const float delta = rw[t * W + w] + (gamma * vn * ndt - vv);
-      g = delta + gamma * lam * ndt * g;
-      const float e = (g + vv) - vv;
-      adv[w * T + t] = g;
-      dv[w * T + t] = e;
-      cl += e * e;
-      s_adv += g;
-      vn = vv;
-    }
-    s_cl += cl / (float)T;
-  }
-  const float n = (float)(W * T);
-  const float mean = block_sum(s_adv, red) / n;
-  const float closs = block_sum(s_cl, red) / (float)W;
-  float s_var = 0.0f;
-  for (int i = tid; i < W * T; i += blockDim.x) {
-    const float d = adv[i] - mean;
-    s_var += d * d;
-  }
-  const float inv_sd = 1.0f / (sqrtf(block_sum(s_var, red) / n) + EPSF);
-  for (int w = tid; w < W; w += blockDim.x) {
-    float ab = 0.0f;
-    for (int t = 0; t < T; ++t) ab += (adv[w * T + t] - mean) * inv_sd;
-    abar[w] = ab / (float)T;
-  }
-  __syncthreads();
-  // ---- per-sample actor / critic gradients
+  A2CStage S;
+  S.carve(lds, W, T);
+  const int a = blockIdx.x, tid = threadIdx.x;
+  const float closs = a2c_stage(S, a, W, T, D, vcrit + (size_t)a * D, tidx, ttime, trew, tdone, gamma, lam, red);
   const float* th = theta + (size_t)a * D * 5;
   float* ga = Ga + (size_t)a * D * 5;
   float* gv = Gv + (size_t)a * D;
   float lastA[5];
 #pragma unroll
   for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
-  const float inv_n = 1.0f / n;
+  const float inv_n = 1.0f / (float)(W * T);
+  const size_t sb = (size_t)a * T * W;
   float accA[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, accV = 0.0f, s_al = 0.0f;
   for (int i = tid; i < W * T; i += blockDim.x) {
-    const int t = i / W, w = i - t * W;
-    const int idx = ix[i];
-    const float c = cc[i];
-    const int act = tact[sb + (size_t)t * W + w];
-    float l[5], p[5], m = -__builtin_inff();
-#pragma unroll
-    for (int j = 0; j < 5; ++j) { l[j] = th[(size_t)idx * 5 + j] + c * lastA[j]; m = fmaxf(m, l[j]); }
-    float z = 0.0f;
-#pragma unroll
-    for (int j = 0; j < 5; ++j) { p[j] = __expf(l[j] - m); z += p[j]; }
-    const float iz = 1.0f / z;
-    float pa = 0.0f, h = 0.0f, gl[5], pg = 0.0f;
+    float d[5], c, al;
+    int idx;
+    const float dvv = a2c_sample(S, i, W, T, th, lastA, tact, sb, ent_coef, inv_n, d, idx, c, al);
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
-      p[j] *= iz;
-      pa = (j == act) ? p[j] : pa;
-      const float lg = __logf(p[j] + EPSF);
-      h -= (p[j] + EPSF) * lg;
-      gl[j] = -(lg + 1.0f);
-      pg += p[j] * gl[j];
-    }
-    const float ab = abar[w];
-    const float rho = pa / (pa + EPSF);
-    const float kap = -ab * inv_n;
-    const float ke = -ent_coef * inv_n;
-    float d[5];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      d[j] = kap * rho * ((j == act ? 1.0f : 0.0f) - p[j]) + ke * p[j] * (gl[j] - pg);
       atomicAdd(&ga[(size_t)idx * 5 + j], d[j]);
       accA[j] += c * d[j];
     }
-    const float dvv = -2.0f * dv[w * T + t] * inv_n;
     atomicAdd(&gv[idx], dvv);
     accV += c * dvv;
-    s_al += -__logf(pa + EPSF) * ab - ent_coef * h;
+    s_al += al;
   }
 #pragma unroll
   for (int j = 0; j < 5; ++j) {
@@ -217,11 +258,54 @@ __global__ void __launch_bounds__(256) k_a2c_apply(int D, float* __restrict__ th
   if (threadIdx.x == 0) step[a] = applied ? st + 1 : st;
 }
 
-// Fused update (grad + apply) with the agent's gradient tables in LDS: the per-sample contributions land in
-// LDS (ds_add_f32 atomics: rows shared by many samples -- the start cell, small grids -- serialise far less
-// than L2 atomics on one cache line), the global norms come from LDS, and only rows with a nonzero gradient
-// are rewritten in HBM (an untouched row's update theta + -(lr * 0) is the identity).  One block per agent;
-// used when D * 6 floats plus the staged trajectory fit the LDS (all_* modes: D = 3201), else grad + apply.
+// ---------------------------------------------------------------------------- deterministic fused update
+// One block (256 threads) per agent, W*T <= 2048 samples.  The reference's gradient is obs^T . dlogits over the
+// agent's [W, T] batch (XLA, deterministic); here every sample's 6-float row cotangent (5 actor + 1 critic) is
+// written to LDS, the keys (row << 11 | sample) are bitonic-sorted, and each row's segment is summed in sample
+// order, chunk partials combined in chunk order -- no atomics, so a replay gives bit-identical tables.  The row
+// sums stay in LDS (in the vector slot of the segment's first sample) until the two global norms are known;
+// then clip + SGD rewrite only the rows that have samples (an untouched row's update th + -(lr * 0) is the
+// identity).  The time row D-1 (every sample contributes c * v) is a block reduction.  LDS does not depend on
+// D: staged trajectory + 2048 keys + W*T*6 floats (~76 KB at W=64, T=20), so two agents share a CU.
+#define A2C_SORT_MAX 2048
+#define A2C_NV 6
+
+// bitonic sort of 2048 keys with 256 threads: wave w owns keys [512 w, 512 w + 512), so every stage with partner
+// distance j < 512 needs only a wave barrier; the three stages with j >= 512 take workgroup barriers.
+TOUED_DEV void a2c_cmp_swap(uint32_t* key, int i, int j, int k) {
+  const int ij = i | j;
+  const uint32_t x = key[i], y = key[ij];
+  if ((x > y) == ((i & k) == 0)) { key[i] = y; key[ij] = x; }
+}
+
+TOUED_DEV void a2c_sort2048(uint32_t* key, int tid) {
+  const int lane = tid & 63, wv = tid >> 6;
+  for (int k = 2; k <= 2048; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const int lj = 31 - __builtin_clz(j);
+      if (j >= 512) {
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {       // 1024 pairs over 256 threads
+          const int pr = tid + 256 * h;
+          a2c_cmp_swap(key, ((pr >> lj) << (lj + 1)) | (pr & (j - 1)), j, k);
+        }
+        __syncthreads();
+      } else {
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {       // this wave's 256 pairs
+          const int pr = lane + 64 * h;
+          a2c_cmp_swap(key, 512 * wv + (((pr >> lj) << (lj + 1)) | (pr & (j - 1))), j, k);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    }
+  }
+  __syncthreads();
+}
+
 __global__ void __launch_bounds__(256) k_a2c_update(int W, int T, int D, float* __restrict__ theta,
                                                     float* __restrict__ vcrit, const int* __restrict__ tidx,
                                                     const int* __restrict__ ttime, const uint8_t* __restrict__ tact,
@@ -229,161 +313,149 @@ __global__ void __launch_bounds__(256) k_a2c_update(int W, int T, int D, float* 
                                                     float gamma, float lam, float ent_coef, float lr_a, float lr_c,
                                                     float max_norm, int* __restrict__ step,
                                                     const int* __restrict__ levels, float* __restrict__ loss_out) {
+  constexpr int NV = A2C_NV, CH = A2C_SORT_MAX / 256;
+  constexpr uint32_t NONE = 0xFFFFFFFFu, SMASK = 2047u;
   extern __shared__ float lds[];
-  const int NO = (T + 1) * W, NS = T * W;
-  float* GA = lds;                                     // [D][5] actor gradient
-  float* GV = GA + (size_t)D * 5;                      // [D] critic gradient
-  float* vt = GV + D;                                  // [T+1][W] V(obs)
-  float* cc = vt + NO;                                 // [T+1][W] 0.001 * time
-  int* ix = reinterpret_cast<int*>(cc + NO);           // [T+1][W] obs row
-  float* rw = reinterpret_cast<float*>(ix + NO);       // [T][W] reward
-  float* nd = rw + NS;                                 // [T][W] 1 - done
-  float* adv = nd + NS;                                // [W*T] worker-major
-  float* dv = adv + NS;                                // [W*T] target - V
-  float* abar = dv + NS;                               // [W]
   __shared__ float red[8];
-  const int a = blockIdx.x;
-  const int tid = threadIdx.x;
+  __shared__ float tot[NV];
+  __shared__ int has_last;
+  const int a = blockIdx.x, tid = threadIdx.x, TW = W * T;
+  A2CStage S;
+  S.carve(lds, W, T);
+  uint32_t* key = reinterpret_cast<uint32_t*>(lds + A2CStage::floats(W, T));   // [2048]
+  float* vec = reinterpret_cast<float*>(key + A2C_SORT_MAX);                    // [W*T][6]
   float* v = vcrit + (size_t)a * D;
   float* th = theta + (size_t)a * D * 5;
-  for (int i = tid; i < D * 6; i += blockDim.x) GA[i] = 0.0f;
-  const float vlast = v[D - 1];
-  const size_t tb = (size_t)a * (T + 1) * W;
-  const size_t sb = (size_t)a * T * W;
-  for (int i = tid; i < NO; i += blockDim.x) {
-    const int idx = tidx[tb + i];
-    const float c = (float)ttime[tb + i] * 0.001f;
-    ix[i] = idx;
-    cc[i] = c;
-    vt[i] = v[idx] + c * vlast;
-  }
-  for (int i = tid; i < NS; i += blockDim.x) {
-    rw[i] = trew[sb + i];
-    nd[i] = tdone[sb + i] ? 0.0f : 1.0f;
-  }
-  __syncthreads();
-  float s_adv = 0.0f, s_cl = 0.0f;
-  for (int w = tid; w < W; w += blockDim.x) {
-    float vn = vt[T * W + w];
-    float g = 0.0f, cl = 0.0f;
-    for (int t = T - 1; t >= 0; --t) {
-      const float vv = vt[t * W + w];
-      const float ndt = nd[t * W + w];
-      const float delta = rw[t * W + w] + (gamma * vn * ndt - vv);
-      g = delta + gamma * lam * ndt * g;
-      const float e = (g + vv) - vv;
-      adv[w * T + t] = g;
-      dv[w * T + t] = e;
-      cl += e * e;
-      s_adv += g;
-      vn = vv;
-    }
-    s_cl += cl / (float)T;
-  }
-  const float n = (float)(W * T);
-  const float mean = block_sum(s_adv, red) / n;
-  const float closs = block_sum(s_cl, red) / (float)W;
-  float s_var = 0.0f;
-  for (int i = tid; i < W * T; i += blockDim.x) {
-    const float d = adv[i] - mean;
-    s_var += d * d;
-  }
-  const float inv_sd = 1.0f / (sqrtf(block_sum(s_var, red) / n) + EPSF);
-  for (int w = tid; w < W; w += blockDim.x) {
-    float ab = 0.0f;
-    for (int t = 0; t < T; ++t) ab += (adv[w * T + t] - mean) * inv_sd;
-    abar[w] = ab / (float)T;
-  }
-  __syncthreads();
+  if (tid == 0) has_last = 0;
+  const float closs = a2c_stage(S, a, W, T, D, v, tidx, ttime, trew, tdone, gamma, lam, red);
+  // 1) per-sample row vectors -> LDS, sort keys, time-row partial sums, actor loss
   float lastA[5];
 #pragma unroll
   for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
-  const float inv_n = 1.0f / n;
-  float accA[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, accV = 0.0f, s_al = 0.0f;
-  for (int i = tid; i < W * T; i += blockDim.x) {
-    const int t = i / W, w = i - t * W;
-    const int idx = ix[i];
-    const float c = cc[i];
-    const int act = tact[sb + (size_t)t * W + w];
-    float l[5], p[5], m = -__builtin_inff();
+  const float inv_n = 1.0f / (float)TW;
+  const size_t sb = (size_t)a * T * W;
+  float part[NV] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, s_al = 0.0f;
+  for (int sl = tid; sl < A2C_SORT_MAX; sl += 256) {
+    uint32_t kk = NONE;
+    if (sl < TW) {
+      float d[5], c, al;
+      int idx;
+      const float dvv = a2c_sample(S, sl, W, T, th, lastA, tact, sb, ent_coef, inv_n, d, idx, c, al);
+      kk = ((uint32_t)idx << 11) | (uint32_t)sl;
 #pragma unroll
-    for (int j = 0; j < 5; ++j) { l[j] = th[(size_t)idx * 5 + j] + c * lastA[j]; m = fmaxf(m, l[j]); }
-    float z = 0.0f;
-#pragma unroll
-    for (int j = 0; j < 5; ++j) { p[j] = __expf(l[j] - m); z += p[j]; }
-    const float iz = 1.0f / z;
-    float pa = 0.0f, h = 0.0f, gl[5], pg = 0.0f;
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      p[j] *= iz;
-      pa = (j == act) ? p[j] : pa;
-      const float lg = __logf(p[j] + EPSF);
-      h -= (p[j] + EPSF) * lg;
-      gl[j] = -(lg + 1.0f);
-      pg += p[j] * gl[j];
+      for (int j = 0; j < 5; ++j) { vec[sl * NV + j] = d[j]; part[j] += c * d[j]; }
+      vec[sl * NV + 5] = dvv;
+      part[5] += c * dvv;
+      s_al += al;
+      if (idx == D - 1) has_last = 1;
     }
-    const float ab = abar[w];
-    const float rho = pa / (pa + EPSF);
-    const float kap = -ab * inv_n;
-    const float ke = -ent_coef * inv_n;
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const float d = kap * rho * ((j == act ? 1.0f : 0.0f) - p[j]) + ke * p[j] * (gl[j] - pg);
-      atomicAdd(&GA[idx * 5 + j], d);
-      accA[j] += c * d;
-    }
-    const float dvv = -2.0f * dv[w * T + t] * inv_n;
-    atomicAdd(&GV[idx], dvv);
-    accV += c * dvv;
-    s_al += -__logf(pa + EPSF) * ab - ent_coef * h;
+    key[sl] = kk;
   }
-  float ra[5];
 #pragma unroll
-  for (int j = 0; j < 5; ++j) ra[j] = block_sum(accA[j], red);
-  const float rv = block_sum(accV, red);
+  for (int j = 0; j < NV; ++j) {
+    const float r = block_sum(part[j], red);
+    if (tid == 0) tot[j] = r;
+  }
   const float al = block_sum(s_al, red) * inv_n;
-  if (tid == 0) {   // every sample's LDS atomic is complete (block_sum's barriers)
+  // 2) sort by (row, sample)
+  a2c_sort2048(key, tid);
+  // 3) segmented sums: thread t sums the runs of its CH sorted entries [CH t, CH t + CH); a run continuing a
+  //    segment begun in an earlier chunk leaves its partial in the vector slot of the chunk's first entry; after
+  //    a barrier each segment's owner adds those in chunk order.  The final row sum goes to the vector slot of
+  //    the segment's first sample (read only by its owner) and its square into the norm partials.
+  float na2 = 0.0f, nc2 = 0.0f;
+  auto emit = [&](uint32_t row, uint32_t first, float (&sum)[NV]) {
+    if ((int)row == D - 1) {
 #pragma unroll
-    for (int j = 0; j < 5; ++j) GA[(D - 1) * 5 + j] += ra[j];
-    GV[D - 1] += rv;
-    loss_out[a * 2 + 0] += al;
-    loss_out[a * 2 + 1] += closs;
+      for (int j = 0; j < NV; ++j) sum[j] += tot[j];
+    }
+    float* slot = vec + (size_t)(first & SMASK) * NV;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) slot[j] = sum[j];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) na2 += sum[j] * sum[j];
+    nc2 += sum[5] * sum[5];
+  };
+  const int i0 = CH * tid, i1 = min(i0 + CH, TW);
+  float run[NV];
+  uint32_t run_row = NONE, run_first = NONE, pend_row = NONE, pend_first = NONE;
+  bool run_owned = false;
+  for (int e = i0; e <= i1; ++e) {
+    const uint32_t ke = e < i1 ? key[e] : NONE;
+    const uint32_t row = ke == NONE ? NONE : ke >> 11;
+    if (row != run_row && run_row != NONE) {
+      const bool cont_next = e == i1 && e < TW && key[e] != NONE && (key[e] >> 11) == run_row;
+      if (!run_owned) {
+        float* slot = vec + (size_t)(key[i0] & SMASK) * NV;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) slot[j] = run[j];
+      } else if (cont_next) {
+        pend_row = run_row;
+        pend_first = run_first;
+      } else {
+        emit(run_row, run_first, run);
+      }
+    }
+    if (ke == NONE || e >= i1) break;
+    if (row != run_row) {
+      run_row = row;
+      run_first = ke;
+      run_owned = e == 0 || (key[e - 1] >> 11) != row;
+#pragma unroll
+      for (int j = 0; j < NV; ++j) run[j] = 0.0f;
+    }
+    const float* ve = vec + (size_t)(ke & SMASK) * NV;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) run[j] += ve[j];
   }
   __syncthreads();
-  // ---- clip_by_global_norm + SGD (models/optim.py:5-11), discarded past the lifetime (a2c.py:71-75)
-  float sa = 0.0f, sc = 0.0f;
-  for (int i = tid; i < D * 5; i += blockDim.x) sa += GA[i] * GA[i];
-  for (int i = tid; i < D; i += blockDim.x) sc += GV[i] * GV[i];
-  const float gna = sqrtf(block_sum(sa, red));
-  const float gnc = sqrtf(block_sum(sc, red));
+  if (pend_row != NONE) {
+    for (int c = tid + 1; CH * c < TW; ++c) {
+      const uint32_t kc = key[CH * c];
+      if (kc == NONE || (kc >> 11) != pend_row) break;
+      const float* slot = vec + (size_t)(kc & SMASK) * NV;
+#pragma unroll
+      for (int j = 0; j < NV; ++j) run[j] += slot[j];
+    }
+    emit(pend_row, pend_first, run);
+  }
+  if (tid == 0 && !has_last) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j) na2 += tot[j] * tot[j];
+    nc2 += tot[5] * tot[5];
+  }
+  // 4) clip_by_global_norm + SGD (models/optim.py:5-11), discarded past the lifetime (a2c.py:71-75)
+  const float gna = sqrtf(block_sum(na2, red));
+  const float gnc = sqrtf(block_sum(nc2, red));
   const int st = step[a];
   const bool applied = (st + 1) <= levels[(size_t)a * LEVEL_WORDS + L_LIFETIME];
   const bool clip_a = !(gna < max_norm), clip_c = !(gnc < max_norm);
-  if (applied) {
-    for (int r = tid; r < D; r += blockDim.x) {
-      float g[5];
-      bool nz = false;
+  auto apply_row = [&](int r, const float* g) {
 #pragma unroll
-      for (int j = 0; j < 5; ++j) { g[j] = GA[r * 5 + j]; nz |= g[j] != 0.0f; }
-      if (nz) {
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-          const float gg = clip_a ? (g[j] / gna) * max_norm : g[j];
-          th[(size_t)r * 5 + j] = th[(size_t)r * 5 + j] + (-(lr_a * gg));
-        }
-      }
-      const float gv = GV[r];
-      if (gv != 0.0f) {
-        const float gg = clip_c ? (gv / gnc) * max_norm : gv;
-        v[r] = v[r] + (-(lr_c * gg));
-      }
+    for (int j = 0; j < 5; ++j) {
+      const float gg = clip_a ? (g[j] / gna) * max_norm : g[j];
+      th[(size_t)r * 5 + j] = th[(size_t)r * 5 + j] + (-(lr_a * gg));
     }
+    const float gg = clip_c ? (g[5] / gnc) * max_norm : g[5];
+    v[r] = v[r] + (-(lr_c * gg));
+  };
+  if (applied) {
+    for (int e = i0; e < i1; ++e) {
+      const uint32_t ke = key[e];
+      if (ke == NONE) break;
+      if (e == 0 || (key[e - 1] >> 11) != (ke >> 11)) apply_row((int)(ke >> 11), vec + (size_t)(ke & SMASK) * NV);
+    }
+    if (tid == 0 && !has_last) apply_row(D - 1, tot);
   }
-  if (tid == 0) step[a] = applied ? st + 1 : st;
+  if (tid == 0) {
+    step[a] = applied ? st + 1 : st;
+    loss_out[a * 2 + 0] += al;
+    loss_out[a * 2 + 1] += closs;
+  }
 }
 
-static size_t a2c_update_lds(int W, int T, int D) {
-  return ((size_t)D * 6 + 3 * (size_t)(T + 1) * W + 4 * (size_t)W * T + W) * sizeof(float);
+static size_t a2c_update_lds(int W, int T) {
+  return (A2CStage::floats(W, T) + A2C_SORT_MAX + (size_t)W * T * A2C_NV) * sizeof(float);
 }
 
 extern "C" {
@@ -401,7 +473,7 @@ int toued_a2c_grad(int N, int W, int T, int D, const float* theta, const float* 
                    const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone, float gamma,
                    float lam, float ent_coef, float* Ga, float* Gv, float* loss_out, hipStream_t stream) {
   TOUED_REQUIRE(N >= 0 && W > 0 && T > 0 && D > 1, "toued_a2c_grad: bad sizes");
-  const size_t lds = (size_t)(3 * (T + 1) * W + 4 * W * T + W) * sizeof(float);
+  const size_t lds = A2CStage::floats(W, T) * sizeof(float);
   TOUED_REQUIRE(lds <= 64 * 1024, "toued_a2c_grad: W*T too large for LDS");
   if (N == 0) return 0;
   hipLaunchKernelGGL(k_a2c_grad, dim3(N), dim3(256), lds, stream, W, T, D, theta, vcrit, tidx, ttime, tact, trew,
@@ -410,19 +482,20 @@ int toued_a2c_grad(int N, int W, int T, int D, const float* theta, const float* 
   return 0;
 }
 
-// 1 when the fused A2C update fits the LDS for these sizes (else use toued_a2c_grad + toued_a2c_apply)
+// 1 when the deterministic fused A2C update supports these sizes (W*T <= 2048, rows < 2^21; else use
+// toued_a2c_grad + toued_a2c_apply)
 int toued_a2c_update_fits(int W, int T, int D) {
-  return W > 0 && T > 0 && D > 1 && a2c_update_lds(W, T, D) <= 150 * 1024 ? 1 : 0;
+  return W > 0 && T > 0 && D > 1 && W * T <= A2C_SORT_MAX && D < (1 << 21) && a2c_update_lds(W, T) <= 150 * 1024
+             ? 1 : 0;
 }
 
 int toued_a2c_update(int N, int W, int T, int D, float* theta, float* vcrit, const int* tidx, const int* ttime,
                      const uint8_t* tact, const float* trew, const uint8_t* tdone, float gamma, float lam,
                      float ent_coef, float lr_a, float lr_c, float max_norm, int* step, const int* levels,
                      float* loss_out, hipStream_t stream) {
-  TOUED_REQUIRE(N >= 0 && W > 0 && T > 0 && D > 1, "toued_a2c_update: bad sizes");
-  const size_t lds = a2c_update_lds(W, T, D);
-  TOUED_REQUIRE(lds <= 150 * 1024, "toued_a2c_update: D=%d W=%d T=%d need %zu B of LDS (use grad + apply)", D, W, T,
-                lds);
+  TOUED_REQUIRE(toued_a2c_update_fits(W, T, D), "toued_a2c_update: D=%d W=%d T=%d unsupported (W*T <= %d; use "
+                "grad + apply)", D, W, T, A2C_SORT_MAX);
+  const size_t lds = a2c_update_lds(W, T);
   if (N == 0) return 0;
   static bool attr_set = false;
   if (!attr_set) {

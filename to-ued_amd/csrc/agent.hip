@@ -791,15 +791,20 @@ __global__ void __launch_bounds__(256) k_embed_bwd(int N, int W, int T, int D, i
 
 // ---------------------------------------------------------------------------- Adam
 __global__ void __launch_bounds__(256) k_adam(int P, float* __restrict__ eta, const float* __restrict__ grad,
-                                              float* __restrict__ m, float* __restrict__ v, float scale, float lr,
-                                              float b1, float b2, float eps, float bc1, float bc2) {
+                                              float* __restrict__ m, float* __restrict__ v, float n_mean, float lr,
+                                              float b1, float omb1, float b2, float omb2, float eps, float bc1,
+                                              float bc2) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P) return;
-  const float g = grad[i] * scale;
-  const float mi = b1 * m[i] + (1.0f - b1) * g;
-  const float vi = b2 * v[i] + (1.0f - b2) * g * g;
+  // meta/train.py:128 x.mean(axis=0): the agent sum divided by the count
+  const float g = grad[i] / n_mean;
+  // optax 0.1.5 update_moment / update_moment_per_elem_norm: (1 - decay) * g + decay * t, with (1 - decay)
+  // rounded once from the python float (omb1, omb2) and g**2 formed before the scale
+  const float mi = omb1 * g + b1 * m[i];
+  const float vi = omb2 * (g * g) + b2 * v[i];
   m[i] = mi;
   v[i] = vi;
+  // bias_correction: t / (1 - decay**count); updates = mu_hat / (sqrt(nu_hat + 0) + eps); scale(lr); scale(-1)
   const float mh = mi / bc1, vh = vi / bc2;
   eta[i] = eta[i] + (-(lr * (mh / (sqrtf(vh) + eps))));
 }
@@ -1470,12 +1475,16 @@ int toued_init_tables_masked(const uint32_t* keys, int n, int cols, int D, float
   return 0;
 }
 
-int toued_adam(int P, float* eta, const float* grad, float* m, float* v, float scale, float lr, float b1, float b2,
+int toued_adam(int P, float* eta, const float* grad, float* m, float* v, float n_mean, float lr, double b1, double b2,
                float eps, int count, hipStream_t stream) {
+  TOUED_REQUIRE(count >= 1 && n_mean > 0.0f, "toued_adam: count=%d n_mean=%g", count, (double)n_mean);
   if (P == 0) return 0;
-  const float bc1 = 1.0f - powf(b1, (float)count), bc2 = 1.0f - powf(b2, (float)count);
-  hipLaunchKernelGGL(k_adam, dim3(nb256(P)), dim3(256), 0, stream, P, eta, grad, m, v, scale, lr, b1, b2, eps, bc1,
-                     bc2);
+  // jax weak-typed python floats: decay -> f32(b), (1 - decay) -> f32(1.0 - b) rounded from double;
+  // decay**count in f32 (int32 count), then 1 - that in f32
+  const float b1f = (float)b1, b2f = (float)b2;
+  const float bc1 = 1.0f - powf(b1f, (float)count), bc2 = 1.0f - powf(b2f, (float)count);
+  hipLaunchKernelGGL(k_adam, dim3(nb256(P)), dim3(256), 0, stream, P, eta, grad, m, v, n_mean, lr, b1f,
+                     (float)(1.0 - b1), b2f, (float)(1.0 - b2), eps, bc1, bc2);
   TOUED_CHECK_LAUNCH();
   return 0;
 }

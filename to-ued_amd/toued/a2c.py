@@ -40,6 +40,9 @@ class A2CTrainer:
         self._bufs = None
         self._graph = None
         self._graph_key = None
+        # test hook: a list here makes train() run eagerly and append, after every update, the actor/critic
+        # tables it started from, the rollout it ran and the tables it produced (tests/test_gpu_plr.py)
+        self.record = None
 
     def _alloc(self, n, D, W, T, U, dev):
         key = (n, D, W, T, U, str(dev))
@@ -60,7 +63,7 @@ class A2CTrainer:
         self._graph = None
         return self._bufs
 
-    def _updates(self, b, n, D, W, T, U):
+    def _updates(self, b, n, D, W, T, U, record=None):
         L = _lib
         st = L.stream_ptr()
         b["loss"].zero_()
@@ -72,6 +75,8 @@ class A2CTrainer:
         fits = bool(L.lib().toued_a2c_update_fits(W, T, D))
         fused = fits if self.fused is None else (self.fused and fits)
         for u in range(U):
+            if record is not None:
+                before = (b["theta"].clone(), b["vcrit"].clone(), b["step"].clone())
             L.call("toued_rollout", self.ro._c, L.ptr(b["levels"]), L.ptr(b["theta"]), D, L.ptr(b["chain"][u]),
                    L.ptr(b["state"]), n, W, T, L.ptr(tr.obs_idx), L.ptr(tr.obs_time), L.ptr(tr.action),
                    L.ptr(tr.reward), L.ptr(tr.done), None, st)
@@ -80,12 +85,18 @@ class A2CTrainer:
                        L.ptr(tr.obs_time), L.ptr(tr.action), L.ptr(tr.reward), L.ptr(tr.done), self.hyp.gamma,
                        self.hyp.gae_lambda, self.hyp.entropy_coeff, lr_a, lr_c, mn, L.ptr(b["step"]),
                        L.ptr(b["levels"]), L.ptr(b["loss"]), st)
-                continue
-            L.call("toued_a2c_grad", n, W, T, D, L.ptr(b["theta"]), L.ptr(b["vcrit"]), L.ptr(tr.obs_idx),
-                   L.ptr(tr.obs_time), L.ptr(tr.action), L.ptr(tr.reward), L.ptr(tr.done), self.hyp.gamma,
-                   self.hyp.gae_lambda, self.hyp.entropy_coeff, L.ptr(b["Ga"]), L.ptr(b["Gv"]), L.ptr(b["loss"]), st)
-            L.call("toued_a2c_apply", n, D, L.ptr(b["theta"]), L.ptr(b["vcrit"]), L.ptr(b["Ga"]), L.ptr(b["Gv"]),
-                   lr_a, lr_c, mn, L.ptr(b["step"]), L.ptr(b["levels"]), st)
+            else:
+                L.call("toued_a2c_grad", n, W, T, D, L.ptr(b["theta"]), L.ptr(b["vcrit"]), L.ptr(tr.obs_idx),
+                       L.ptr(tr.obs_time), L.ptr(tr.action), L.ptr(tr.reward), L.ptr(tr.done), self.hyp.gamma,
+                       self.hyp.gae_lambda, self.hyp.entropy_coeff, L.ptr(b["Ga"]), L.ptr(b["Gv"]), L.ptr(b["loss"]),
+                       st)
+                L.call("toued_a2c_apply", n, D, L.ptr(b["theta"]), L.ptr(b["vcrit"]), L.ptr(b["Ga"]), L.ptr(b["Gv"]),
+                       lr_a, lr_c, mn, L.ptr(b["step"]), L.ptr(b["levels"]), st)
+            if record is not None:
+                record.append({"theta": before[0], "vcrit": before[1], "step": before[2],
+                               "traj": Transition(tr.obs_idx.clone(), tr.obs_time.clone(), tr.action.clone(), tr.reward.clone(),
+                                                  tr.done.clone()), "theta_out": b["theta"].clone(),
+                               "vcrit_out": b["vcrit"].clone(), "step_out": b["step"].clone()})
 
     def train(self, rng: torch.Tensor, theta: torch.Tensor, vcrit: torch.Tensor, step: torch.Tensor,
               levels: torch.Tensor, state: torch.Tensor, num_train_steps: int):
@@ -101,7 +112,9 @@ class A2CTrainer:
         for name, src in (("rng", rng), ("theta", theta), ("vcrit", vcrit.reshape(n, D)), ("step", step),
                           ("levels", levels), ("state", state)):
             b[name].copy_(src)
-        if self.use_graph and U > 0:
+        if self.record is not None:
+            self._updates(b, n, D, W, T, U, self.record)
+        elif self.use_graph and U > 0:
             if self._graph is None:
                 # warm the path once outside capture (library load, kernel code objects)
                 s = torch.cuda.Stream(device=theta.device)

@@ -136,8 +136,9 @@ class LevelSampler:
     def initial_sample(self, rng, level_buffer, batch_size: int, create_value_critics_flag: bool, sl=None):
         """level_sampler.py:103-132.  ``sl`` = (lo, hi, total) agent slice of this rank."""
         n_local = batch_size if sl is None else sl[1] - sl[0]
-        rng, sub = self._split2(rng)
         if self.score_function == "random":
+            # only the random branch splits here (level_sampler.py:112-114); the buffer branch does not
+            rng, sub = self._split2(rng)
             levels = self._sample_random_levels(sub, batch_size, sl)
         else:
             levels = self._slice(level_buffer.levels[:batch_size], sl)

@@ -255,7 +255,7 @@ class MetaGradStep:
             self.world.all_reduce_sum(self.grad)
             n_total = N * self.world.size
         adam.count += 1
-        L.call("toued_adam", self.lay.size, ptr(eta), ptr(self.grad), ptr(adam.m), ptr(adam.v), 1.0 / n_total,
+        L.call("toued_adam", self.lay.size, ptr(eta), ptr(self.grad), ptr(adam.m), ptr(adam.v), float(n_total),
                hyp.lpg_lr, 0.9, 0.999, 1e-8, adam.count, st)
         # ---------------- agent state out + metrics
         main.wait_stream(self.side)
