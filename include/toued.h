@@ -56,6 +56,9 @@ int toued_fold_in(const uint32_t* keys, int n, uint32_t data, uint32_t* out, hip
 int toued_random_bits(const uint32_t* keys, int n, int m, uint32_t* out, hipStream_t stream);
 /* out[i][j] = jax.random.uniform(keys[i], (m,), minval=lo, maxval=hi)[j] */
 int toued_uniform(const uint32_t* keys, int n, int m, float lo, float hi, float* out, hipStream_t stream);
+/* out[i][j] = jax.random.normal(keys[i], (m,))[j] in f32 (sqrt2 * erf_inv(uniform(nextafter(-1, 0), 1)));
+ * used by the flax orthogonal initialiser of the LPG GRU (jax/_src/nn/initializers.py orthogonal) */
+int toued_normal(const uint32_t* keys, int n, int m, float* out, hipStream_t stream);
 
 /* ---- Level generator: environments/environments.py:22-37 reset_env_params
  *      + environments/gridworld/configs.py:12-126 (vmapped over keys). ---- */

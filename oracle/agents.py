@@ -3,8 +3,8 @@
 agents/agents.py:31-56  create_agent: actor_rng, critic_rng = split(rng); each TrainState's
                         params = model.init(rng, ones(obs_shape)) (models/agent.py:7-45)
 flax 0.6.11 (setup/requirements-base.txt:4, not vendored) initialises the Dense kernel with
-  key = fold_in(fold_in(rng, sha1("Dense_0")[:4] big-endian), 1)   (core/scope.py LazyRng /
-        _legacy_rng_fold_in: the child scope name, then the 'params' counter)
+  key = fold_in(rng, sha1("Dense_0" + b"\x01")[:4] big-endian)   (core/scope.py lazy RNG: the module
+        path and the 'params' counter hashed together, oracle/flaxinit.py)
   lecun_normal = truncated_normal(key, -2, 2, (D, cols)) * sqrt(1/D) / .87962566103423978
 agents/agents.py:98-106 eval_agent.
 This derivation is restated from the flax sources' published algorithm; no reference output
@@ -12,20 +12,15 @@ pins it (parity unpinned beyond the PRNG known-answer vectors).
 """
 from __future__ import annotations
 
-import hashlib
-
 import numpy as np
 
+from . import flaxinit
 from . import jaxrand as jr
 from . import rollout as oro
 
-DENSE0_HASH = int.from_bytes(hashlib.sha1(b"Dense_0").digest()[:4], "big")
-
 
 def lecun_table(key, D: int, cols: int) -> np.ndarray:
-    k = jr.fold_in(jr.fold_in(key, DENSE0_HASH), 1)
-    std = np.float32(np.sqrt(np.float32(1.0 / D))) / np.float32(0.87962566103423978)
-    return (jr.truncated_normal(k, -2.0, 2.0, (D, cols)) * std).astype(np.float32)
+    return flaxinit.dense0_table(key, D, cols)
 
 
 def create_agent(key, D: int, critic_dims: int):

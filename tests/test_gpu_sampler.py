@@ -131,3 +131,32 @@ def test_initial_sample_buffer_mode_agent_keys():
     lv, th, ph, st, _ = osp.initial_sample(spec, mode, "alg_regret", k_init, obuf, N, 64, 8, False)
     _check_agents(spec, agents, lv, th, ph, st, None, np.zeros(N, np.int32))
     assert buf.active.cpu().numpy().tolist() == [True] * N + [False] * (B - N)
+
+
+@pytest.mark.parametrize("F", [5, 7])
+def test_flax_lpg_init_matches_oracle(F):
+    """create_lpg_train_state (meta/meta.py:21-22): the device's flax init of eta from lpg_rng vs
+    oracle/flaxinit.lpg_init — lecun_normal kernels bit-exact, orthogonal recurrent kernels within 1e-6
+    (float64 QR of bit-exact normal draws on both sides), zero biases; and Trainer starts from it."""
+    from oracle import flaxinit
+    from toued.lpg import LPGLayout, flax_init_lpg_params
+    key = jr.split(jr.PRNGKey(0), 3)[1]                       # train.py:17 rng, lpg_rng, buffer_rng
+    got = flax_init_lpg_params(dk(key), F).cpu().numpy()
+    ref = flaxinit.lpg_init(key, F)
+    lay = LPGLayout(F)
+    for name, shape in lay.shapes.items():
+        o = lay.offsets[name]
+        g, r = got[o:o + int(np.prod(shape))], ref[o:o + int(np.prod(shape))]
+        if name in ("hn_w", "hr_w", "hz_w"):
+            np.testing.assert_allclose(g, r, atol=1e-6, rtol=0, err_msg=name)
+            q = g.reshape(shape).astype(np.float64)
+            np.testing.assert_allclose(q.T @ q, np.eye(shape[0]), atol=1e-5)
+        else:
+            assert np.array_equal(g, r), name
+    from toued.parse_args import parse_args
+    from toued.train import Trainer
+    args = ["--env_mode", "dense", "--num_agents", "2", "--num_mini_batches", "1"]
+    if F == 7:
+        args.append("--lifetime_conditioning")
+    tr = Trainer(parse_args(args))
+    assert np.array_equal(tr.eta.cpu().numpy(), got)

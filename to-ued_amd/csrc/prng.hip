@@ -43,6 +43,17 @@ __global__ void __launch_bounds__(256) k_uniform(const uint32_t* __restrict__ ke
                              hi);
 }
 
+// normal(keys[i], (m,))[j] (jax.random.normal, f32): sqrt2 * erf_inv(uniform(nextafter(-1, 0), 1))
+__global__ void __launch_bounds__(256) k_normal(const uint32_t* __restrict__ keys, int m, float* __restrict__ out,
+                                                int n) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)n * m) return;
+  const int i = (int)(t / m), j = (int)(t - (long)i * m);
+  const float u = uniform_from_bits(random_bits_at(make_uint2(keys[2 * i], keys[2 * i + 1]), (uint32_t)m, (uint32_t)j),
+                                    -0.99999994f, 1.0f);
+  out[t] = __fmul_rn(1.41421354f, erfinv_giles(u));
+}
+
 }  // namespace
 
 extern "C" {
@@ -78,6 +89,15 @@ int toued_uniform(const uint32_t* keys, int n, int m, float lo, float hi, float*
   const long tot = (long)n * m;
   if (tot == 0) return 0;
   hipLaunchKernelGGL(k_uniform, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, keys, m, lo, hi, out, n);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_normal(const uint32_t* keys, int n, int m, float* out, hipStream_t stream) {
+  TOUED_REQUIRE(n >= 0 && m >= 1, "toued_normal: n=%d m=%d", n, m);
+  const long tot = (long)n * m;
+  if (tot == 0) return 0;
+  hipLaunchKernelGGL(k_normal, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, keys, m, out, n);
   TOUED_CHECK_LAUNCH();
   return 0;
 }

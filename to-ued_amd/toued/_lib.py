@@ -36,6 +36,7 @@ _SIGS = {
     "toued_fold_in": [_P, _I, _U, _P, _P],
     "toued_random_bits": [_P, _I, _I, _P, _P],
     "toued_uniform": [_P, _I, _I, _F, _F, _P, _P],
+    "toued_normal": [_P, _I, _I, _P, _P],
     "toued_mode_program_bytes": [],
     "toued_level_gen": [_P, _P, _P, _P, _P, _I, _P],
     "toued_level_gen_masked": [_P, _P, _P, _P, _I, _P, _P],

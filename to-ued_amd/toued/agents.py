@@ -23,9 +23,20 @@ from .env import get_agent_hypers
 # lax.erf(-+2 / sqrt2) in float32 (XLA's f32 erf; equals the correctly rounded value here)
 TN_LO = -0.9544997215270996
 TN_HI = 0.9544997215270996
-# flax 0.6.11 param-key derivation (core/scope.py LazyRng + _legacy_rng_fold_in): the kernel of
-# the module's inline Dense is drawn with fold_in(fold_in(rng, sha1("Dense_0")[:4]), 1).
-DENSE0_HASH = int.from_bytes(hashlib.sha1(b"Dense_0").digest()[:4], "big")
+
+
+def flax_static_hash(path) -> int:
+    """flax 0.6.11 param-key derivation (core/scope.py, lazy RNG): ``self.param`` draws with
+    fold_in(rng, h) where h = the first 4 bytes (big-endian) of sha1 over the module path names and the
+    scope's 'params' counter (minimal big-endian bytes), hashed together without separators."""
+    m = hashlib.sha1()
+    for x in path:
+        m.update(x.encode("utf-8") if isinstance(x, str) else x.to_bytes((x.bit_length() + 7) // 8, "big"))
+    return int.from_bytes(m.digest()[:4], "big")
+
+
+# the kernel of Actor / Critic's inline Dense (models/agent.py:7-45, actor_net=()): path Dense_0, counter 1
+DENSE0_HASH = flax_static_hash(("Dense_0", 1))
 
 
 @dataclass
@@ -57,7 +68,7 @@ def lecun_tables(keys: torch.Tensor, D: int, cols: int) -> torch.Tensor:
     stddev = sqrt(1/D) / .87962566103423978 in float32.  Returns [n, D, cols], one per key."""
     n = keys.shape[0]
     out = torch.empty((n, D, cols), dtype=torch.float32, device=keys.device)
-    pkeys = prng.fold_in(prng.fold_in(keys.contiguous(), DENSE0_HASH), 1)
+    pkeys = prng.fold_in(keys.contiguous(), DENSE0_HASH)
     std = float(np.float32(np.sqrt(np.float32(1.0 / D))) / np.float32(0.87962566103423978))
     _lib.call("toued_init_tables", _lib.ptr(pkeys.contiguous()), n, cols, D, TN_LO, TN_HI, std, _lib.ptr(out),
               _lib.stream_ptr())
@@ -68,7 +79,7 @@ def lecun_tables_into(keys: torch.Tensor, out: torch.Tensor, mask: torch.Tensor)
     """``lecun_tables(keys, D, cols)`` written in place into ``out`` [n, D, cols] for the tables with
     ``mask`` (u8 [n]) set; the others keep their values (the level sampler's where(terminated, new, old))."""
     n, D, cols = out.shape
-    pkeys = prng.fold_in(prng.fold_in(keys.contiguous(), DENSE0_HASH), 1)
+    pkeys = prng.fold_in(keys.contiguous(), DENSE0_HASH)
     std = float(np.float32(np.sqrt(np.float32(1.0 / D))) / np.float32(0.87962566103423978))
     _lib.call("toued_init_tables_masked", _lib.ptr(pkeys.contiguous()), n, cols, D, TN_LO, TN_HI, std, _lib.ptr(out),
               _lib.ptr(mask), _lib.stream_ptr())

@@ -22,7 +22,7 @@ from collections import OrderedDict
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, prng
 
 H, Y, E = 256, 8, 16
 _OFF_ORDER = ("pi_b", "pi_w", "y_b", "y_w", "hn_b", "hn_w", "hr_w", "hz_w", "in_b", "in_w", "ir_b", "ir_w",
@@ -64,13 +64,59 @@ class LPGLayout:
         return self._c_off
 
 
-def init_lpg_params(seed: int, F: int, device=None) -> torch.Tensor:
-    """flax-like LPG initialisation (lecun-normal kernels, orthogonal recurrent kernels, zero biases).
+# create_lpg_train_state (meta/meta.py:21-22): the flax module path of each weight (models/lpg.py:38-85 --
+# MLP_0 embedding, LPGGRU_0/GRUCell_0 gates under nn.scan with split_rngs={"params": False}, Dense_0/Dense_1
+# heads) and its initialiser (flax 0.6.11 Dense: lecun_normal kernel, zero bias; GRUCell: lecun_normal input
+# kernels, orthogonal recurrent kernels, zero biases).  Every kernel is its module's first param (counter 1).
+_GRU_PATH = ("LPGGRU_0", "GRUCell_0")
+FLAX_PARAM_PATHS = {
+    "pi_w": ("lecun", ("Dense_0",)), "y_w": ("lecun", ("Dense_1",)),
+    "hn_w": ("orth", _GRU_PATH + ("hn",)), "hr_w": ("orth", _GRU_PATH + ("hr",)),
+    "hz_w": ("orth", _GRU_PATH + ("hz",)), "in_w": ("lecun", _GRU_PATH + ("in",)),
+    "ir_w": ("lecun", _GRU_PATH + ("ir",)), "iz_w": ("lecun", _GRU_PATH + ("iz",)),
+    "e1_w": ("lecun", ("MLP_0", "Dense_0")), "e2_w": ("lecun", ("MLP_0", "Dense_1")),
+}
 
-    flax's exact init RNG derivation (per-module fold_in of the init key) is not
-    reproduced — parity unpinned, documented in DESIGN.md; the distribution matches.
-    Runs once at start-up on the host (numpy), then lives on the GPU.
-    """
+
+def flax_init_lpg_params(lpg_rng: torch.Tensor, F: int) -> torch.Tensor:
+    """``lpg_model.init(lpg_rng, ...)["params"]`` (meta/meta.py:21-22) as the flat f32 eta on lpg_rng's device.
+
+    Per-weight keys: fold_in(lpg_rng, sha1(path + counter)) (flax lazy RNG, toued.agents.flax_static_hash).
+    lecun_normal kernels are drawn by the truncated-normal table kernel (toued_init_tables); the orthogonal
+    recurrent kernels draw normal(key, (256, 256)) on the device (toued_normal) and take the sign-fixed QR
+    factor Q * sign(diag R) (jax/_src/nn/initializers.py orthogonal) -- one 256x256 float64 QR per gate at
+    start-up, on the host."""
+    from .agents import TN_HI, TN_LO, flax_static_hash
+    dev = lpg_rng.device
+    out = torch.zeros(LPGLayout(F).size, dtype=torch.float32, device=dev)
+    lay = LPGLayout(F)
+    key = lpg_rng.reshape(1, 2).contiguous()
+    for name, shape in layout(F).items():
+        if name.endswith("_b"):
+            continue
+        kind, path = FLAX_PARAM_PATHS[name]
+        pk = prng.fold_in(key, flax_static_hash(path + (1,))).contiguous()
+        dst = lay.view(out, name)
+        if kind == "orth":
+            n = shape[0]
+            a = torch.empty(n * n, dtype=torch.float32, device=dev)
+            _lib.call("toued_normal", _lib.ptr(pk), 1, n * n, _lib.ptr(a), _lib.stream_ptr())
+            q, r = torch.linalg.qr(a.reshape(n, n).cpu().double())
+            dst.copy_((q * torch.sign(torch.diagonal(r))[None, :]).float())
+        else:
+            fan_in, cols = shape
+            std = float(np.float32(np.sqrt(np.float32(1.0 / fan_in))) / np.float32(0.87962566103423978))
+            tab = torch.empty((fan_in, cols), dtype=torch.float32, device=dev)
+            _lib.call("toued_init_tables", _lib.ptr(pk), 1, cols, fan_in, TN_LO, TN_HI, std, _lib.ptr(tab),
+                      _lib.stream_ptr())
+            dst.copy_(tab)
+    return out
+
+
+def init_lpg_params(seed: int, F: int, device=None) -> torch.Tensor:
+    """Random LPG parameters with flax's init distributions (lecun-normal kernels, orthogonal recurrent
+    kernels, zero biases) seeded from numpy -- a test utility for arbitrary eta; the training driver uses
+    flax_init_lpg_params (the reference's own values).  Runs on the host, then lives on the GPU."""
     rs = np.random.RandomState(seed)
     parts = []
     for k, s in layout(F).items():

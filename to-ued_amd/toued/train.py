@@ -22,7 +22,7 @@ import torch
 from . import prng
 from .dist import World, init_from_env
 from .level_sampler import LevelSampler
-from .lpg import init_lpg_params
+from .lpg import flax_init_lpg_params
 from .meta import AdamState, LpgHyperparams, MetaGradStep
 from .parse_args import parse_args
 
@@ -60,8 +60,8 @@ class Trainer:
         ks = prng.split(rng, 3)
         self.rng, lpg_rng, buffer_rng = ks[0].contiguous(), ks[1].contiguous(), ks[2].contiguous()
         F = 7 if args.lifetime_conditioning else 5
-        # LPG init: flax init key derivation unpinned -> seeded by the key's low word
-        self.eta = init_lpg_params(int(prng.to_uint32_numpy(lpg_rng)[1]), F, self.dev)
+        # create_lpg_train_state (meta/meta.py:21-22): flax's init of the LPG from lpg_rng
+        self.eta = flax_init_lpg_params(lpg_rng, F)
         self.sampler = LevelSampler(args, self.dev, self.world)
         self.buffer = self.sampler.initialize_buffer(buffer_rng)
         ks = prng.split(self.rng, 2)
