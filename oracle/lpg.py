@@ -87,10 +87,13 @@ def embed(P, y):
 
 
 def lpg_apply(flat, r, d, pi, yt, yt1, step=None, lifetime=None, H: int = 256, Y: int = 8, E: int = 16,
-              return_states=False):
+              return_states=False, relu_mask=None, h_record=None):
     """models/lpg.py:48-85.  r,d,pi [B,T]; yt,yt1 [B,T,Y] -> pi_hat [B,T], y_hat [B,T,Y].
 
     step/lifetime: per-batch-row scalars [B] (raw values) when lifetime conditioning.
+    relu_mask [B,T,H] (0/1), when given, replaces the ``h > 0`` decision of nn.relu(x) (models/lpg.py:81):
+    a caller comparing with a float32 implementation takes its branch at outputs within rounding of the
+    kink (the tests check that every disagreement sits there).  h_record (list) receives h_out [B,T,H].
     """
     F = 7 if step is not None else 5
     P = unflatten(flat, F, H, Y, E)
@@ -120,7 +123,9 @@ def lpg_apply(flat, r, d, pi, yt, yt1, step=None, lifetime=None, H: int = 256, Y
         h = (1.0 - zg) * ng + zg * h
         outs[t] = h
     hs = torch.stack(outs, dim=1)                           # [B,T,H]
-    a = torch.relu(hs)
+    if h_record is not None:
+        h_record.append(hs.detach())
+    a = torch.relu(hs) if relu_mask is None else hs * relu_mask.to(hs.dtype)
     pi_hat = (a @ P["pi_w"] + P["pi_b"])[..., 0]
     y_hat = torch.softmax(a @ P["y_w"] + P["y_b"], dim=-1)
     if return_states:

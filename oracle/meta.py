@@ -43,7 +43,7 @@ class Hypers:
     gamma: float = 0.99
     gae_lambda: float = 0.95
     lifetime_conditioning: bool = False
-    stop_gradient: bool = True   # lpg_agent.py:170-172; False only for finite-difference self-tests
+    stop_gradient: bool = True   # agents/lpg_agent.py:54-56; False only for finite-difference self-tests
 
 
 def linear_logits(table, idx, time):
@@ -65,8 +65,9 @@ def entropy(probs):
     return -torch.mean(torch.sum(p * torch.log(p), dim=-1))
 
 
-def lpg_agent_step(theta, phi, step, lifetime, eta, traj, hyp: Hypers):
+def lpg_agent_step(theta, phi, step, lifetime, eta, traj, hyp: Hypers, relu_mask=None, h_record=None):
     """agents/lpg_agent.py:31-85 for one agent.  traj: dict of numpy arrays [W,T(+1)].
+    relu_mask / h_record: see oracle/lpg.lpg_apply.
 
     Returns (theta', phi', step', metrics dict, (pi_hat, y_hat))."""
     idx, tm = traj["idx"], traj["time"]
@@ -83,9 +84,11 @@ def lpg_agent_step(theta, phi, step, lifetime, eta, traj, hyp: Hypers):
     if hyp.lifetime_conditioning:
         st = torch.full((W,), float(step), dtype=theta.dtype)
         lt = torch.full((W,), float(lifetime), dtype=theta.dtype)
-        pi_hat, y_hat = olpg.lpg_apply(eta, r, d, sg(pi), sg(y_t), sg(y_tp1), st, lt)
+        pi_hat, y_hat = olpg.lpg_apply(eta, r, d, sg(pi), sg(y_t), sg(y_tp1), st, lt, relu_mask=relu_mask,
+                                       h_record=h_record)
     else:
-        pi_hat, y_hat = olpg.lpg_apply(eta, r, d, sg(pi), sg(y_t), sg(y_tp1))
+        pi_hat, y_hat = olpg.lpg_apply(eta, r, d, sg(pi), sg(y_t), sg(y_tp1), relu_mask=relu_mask,
+                                       h_record=h_record)
     y_l2 = torch.mean(torch.sum(y_hat * y_hat, -1))
     kl = torch.sum(y_t * (torch.log(y_t + EPS) - torch.log(y_hat + EPS)), -1)        # [W,T]
     actor_loss = torch.log(pi) * pi_hat
@@ -114,13 +117,16 @@ def gae(value, reward, done, gamma, lam):
     return adv, adv + value[..., :-1]
 
 
-def train_agent_meta(eta, theta0, phi0, step0, lifetime, vcrit, trajs, eval_traj, hyp: Hypers, K: int):
-    """meta/train.py:88-170 (_train_agent) for one agent, given K train trajectories and the
-    eval trajectory (all dicts of numpy [W, T(+1)]).  Returns (reg_lpg_loss, aux dict)."""
+def train_agent_meta(eta, theta0, phi0, step0, lifetime, vcrit, trajs, eval_traj, hyp: Hypers, K: int,
+                     relu_masks=None, h_record=None):
+    """meta/train.py:36-100 (_train_agent) for one agent, given K train trajectories and the
+    eval trajectory (all dicts of numpy [W, T(+1)]).  Returns (reg_lpg_loss, aux dict).
+    relu_masks: optional per-update LPG relu decisions [W,T,H] (oracle/lpg.lpg_apply)."""
     theta, phi, step = theta0, phi0, step0
     mets = []
     for k in range(K):
-        theta, phi, step, m, _ = lpg_agent_step(theta, phi, step, lifetime, eta, trajs[k], hyp)
+        mk = None if relu_masks is None else torch.as_tensor(relu_masks[k])
+        theta, phi, step, m, _ = lpg_agent_step(theta, phi, step, lifetime, eta, trajs[k], hyp, mk, h_record)
         tr = trajs[k]
         m["policy_entropy"] = entropy(torch.softmax(linear_logits(theta, tr["idx"][:, :-1], tr["time"][:, :-1]), -1))
         m["critic_entropy"] = entropy(torch.softmax(linear_logits(phi, tr["idx"][:, :-1], tr["time"][:, :-1]), -1))
@@ -158,7 +164,8 @@ def meta_gradient(eta_np, agents, hyp: Hypers, K: int, dtype=torch.float64):
         theta = torch.tensor(ag["theta"], dtype=dtype, requires_grad=True)
         phi = torch.tensor(ag["phi"], dtype=dtype, requires_grad=True)
         vc = torch.tensor(ag["vcrit"], dtype=dtype)
-        reg, aux = train_agent_meta(eta, theta, phi, ag["step"], ag["lifetime"], vc, ag["trajs"], ag["eval"], hyp, K)
+        reg, aux = train_agent_meta(eta, theta, phi, ag["step"], ag["lifetime"], vc, ag["trajs"], ag["eval"], hyp, K,
+                                    ag.get("relu_masks"), ag.get("h_record"))
         g = torch.autograd.grad(reg, eta)[0]
         grads.append(g.detach().numpy())
         auxs.append({k: (v.detach().numpy() if torch.is_tensor(v) else
