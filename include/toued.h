@@ -139,6 +139,13 @@ int toued_a2c_update(int N, int W, int T, int D, float* theta, float* vcrit, con
                      const uint8_t* tact, const float* trew, const uint8_t* tdone, float gamma, float lam,
                      float ent_coef, float lr_a, float lr_c, float max_norm, int* step, const int* levels,
                      float* loss_out, hipStream_t stream);
+/* --fix_value_critic: one update of the meta-gradient value critics vcrit [N][D] on a trajectory (meta/train.py:61-81
+ * with the discarded `.replace` fixed): critic loss mean_w mean_t (target - V)^2 on stop-gradient GAE targets,
+ * clip_by_global_norm + SGD (lr, max_norm), vstep[i] += 1; loss_out[i][1] += the loss before the update.
+ * Deterministic (the sorted-segment kernel of toued_a2c_update); W*T <= 2048. */
+int toued_value_critic_update(int N, int W, int T, int D, float* vcrit, const int* tidx, const int* ttime,
+                              const float* trew, const uint8_t* tdone, float gamma, float lam, float lr,
+                              float max_norm, int* vstep, float* loss_out, hipStream_t stream);
 /* apply_gradients (clip_by_global_norm + SGD, models/optim.py:5-11) for actor and value critic,
  * kept only while step+1 <= levels[i].lifetime (a2c.py:71-75); zeroes Ga/Gv. */
 int toued_a2c_apply(int N, int D, float* theta, float* vcrit, float* Ga, float* Gv, float lr_a, float lr_c,

@@ -44,6 +44,7 @@ class Hypers:
     gae_lambda: float = 0.95
     lifetime_conditioning: bool = False
     stop_gradient: bool = True   # agents/lpg_agent.py:54-56; False only for finite-difference self-tests
+    fix_value_critic: bool = False   # train the value critic (meta/train.py:61-81 without the discarded .replace)
 
 
 def linear_logits(table, idx, time):
@@ -132,7 +133,12 @@ def train_agent_meta(eta, theta0, phi0, step0, lifetime, vcrit, trajs, eval_traj
         m["critic_entropy"] = entropy(torch.softmax(linear_logits(phi, tr["idx"][:, :-1], tr["time"][:, :-1]), -1))
         mets.append(m)
     agent = {k: torch.mean(torch.stack([m[k] for m in mets])) for k in mets[0]}
-    # value critic (frozen: SURVEY B.3), advantage on the eval rollout (agents.py:109-116)
+    # value critic (frozen: SURVEY B.3), advantage on the eval rollout (agents.py:109-116); with
+    # fix_value_critic the scan of _update_critic over the K train rollouts runs first (meta/train.py:74-77)
+    if hyp.fix_value_critic:
+        vcrit = vcrit.detach()
+        for k in range(K):
+            vcrit, _ = value_critic_step(vcrit, trajs[k], hyp)
     ev = eval_traj
     v = linear_logits(vcrit, ev["idx"], ev["time"])[..., 0]                      # [W,T+1]
     r = torch.from_numpy(ev["reward"].astype(np.float64)).to(v.dtype)
@@ -149,7 +155,24 @@ def train_agent_meta(eta, theta0, phi0, step0, lifetime, vcrit, trajs, eval_traj
            - hyp.target_entropy_coeff * agent["critic_entropy"] + hyp.target_l2_coeff * agent["critic_l2"])
     aux = {"lpg_loss": lpg_loss, "reg_lpg_loss": reg, "value_loss": value_loss, "lpg_agent": agent,
            "theta": theta, "phi": phi, "step": step}
+    if hyp.fix_value_critic:        # meta/train.py:78-81: the eval-rollout update after its loss and advantages
+        aux["vcrit"], _ = value_critic_step(vcrit, ev, hyp)
     return reg, aux
+
+
+def value_critic_step(vcrit, traj, hyp: Hypers):
+    """_update_critic (meta/train.py:61-72) as the reference means it: compute_advantage (agents/agents.py:109-116)
+    per worker -- mean_t (target - V)^2 on stop-gradient GAE targets -- mean over workers, its gradient,
+    clip_by_global_norm + SGD (critic lr, max_norm).  vcrit [D, 1].  Returns (vcrit', loss)."""
+    vc = vcrit.detach().requires_grad_(True)
+    v = linear_logits(vc, traj["idx"], traj["time"])[..., 0]
+    r = torch.from_numpy(traj["reward"].astype(np.float64)).to(v.dtype)
+    dn = torch.from_numpy(traj["done"].astype(np.float64)).to(v.dtype)
+    adv, target = gae(v, r, dn, hyp.gamma, hyp.gae_lambda)
+    loss = torch.mean(torch.mean((target.detach() - v[:, :-1]) ** 2, -1))
+    g = torch.autograd.grad(loss, vc)[0]
+    with torch.no_grad():
+        return clip_sgd(vc, g, hyp.critic_lr, hyp.max_grad_norm).detach(), float(loss)
 
 
 def meta_gradient(eta_np, agents, hyp: Hypers, K: int, dtype=torch.float64):

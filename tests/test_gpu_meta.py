@@ -317,3 +317,124 @@ def test_train_main_writes_checkpoints(tmp_path, extra):
     if extra:
         b = restore_checkpoint(str(tmp_path), prefix="buffer_")
         assert b["levels"].shape[1] == 64 and b["score"].dtype == np.float32
+
+
+def _agents_for(mode, N, W, T, seed):
+    from toued import prng
+    from toued.agents import AgentBatch, create_agents, create_value_critics
+    from toued.env import LevelGenerator
+    from toued.rollout import RolloutWrapper
+    dk = lambda a: prng.from_uint32_numpy(a, "cuda")
+    levels = LevelGenerator(mode)(dk(jr.split(jr.PRNGKey(seed), N)))
+    ro = RolloutWrapper(mode, T, env_workers=W)
+    theta, phi = create_agents(dk(jr.split(jr.PRNGKey(seed + 1), N)), ro.obs_dim, 8)
+    vcrit = create_value_critics(dk(jr.split(jr.PRNGKey(seed + 2), N)), ro.obs_dim)
+    (_, _), state = ro.batch_reset(dk(jr.split(jr.PRNGKey(seed + 3), N)), levels)
+    z = lambda: torch.zeros(N, dtype=torch.int32, device="cuda")
+    return ro, AgentBatch(levels, theta, phi, z(), state, vcrit, z())
+
+
+def _clone_agents(ag):
+    from toued.agents import AgentBatch
+    return AgentBatch(*(None if x is None else x.clone() for x in
+                        (ag.levels, ag.theta, ag.phi, ag.step, ag.state, ag.vcrit, ag.vstep)))
+
+
+@pytest.mark.parametrize("nmb", [2, 4])
+def test_mini_batches_match_full_batch(nmb):
+    """--num_mini_batches (util/jax.py:25-41 mini_batch_vmap, a numerical no-op): sequential agent chunks give
+    bit-identical agents, env states and metrics, and the same summed meta-gradient up to the summation
+    grouping (1e-6)."""
+    from toued.lpg import init_lpg_params
+    from toued.meta import AdamState, LpgHyperparams, MetaGradStep
+    N, W, T, K = 8, 64, 20, 2
+    ro, ag0 = _agents_for("dense", N, W, T, 70)
+    eta0 = init_lpg_params(71, 5)
+    rng = torch.tensor([0, 123], dtype=torch.int32, device="cuda")
+    out = []
+    for m in (1, nmb):
+        ag = _clone_agents(ag0)
+        eta = eta0.clone()
+        step = MetaGradStep(ro, N, LpgHyperparams(num_agent_updates=K), False, num_mini_batches=m)
+        met = step(rng, eta, AdamState(eta.numel(), "cuda"), ag)
+        torch.cuda.synchronize()
+        out.append((ag, step.grad.clone(), met, eta))
+    (a1, g1, m1, e1), (a2, g2, m2, e2) = out
+    for name in ("theta", "phi", "step", "state", "vstep"):
+        assert torch.equal(getattr(a1, name), getattr(a2, name)), name
+    for k in ("lpg_loss", "value_loss", "lpg_agent_return"):
+        assert torch.equal(m1[k], m2[k]), k
+    for k in m1["lpg_agent"]:
+        assert torch.equal(m1["lpg_agent"][k], m2["lpg_agent"][k]), k
+    assert float((g1 - g2).norm() / g1.norm()) < 1e-6
+    assert float((e1 - e2).abs().max()) < 1e-7
+
+
+def test_1024_agents_two_mini_batches_on_one_gpu():
+    """A reference-legal --num_agents 1024 --num_mini_batches 2 on one GPU (one 512-agent batch alone is the
+    bench's size; 1024 at once exceeds the GRU kernels' 4 GiB operand range): each chunk equals an unchunked
+    512-agent step over the same agents and keys (rank_slice = the chunk of split(rng, 1024))."""
+    from toued.lpg import init_lpg_params
+    from toued.meta import AdamState, LpgHyperparams, MetaGradStep
+    N, W, T, K = 1024, 64, 20, 5
+    ro, ag0 = _agents_for("tabular", N, W, T, 80)
+    eta0 = init_lpg_params(81, 5)
+    rng = torch.tensor([3, 4], dtype=torch.int32, device="cuda")
+    hyp = LpgHyperparams(num_agent_updates=K)
+    ag = _clone_agents(ag0)
+    eta = eta0.clone()
+    big = MetaGradStep(ro, N, hyp, False, num_mini_batches=2)
+    met = big(rng, eta, AdamState(eta.numel(), "cuda"), ag)
+    torch.cuda.synchronize()
+    g_big = big.grad.clone()
+    assert torch.isfinite(g_big).all() and torch.isfinite(met["lpg_agent_return"]).all()
+    del big
+    half = MetaGradStep(ro, 512, hyp, False)
+    g_sum = torch.zeros_like(g_big)
+    for lo in (0, 512):
+        sub = _clone_agents(ag0)
+        from toued.agents import AgentBatch
+        part = AgentBatch(sub.levels[lo:lo + 512].contiguous(), sub.theta[lo:lo + 512].contiguous(),
+                          sub.phi[lo:lo + 512].contiguous(), sub.step[lo:lo + 512].contiguous(),
+                          sub.state[:, lo * W:(lo + 512) * W].contiguous(), sub.vcrit[lo:lo + 512].contiguous(),
+                          sub.vstep[lo:lo + 512].contiguous())
+        half(rng, eta0.clone(), AdamState(eta0.numel(), "cuda"), part, (lo, lo + 512, N))
+        torch.cuda.synchronize()
+        g_sum += half.grad
+        assert torch.equal(part.theta, ag.theta[lo:lo + 512])
+        assert torch.equal(part.state, ag.state[:, lo * W:(lo + 512) * W])
+    assert float((g_sum - g_big).norm() / g_big.norm()) < 1e-6
+
+
+def test_fix_value_critic_matches_oracle():
+    """--fix_value_critic (SURVEY B.3 fixed): the value critic takes K SGD updates on the train rollouts, the
+    eval advantages / value loss use those parameters, then one update on the eval rollout — vs the float64
+    oracle (oracle/meta.value_critic_step); the meta-gradient and agent tables as in the frozen case."""
+    N, W, T, K = 3, 64, 20, 3
+    agents, step, eta, adam, hyp, D = _setup("dense", N, W, T, K)
+    step.hyp.fix_value_critic = True
+    th0, ph0, vc0 = agents.theta.cpu().numpy(), agents.phi.cpu().numpy(), agents.vcrit.cpu().numpy()
+    lv = agents.levels.cpu().numpy()
+    eta0 = eta.cpu().numpy().astype(np.float64)
+    metrics = step(torch.tensor([0, 41], dtype=torch.int32, device="cuda"), eta, adam, agents)
+    torch.cuda.synchronize()
+    tr = step.traj
+    idx, tm, act = tr.obs_idx.cpu().numpy(), tr.obs_time.cpu().numpy(), tr.action.cpu().numpy()
+    rew, dn = tr.reward.cpu().numpy(), tr.done.cpu().numpy()
+
+    def tr_of(k, a):
+        return {"idx": idx[k, a].T.copy(), "time": tm[k, a].T.copy(), "action": act[k, a].T.astype(np.int64),
+                "reward": rew[k, a].T.copy(), "done": dn[k, a].T.astype(bool)}
+    ags = [dict(theta=th0[a], phi=ph0[a], vcrit=vc0[a][:, None], step=0, lifetime=int(lv[a, 5]),
+                trajs=[tr_of(k, a) for k in range(K)], eval=tr_of(K, a)) for a in range(N)]
+    g_ref, aux, _ = ometa.meta_gradient(eta0, ags, ometa.Hypers(fix_value_critic=True), K)
+    vc = agents.vcrit.cpu().numpy().astype(np.float64)
+    for a in range(N):
+        dv, dv_ref = vc[a] - vc0[a], aux[a]["vcrit"][:, 0] - vc0[a]
+        assert np.linalg.norm(dv - dv_ref) <= 2e-5 * np.linalg.norm(dv_ref) + 1e-9, a
+    assert agents.vstep.cpu().tolist() == [K + 1] * N
+    np.testing.assert_allclose(metrics["value_loss"].cpu().numpy(), [x["value_loss"] for x in aux], rtol=2e-5)
+    np.testing.assert_allclose(metrics["lpg_loss"].cpu().numpy(), [x["lpg_loss"] for x in aux], rtol=2e-5,
+                               atol=1e-7)
+    g = step.grad.cpu().numpy() / N
+    assert np.linalg.norm(g - g_ref) / np.linalg.norm(g_ref) < 1e-5

@@ -306,6 +306,10 @@ TOUED_DEV void a2c_sort2048(uint32_t* key, int tid) {
   __syncthreads();
 }
 
+// CRITIC_ONLY: the meta-gradient value critic's own update (meta/train.py:61-81 with the reference's discarded
+// `.replace` fixed, --fix_value_critic): the same critic loss and SGD, no actor, no lifetime discard, `step` is
+// the value critic's TrainState step.
+template <bool CRITIC_ONLY>
 __global__ void __launch_bounds__(256) k_a2c_update(int W, int T, int D, float* __restrict__ theta,
                                                     float* __restrict__ vcrit, const int* __restrict__ tidx,
                                                     const int* __restrict__ ttime, const uint8_t* __restrict__ tact,
@@ -325,22 +329,31 @@ __global__ void __launch_bounds__(256) k_a2c_update(int W, int T, int D, float* 
   uint32_t* key = reinterpret_cast<uint32_t*>(lds + A2CStage::floats(W, T));   // [2048]
   float* vec = reinterpret_cast<float*>(key + A2C_SORT_MAX);                    // [W*T][6]
   float* v = vcrit + (size_t)a * D;
-  float* th = theta + (size_t)a * D * 5;
+  float* th = CRITIC_ONLY ? nullptr : theta + (size_t)a * D * 5;
   if (tid == 0) has_last = 0;
   const float closs = a2c_stage(S, a, W, T, D, v, tidx, ttime, trew, tdone, gamma, lam, red);
   // 1) per-sample row vectors -> LDS, sort keys, time-row partial sums, actor loss
-  float lastA[5];
+  float lastA[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  if (!CRITIC_ONLY) {
 #pragma unroll
-  for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
+    for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
+  }
   const float inv_n = 1.0f / (float)TW;
   const size_t sb = (size_t)a * T * W;
   float part[NV] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, s_al = 0.0f;
   for (int sl = tid; sl < A2C_SORT_MAX; sl += 256) {
     uint32_t kk = NONE;
     if (sl < TW) {
-      float d[5], c, al;
+      float d[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, c, al = 0.0f, dvv;
       int idx;
-      const float dvv = a2c_sample(S, sl, W, T, th, lastA, tact, sb, ent_coef, inv_n, d, idx, c, al);
+      if (CRITIC_ONLY) {
+        const int t = sl / W, w = sl - t * W;
+        idx = S.ix[sl];
+        c = S.cc[sl];
+        dvv = -2.0f * S.dv[w * T + t] * inv_n;
+      } else {
+        dvv = a2c_sample(S, sl, W, T, th, lastA, tact, sb, ent_coef, inv_n, d, idx, c, al);
+      }
       kk = ((uint32_t)idx << 11) | (uint32_t)sl;
 #pragma unroll
       for (int j = 0; j < 5; ++j) { vec[sl * NV + j] = d[j]; part[j] += c * d[j]; }
@@ -428,13 +441,15 @@ __global__ void __launch_bounds__(256) k_a2c_update(int W, int T, int D, float* 
   const float gna = sqrtf(block_sum(na2, red));
   const float gnc = sqrtf(block_sum(nc2, red));
   const int st = step[a];
-  const bool applied = (st + 1) <= levels[(size_t)a * LEVEL_WORDS + L_LIFETIME];
+  const bool applied = CRITIC_ONLY || (st + 1) <= levels[(size_t)a * LEVEL_WORDS + L_LIFETIME];
   const bool clip_a = !(gna < max_norm), clip_c = !(gnc < max_norm);
   auto apply_row = [&](int r, const float* g) {
+    if (!CRITIC_ONLY) {
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const float gg = clip_a ? (g[j] / gna) * max_norm : g[j];
-      th[(size_t)r * 5 + j] = th[(size_t)r * 5 + j] + (-(lr_a * gg));
+      for (int j = 0; j < 5; ++j) {
+        const float gg = clip_a ? (g[j] / gna) * max_norm : g[j];
+        th[(size_t)r * 5 + j] = th[(size_t)r * 5 + j] + (-(lr_a * gg));
+      }
     }
     const float gg = clip_c ? (g[5] / gnc) * max_norm : g[5];
     v[r] = v[r] + (-(lr_c * gg));
@@ -499,13 +514,33 @@ int toued_a2c_update(int N, int W, int T, int D, float* theta, float* vcrit, con
   if (N == 0) return 0;
   static bool attr_set = false;
   if (!attr_set) {
-    TOUED_REQUIRE(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_a2c_update),
+    TOUED_REQUIRE(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_a2c_update<false>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) == hipSuccess,
                   "toued_a2c_update: cannot raise the dynamic LDS limit");
     attr_set = true;
   }
-  hipLaunchKernelGGL(k_a2c_update, dim3(N), dim3(256), lds, stream, W, T, D, theta, vcrit, tidx, ttime, tact, trew,
-                     tdone, gamma, lam, ent_coef, lr_a, lr_c, max_norm, step, levels, loss_out);
+  hipLaunchKernelGGL(k_a2c_update<false>, dim3(N), dim3(256), lds, stream, W, T, D, theta, vcrit, tidx, ttime, tact,
+                     trew, tdone, gamma, lam, ent_coef, lr_a, lr_c, max_norm, step, levels, loss_out);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_value_critic_update(int N, int W, int T, int D, float* vcrit, const int* tidx, const int* ttime,
+                              const float* trew, const uint8_t* tdone, float gamma, float lam, float lr,
+                              float max_norm, int* vstep, float* loss_out, hipStream_t stream) {
+  TOUED_REQUIRE(toued_a2c_update_fits(W, T, D), "toued_value_critic_update: D=%d W=%d T=%d unsupported (W*T <= %d)",
+                D, W, T, A2C_SORT_MAX);
+  if (N == 0) return 0;
+  const size_t lds = a2c_update_lds(W, T);
+  static bool attr_set = false;
+  if (!attr_set) {
+    TOUED_REQUIRE(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_a2c_update<true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) == hipSuccess,
+                  "toued_value_critic_update: cannot raise the dynamic LDS limit");
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k_a2c_update<true>, dim3(N), dim3(256), lds, stream, W, T, D, nullptr, vcrit, tidx, ttime,
+                     nullptr, trew, tdone, gamma, lam, 0.0f, 0.0f, lr, max_norm, vstep, nullptr, loss_out);
   TOUED_CHECK_LAUNCH();
   return 0;
 }

@@ -397,6 +397,44 @@ __global__ void __launch_bounds__(256) k_entropy(int N, int W, int T, int D, con
   }
 }
 
+// Metric mode of the entropies (train_lpg_agent's batch_rollout_entropy, lpg_agent.py:119-120): one block per
+// agent, fixed summation order (per-thread strided partials, then a block reduction), one writer per metric.
+__global__ void __launch_bounds__(256) k_entropy_metric(int W, int T, int D, const float* __restrict__ theta,
+                                                        const float* __restrict__ phi, const int* __restrict__ tidx,
+                                                        const int* __restrict__ ttime, float* __restrict__ met) {
+  __shared__ float red[2][4];
+  const int a = blockIdx.x, tid = threadIdx.x;
+  const float* th = theta + (size_t)a * D * 5;
+  const float* ph = phi + (size_t)a * D * 8;
+  float lastA[5], lastC[8];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
+  float ha = 0.0f, hc = 0.0f;
+  for (int i = tid; i < T * W; i += 256) {
+    const int t = i / W, w = i - t * W;
+    const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
+    const int idx = tidx[o0];
+    const float c = (float)ttime[o0] * 0.001f;
+    float p[5], y[8];
+    probs_of<5>(th, lastA, idx, c, p);
+    probs_of<8>(ph, lastC, idx, c, y);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) ha -= (p[j] + EPSF) * __logf(p[j] + EPSF);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) hc -= (y[j] + EPSF) * __logf(y[j] + EPSF);
+  }
+  ha = wave_sum(ha);
+  hc = wave_sum(hc);
+  if ((tid & 63) == 0) { red[0][tid >> 6] = ha; red[1][tid >> 6] = hc; }
+  __syncthreads();
+  if (tid == 0) {
+    met[a * 8 + 3] += (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    met[a * 8 + 4] += (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  }
+}
+
 // ---------------------------------------------------------------------------- eval loss
 // One block (64 threads) per agent; eval trajectory (T steps).  Outputs per agent:
 // out[a] = {lpg_loss, value_loss}; abar[a*W + w] = mean_t normalised advantage.
@@ -1361,6 +1399,11 @@ int toued_entropy(int N, int W, int T, int D, const float* theta, const float* p
   if (adj_th && !met) {
     EntropyBwdOp op{theta, phi, tidx, ttime, coef_a, coef_c, adj_th, adj_ph, N, W, T, D};
     if (launch_sorted(op, N, stream)) { TOUED_CHECK_LAUNCH(); return 0; }
+  }
+  if (met && !adj_th) {   // metrics only: deterministic per-agent reduction
+    hipLaunchKernelGGL(k_entropy_metric, dim3(N), dim3(256), 0, stream, W, T, D, theta, phi, tidx, ttime, met);
+    TOUED_CHECK_LAUNCH();
+    return 0;
   }
   if (W % 64 == 0)
     hipLaunchKernelGGL(k_entropy<true>, dim3(nb256(n)), dim3(256), 0, stream, N, W, T, D, theta, phi, tidx, ttime,

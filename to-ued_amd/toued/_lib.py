@@ -69,6 +69,7 @@ _SIGS = {
     "toued_choice_cdf": [_P, _P, _I, _I, _P, _P],
     "toued_key_chain": [_P, _I, _I, _P, _P],
     "toued_a2c_grad": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _P, _P, _P, _P],
+    "toued_value_critic_update": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _F, _F, _F, _F, _P, _P, _P],
     "toued_a2c_apply": [_I, _I, _P, _P, _P, _P, _F, _F, _F, _P, _P, _P],
     "toued_a2c_update_fits": [_I, _I, _I],
     "toued_a2c_update": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _F, _P, _P, _P, _P],

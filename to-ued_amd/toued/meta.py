@@ -41,6 +41,7 @@ class LpgHyperparams:
     max_grad_norm: float = 0.5
     lpg_lr: float = 1e-4
     eval_workers: int = 4        # meta/train.py:115
+    fix_value_critic: bool = False   # train the value critic (the reference discards its update)
 
 
 class AdamState:
@@ -87,8 +88,19 @@ class KernelTimers:
 
 
 class MetaGradStep:
+    """``n_agents`` is the agents per call (this rank's); with ``num_mini_batches`` > 1 they run as that many
+    sequential chunks of n_agents / num_mini_batches (util/jax.py:25-41 mini_batch_vmap: chunk i holds agents
+    [i N/nmb, (i+1) N/nmb)), accumulating the summed meta-gradient before the one all-reduce and Adam step.
+    The per-chunk buffers (GRU saves etc.) are sized for one chunk."""
+
     def __init__(self, rollout: RolloutWrapper, n_agents: int, hyp: LpgHyperparams, lifetime_conditioning: bool,
-                 device=None, world=None):
+                 device=None, world=None, num_mini_batches: int = 1):
+        if num_mini_batches < 1 or n_agents % num_mini_batches:
+            raise ValueError(f"this rank's {n_agents} agents do not split into num_mini_batches={num_mini_batches} "
+                             "equal chunks")
+        self.n_total_local = n_agents
+        self.n_chunks = num_mini_batches
+        n_agents //= num_mini_batches
         self.ro = rollout
         self.N = n_agents
         self.W = rollout.env_workers
@@ -123,6 +135,7 @@ class MetaGradStep:
         self.adv = z(N, W, T)
         self.abar = z(N, W)
         self.loss_out = z(N, 2)
+        self.vc_loss = z(N, 2)           # --fix_value_critic update losses (scratch)
         self.adj_th = [z(N, D, 5)]       # adjoint tables, accumulated in place over k (toued_hvp)
         self.adj_ph = [z(N, D, Y)]
         self.coef = z(N, 4)
@@ -151,21 +164,50 @@ class MetaGradStep:
     def __call__(self, rng: torch.Tensor, eta: torch.Tensor, adam: AdamState, agents, rank_slice=None):
         """One meta-gradient train step (meta/train.py:14-130).
 
-        rng: device key [2]; eta: flat LPG params (updated in place); agents: AgentBatch (updated in place:
-        actor/critic tables, steps, env state).  Returns a dict of per-agent metric tensors.
+        rng: device key [2]; eta: flat LPG params (updated in place); agents: AgentBatch of this rank's
+        agents (updated in place: actor/critic tables, steps, env state).  Returns a dict of per-agent metric
+        tensors.
         """
+        # meta/train.py:121 rng = split(rng, num_agents); under data parallelism every rank derives all N
+        # keys and keeps its contiguous slice (identical keys at any world size)
+        n_all = self.n_total_local if rank_slice is None else rank_slice[2]
+        lo = 0 if rank_slice is None else rank_slice[0]
+        keys_all = prng.split(rng, n_all)
+        self.gru.pack(eta)
+        self.grad.zero_()
+        parts = []
+        for c in range(self.n_chunks):
+            a0, a1 = c * self.N, (c + 1) * self.N
+            if self.n_chunks == 1:
+                ag = agents
+            else:
+                ag = AgentChunk(agents, a0, a1, self.W)
+            m = self._chunk(keys_all[lo + a0:lo + a1].contiguous(), eta, ag)
+            if self.n_chunks > 1:     # the metric tensors view per-chunk buffers the next chunk overwrites
+                m = _map_metrics(m, torch.clone)
+                ag.write_back()
+            parts.append(m)
+        # ---------------- mean over agents (+ all-reduce across ranks), Adam (meta/train.py:127-129)
+        n_total = n_all
+        if self.world is not None and self.world.size > 1:
+            self.world.all_reduce_sum(self.grad)
+        adam.count += 1
+        _lib.call("toued_adam", self.lay.size, _lib.ptr(eta), _lib.ptr(self.grad), _lib.ptr(adam.m), _lib.ptr(adam.v),
+                  float(n_total), self.hyp.lpg_lr, 0.9, 0.999, 1e-8, adam.count, _lib.stream_ptr())
+        if len(parts) == 1:
+            return parts[0]
+        return _cat_metrics(parts)
+
+    def _chunk(self, agent_keys: torch.Tensor, eta: torch.Tensor, agents):
+        """_train_agent (meta/train.py:36-117) for one chunk of N agents: the forward, the eval, and the
+        explicit adjoint accumulated into self.grad."""
         L = _lib
         N, W, T, K, D, R = self.N, self.W, self.T, self.K, self.D, self.R
         hyp = self.hyp
         st = L.stream_ptr()
         ptr = L.ptr
-        # meta/train.py:173 rng = split(rng, num_agents); under data parallelism every rank
-        # derives all N keys and keeps its contiguous slice (identical keys at any world size).
-        keys_all = prng.split(rng, agents_total := (self.N if rank_slice is None else rank_slice[2]))
-        agent_keys = keys_all if rank_slice is None else keys_all[rank_slice[0]:rank_slice[1]].contiguous()
         L.call("toued_meta_keys", ptr(agent_keys), N, K, ptr(self.keys_roll), ptr(self.keys_eval),
                ptr(self.keys_ea_reset), ptr(self.keys_ea_roll), st)
-        self.gru.pack(eta)
         self.theta_h[0].copy_(agents.theta)
         self.phi_h[0].copy_(agents.phi)
         self.G_th.zero_()
@@ -197,15 +239,24 @@ class MetaGradStep:
                    ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(self.gstat[k]), st)
             L.call("toued_entropy", N, W, T, D, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(tk.obs_idx),
                    ptr(tk.obs_time), ptr(self.met[k]), 0.0, 0.0, None, None, st)
-        # ---------------- eval rollout + lpg loss (meta/train.py:98-145)
+        # ---------------- value critic on the train rollouts (--fix_value_critic), eval rollout, lpg loss
+        if hyp.fix_value_critic:
+            self.vc_loss.zero_()
+            for k in range(K):
+                self._value_critic_update(self._t(k), agents)
         te = self._t(K)
         self.ro.batch_rollout(self.keys_eval, self.theta_h[K], agents.levels, state, out=te, inplace_state=True)
         L.call("toued_eval_loss", N, W, T, D, ptr(self.theta_h[K]), ptr(agents.vcrit), ptr(te.obs_idx),
                ptr(te.obs_time), ptr(te.action), ptr(te.reward), ptr(te.done), hyp.gamma, hyp.gae_lambda,
                ptr(self.adv), ptr(self.abar), ptr(self.loss_out), st)
-        # value critic "update" (meta/train.py:113-133): the gradient is identically zero,
-        # so only the TrainState step advances (K train rollouts + 1 eval rollout).
-        agents.vstep.add_(K + 1)
+        if hyp.fix_value_critic:
+            self._value_critic_update(te, agents)
+        # value critic (meta/train.py:61-81).  Reference: `value_critic_state.replace(params=...)` is discarded, the
+        # gradient is identically zero, so only the TrainState step advances (K train rollouts + 1
+        # eval rollout) and the advantages come from the frozen critic.  --fix_value_critic: K updates on the
+        # train rollouts, the advantages and value loss at those parameters, then the eval-rollout update.
+        if not hyp.fix_value_critic:
+            agents.vstep.add_(K + 1)
         # eval_agent (agents/agents.py:98-106): fresh 4-worker reset, eval-length rollout, mean return.
         # It only reads theta_K and the levels, and its long sequential rollout occupies few CUs, so it
         # runs on a side stream concurrently with the MFMA-bound backward pass.
@@ -237,7 +288,6 @@ class MetaGradStep:
                    ptr(self.G_ph[k]), ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]), ptr(self.coef), hyp.actor_lr,
                    hyp.critic_lr, hyp.agent_target_coeff, hyp.policy_l2_coeff, hyp.target_l2_coeff,
                    ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]), ptr(self.d_pi_hat[k]), ptr(self.d_y_hat[k]), st)
-        self.grad.zero_()
         self.gru.backward(self.traj.done, eta, self.y_hat, self.d_pi_hat, self.d_y_hat, self.X, self.grad,
                           self.timers)
         tr = self.traj
@@ -249,14 +299,6 @@ class MetaGradStep:
         self._eta(self.grad, "e1_w").add_(emb[16:144].view(8, 16))
         self._eta(self.grad, "e2_b").add_(emb[144:145])
         self._eta(self.grad, "e2_w").add_(emb[145:161].view(16, 1))
-        # ---------------- mean over agents (+ all-reduce across ranks), Adam (meta/train.py:180-181)
-        n_total = N
-        if self.world is not None and self.world.size > 1:
-            self.world.all_reduce_sum(self.grad)
-            n_total = N * self.world.size
-        adam.count += 1
-        L.call("toued_adam", self.lay.size, ptr(eta), ptr(self.grad), ptr(adam.m), ptr(adam.v), float(n_total),
-               hyp.lpg_lr, 0.9, 0.999, 1e-8, adam.count, st)
         # ---------------- agent state out + metrics
         main.wait_stream(self.side)
         ea_cum.record_stream(main)
@@ -276,6 +318,12 @@ class MetaGradStep:
             "lpg_agent_return": ea_cum.mean(dim=1),
         }
 
+    def _value_critic_update(self, tk: Transition, agents):
+        L = _lib
+        L.call("toued_value_critic_update", self.N, self.W, self.T, self.D, L.ptr(agents.vcrit), L.ptr(tk.obs_idx),
+               L.ptr(tk.obs_time), L.ptr(tk.reward), L.ptr(tk.done), self.hyp.gamma, self.hyp.gae_lambda,
+               self.hyp.critic_lr, self.hyp.max_grad_norm, L.ptr(agents.vstep), L.ptr(self.vc_loss), L.stream_ptr())
+
     def _eval_rollout(self, keys, theta, levels, state):
         """Eval-length rollout that only accumulates returns (no trajectory storage)."""
         N = keys.shape[0]
@@ -285,3 +333,38 @@ class MetaGradStep:
         L.call("toued_rollout", self.ro._c, L.ptr(levels), L.ptr(theta), theta.shape[1], L.ptr(keys), L.ptr(state),
                N, n // N, self.ro.eval_rollout_len, None, None, None, None, None, L.ptr(cum), L.stream_ptr())
         return cum
+
+
+class AgentChunk:
+    """Agents [a0, a1) of an AgentBatch as the step sees them: row views of the tables (written in place) and a
+    contiguous copy of the chunk's env-state columns [12, n*W] (the rollout updates it in place), copied back
+    by write_back()."""
+
+    def __init__(self, agents, a0: int, a1: int, W: int):
+        self._src = agents
+        self._cols = (a0 * W, a1 * W)
+        self.levels = agents.levels[a0:a1]
+        self.theta = agents.theta[a0:a1]
+        self.phi = agents.phi[a0:a1]
+        self.step = agents.step[a0:a1]
+        self.vcrit = None if agents.vcrit is None else agents.vcrit[a0:a1]
+        self.vstep = None if agents.vstep is None else agents.vstep[a0:a1]
+        self.state = agents.state[:, self._cols[0]:self._cols[1]].contiguous()
+
+    @property
+    def n(self) -> int:
+        return self.levels.shape[0]
+
+    def write_back(self):
+        self._src.state[:, self._cols[0]:self._cols[1]].copy_(self.state)
+
+
+def _map_metrics(m, fn):
+    return {k: (_map_metrics(v, fn) if isinstance(v, dict) else fn(v)) for k, v in m.items()}
+
+
+def _cat_metrics(parts):
+    out = {}
+    for k, v in parts[0].items():
+        out[k] = _cat_metrics([p[k] for p in parts]) if isinstance(v, dict) else torch.cat([p[k] for p in parts])
+    return out

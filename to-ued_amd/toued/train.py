@@ -5,10 +5,10 @@
 
 One process per GPU (torchrun): agents are sharded over ranks; the LPG
 parameters are replicated and updated identically on every rank after the
-meta-gradient all-reduce.  ``--num_mini_batches`` is accepted and validated
-(the reference's divisibility check) but the whole agent batch runs at once:
-mini-batching is numerically a no-op (util/jax.py:25-41) and 288 GB of HBM
-holds the full batch.
+meta-gradient all-reduce.  ``--num_mini_batches`` splits each rank's agents into
+that many sequential chunks for the meta-gradient (util/jax.py:25-41
+mini_batch_vmap: numerically a no-op, a memory bound); 1 runs the whole batch at
+once, which 288 GB of HBM holds up to ~620 agents per GPU at W=64, T=20, K=5.
 """
 from __future__ import annotations
 
@@ -34,7 +34,8 @@ def lpg_hypers_from_args(args, sampler: LevelSampler) -> LpgHyperparams:
         policy_entropy_coeff=args.lpg_policy_entropy_coeff, target_entropy_coeff=args.lpg_target_entropy_coeff,
         policy_l2_coeff=args.lpg_policy_l2_coeff, target_l2_coeff=args.lpg_target_l2_coeff, gamma=args.gamma,
         gae_lambda=args.gae_lambda, actor_lr=ah.actor_learning_rate, critic_lr=ah.critic_learning_rate,
-        max_grad_norm=ah.max_grad_norm, lpg_lr=args.lpg_learning_rate)
+        max_grad_norm=ah.max_grad_norm, lpg_lr=args.lpg_learning_rate,
+        fix_value_critic=bool(getattr(args, "fix_value_critic", False)))
 
 
 def check_supported(args):
@@ -75,7 +76,7 @@ class Trainer:
         else:
             self.hyp = lpg_hypers_from_args(args, self.sampler)
             self.step_fn = MetaGradStep(self.sampler.rollout_manager, n_local, self.hyp, args.lifetime_conditioning,
-                                        self.dev, self.world)
+                                        self.dev, self.world, num_mini_batches=args.num_mini_batches)
             self.adam = AdamState(self.eta.numel(), self.dev)
 
     def meta_step(self):
