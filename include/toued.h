@@ -218,11 +218,14 @@ int toued_gru_fwd(int R, int T, int W, int F, const float* X, long xs_f, long xs
                   float* s_r, float* s_z, float* s_n, float* s_hn, long M, hipStream_t stream);
 /* VJP over K updates (M = K*T*R columns): gate cotangents DG [4][256][M] (dr, dz, d(W_hn h + b_hn), dn),
  * relu(h_out) RH [256][M] (row 256 of the caller's [257][M] buffer holds ones), head cotangents DH [9][M],
- * input cotangents dX3/dX4 [K][T][R] */
+ * input cotangents dX3/dX4 [K][T][R]; col_exp [M] (optional, written when toued_gru_bwd_col_exp(R)): each
+ * column's cotangent scale exponent for toued_wgrad_bfp */
 int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_stride_k, const float* bwdA,
                   const float* eta, const int* off, const float* y_hat, const float* d_pi_hat, const float* d_y_hat,
                   const float* s_hin, const float* s_r, const float* s_z, const float* s_n, const float* s_hn, long M,
-                  float* DG, float* RH, float* DH, float* dX3, float* dX4, hipStream_t stream);
+                  float* DG, float* RH, float* DH, float* dX3, float* dX4, int8_t* col_exp, hipStream_t stream);
+/* 1 when toued_gru_bwd runs its lockstep split-precision kernel for R rows (the one that writes col_exp) */
+int toued_gru_bwd_col_exp(int R);
 /* the backward's small weight-gradient products: GI = [8][256] ([X; 1; 0] . dn^T: dW_in rows, b_in) followed by
  * [9][257] (DH . [relu(h_out); 1]^T: head kernels and biases); X rows start at s_hin + 256*M.
  * `work`: toued_gru_bwd_small_work_floats(M) floats. */
@@ -237,6 +240,12 @@ int toued_gru_bwd_small(long M, const float* s_hin, const float* DG, const float
 size_t toued_wgrad_workspace_floats(int ra, int rb, long K);
 int toued_wgrad(int ra, int rb, long K, const float* A, long lda, const float* B, long ldb, float* C, float* work,
                 size_t work_floats, hipStream_t stream);
+/* The LPG's main weight-gradient reduction on block-floating-point fp16 pairs (3 products instead of the bf16
+ * split's 6): rows [0, a_unit_rows) of A must satisfy |a| <= 1 (scale 2^14), the others are scaled from their
+ * measured maximum; col_exp[m] (from toued_gru_bwd) scales B's columns per K chunk.  Deterministic. */
+size_t toued_wgrad_bfp_workspace_floats(int ra, int rb, long K);
+int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit_rows, const float* B, long ldb,
+                    const int8_t* col_exp, float* C, float* work, size_t work_floats, hipStream_t stream);
 
 /* ES inference path: pack n candidates' forward fragments (candidate c at eta + c*eta_stride) */
 int toued_gru_pack_fwd_multi(const float* eta, long eta_stride, int n, const int* off, int F, float* fwdA,

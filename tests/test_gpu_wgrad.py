@@ -68,3 +68,47 @@ def test_wgrad_empty_k_and_errors():
         L.call("toued_wgrad", 3, 5, 33, L.ptr(A), 36, L.ptr(A), 36, L.ptr(C), L.ptr(A), 12, L.stream_ptr())
     with pytest.raises(Exception, match="workspace"):
         L.call("toued_wgrad", 3, 5, 64, L.ptr(A), 64, L.ptr(A), 64, L.ptr(C), L.ptr(A), 1, L.stream_ptr())
+
+
+def _col_exp(B):
+    """the backward's per-column exponent: 2^e * max_j |B[j][m]| < 2^14 (127 for an all-zero column)"""
+    mx = B.abs().amax(dim=0)
+    _, e = torch.frexp(mx)
+    ce = (14 - e).clamp(-126, 126)
+    return torch.where(mx > 0, ce, torch.full_like(ce, 127)).to(torch.int8).contiguous()
+
+
+@pytest.mark.parametrize("K,spread", [(32 * 700, 12.0), (32 * 2000, 3.0), (32 * 37, 20.0)])
+def test_wgrad_bfp_matches_float64(K, spread):
+    """toued_wgrad_bfp (block-floating-point fp16 pairs) on the LPG shape: rows 0..255 bounded by 1 (the GRU
+    carry), feature rows of magnitudes 1e-3..1e3 (one all-zero), B columns spread over `spread` decades (one
+    all-zero): the same f32-class bound as the bf16-triple kernel, and deterministic."""
+    from toued import _lib as L
+    ra, rb = 262, 768
+    g = torch.Generator(device="cuda").manual_seed(int(K + spread))
+    A = torch.empty(ra, K, device="cuda")
+    A[:256].uniform_(-1, 1, generator=g)
+    A[256:] = torch.randn(6, K, generator=g, device="cuda") * torch.tensor([1e-3, 1.0, 1e3, 7.0, 0.0, 1.0],
+                                                                            device="cuda")[:, None]
+    A[261] = 1.0
+    B = torch.randn(rb, K, generator=g, device="cuda")
+    B *= torch.pow(10.0, -spread * torch.rand(K, generator=g, device="cuda"))[None, :]
+    B[:, 5] = 0.0
+    CE = _col_exp(B)
+    C = torch.full((ra, rb), float("nan"), device="cuda")
+    work = torch.empty(int(L.lib().toued_wgrad_bfp_workspace_floats(ra, rb, K)), device="cuda")
+    L.call("toued_wgrad_bfp", ra, rb, K, L.ptr(A), K, 256, L.ptr(B), K, L.ptr(CE), L.ptr(C), L.ptr(work),
+           work.numel(), L.stream_ptr())
+    torch.cuda.synchronize()
+    ref = A.double() @ B.double().t()
+    mag = A.double().abs() @ B.double().abs().t()
+    err = (C.double() - ref).abs()
+    assert torch.isfinite(C).all()
+    assert (err <= 2e-6 * math.sqrt(K) * mag + 1e-300).all(), float((err / (mag + 1e-300)).max())
+    rel = float((err.norm() / ref.norm()))
+    assert rel < 2e-6, rel
+    C2 = torch.empty_like(C)
+    L.call("toued_wgrad_bfp", ra, rb, K, L.ptr(A), K, 256, L.ptr(B), K, L.ptr(CE), L.ptr(C2), L.ptr(work),
+           work.numel(), L.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(C, C2)

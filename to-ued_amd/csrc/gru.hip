@@ -795,6 +795,8 @@ struct BwdArgs {
   float* RH;        // [256][M] relu(h_out)
   float* DH;        // [9][M] head cotangents (d pi_hat, d y_logits)
   float* dX3; float* dX4;   // [K][T][R]
+  int8_t* CE;       // [M] (optional, lockstep kernel): column m's cotangent scale exponent for the weight-gradient
+                    // reduction (2^CE[m] max over dr, dz, dhn of column m < 2^14; 127 = all zero)
 };
 
 // NT row tiles of 32 rows per workgroup.  NT = 2: one workgroup per CU (150 KB LDS, 256 VGPRs), every
@@ -1220,13 +1222,15 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       float m = 0.0f;
 #pragma unroll
       for (int w8 = 0; w8 < 8; ++w8) m = fmaxf(m, rmx[w8 * RBT + RB * h + col]);
-      int sc = 0;
+      int sc = 0, ce = 127;
       if (m > 0.0f && m <= 3.0e38f) {
         int e;
         frexpf(m, &e);
         sc = min(40, max(-40, 14 - e));
+        ce = min(126, max(-126, 14 - e));
       }
       bs[h] = ldexpf(1.0f, sc);
+      if (p.CE && wave == 0 && hi == 0) p.CE[ctr + r0 + RB * h + col] = (int8_t)ce;
     }
     // a lane's four units ub + 8 g4 .. +3 of batch row `row` of gate cotangent g to DG (lane = row: 128-byte
     // segments), issued beside the contraction's MFMAs where the memory pipe is otherwise idle
@@ -1427,10 +1431,13 @@ int toued_gru_fwd_multi(int R, int T, int W, int F, int rows_per_cand, const flo
                         nullptr, nullptr, 0, 0, rows_per_cand, eta_stride, stream);
 }
 
+// 1 when toued_gru_bwd runs the lockstep split-precision kernel for R rows, which writes col_exp
+int toued_gru_bwd_col_exp(int R) { return R % (2 * RB) == 0 && !gru_f32_forced() ? 1 : 0; }
+
 int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_stride_k, const float* bwdA,
                   const float* eta, const int* off, const float* y_hat, const float* d_pi_hat, const float* d_y_hat,
                   const float* s_hin, const float* s_r, const float* s_z, const float* s_n, const float* s_hn, long M,
-                  float* DG, float* RH, float* DH, float* dX3, float* dX4, hipStream_t stream) {
+                  float* DG, float* RH, float* DH, float* dX3, float* dX4, int8_t* col_exp, hipStream_t stream) {
   TOUED_REQUIRE(R % RB == 0 && W % RB == 0, "toued_gru_bwd: rows R=%d and workers W=%d must be multiples of 32", R, W);
   TOUED_REQUIRE((double)M * 264.0 * 4.0 < 4294967295.0, "toued_gru_bwd: M=%ld columns exceed the 4 GiB buffer range",
                 M);
@@ -1441,8 +1448,8 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
   memcpy(&p.o, off, sizeof(EtaOff));
   p.y_hat = y_hat; p.d_pi_hat = d_pi_hat; p.d_y_hat = d_y_hat;
   p.s_hin = s_hin; p.s_r = s_r; p.s_z = s_z; p.s_n = s_n; p.s_hn = s_hn; p.M = M;
-  p.DG = DG; p.RH = RH; p.DH = DH; p.dX3 = dX3; p.dX4 = dX4;
-  if (R % (2 * RB) == 0 && !gru_f32_forced())
+  p.DG = DG; p.RH = RH; p.DH = DH; p.dX3 = dX3; p.dX4 = dX4; p.CE = col_exp;
+  if (toued_gru_bwd_col_exp(R))
     hipLaunchKernelGGL(k_gru_bwd6n, dim3(K * (R / (2 * RB))), dim3(512), 0, stream, p);
   else
     hipLaunchKernelGGL(k_gru_bwd<1>, dim3(K * (R / RB)), dim3(512), 0, stream, p);

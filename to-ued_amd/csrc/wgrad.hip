@@ -285,6 +285,217 @@ __global__ void __launch_bounds__(64 * X6_NW, 1) k_wgrad_x6(const float* __restr
       for (int r = 0; r < 4; ++r) out[(long)(16 * i + 4 * oct + r) * rbp + brow[t]] = acc[i][t][r];
 }
 
+// ------------------------------------------------------------------ block-floating-point fp16-pair kernel
+// k_wgrad_h3: the main reduction on scaled fp16 pairs, three products per element pair instead of six.  Every
+// operand is scaled by a power of two so that its magnitude stays below 2^14 and split exactly into
+// y = x0 + x1 (x0 = fp16(y), x1 = fp16(y - x0): 22 significand bits); a0b0 + a0b1 + a1b0 are exact products
+// accumulated in f32, the dropped a1b1 is below 2^-22 relative.  Scales:
+//   * A row i: 2^14 for the rows known to be bounded by 1 (the GRU carry h_in), else 2^(14 - e_i) from the
+//     row's measured maximum |a| < 2^e_i (k_wgrad_rowmax; the x feature rows) -- rows 256.. of [h_in; x; 1];
+//   * B (the gate cotangents, per column m of very different magnitude): the backward writes each column's
+//     exponent t_m (2^t_m max_j |B[j][m]| < 2^14); a workgroup's K chunk uses c = min_m t_m over its columns,
+//     so the chunk's largest column sits below 2^14 and a column 2^d smaller keeps 22 bits while d < 24 and an
+//     absolute error below 2^-38 of the chunk maximum beyond -- f32-accumulation class.
+// The partial sums are unscaled exactly (powers of two) before the chunk-ordered reduction.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+TOUED_DEV floatx4 mfma_h(f16x8 a, f16x8 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+template <typename V>
+TOUED_DEV void split2_f16(float y, V& p0, V& p1, int e) {
+  const _Float16 h = (_Float16)y;
+  p0[e] = h;
+  p1[e] = (_Float16)(y - (float)h);
+}
+
+// exponent e with 2^e > |x| >= 2^(e-1) (frexp), for the scale 2^(14 - e)
+TOUED_DEV int scale_exp_of(float mx) {
+  if (!(mx > 0.0f) || !(mx <= 3.0e38f)) return 0;
+  int e;
+  frexpf(mx, &e);
+  return min(126, max(-126, 14 - e));
+}
+
+// bits[row - r0] = max over k of |A[row][k]| as float bits (non-negative floats order like ints)
+__global__ void __launch_bounds__(256) k_wgrad_rowmax(const float* __restrict__ A, long lda, int r0, long K,
+                                                      long kper, int* __restrict__ bits) {
+  const int row = r0 + blockIdx.y;
+  const long kb = (long)blockIdx.x * kper, ke = kb + kper < K ? kb + kper : K;
+  const float* a = A + (long)row * lda;
+  float m = 0.0f;
+  for (long k = kb + threadIdx.x * 4; k < ke; k += 256 * 4) {
+    const float4 v = *reinterpret_cast<const float4*>(a + k);
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(&bits[blockIdx.y], __float_as_int(m));
+}
+
+__global__ void __launch_bounds__(64 * X6_NW, 1) k_wgrad_h3(const float* __restrict__ A, long lda, int ra,
+                                                             int a_unit_rows, const int* __restrict__ rowmax_bits,
+                                                             const float* __restrict__ B, long ldb, int rb,
+                                                             const int8_t* __restrict__ colexp, long K, long kchunk,
+                                                             float* __restrict__ part) {
+  constexpr int NT = 64 * X6_NW;
+  const int G = gridDim.x, ncol = (rb + X6_CT - 1) / X6_CT;
+  const int xcd = blockIdx.x & 7;
+  const int L = xcd * (G >> 3) + (xcd < (G & 7) ? xcd : (G & 7)) + (blockIdx.x >> 3);
+  __shared__ f16x8 As[2][2][X6_RA * 4];    // [buffer][piece][slot]: 69,632 B
+  __shared__ float asc[X6_RA];             // 2^s_i of A row i
+  __shared__ int cred[X6_NW];
+  const int tid = threadIdx.x, lane = tid & 63, q16 = lane & 15, oct = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ct = L % ncol, sc = L / ncol;
+  const long kb = (long)sc * kchunk;
+  const long ke = kb + kchunk < K ? kb + kchunk : K;
+  const int nslab = (int)((ke - kb) / 32);
+  // chunk B exponent c = min over the chunk's columns (127 = an all-zero column, no constraint)
+  int cm = 127;
+  for (long m = kb + 16L * tid; m < ke; m += 16L * NT) {
+    const int4 v = *reinterpret_cast<const int4*>(colexp + m);
+    const int w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) cm = min(cm, (int)(int8_t)(w4[q] >> (8 * b)));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cm = min(cm, __shfl_xor(cm, o, 64));
+  if (lane == 0) cred[wave] = cm;
+  for (int i = tid; i < X6_RA; i += NT) {
+    const int r = i < ra ? i : ra - 1;
+    asc[i] = r < a_unit_rows ? 16384.0f : ldexpf(1.0f, scale_exp_of(__int_as_float(rowmax_bits[r - a_unit_rows])));
+  }
+  __syncthreads();
+  int cexp = cred[0];
+#pragma unroll
+  for (int w = 1; w < X6_NW; ++w) cexp = min(cexp, cred[w]);
+  if (cexp == 127) cexp = 0;
+  const float bsc = ldexpf(1.0f, cexp);
+  const float4* Bp[X6_BT];
+  int brow[X6_BT];
+#pragma unroll
+  for (int t = 0; t < X6_BT; ++t) {
+    brow[t] = ct * X6_CT + 16 * (X6_BT * wave + t) + q16;
+    Bp[t] = reinterpret_cast<const float4*>(B + (long)(brow[t] < rb ? brow[t] : 0) * ldb + kb) + 2 * oct;
+  }
+  float4 ast[X6_NS];
+  auto a_index = [&](int j) {
+    const int i = tid + NT * j;
+    return j < X6_NS - 1 || i < X6_AQ ? i : i - NT;
+  };
+  auto load_a = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < X6_NS; ++j) {
+      const int i = a_index(j);
+      const int row = (i >> 3) < ra ? (i >> 3) : ra - 1;
+      ast[j] = *reinterpret_cast<const float4*>(A + (long)row * lda + kb + 32L * s + 4 * (i & 7));
+    }
+  };
+  auto write_a = [&](int buf, int j) {
+    const int i = a_index(j);
+    const int row = i >> 3, kq = i & 7;
+    const int slot = x6_slot(row, kq >> 1);
+    const float s = asc[row];
+    f16x4 p0, p1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split2_f16(f4(ast[j], e) * s, p0, p1, e);
+    reinterpret_cast<f16x4*>(&As[buf][0][slot])[kq & 1] = p0;
+    reinterpret_cast<f16x4*>(&As[buf][1][slot])[kq & 1] = p1;
+  };
+  float4 bq[X6_BT][2];
+  auto issue_b = [&](int s) {
+#pragma unroll
+    for (int t = 0; t < X6_BT; ++t) { bq[t][0] = Bp[t][8 * s]; bq[t][1] = Bp[t][8 * s + 1]; }
+  };
+  auto split_b = [&](f16x8 (&dst)[X6_BT][2], int t, int half) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split2_f16(f4(bq[t][half], e) * bsc, dst[t][0], dst[t][1], 4 * half + e);
+  };
+  floatx4 acc[17][X6_BT];
+#pragma unroll
+  for (int i = 0; i < 17; ++i)
+#pragma unroll
+    for (int t = 0; t < X6_BT; ++t) acc[i][t] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+
+  auto slab = [&](int s, f16x8 (&bp)[X6_BT][2], f16x8 (&bpn)[X6_BT][2]) {
+    const int buf = s & 1;
+    load_a(s + 1 < nslab ? s + 1 : s);
+    const f16x8* a0p = As[buf][0];
+    const f16x8* a1p = As[buf][1];
+    f16x8 a[2];
+    {
+      const int slot = x6_slot(q16, oct);
+      a[0] = a0p[slot]; a[1] = a1p[slot];
+    }
+#pragma unroll
+    for (int i = 0; i < 17; ++i) {
+      f16x8 an[2];
+      if (i + 1 < 17) {
+        const int slot = x6_slot(16 * (i + 1) + q16, oct);
+        an[0] = a0p[slot]; an[1] = a1p[slot];
+      }
+#pragma unroll
+      for (int t = 0; t < X6_BT; ++t) {
+        floatx4 c = acc[i][t];
+        c = mfma_h(a[1], bp[t][0], c);
+        c = mfma_h(a[0], bp[t][1], c);
+        c = mfma_h(a[0], bp[t][0], c);
+        acc[i][t] = c;
+      }
+      if (i < 2 * X6_BT) split_b(bpn, i >> 1, i & 1);
+      if (i == 2 * X6_BT) issue_b(s + 2 < nslab ? s + 2 : nslab - 1);
+      if (i >= 8) write_a(buf ^ 1, i - 8);
+      if (i + 1 < 17) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // next tile's fragment reads first
+      }
+#pragma unroll
+      for (int m = 0; m < 3 * X6_BT; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);   // side-work VALU
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (i + 1 < 17) { a[0] = an[0]; a[1] = an[1]; }
+    }
+    __syncthreads();
+  };
+
+  f16x8 bpa[X6_BT][2], bpb[X6_BT][2];
+  if (nslab > 0) {
+    load_a(0);
+    issue_b(0);
+#pragma unroll
+    for (int j = 0; j < X6_NS; ++j) write_a(0, j);
+#pragma unroll
+    for (int t = 0; t < X6_BT; ++t) { split_b(bpa, t, 0); split_b(bpa, t, 1); }
+    issue_b(nslab > 1 ? 1 : 0);
+  }
+  __syncthreads();
+  for (int s = 0; s < nslab; ++s) {
+    slab(s, bpa, bpb);
+#pragma unroll
+    for (int t = 0; t < X6_BT; ++t)
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) bpa[t][pc] = bpb[t][pc];
+  }
+  // D map: lane l, reg r -> C[16i + 4 oct + r][brow]; unscale by 2^-(s_row + c) (two exact steps)
+  const int rbp = ncol * X6_CT;
+  float* out = part + (long)sc * X6_RA * rbp;
+  const float ib = ldexpf(1.0f, -cexp);
+#pragma unroll
+  for (int i = 0; i < 17; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float ia = 1.0f / asc[16 * i + 4 * oct + r];
+#pragma unroll
+      for (int t = 0; t < X6_BT; ++t) out[(long)(16 * i + 4 * oct + r) * rbp + brow[t]] = (acc[i][t][r] * ia) * ib;
+    }
+}
+
 // C[i][j] = sum over chunks (in chunk order) of part[s][i][j], i < ra, j < rb
 __global__ void k_wgrad_reduce(const float* __restrict__ part, int S, int RA, int rbp, int ra, int rb,
                                float* __restrict__ C) {
@@ -388,6 +599,46 @@ int toued_wgrad(int ra, int rb, long K, const float* A, long lda, const float* B
   else
     hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, work, p.S,
                        p.nrt * 16, p.ncol * p.ct, ra, rb, C);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+// Main LPG weight-gradient reduction on block-floating-point fp16 pairs (k_wgrad_h3): rows [0, a_unit_rows) of A
+// must be bounded by 1 in magnitude; col_exp[m] is B column m's scale exponent (127 = zero column).
+size_t toued_wgrad_bfp_workspace_floats(int ra, int rb, long K) {
+  if (ra <= 0 || rb <= 0 || K <= 0) return 0;
+  Plan p = plan(ra > 16 ? ra : 17, rb, K);
+  return (size_t)p.S * 17 * 16 * p.ncol * X6_CT + X6_RA;
+}
+
+int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit_rows, const float* B, long ldb,
+                    const int8_t* col_exp, float* C, float* work, size_t work_floats, hipStream_t stream) {
+  TOUED_REQUIRE(ra > 16 && ra <= X6_RA && rb >= 1 && a_unit_rows >= 0 && a_unit_rows <= ra,
+                "toued_wgrad_bfp: ra=%d (17..%d) rb=%d a_unit_rows=%d", ra, X6_RA, rb, a_unit_rows);
+  TOUED_REQUIRE(K > 0 && K % 32 == 0, "toued_wgrad_bfp: K=%ld must be a positive multiple of 32", K);
+  TOUED_REQUIRE(lda % 4 == 0 && ldb % 4 == 0, "toued_wgrad_bfp: lda=%ld ldb=%ld must be multiples of 4", lda, ldb);
+  TOUED_REQUIRE(A && B && C && col_exp, "toued_wgrad_bfp: null operand");
+  TOUED_REQUIRE((reinterpret_cast<uintptr_t>(col_exp) & 15) == 0, "toued_wgrad_bfp: col_exp must be 16-byte aligned");
+  Plan p = plan(ra, rb, K);
+  p.ct = X6_CT;
+  p.ncol = (rb + X6_CT - 1) / X6_CT;
+  TOUED_REQUIRE(p.kchunk % 16 == 0, "toued_wgrad_bfp: chunk %ld", p.kchunk);
+  const size_t need = (size_t)p.S * 17 * 16 * p.ncol * X6_CT;
+  TOUED_REQUIRE(work && work_floats >= need + X6_RA, "toued_wgrad_bfp: workspace of %zu floats needed (got %zu)",
+                need + X6_RA, work_floats);
+  int* bits = reinterpret_cast<int*>(work + need);
+  const int nmeas = ra - a_unit_rows;
+  TOUED_REQUIRE(hipMemsetAsync(bits, 0, sizeof(int) * X6_RA, stream) == hipSuccess, "toued_wgrad_bfp: memset");
+  if (nmeas > 0) {
+    const long kper = 65536;
+    hipLaunchKernelGGL(k_wgrad_rowmax, dim3((unsigned)((K + kper - 1) / kper), nmeas), dim3(256), 0, stream, A, lda,
+                       a_unit_rows, K, kper, bits);
+  }
+  hipLaunchKernelGGL(k_wgrad_h3, dim3(p.ncol * p.S), dim3(64 * X6_NW), 0, stream, A, lda, ra, a_unit_rows, bits, B,
+                     ldb, rb, col_exp, K, p.kchunk, work);
+  const long n = (long)ra * rb;
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, work, p.S, 17 * 16,
+                     p.ncol * X6_CT, ra, rb, C);
   TOUED_CHECK_LAUNCH();
   return 0;
 }

@@ -63,7 +63,10 @@ _SIGS = {
     "toued_gru_packed_floats": [_I],
     "toued_gru_fwd": [_I, _I, _I, _I, _P, _L, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _P],
     "toued_gru_bwd": [_I, _I, _I, _I, _P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _P, _P, _P, _P, _P,
-                      _P],
+                      _P, _P],
+    "toued_gru_bwd_col_exp": [_I],
+    "toued_wgrad_bfp_workspace_floats": [_I, _I, _L],
+    "toued_wgrad_bfp": [_I, _I, _L, _P, _L, _I, _P, _L, _P, _P, _P, ctypes.c_size_t, _P],
     "toued_gru_bwd_small_work_floats": [_L],
     "toued_gru_bwd_small": [_L, _P, _P, _P, _P, _P, _P, ctypes.c_size_t, _P],
     "toued_choice_cdf": [_P, _P, _I, _I, _P, _P],
@@ -87,7 +90,7 @@ _SIGS = {
 }
 _RESTYPES = {"toued_last_error": ctypes.c_char_p, "toued_mode_program_bytes": ctypes.c_size_t,
              "toued_gru_packed_floats": ctypes.c_size_t, "toued_wgrad_workspace_floats": ctypes.c_size_t,
-             "toued_gru_bwd_small_work_floats": ctypes.c_size_t}
+             "toued_gru_bwd_small_work_floats": ctypes.c_size_t, "toued_wgrad_bfp_workspace_floats": ctypes.c_size_t}
 
 _lib = None
 

@@ -16,6 +16,7 @@ kernels are built for.
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 from collections import OrderedDict
 
@@ -166,7 +167,13 @@ class LPGGRU:
         self.G = torch.empty((H + lay.F + 1, 3 * H), dtype=f32, device=dev)
         # the backward's small products: [8][256] ([X; 1; 0] . dn^T) then [9][257] (DH . [relu(h_out); 1]^T)
         self.GI = torch.empty(8 * H + 9 * (H + 1), dtype=f32, device=dev)
+        # per-column cotangent exponents from the lockstep backward -> the block-floating-point fp16 reduction
+        # (toued_wgrad_bfp, 3 products); else (or TOUED_WGRAD_X6=1) the bf16-triple reduction (toued_wgrad)
+        self.bfp = bool(L.toued_gru_bwd_col_exp(R)) and os.environ.get("TOUED_WGRAD_X6") != "1" and \
+            os.environ.get("TOUED_WGRAD_F32") != "1"
+        self.CE = torch.empty(M if self.bfp else 0, dtype=torch.int8, device=dev)
         need = max(int(L.toued_wgrad_workspace_floats(H + lay.F + 1, 3 * H, M)),
+                   int(L.toued_wgrad_bfp_workspace_floats(H + lay.F + 1, 3 * H, M)),
                    int(L.toued_gru_bwd_small_work_floats(M)))
         self.wg_work = torch.empty(max(need, 1), dtype=f32, device=dev)
 
@@ -200,7 +207,7 @@ class LPGGRU:
                   self.lay.c_offsets, _lib.ptr(y_hat), _lib.ptr(d_pi_hat), _lib.ptr(d_y_hat),
                   _lib.ptr(self.A), _lib.ptr(S[0]), _lib.ptr(S[1]), _lib.ptr(S[2]), _lib.ptr(S[3]), M,
                   _lib.ptr(self.DG), _lib.ptr(self.RH), _lib.ptr(self.DH), _lib.ptr(self.dX3), _lib.ptr(self.dX4),
-                  _lib.stream_ptr())
+                  _lib.ptr(self.CE) if self.bfp else None, _lib.stream_ptr())
         if timers is not None:
             timers.stop(tok)
             tok = timers.start("wgrad_gemm")
@@ -215,7 +222,12 @@ class LPGGRU:
         st = _lib.stream_ptr()
         _lib.call("toued_gru_bwd_small", M, _lib.ptr(self.A), _lib.ptr(DG), _lib.ptr(self.RH), _lib.ptr(self.DH),
                   _lib.ptr(self.GI), ws, wn, st)
-        _lib.call("toued_wgrad", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, _lib.ptr(DG), M, _lib.ptr(G), ws, wn, st)
+        if self.bfp:
+            _lib.call("toued_wgrad_bfp", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, H, _lib.ptr(DG), M,
+                      _lib.ptr(self.CE), _lib.ptr(G), ws, wn, st)
+        else:
+            _lib.call("toued_wgrad", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, _lib.ptr(DG), M, _lib.ptr(G), ws, wn,
+                      st)
         lay.view(grad, "hr_w").add_(G[0:H, 0:H])
         lay.view(grad, "hz_w").add_(G[0:H, H:2 * H])
         lay.view(grad, "hn_w").add_(G[0:H, 2 * H:3 * H])

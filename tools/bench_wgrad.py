@@ -32,7 +32,15 @@ def main():
                            int(L.lib().toued_wgrad_workspace_floats(6, 256, M)),
                            int(L.lib().toued_wgrad_workspace_floats(9, 257, M))), device="cuda")
     res["toued_wgrad"] = timed(lambda: L.call("toued_wgrad", 262, 768, M, L.ptr(A), M, L.ptr(B), M, L.ptr(C), L.ptr(work), work.numel(), L.stream_ptr()))
+    A[:256].uniform_(-1, 1)
+    CE = torch.full((M,), 0, dtype=torch.int8, device="cuda")      # columns of N(0,1) data: max < 8 -> 2^11
+    CE.fill_(11)
+    wb = torch.empty(int(L.lib().toued_wgrad_bfp_workspace_floats(262, 768, M)), device="cuda")
+    res["toued_wgrad_bfp"] = timed(lambda: L.call("toued_wgrad_bfp", 262, 768, M, L.ptr(A), M, 256, L.ptr(B), M,
+                                                  L.ptr(CE), L.ptr(C), L.ptr(wb), wb.numel(), L.stream_ptr()))
     ref = torch.mm(A[:262], B.t())
+    res["bfp_max_rel_vs_mm"] = float(((C - ref).abs().max() / ref.abs().max()))
+    L.call("toued_wgrad", 262, 768, M, L.ptr(A), M, L.ptr(B), M, L.ptr(C), L.ptr(work), work.numel(), L.stream_ptr())
     res["max_rel_vs_mm"] = float(((C - ref).abs().max() / ref.abs().max()))
     X6 = A[256:262]
     res["mm_Gn"] = timed(lambda: torch.mm(X6, DG[3].t()))
