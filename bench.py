@@ -179,7 +179,60 @@ def cpu_baseline(env_mode: str, lifetime_conditioning: bool, n_agents: int = 0):
     return {"value": round(n_agents * W * T * K / dt, 1), "unit": "agent-env-steps/sec",
             "cores": torch.get_num_threads(), "kind": "port",
             "sample": f"oracle restatement (numpy rollouts + torch-CPU f32 autograd meta-gradient), one meta-step of "
-                      f"{n_agents} agents x W={W} x T={T} x K={K}, env_mode={env_mode}; {dt:.1f} s"}
+                      f"{n_agents} agents x W={W} x T={T} x K={K}, env_mode={env_mode}; {dt:.1f} s",
+            "cpp_rollout": cpp_rollout_baseline(env_mode)}
+
+
+def cpp_rollout_baseline(env_mode: str, n_agents: int = 512, target_s: float = 5.0):
+    """BASELINE.md §2 variant 2: the C++/OpenMP restatement (oracle/cpu, g++ -O3, bit-exact with the numpy oracle)
+    of the rollout + GAE on all host cores: the K train rollouts of N agents x W x T with GAE over each, repeated
+    to ~target_s.  agent-env-steps/sec of the rollout part only (no LPG / meta-gradient)."""
+    import ctypes
+    import numpy as np
+
+    from oracle import cpu
+    from oracle import jaxrand as jr
+    from oracle import levels as olv
+    W, T, K = 64, 20, 5
+    spec = olv.env_spec(env_mode)
+    D = spec.obs_dim
+    p, lt = olv.reset_env_params(jr.split(jr.PRNGKey(0), n_agents), env_mode)
+    lev = np.ascontiguousarray(olv.pack_levels(p, lt, spec))
+    rs = np.random.RandomState(0)
+    theta = (rs.randn(n_agents, D, 5) * 0.5).astype(np.float32)
+    vc = (rs.randn(n_agents, D) * 0.1).astype(np.float32)
+    from oracle import rollout as oro
+    st = oro.batch_reset(spec, jr.split(jr.PRNGKey(1), n_agents), p, W)
+    n = n_agents * W
+    state = np.zeros((12, n), np.int32)
+    state[0], state[1], state[3] = st["time"], st["pos"], st["early_term"]
+    state[2] = np.sum(st["obj_existss"] * (1 << np.arange(spec.max_n_objs))[None, :], axis=1)
+    state[4:4 + spec.max_n_objs] = st["obj_poss"].T
+    idx = np.zeros((n_agents, T + 1, W), np.int32)
+    tm = np.zeros_like(idx)
+    act = np.zeros((n_agents, T, W), np.uint8)
+    rew = np.zeros((n_agents, T, W), np.float32)
+    dn = np.zeros_like(act)
+    adv = np.zeros((n, T), np.float32)
+    tgt = np.zeros_like(adv)
+    L = cpu.lib()
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    reps, t0, key = 0, time.perf_counter(), 2
+    while True:
+        for _ in range(K):
+            keys = np.ascontiguousarray(jr.split(jr.PRNGKey(key), n_agents))
+            key += 1
+            L.toued_cpu_rollout(spec.max_grid_size, spec.max_n_objs, spec.max_n_obj_types, int(spec.tabular), P(lev),
+                                P(theta), D, P(keys), P(state), T, W, n_agents, P(idx), P(tm), P(act), P(rew), P(dn),
+                                None)
+            L.toued_cpu_gae(P(vc), D, P(idx), P(tm), P(rew), P(dn), T, W, n_agents, 0.99, 0.95, P(adv), P(tgt))
+        reps += 1
+        dt = time.perf_counter() - t0
+        if dt >= target_s:
+            break
+    return {"value": round(reps * K * n * T / dt, 1), "unit": "agent-env-steps/sec", "cores": cpu.threads(),
+            "kind": "port", "sample": f"C++/OpenMP restatement (oracle/cpu: rollout + GAE only, no LPG), {reps} x K={K} "
+                                      f"rollouts of {n_agents} agents x W={W} x T={T}, env_mode={env_mode}; {dt:.1f} s"}
 
 
 def main():
