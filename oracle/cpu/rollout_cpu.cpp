@@ -24,7 +24,7 @@
 namespace {
 
 enum { L_MAX_STEPS = 0, L_GRID = 1, L_START = 2, L_NOBJS = 3, L_RANDRESP = 4, L_OBJ_IDS = 8, L_STATIC = 16,
-       L_REW = 24, L_PTERM = 32, L_PRESP = 40, L_WALLS = 48, LW = 64 };
+       L_REW = 24, L_PTERM = 32, L_PRESP = 40, L_WALLS = 48, LW = 80 };
 enum { S_TIME = 0, S_POS = 1, S_EXISTS = 2, S_TERM = 3, S_OBJ = 4 };
 
 struct Key { uint32_t a, b; };

@@ -166,15 +166,17 @@ def reset_env_params(key, mode: str):
 
 
 # ---------------------------------------------------------------------------
-# Packed device layout (int32[64] per level) shared with the HIP kernels.
-LEVEL_WORDS = 64
+# Packed device layout (int32[80] per level) shared with the HIP kernels.
+LEVEL_WORDS = 80
 L_MAX_STEPS, L_GRID, L_START, L_NOBJS, L_RANDRESP, L_LIFETIME, L_BUFID = 0, 1, 2, 3, 4, 5, 6
 L_OBJ_IDS, L_STATIC, L_REW, L_PTERM, L_PRESP, L_WALLS = 8, 16, 24, 32, 40, 48
+L_TREW, L_TPTERM, L_TPRESP, L_AUTOC = 64, 69, 74, 79    # per-type EnvParams tables, auto_collect
 
 
 def pack_levels(params, lifetime, spec: EnvSpec, buffer_id=None) -> np.ndarray:
-    """Pack params into int32[B, 64]: scalars, raw obj_ids, static positions, the per-object
-    resolved type tables (jnp.take with -1 wrap, gridworld.py:87,115,122) and a walls bitmask."""
+    """Pack params into int32[B, 80]: scalars, raw obj_ids, static positions, the per-object
+    resolved type tables (jnp.take with -1 wrap, gridworld.py:87,115,122), a walls bitmask, and the
+    per-type tables + auto_collect of EnvParams (gridworld.py:21-35) for the checkpoint round trip."""
     B = params["start_pos"].shape[0]
     n = spec.max_n_objs
     out = np.zeros((B, LEVEL_WORDS), np.int32)
@@ -196,4 +198,8 @@ def pack_levels(params, lifetime, spec: EnvSpec, buffer_id=None) -> np.ndarray:
     for c in range(walls.shape[1]):
         w = c // 32
         out[:, L_WALLS + w] |= (walls[:, c].astype(np.int64) << (c % 32)).astype(np.uint32).view(np.int32)
+    nt = params["obj_rewards"].shape[1]
+    for off, name in ((L_TREW, "obj_rewards"), (L_TPTERM, "obj_p_terminate"), (L_TPRESP, "obj_p_respawn")):
+        out[:, off:off + nt] = params[name].astype(F32).view(np.int32)
+    out[:, L_AUTOC] = 1
     return out

@@ -316,7 +316,8 @@ def test_train_main_writes_checkpoints(tmp_path, extra):
     assert files == (["buffer_2", "checkpoint_2"] if extra else ["checkpoint_2"])
     if extra:
         b = restore_checkpoint(str(tmp_path), prefix="buffer_")
-        assert b["levels"].shape[1] == 64 and b["score"].dtype == np.float32
+        assert b["level"]["env_params"]["walls"].shape == (4000, 100) and b["score"].dtype == np.float32
+        assert b["level"]["env_params"]["obj_rewards"].shape == (4000, 5)
 
 
 def _agents_for(mode, N, W, T, seed):

@@ -18,8 +18,12 @@
 enum {
   L_MAX_STEPS = 0, L_GRID = 1, L_START = 2, L_NOBJS = 3, L_RANDRESP = 4, L_LIFETIME = 5,
   L_BUFID = 6, L_OBJ_IDS = 8, L_STATIC = 16, L_REW = 24, L_PTERM = 32, L_PRESP = 40,
-  L_WALLS = 48, LEVEL_WORDS = 64
+  L_WALLS = 48,
+  // the EnvParams per-type tables (obj_rewards, obj_p_terminate, obj_p_respawn, zero past max_n_obj_types) and
+  // auto_collect, kept so that a level round-trips to the reference's Level pytree (checkpoints)
+  L_TREW = 64, L_TPTERM = 69, L_TPRESP = 74, L_AUTOC = 79, LEVEL_WORDS = 80
 };
+#define TOUED_MAX_TYPES 5
 // Env state, SoA over workers: field f of worker i at state[f * n + i].
 enum { S_TIME = 0, S_POS = 1, S_EXISTS = 2, S_TERM = 3, S_OBJ = 4, S_FIELDS = 12 };
 #define TOUED_MAX_OBJS 8

@@ -185,6 +185,13 @@ TOUED_DEV void gen_level(const ModeSpec& m, const ModeProgram& prog, uint2 rng, 
     out[L_PRESP + i] = __float_as_int(in_src ? presp[rid] : 0.0f);
   }
   for (int w = 0; w < 8; ++w) out[L_WALLS + w] = (int)wall_bits[w];
+  for (int j = 0; j < prog.dst_n_types && j < TOUED_MAX_TYPES; ++j) {
+    const bool in_src = j < m.n_types;
+    out[L_TREW + j] = __float_as_int(in_src ? rew[j] : 0.0f);
+    out[L_TPTERM + j] = __float_as_int(in_src ? pterm[j] : 0.0f);
+    out[L_TPRESP + j] = __float_as_int(in_src ? presp[j] : 0.0f);
+  }
+  out[L_AUTOC] = 1;   // every ENV_MODE_PARAMS entry sets auto_collect=True (configs.py:29)
 }
 
 __global__ void __launch_bounds__(64) k_level_gen(const ModeProgram* __restrict__ prog_g,

@@ -17,6 +17,7 @@ import torch
 
 from . import _lib
 from .agents import AgentHyperparams
+from .env import LEVEL_WORDS
 from .rollout import RolloutWrapper, Transition
 
 
@@ -57,7 +58,7 @@ class A2CTrainer:
             "chain": z(U, n, 2, dt=torch.int32),
             # graph-static inputs
             "rng": z(n, 2, dt=torch.int32), "theta": z(n, D, 5), "vcrit": z(n, D),
-            "step": z(n, dt=torch.int32), "levels": z(n, 64, dt=torch.int32),
+            "step": z(n, dt=torch.int32), "levels": z(n, LEVEL_WORDS, dt=torch.int32),
             "state": z(12, n * W, dt=torch.int32),
         }
         self._graph = None

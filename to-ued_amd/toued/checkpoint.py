@@ -16,10 +16,15 @@ unpinned, no reference checkpoint exists to read back:
 ``lpg_train_state_dict`` builds ``to_state_dict`` of the meta-gradient TrainState (meta/meta.py:10-30): ``step``,
 ``params`` (the flax module tree of models/lpg.py, see toued/lpg.py for the names) and ``opt_state`` of
 ``optax.chain(scale_by_adam(), scale(lr), scale(-1))`` = ``{"0": {"count", "mu", "nu"}, "1": {}, "2": {}}``
-(apply_fn and tx are static fields and not serialised).  The level buffer is written in the same container with
-this build's packed level rows (``levels`` int32 [B, 64], see toued/env.py) plus ``score``/``active``/``new``;
-the reference's ``Level`` pytree (EnvParams with per-type object tables) is not reconstructible from the packed
-rows, so buffer checkpoints round-trip here but are not reference-readable.
+(apply_fn and tx are static fields and not serialised).
+
+``level_buffer_state_dict`` writes the reference's ``LevelBuffer`` pytree (level_sampler.py:30-52): ``level``
+= ``Level(env_params, lifetime, buffer_id)`` (util/data.py:46-51) with every ``EnvParams`` field
+(gridworld.py:21-35, per-type object tables included: the packed rows carry them), then ``score``, ``active``,
+``new`` -- in dataclass field order, as flax's to_state_dict emits them.  ``es_train_state_dict`` writes
+``ESTrainState`` (util/data.py:63-68): ``train_state`` (the LPG TrainState, which the ES step never updates),
+``es_params`` and ``es_state`` of evosax 0.1.4's OpenES (EvoParams / EvoState with the optimiser's
+OptParams / OptState; evosax is not installed or vendored: field names, order and defaults restated, unpinned).
 """
 from __future__ import annotations
 
@@ -172,8 +177,66 @@ def lpg_train_state_dict(eta: torch.Tensor, lay, step: int, adam=None) -> dict:
                           "1": {}, "2": {}}}
 
 
-def level_buffer_state_dict(buffer) -> dict:
-    return {"levels": buffer.levels, "score": buffer.score, "active": buffer.active, "new": buffer.new}
+def level_buffer_state_dict(buffer, spec) -> dict:
+    """to_state_dict(LevelBuffer) of the reference (level_sampler.py:30-52) from the packed device buffer."""
+    from .env import unpack_levels
+    params, lifetime, buffer_id = unpack_levels(buffer.levels, spec)
+    return {"level": {"env_params": params, "lifetime": lifetime.astype(np.int32), "buffer_id": buffer_id.astype(np.int32)},
+            "score": buffer.score.detach().cpu().numpy().astype(np.float32),
+            "active": buffer.active.detach().cpu().numpy().astype(bool),
+            "new": buffer.new.detach().cpu().numpy().astype(bool)}
+
+
+def level_buffer_from_state_dict(state: dict, spec, device):
+    """A reference (or this build's) buffer checkpoint back into the device LevelBuffer."""
+    from .env import pack_levels
+    from .level_sampler import LevelBuffer
+    lv = state["level"]
+    packed = pack_levels(lv["env_params"], np.asarray(lv["lifetime"]).astype(np.int32),
+                         np.asarray(lv["buffer_id"]).astype(np.int32), spec)
+    t = lambda a, dt: torch.as_tensor(np.array(a), dtype=dt, device=device)
+    return LevelBuffer(t(packed, torch.int32), t(state["score"], torch.float32), t(state["active"], torch.bool),
+                       t(state["new"], torch.bool))
+
+
+_F32_MAX = float(np.finfo(np.float32).max)
+
+
+def es_train_state_dict(es, eta_train_state: torch.Tensor, lay, lpg_opt: str, best_member=None,
+                        best_fitness=_F32_MAX) -> dict:
+    """to_state_dict(ESTrainState) (util/data.py:63-68; meta/meta.py:24-30).  ``es`` is toued.es.OpenES;
+    ``eta_train_state`` the params of the wrapped TrainState (the LPG init: lpg_es_train_step only replaces
+    es_state, meta/train.py:214-216).  evosax 0.1.4 OpenES: EvoParams(opt_params, sigma_init, sigma_decay,
+    sigma_limit, init_min=0, init_max=0, clip_min=-f32max, clip_max=f32max), EvoState(mean, sigma, opt_state,
+    best_member, best_fitness, gen_counter); Adam/SGD OptParams(lrate_init, lrate_decay, lrate_limit, momentum,
+    beta_1, beta_2, beta_3, eps, max_speed) and OptState(lrate, m, v, n, last_grads, gen_counter)."""
+    f = lambda x: np.asarray(x, np.float32)
+    adam = es.opt == 1
+    nd = es.nd
+    opt_params = {"lrate_init": f(es.lrate_init), "lrate_decay": f(es.lrate_decay), "lrate_limit": f(es.lrate_limit),
+                  "momentum": None if adam else f(0.0), "beta_1": f(0.99) if adam else None,
+                  "beta_2": f(0.999) if adam else None, "beta_3": None, "eps": f(1e-8) if adam else None,
+                  "max_speed": None}
+    es_params = {"opt_params": opt_params, "sigma_init": f(es.sigma_init), "sigma_decay": f(es.sigma_decay),
+                 "sigma_limit": f(es.sigma_limit), "init_min": f(0.0), "init_max": f(0.0), "clip_min": f(-_F32_MAX),
+                 "clip_max": f(_F32_MAX)}
+    mean = es.mean.detach().cpu().numpy().astype(np.float32)
+    opt_state = {"lrate": f(es.lrate), "m": es.m.detach().cpu().numpy().astype(np.float32),
+                 "v": es.v.detach().cpu().numpy().astype(np.float32) if adam else None, "n": None, "last_grads": None,
+                 "gen_counter": np.asarray(es.n, np.int32)}
+    bm = mean if best_member is None else (best_member.detach().cpu().numpy() if torch.is_tensor(best_member)
+                                           else np.asarray(best_member)).astype(np.float32)
+    es_state = {"mean": mean, "sigma": f(es.sigma), "opt_state": opt_state, "best_member": bm,
+                "best_fitness": f(best_fitness), "gen_counter": np.asarray(es.gen_counter, np.int32)}
+    if lpg_opt.lower() == "adam":
+        zeros = torch.zeros(lay.size)
+        tx_state = {"0": {"count": np.asarray(0, np.int32), "mu": lpg_params_tree(zeros, lay),
+                          "nu": lpg_params_tree(zeros, lay)}, "1": {}, "2": {}}
+    else:   # optax.chain(clip_by_global_norm, scale, scale): three empty states
+        tx_state = {"0": {}, "1": {}, "2": {}}
+    train_state = {"step": np.asarray(0, np.int32), "params": lpg_params_tree(eta_train_state, lay),
+                   "opt_state": tx_state}
+    return {"train_state": train_state, "es_params": es_params, "es_state": es_state}
 
 
 def save_checkpoint(ckpt_dir: str, target: dict, step: int, prefix: str = "checkpoint_", keep: int = 1) -> str:

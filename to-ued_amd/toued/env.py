@@ -5,7 +5,7 @@ environments/environments.py:22-63 (get_env / reset_env_params / get_env_spec /
 get_agent_hypers) and configs.py's mode tables — batched ("vmapped") over
 levels/workers, with all state resident on the GPU.
 
-Levels are packed int32[n, 64] tensors (include/toued.h); env state is
+Levels are packed int32[n, 80] tensors (include/toued.h); env state is
 int32[12, n] SoA; observations are compact (tab_idx, time) int32 pairs.
 """
 from __future__ import annotations
@@ -18,10 +18,61 @@ from . import _lib
 from . import modes as M
 
 STATE_FIELDS = 12
-LEVEL_WORDS = 64
+LEVEL_WORDS = 80
 # packed-level word offsets (csrc/common.h)
 L_MAX_STEPS, L_GRID, L_START, L_NOBJS, L_RANDRESP, L_LIFETIME, L_BUFID = 0, 1, 2, 3, 4, 5, 6
 L_OBJ_IDS, L_STATIC, L_REW, L_PTERM, L_PRESP, L_WALLS = 8, 16, 24, 32, 40, 48
+L_TREW, L_TPTERM, L_TPRESP, L_AUTOC = 64, 69, 74, 79
+
+
+def unpack_levels(levels, spec: "EnvSpec"):
+    """Packed rows [B, 80] -> the reference's Level pytree fields (util/data.py:46-51; EnvParams
+    gridworld.py:21-35) as numpy arrays: ({EnvParams field: array}, lifetime, buffer_id)."""
+    import numpy as np
+    lv = np.ascontiguousarray(levels.detach().cpu().numpy() if torch.is_tensor(levels) else levels, np.int32)
+    n, t, g2 = spec.max_n_objs, spec.max_n_obj_types, spec.g2
+    bits = lv[:, L_WALLS:L_WALLS + 8].view(np.uint32)
+    cells = np.arange(g2)
+    walls = ((bits[:, cells // 32] >> (cells % 32).astype(np.uint32)) & 1).astype(bool)
+    f = lambda off: lv[:, off:off + t].view(np.float32).copy()
+    params = {
+        "max_steps_in_episode": lv[:, L_MAX_STEPS].copy(), "random_respawn": lv[:, L_RANDRESP].astype(bool),
+        "auto_collect": lv[:, L_AUTOC].astype(bool), "grid_size": lv[:, L_GRID].copy(), "walls": walls,
+        "start_pos": lv[:, L_START].copy(), "n_objs": lv[:, L_NOBJS].copy(),
+        "obj_ids": lv[:, L_OBJ_IDS:L_OBJ_IDS + n].copy(), "static_obj_poss": lv[:, L_STATIC:L_STATIC + n].copy(),
+        "obj_rewards": f(L_TREW), "obj_p_terminate": f(L_TPTERM), "obj_p_respawn": f(L_TPRESP),
+    }
+    return params, lv[:, L_LIFETIME].copy(), lv[:, L_BUFID].copy()
+
+
+def pack_levels(params: dict, lifetime, buffer_id, spec: "EnvSpec"):
+    """Inverse of unpack_levels: the packed rows (with the per-object tables resolved through obj_ids, a -1 id
+    taking the last type as jnp.take does, gridworld.py:87,115,122) as an int32 numpy array [B, 80]."""
+    import numpy as np
+    B = np.asarray(params["start_pos"]).shape[0]
+    n, t = spec.max_n_objs, spec.max_n_obj_types
+    out = np.zeros((B, LEVEL_WORDS), np.int32)
+    out[:, L_MAX_STEPS] = params["max_steps_in_episode"]
+    out[:, L_GRID] = params["grid_size"]
+    out[:, L_START] = params["start_pos"]
+    out[:, L_NOBJS] = params["n_objs"]
+    out[:, L_RANDRESP] = np.asarray(params["random_respawn"]).astype(np.int32)
+    out[:, L_LIFETIME] = lifetime
+    out[:, L_BUFID] = buffer_id
+    ids = np.asarray(params["obj_ids"], np.int32)
+    out[:, L_OBJ_IDS:L_OBJ_IDS + n] = ids
+    out[:, L_STATIC:L_STATIC + n] = params["static_obj_poss"]
+    rid = np.where(ids < 0, ids + t, ids)
+    for off, toff, name in ((L_REW, L_TREW, "obj_rewards"), (L_PTERM, L_TPTERM, "obj_p_terminate"),
+                            (L_PRESP, L_TPRESP, "obj_p_respawn")):
+        tab = np.asarray(params[name], np.float32)
+        out[:, off:off + n] = np.take_along_axis(tab, rid, axis=1).view(np.int32)
+        out[:, toff:toff + t] = tab.view(np.int32)
+    walls = np.asarray(params["walls"], bool)
+    for c in range(walls.shape[1]):
+        out[:, L_WALLS + c // 32] |= (walls[:, c].astype(np.int64) << (c % 32)).astype(np.uint32).view(np.int32)
+    out[:, L_AUTOC] = np.asarray(params.get("auto_collect", True)).astype(np.int32)
+    return out
 
 
 @dataclass(frozen=True)

@@ -42,6 +42,10 @@ class OpenES:
             raise NotImplementedError("es_mean_decay != 0 is not implemented (reference default 0.0)")
         self.popsize = popsize
         self.nd = num_dims
+        self.lrate_init, self.sigma_init = np.float32(lrate_init), np.float32(sigma_init)
+        # evosax Strategy.tell's best-member tracker (get_best_fitness_member on the fitness given to tell)
+        self.best_member = None
+        self.best_fitness = np.float32(np.finfo(np.float32).max)
         self.opt = 1 if opt_name == "adam" else 0
         self.lrate_decay, self.lrate_limit = np.float32(lrate_decay), np.float32(lrate_limit)
         self.sigma_decay, self.sigma_limit = np.float32(sigma_decay), np.float32(sigma_limit)
@@ -60,6 +64,24 @@ class OpenES:
         _lib.call("toued_es_ask", _lib.ptr(rng.contiguous()), self.nd, self.popsize // 2, row_lo, n_rows,
                   _lib.ptr(self.mean), float(self.sigma), _lib.ptr(out), _lib.stream_ptr())
         return out
+
+    def track_best(self, x_local: torch.Tensor, rank_fitness: torch.Tensor, lo: int, world=None):
+        """evosax 0.1.4 get_best_fitness_member (maximize=True) on the full rank-fitness vector, before the
+        generation counter advances: the first candidate with the largest fitness replaces the best member when
+        it beats the stored best (compared in the minimisation frame; restated, unpinned)."""
+        fit = rank_fitness.float().cpu().numpy()
+        fmin = -fit
+        idx = int(np.argmin(fmin))
+        best_min = (-self.best_fitness) if self.gen_counter > 0 else self.best_fitness
+        if fmin[idx] < best_min:
+            row = torch.zeros(self.nd, dtype=torch.float32, device=self.mean.device)
+            if lo <= idx < lo + x_local.shape[0]:
+                row.copy_(x_local[idx - lo])
+            if world is not None:
+                world.all_reduce_sum(row)
+            self.best_member = row
+            best_min = fmin[idx]
+        self.best_fitness = np.float32(-best_min)
 
     def tell(self, x_local: torch.Tensor, rank_fitness_local: torch.Tensor, world=None):
         fit = (-rank_fitness_local).float().contiguous()          # FitnessShaper(maximize=True)
@@ -193,8 +215,11 @@ class ESTrainStep:
         agents.phi.copy_(self.phi[cur][sel])
         agents.step.copy_(step[sel])
         agents.state.copy_(state.view(12, C, W)[:, sel].reshape(12, N * W))
-        # ---- tell (:214-217)
-        self.es.tell(self.x, rank, self.world if (self.world is not None and self.world.size > 1) else None)
+        # ---- tell (:214-217); evosax tracks the best member on the fitness passed to tell (the rank fitness)
+        multi = self.world is not None and self.world.size > 1
+        rank_all = self.world.all_gather_cat(rank) if multi else rank
+        self.es.track_best(self.x, rank_all, 2 * lo, self.world if multi else None)
+        self.es.tell(self.x, rank, self.world if multi else None)
         inv = 1.0 / (W * T * max(K, 1))
         m = self.met * inv
         fit_all = fitness if self.world is None or self.world.size == 1 else self.world.all_gather_cat(fitness)

@@ -63,6 +63,7 @@ class Trainer:
         F = 7 if args.lifetime_conditioning else 5
         # create_lpg_train_state (meta/meta.py:21-22): flax's init of the LPG from lpg_rng
         self.eta = flax_init_lpg_params(lpg_rng, F)
+        self.eta_init = self.eta.clone()
         self.sampler = LevelSampler(args, self.dev, self.world)
         self.buffer = self.sampler.initialize_buffer(buffer_rng)
         ks = prng.split(self.rng, 2)
@@ -70,6 +71,11 @@ class Trainer:
         n_local = args.num_agents if sl is None else sl[1] - sl[0]
         self.buffer, self.agents = self.sampler.initial_sample(sub, self.buffer, args.num_agents,
                                                                not args.use_es, sl)
+        self.buffer_init = None
+        if self.buffer is not None and getattr(args, "ref_quirk_checkpoint_init", False):
+            from .level_sampler import LevelBuffer
+            b = self.buffer
+            self.buffer_init = LevelBuffer(b.levels.clone(), b.score.clone(), b.active.clone(), b.new.clone())
         if args.use_es:
             from .es import ESTrainStep
             self.step_fn = ESTrainStep(args, self.sampler, n_local, self.eta, self.dev, self.world)
@@ -126,24 +132,28 @@ def main(cmd_args=None):
 
 
 def save_final_checkpoints(ckpt_dir: str, tr: "Trainer", steps: int):
-    """log_results (experiments/logging.py:31-46) without wandb: the LPG train state as checkpoint_<steps>
-    and, for buffer-based score functions, the level buffer as buffer_checkpoint_<steps> (toued/checkpoint.py)."""
-    from .checkpoint import level_buffer_state_dict, lpg_params_tree, lpg_train_state_dict, save_checkpoint
+    """log_results (experiments/logging.py:31-46) without wandb: the LPG train state as checkpoint_<steps> and, for
+    buffer-based score functions, the level buffer as buffer_checkpoint_<steps> (toued/checkpoint.py), both in the
+    reference's pytree layouts.  With --ref_quirk_checkpoint_init the states written are the ones the reference's
+    _train_fn actually returns -- the initial train state and level buffer, because the scan's final carry is never
+    unpacked (train.py:52-57) -- instead of the trained ones."""
+    from .checkpoint import es_train_state_dict, level_buffer_state_dict, lpg_train_state_dict, save_checkpoint
     from .lpg import LPGLayout
     lay = LPGLayout(7 if tr.args.lifetime_conditioning else 5)
+    init = bool(getattr(tr.args, "ref_quirk_checkpoint_init", False))
     if tr.args.use_es:
-        # ESTrainState (meta/meta.py:29): the search mean as the LPG params, plus the OpenES state (this build's
-        # field names; the evosax state pytree is not reproduced)
         es = tr.step_fn.es
-        target = {"step": np.asarray(steps, np.int32), "params": lpg_params_tree(es.mean, lay),
-                  "es_state": {"mean": es.mean, "m": es.m, "v": es.v, "lrate": np.float32(es.lrate),
-                               "sigma": np.float32(es.sigma), "gen_counter": np.asarray(es.gen_counter, np.int32)}}
+        if init:
+            from .es import OpenES
+            a = tr.args
+            es = OpenES(es.popsize, es.nd, a.lpg_opt, a.lpg_learning_rate, a.es_lrate_decay, a.es_lrate_limit,
+                        a.es_sigma_init, a.es_sigma_decay, a.es_sigma_limit, a.es_mean_decay, tr.dev)
+        target = es_train_state_dict(es, tr.eta_init, lay, tr.args.lpg_opt, es.best_member, es.best_fitness)
+    elif init:
+        target = lpg_train_state_dict(tr.eta_init, lay, 0, None)
     else:
         target = lpg_train_state_dict(tr.eta, lay, steps, tr.adam)
     save_checkpoint(ckpt_dir, target, steps)
-    if tr.buffer is not None:
-        save_checkpoint(ckpt_dir, level_buffer_state_dict(tr.buffer), steps, prefix="buffer_")
-
-
-if __name__ == "__main__":
-    main(sys.argv[1:])
+    buf = tr.buffer_init if init else tr.buffer
+    if buf is not None:
+        save_checkpoint(ckpt_dir, level_buffer_state_dict(buf, tr.sampler.spec), steps, prefix="buffer_")
