@@ -96,6 +96,14 @@ int toued_batch_reset_masked(EnvSpec spec, const int* levels, const uint32_t* ag
 int toued_rollout(EnvSpec spec, const int* levels, const float* theta, int D, const uint32_t* agent_keys,
                   int* state, int n_agents, int W, int T, int* traj_idx, int* traj_time, uint8_t* traj_action,
                   float* traj_reward, uint8_t* traj_done, float* cum_return, hipStream_t stream);
+/* The same returns-only rollout (eval_agent, agents/agents.py:98-106 over rollout.py:45-102) in three launches,
+ * bit-identical: the per-worker key chain (chain: uint32[T][n][4], n = n_agents*W), every state-independent draw of
+ * every step in parallel (draws: uint32[T][n][4]), then the env chain on those draws (`state` read only). */
+int toued_eval_keys(const uint32_t* agent_keys, int n_agents, int W, int T, uint32_t* chain, hipStream_t stream);
+int toued_eval_draws(EnvSpec spec, const int* levels, int n_agents, int W, int T, const uint32_t* chain,
+                     uint32_t* draws, hipStream_t stream);
+int toued_eval_returns(EnvSpec spec, const int* levels, const float* theta, int D, const int* state, int n_agents,
+                       int W, int T, const uint32_t* draws, float* cum_return, hipStream_t stream);
 
 
 /* ---- Level sampler (environments/level_sampler.py) ---- */
@@ -246,6 +254,11 @@ int toued_wgrad(int ra, int rb, long K, const float* A, long lda, const float* B
 size_t toued_wgrad_bfp_workspace_floats(int ra, int rb, long K);
 int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit_rows, const float* B, long ldb,
                     const int8_t* col_exp, float* C, float* work, size_t work_floats, hipStream_t stream);
+
+/* CUs the split-K weight-gradient plans leave free (default 0): a kernel running on a side stream beside them (the
+ * eval_agent rollout) then occupies its own CUs instead of pushing one workgroup of every chunk into a second
+ * round.  Workspace sizes queried before the change stay sufficient (fewer chunks).  Returns the previous value. */
+int toued_set_reserved_cus(int n);
 
 /* ES inference path: pack n candidates' forward fragments (candidate c at eta + c*eta_stride) */
 int toued_gru_pack_fwd_multi(const float* eta, long eta_stride, int n, const int* off, int F, float* fwdA,

@@ -153,3 +153,31 @@ def test_rollout_large_properties():
     # a second run with the same keys is identical (determinism)
     tr2, _, cum2 = rw.batch_rollout(dev_keys(jr.split(jr.PRNGKey(2), N)), th, lev, st)
     assert torch.equal(tr.obs_idx, tr2.obs_idx) and torch.equal(cum, cum2)
+
+
+@pytest.mark.parametrize("mode,N,W", [("tabular", 96, 4), ("dense", 40, 4), ("longer", 24, 4), ("all_shortlife", 64, 4),
+                                      ("all_vrandlife", 64, 4), ("sparse", 33, 3), ("debug", 17, 5)])
+def test_eval_returns_three_launches(mode, N, W):
+    """eval_agent's returns-only rollout as key chain + parallel draws + env chain (toued_eval_keys/_draws/_returns)
+    is bit-identical to the single-kernel returns-only mode (itself checked against the oracle below and in
+    tests/test_gpu_plr.py), on peaked and uniform actors over the full eval length."""
+    from toued.rollout import RolloutWrapper
+    keys = jr.split(jr.PRNGKey(31), N)
+    spec, p, lt, packed = oracle_levels(mode, keys)
+    rw = RolloutWrapper(mode, 20, env_workers=W)
+    lev = torch.from_numpy(packed).cuda()
+    (_, _), st = rw.batch_reset(dev_keys(jr.split(jr.PRNGKey(32), N)), lev)
+    st0 = st.clone()
+    for scale in (3.0, 0.0):
+        theta = (np.random.RandomState(2).randn(N, spec.obs_dim, 5) * scale).astype(np.float32)
+        th = torch.from_numpy(theta).cuda()
+        ak = dev_keys(jr.split(jr.PRNGKey(33), N))
+        ref = rw.eval_returns(ak, th, lev, st)
+        draws = rw.eval_draws(ak, lev, W)
+        got = rw.eval_returns_from_draws(draws, th, lev, st)
+        np.testing.assert_array_equal(got.cpu().numpy(), ref.cpu().numpy())
+        assert torch.equal(st, st0)
+    if mode == "sparse":   # short episodes: the numpy oracle over the whole eval length is cheap here
+        _, _, ocum = oro.batch_rollout(spec, jr.split(jr.PRNGKey(33), N), theta, p, _state_np(st0, spec),
+                                       rw.eval_rollout_len)
+        np.testing.assert_array_equal(got.cpu().numpy(), ocum)

@@ -21,13 +21,40 @@ struct EnvState {
 
 TOUED_DEV int lev_i(const int* lev, int w) { return lev[w]; }
 TOUED_DEV float lev_f(const int* lev, int w) { return __int_as_float(lev[w]); }
+TOUED_DEV uint32_t wall_word(const int* lev, int w) { return (uint32_t)lev[L_WALLS + w]; }
 
-TOUED_DEV bool wall_at(const int* lev, int cell) {
-  return (((uint32_t)lev[L_WALLS + (cell >> 5)]) >> (cell & 31)) & 1u;
+// The level record held in registers (the tabular rollouts): words [0, L_WALLS + 8) loaded once per lane before
+// the step loop, so no step waits on a level load (the step maths reads them under data-dependent branches, where
+// the compiler cannot hoist loads).  Every index is a compile-time constant after unrolling except the wall word,
+// which is selected from registers.
+struct LevR {
+  int v[L_WALLS + 8];
+};
+TOUED_DEV LevR lev_regs(const int* lev) {
+  LevR r;
+#pragma unroll
+  for (int i = 0; i < L_WALLS + 8; ++i) r.v[i] = lev[i];
+  return r;
+}
+TOUED_DEV int lev_i(const LevR& l, int w) { return l.v[w]; }
+TOUED_DEV float lev_f(const LevR& l, int w) { return __int_as_float(l.v[w]); }
+TOUED_DEV uint32_t wall_word(const LevR& l, int w) {
+  // masks, not selects: a select between two array elements is folded into a load from a selected address,
+  // which would move the whole record to scratch
+  uint32_t x = 0u;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x |= (uint32_t)l.v[L_WALLS + i] & (0u - (uint32_t)(w == i));
+  return x;
+}
+
+template <typename LV>
+TOUED_DEV bool wall_at(const LV& lev, int cell) {
+  return (wall_word(lev, cell >> 5) >> (cell & 31)) & 1u;
 }
 
 // _get_next_pos, gridworld.py:138-146
-TOUED_DEV int next_pos(const int* lev, int pos, int action) {
+template <typename LV>
+TOUED_DEV int next_pos(const LV& lev, int pos, int action) {
   const int g = lev_i(lev, L_GRID);
   const int top = pos < g, bottom = pos >= g * (g - 1);
   const int left = (pos % g) == 0, right = (pos % g) == g - 1;
@@ -35,6 +62,20 @@ TOUED_DEV int next_pos(const int* lev, int pos, int action) {
                    (action == 2) * (1 - left) * -1 + (action == 3) * (1 - right) * 1;
   const int nxt = pos + step;
   return wall_at(lev, nxt) ? pos : nxt;
+}
+
+// the same on the level's wall bitmask held in registers (wl = lev[L_WALLS .. +7])
+TOUED_DEV int next_pos_r(int g, const uint32_t (&wl)[8], int pos, int action) {
+  const int top = pos < g, bottom = pos >= g * (g - 1);
+  const int left = (pos % g) == 0, right = (pos % g) == g - 1;
+  const int step = (action == 0) * (1 - top) * -g + (action == 1) * (1 - bottom) * g +
+                   (action == 2) * (1 - left) * -1 + (action == 3) * (1 - right) * 1;
+  const int nxt = pos + step;
+  const int w = nxt >> 5;
+  uint32_t x = 0u;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x |= wl[i] & (0u - (uint32_t)(w == i));
+  return ((x >> (nxt & 31)) & 1u) ? pos : nxt;
 }
 
 // Gumbel top-k choice over the max_grid^2 cells (jax.random.choice replace=False, p given):
@@ -75,7 +116,7 @@ TOUED_DEV void gumbel_topk(uint2 key, int g2, ValidFn valid, int* out) {
 
 // _get_valid_obj_idxs, gridworld.py:149-155, with the isin(idx, bool walls) quirk
 struct ValidCells {
-  const int* lev; int pos; int g2grid; bool has_false, has_true; int excl[TOUED_MAX_OBJS]; int n_excl;
+  int pos; int g2grid; bool has_false, has_true; int excl[TOUED_MAX_OBJS]; int n_excl;
   TOUED_DEV bool operator()(int c) const {
     bool v = (c != pos) && (c < g2grid);
     v = v && !((c == 0 && has_false) || (c == 1 && has_true));
@@ -84,9 +125,10 @@ struct ValidCells {
   }
 };
 
-TOUED_DEV ValidCells make_valid(const int* lev, int G2, int pos) {
+template <typename LV>
+TOUED_DEV ValidCells make_valid(const LV& lev, int G2, int pos) {
   ValidCells vc;
-  vc.lev = lev; vc.pos = pos;
+  vc.pos = pos;
   const int g = lev_i(lev, L_GRID);
   vc.g2grid = g * g;
   bool any_t = false, any_f = false;
@@ -95,7 +137,7 @@ TOUED_DEV ValidCells make_valid(const int* lev, int G2, int pos) {
     if (lo >= G2) break;
     const int nb = (G2 - lo) < 32 ? (G2 - lo) : 32;
     const uint32_t mask = nb == 32 ? 0xffffffffu : ((1u << nb) - 1u);
-    const uint32_t bits = (uint32_t)lev[L_WALLS + w] & mask;
+    const uint32_t bits = wall_word(lev, w) & mask;
     any_t |= bits != 0u;
     any_f |= bits != mask;
   }
@@ -104,8 +146,8 @@ TOUED_DEV ValidCells make_valid(const int* lev, int G2, int pos) {
 }
 
 // reset_env, gridworld.py:157-182
-template <int NMAX, bool TAB>
-TOUED_DEV void reset_env(const EnvSpec& sp, const int* lev, uint2 key, EnvState& s) {
+template <int NMAX, bool TAB, typename LV>
+TOUED_DEV void reset_env(const EnvSpec& sp, const LV& lev, uint2 key, EnvState& s) {
   const int G2 = sp.max_grid * sp.max_grid;
   s.time = 0;
   s.pos = lev_i(lev, L_START);
@@ -132,15 +174,50 @@ TOUED_DEV void reset_env(const EnvSpec& sp, const int* lev, uint2 key, EnvState&
   for (int i = 0; i < NMAX; ++i) s.obj[i] += lev_i(lev, L_OBJ_IDS + i) * G2;
 }
 
+// respawn = bernoulli(respawn_key, p_respawn[obj_ids]) over NMAX draws (gridworld.py:99-101) for the objects in
+// `miss`; respawn_key = (c2.x, c0.y).  Block b covers draws b and b + nb; only blocks holding a missing object's
+// draw are evaluated (the others cannot change the OR into `exists`).
+template <int NMAX, typename LV>
+TOUED_DEV int respawn_draws(const LV& lev, int miss, uint2 respawn_key) {
+  int respawn = 0;
+  if (miss == 0) return 0;
+  constexpr uint32_t nb = (NMAX + 1) / 2;
+#pragma unroll
+  for (uint32_t b = 0; b < nb; ++b) {
+    const uint32_t hi = b + nb;
+    const bool want = ((miss >> b) & 1) || (hi < (uint32_t)NMAX && ((miss >> hi) & 1));
+    if (!want) continue;
+    const uint2 y = threefry(respawn_key.x, respawn_key.y, b, hi < (uint32_t)NMAX ? hi : 0u);
+    const float u0 = bits_to_unit(y.x);
+    if (u0 < lev_f(lev, L_PRESP + b)) respawn |= 1 << b;
+    if (hi < (uint32_t)NMAX) {
+      const float u1 = bits_to_unit(y.y);
+      if (u1 < lev_f(lev, L_PRESP + hi)) respawn |= 1 << hi;
+    }
+  }
+  return respawn;
+}
+
+// the objects a tabular step_env can respawn: missing ones among the level's n_objs
+template <int NMAX, typename LV>
+TOUED_DEV int missing_objs(const LV& lev, int exists) {
+  const int nobj = lev_i(lev, L_NOBJS);
+  const int used = nobj >= 32 ? -1 : ((1 << nobj) - 1);
+  return ~exists & used & ((1 << NMAX) - 1);
+}
+
 // gymnax Environment.step -> step_env (gridworld.py:72-136) + auto-reset select (RESET = false: the caller
 // discards the state after a done, so the reset and its key are skipped).
 // PRE: the state-independent blocks d0, d1 (split(key)) and c0 (first block of split(key_s, 3)) come
 // precomputed in pre[0..2] (the rollout computes them a step ahead, beside the actor-row gather).
-template <int NMAX, bool TAB, bool RESET = true, bool PRE = false>
-TOUED_DEV void env_step(const EnvSpec& sp, const int* lev, uint2 key, EnvState& s, int action,
-                        float& reward, bool& done, const uint2* pre = nullptr) {
+// resp_pre >= 0 (TAB with PRE only): the step's respawn mask, already drawn by the caller (respawn_draws);
+// pos_pre >= 0: next_pos(s.pos, action), already computed by the caller.
+template <int NMAX, bool TAB, bool RESET = true, bool PRE = false, typename LV>
+TOUED_DEV void env_step(const EnvSpec& sp, const LV& lev, uint2 key, EnvState& s, int action,
+                        float& reward, bool& done, const uint2* pre = nullptr, int resp_pre = -1,
+                        int pos_pre = -1) {
   const int G2 = sp.max_grid * sp.max_grid;
-  const int pos = next_pos(lev, s.pos, action);
+  const int pos = pos_pre >= 0 ? pos_pre : next_pos(lev, s.pos, action);
   int old[NMAX];
   int collected = 0;
 #pragma unroll
@@ -161,6 +238,7 @@ TOUED_DEV void env_step(const EnvSpec& sp, const int* lev, uint2 key, EnvState& 
   // obj = (c1.y, c2.y).
   const int miss = ~s.exists & (TAB ? used : -1) & ((1 << NMAX) - 1);
   const bool need_term = collected != 0;
+  const bool have_resp = TAB && PRE && resp_pre >= 0;
   bool have_d = false, have_c1 = false;
   uint2 d0 = make_uint2(0u, 0u), d1 = d0, c0 = d0, c1 = d0, c2 = d0;
   if (PRE) {
@@ -168,7 +246,7 @@ TOUED_DEV void env_step(const EnvSpec& sp, const int* lev, uint2 key, EnvState& 
     d1 = pre[1];
     c0 = pre[2];
     have_d = true;
-    if (miss != 0) c2 = threefry(d0.x, d1.x, 2u, 5u);
+    if (miss != 0 && !have_resp) c2 = threefry(d0.x, d1.x, 2u, 5u);
     if (need_term) { c1 = threefry(d0.x, d1.x, 1u, 4u); have_c1 = true; }
   } else if (need_term || miss != 0) {
     d0 = threefry(key.x, key.y, 0u, 2u);
@@ -178,25 +256,7 @@ TOUED_DEV void env_step(const EnvSpec& sp, const int* lev, uint2 key, EnvState& 
     if (miss != 0) c2 = threefry(d0.x, d1.x, 2u, 5u);
     if (need_term) { c1 = threefry(d0.x, d1.x, 1u, 4u); have_c1 = true; }
   }
-  // respawn = bernoulli(respawn_key, p_respawn[obj_ids]) over NMAX draws (block b covers draws b, b + nb)
-  int respawn = 0;
-  if (miss != 0) {
-    const uint2 respawn_key = make_uint2(c2.x, c0.y);
-    constexpr uint32_t nb = (NMAX + 1) / 2;
-#pragma unroll
-    for (uint32_t b = 0; b < nb; ++b) {
-      const uint32_t hi = b + nb;
-      const bool want = ((miss >> b) & 1) || (hi < (uint32_t)NMAX && ((miss >> hi) & 1));
-      if (!want) continue;
-      const uint2 y = threefry(respawn_key.x, respawn_key.y, b, hi < (uint32_t)NMAX ? hi : 0u);
-      const float u0 = bits_to_unit(y.x);
-      if (u0 < lev_f(lev, L_PRESP + b)) respawn |= 1 << b;
-      if (hi < (uint32_t)NMAX) {
-        const float u1 = bits_to_unit(y.y);
-        if (u1 < lev_f(lev, L_PRESP + hi)) respawn |= 1 << hi;
-      }
-    }
-  }
+  const int respawn = have_resp ? resp_pre : respawn_draws<NMAX>(lev, miss, make_uint2(c2.x, c0.y));
   int exists = s.exists | respawn;
   int newpos[NMAX];
 #pragma unroll
@@ -405,7 +465,7 @@ __global__ void __launch_bounds__(256) k_rollout(EnvSpec sp, const int* __restri
   int a = i / W;
   if (UNIFORM) a = __builtin_amdgcn_readfirstlane(a);
   const int w = i - a * W;
-  const int* lev = levels + (size_t)a * LEVEL_WORDS;
+  const LevR lev = lev_regs(levels + (size_t)a * LEVEL_WORDS);
   const float* tab = theta + (size_t)a * D * 5;
   float last[5];
 #pragma unroll
@@ -434,21 +494,63 @@ __global__ void __launch_bounds__(256) k_rollout(EnvSpec sp, const int* __restri
     return k;
   };
   StepKeys kc = keys_of(rng);
-  for (int t = 0; t < T; ++t) {
-    const int idx = tab_index(sp, s);
-    const int tm = s.time;
-    float row[5];
+  // Candidate-row prefetch (tabular): given the state and the step's keys, the next observation of a step that
+  // does not end the episode is a function of the action alone -- position next_pos(pos, a), objects
+  // (exists | respawn) & ~collected(a) & used, with the respawn draws state-independent blocks -- so the five
+  // possible next actor rows are gathered at the start of the step and the taken one is selected afterwards.
+  // The gather then overlaps the whole step instead of sitting on the chain.  A miss (the episode ended and the
+  // auto-reset moved the agent) re-gathers; the selection never changes a value.
+  int idx = tab_index(sp, s);
+  float row[5];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) row[j] = tab[(size_t)idx * 5 + j];
-    const StepKeys kn = keys_of(kc.rng);      // next step's keys while the gather is in flight
+  for (int j = 0; j < 5; ++j) row[j] = tab[(size_t)idx * 5 + j];
+  const int G2 = sp.max_grid * sp.max_grid;
+  const int nobj = lev_i(lev, L_NOBJS);
+  const int used = nobj >= 32 ? -1 : ((1 << nobj) - 1);
+  int objpos[NMAX];
+#pragma unroll
+  for (int o = 0; o < NMAX; ++o) objpos[o] = s.obj[o] - lev_i(lev, L_OBJ_IDS + o) * G2;   // static in TAB
+  const int grid = lev_i(lev, L_GRID);
+  uint32_t wl[8];   // the wall bitmask in registers: no dependent level load on the step chain
+#pragma unroll
+  for (int i = 0; i < 8; ++i) wl[i] = (uint32_t)lev_i(lev, L_WALLS + i);
+  for (int t = 0; t < T; ++t) {
+    const int tm = s.time;
+    int cidx[5], cpos[5];
+    float crow[5][5];
+    int resp = -1;
+    if (TAB) {
+      const int miss = missing_objs<NMAX>(lev, s.exists);
+      resp = miss ? respawn_draws<NMAX>(lev, miss, make_uint2(threefry(kc.pre[0].x, kc.pre[1].x, 2u, 5u).x,
+                                                               kc.pre[2].y))
+                  : 0;
+#pragma unroll
+      for (int a = 0; a < 5; ++a) {
+        const int p = next_pos_r(grid, wl, s.pos, a);
+        cpos[a] = p;
+        int col = 0;
+#pragma unroll
+        for (int o = 0; o < NMAX; ++o)
+          if (((s.exists >> o) & 1) && objpos[o] == p) col |= 1 << o;
+        cidx[a] = p + G2 * ((s.exists | resp) & ~col & used);
+#pragma unroll
+        for (int j = 0; j < 5; ++j) crow[a][j] = tab[(size_t)cidx[a] * 5 + j];
+      }
+    }
+    const StepKeys kn = keys_of(kc.rng);      // next step's keys while the gathers are in flight
     float p[5];
     actor_probs5_row(row, last, tm, p);
     const int action = choice5_bits(kc.cbits, p);
     float r; bool d;
+    int npos = -1;
+    if (TAB) {
+#pragma unroll
+      for (int a = 0; a < 5; ++a) npos = a == action ? cpos[a] : npos;
+    }
     if (traj_idx)
-      env_step<NMAX, TAB, true, true>(sp, lev, kc.sub_env, s, action, r, d, kc.pre);
+      env_step<NMAX, TAB, true, true>(sp, lev, kc.sub_env, s, action, r, d, kc.pre, resp, npos);
     else
-      env_step<NMAX, TAB, false, true>(sp, lev, kc.sub_env, s, action, r, d, kc.pre);   // returns-only
+      env_step<NMAX, TAB, false, true>(sp, lev, kc.sub_env, s, action, r, d, kc.pre, resp, npos);   // returns-only
     cum = __fadd_rn(cum, __fmul_rn(r, valid));
     valid = __fmul_rn(valid, d ? 0.0f : 1.0f);
     // returns-only mode (eval_agent): nothing after the first episode can change cum_return
@@ -460,6 +562,22 @@ __global__ void __launch_bounds__(256) k_rollout(EnvSpec sp, const int* __restri
       traj_reward[base_t + (size_t)t * W] = r;
       traj_done[base_t + (size_t)t * W] = d ? 1 : 0;
     }
+    const int nidx = tab_index(sp, s);
+    bool hit = false;
+    if (TAB) {
+#pragma unroll
+      for (int a = 0; a < 5; ++a)
+        if (a == action) {
+          hit = cidx[a] == nidx;
+#pragma unroll
+          for (int j = 0; j < 5; ++j) row[j] = crow[a][j];
+        }
+    }
+    if (!hit) {
+#pragma unroll
+      for (int j = 0; j < 5; ++j) row[j] = tab[(size_t)nidx * 5 + j];
+    }
+    idx = nidx;
     kc = kn;
   }
   if (traj_idx) {
@@ -468,6 +586,137 @@ __global__ void __launch_bounds__(256) k_rollout(EnvSpec sp, const int* __restri
   }
   if (traj_idx) store_state<NMAX>(state, n, i, s);   // returns-only mode leaves the state untouched
   if (cum_return) cum_return[i] = cum;
+}
+
+// ---------------------------------------------------------------- eval_agent returns in three launches
+// eval_agent (agents/agents.py:98-106) rolls every agent's 4 workers for the eval length (2000 steps on the tabular
+// levels) and keeps only the return.  Per step a worker spends ~10 threefry blocks on draws that do not depend on the
+// env state, and that chain, not the env, set the single-kernel rollout's step time.  Split by dependence:
+//   k_eval_keys    the per-worker key chain ((rng, sub) = split(rng), (rng, sub_env) = split(rng) per step:
+//                  two dependent splits) -> chain[t][i] = (sub, sub_env);
+//   k_eval_draws   one thread per (step, worker): the choice bits bits1(sub), the termination uniform's bits
+//                  bits1(term_key) and the respawn bernoullis of ALL objects -> draws[t][i] (state-independent: the
+//                  step uses resp & missing, and the termination draw only when something was collected);
+//   k_eval_returns the env chain on those draws (the tabular step_env algebra, returns-only: no auto-reset),
+//                  the draws loaded two steps ahead and the next actor row by candidate prefetch.
+// Bit-identical to k_rollout's returns-only mode (tests/test_gpu_env.py::test_eval_returns_three_launches).
+__global__ void __launch_bounds__(256) k_eval_keys(const uint32_t* __restrict__ agent_keys, int W, int T, int n,
+                                                   uint4* __restrict__ chain) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int a = i / W, w = i - a * W;
+  uint2 r = split_at(make_uint2(agent_keys[2 * a], agent_keys[2 * a + 1]), (uint32_t)W, (uint32_t)w);
+  for (int t = 0; t < T; ++t) {
+    uint2 sub, sub_env;
+    split2(r, r, sub);
+    split2(r, r, sub_env);
+    chain[(size_t)t * n + i] = make_uint4(sub.x, sub.y, sub_env.x, sub_env.y);
+  }
+}
+
+template <int NMAX>
+__global__ void __launch_bounds__(256) k_eval_draws(const int* __restrict__ levels, int W, int n, long total,
+                                                    const uint4* __restrict__ chain, uint4* __restrict__ draws) {
+  const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= total) return;
+  const int i = (int)(j % n);
+  const int* lev = levels + (size_t)(i / W) * LEVEL_WORDS;
+  const uint4 c = chain[j];
+  const uint32_t cbits = bits1(make_uint2(c.x, c.y));
+  // split(sub_env) blocks d0, d1; split(key_s, 3) blocks c0, c1, c2 (env_step's naming)
+  const uint2 d0 = threefry(c.z, c.w, 0u, 2u), d1 = threefry(c.z, c.w, 1u, 3u);
+  const uint2 c0 = threefry(d0.x, d1.x, 0u, 3u), c1 = threefry(d0.x, d1.x, 1u, 4u), c2 = threefry(d0.x, d1.x, 2u, 5u);
+  const int resp = respawn_draws<NMAX>(lev, (1 << NMAX) - 1, make_uint2(c2.x, c0.y));
+  const uint32_t tbits = threefry(c0.x, c1.x, 0u, 0u).x;
+  draws[j] = make_uint4(cbits, tbits, (uint32_t)resp, 0u);
+}
+
+template <int NMAX>
+__global__ void __launch_bounds__(256) k_eval_returns(EnvSpec sp, const int* __restrict__ levels,
+                                                      const float* __restrict__ theta, int D,
+                                                      const int* __restrict__ state, int T, int W, int n,
+                                                      const uint4* __restrict__ draws, float* __restrict__ cum_return) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int a = i / W;
+  const LevR lev = lev_regs(levels + (size_t)a * LEVEL_WORDS);
+  const float* tab = theta + (size_t)a * D * 5;
+  float last[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) last[j] = tab[(size_t)(D - 1) * 5 + j];
+  EnvState s;
+  load_state<NMAX>(state, n, i, s);
+  const int G2 = sp.max_grid * sp.max_grid;
+  const int nobj = lev_i(lev, L_NOBJS);
+  const int used = nobj >= 32 ? -1 : ((1 << nobj) - 1);
+  const int max_steps = lev_i(lev, L_MAX_STEPS);
+  const int grid = lev_i(lev, L_GRID);
+  uint32_t wl[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) wl[k] = wall_word(lev, k);
+  int objpos[NMAX];
+#pragma unroll
+  for (int o = 0; o < NMAX; ++o) objpos[o] = s.obj[o] - lev_i(lev, L_OBJ_IDS + o) * G2;   // static in TAB
+  float row[5];
+  {
+    const int idx = tab_index(sp, s);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) row[j] = tab[(size_t)idx * 5 + j];
+  }
+  float cum = 0.0f;
+  uint4 dr0 = T > 0 ? draws[i] : make_uint4(0u, 0u, 0u, 0u);
+  uint4 dr1 = T > 1 ? draws[(size_t)n + i] : dr0;
+  for (int t = 0; t < T; ++t) {
+    const uint4 dr = dr0;
+    dr0 = dr1;
+    if (t + 2 < T) dr1 = draws[(size_t)(t + 2) * n + i];
+    // next state of each action while the episode goes on: position, objects left
+    int cpos[5], cex[5];
+    float crow[5][5];
+#pragma unroll
+    for (int act = 0; act < 5; ++act) {
+      const int p = next_pos_r(grid, wl, s.pos, act);
+      int col = 0;
+#pragma unroll
+      for (int o = 0; o < NMAX; ++o)
+        if (((s.exists >> o) & 1) && objpos[o] == p) col |= 1 << o;
+      cpos[act] = p;
+      cex[act] = col;
+      const int ci = p + G2 * ((s.exists | (int)dr.z) & ~col & used);
+#pragma unroll
+      for (int j = 0; j < 5; ++j) crow[act][j] = tab[(size_t)ci * 5 + j];
+    }
+    float p[5];
+    actor_probs5_row(row, last, s.time, p);
+    const int action = choice5_bits(dr.x, p);
+    int pos = 0, collected = 0;
+#pragma unroll
+    for (int act = 0; act < 5; ++act)
+      if (act == action) {
+        pos = cpos[act];
+        collected = cex[act];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) row[j] = crow[act][j];
+      }
+    // step_env (gridworld.py:72-136), tabular: the same operation order as env_step
+    float p_t = 0.0f, rew = 0.0f;
+#pragma unroll
+    for (int o = 0; o < NMAX; ++o) {
+      const float co = ((collected >> o) & 1) ? 1.0f : 0.0f;
+      p_t = __fadd_rn(p_t, __fmul_rn(lev_f(lev, L_PTERM + o), co));
+      if ((collected >> o) & 1) rew = __fadd_rn(rew, lev_f(lev, L_REW + o));
+    }
+    const bool hit = collected != 0 && bits_to_unit(dr.y) < p_t;
+    const int term = hit || s.early_term;
+    const int time = s.time + 1;
+    cum = __fadd_rn(cum, rew);   // valid = 1 until the first done, after which the worker stops
+    if ((time >= max_steps) || term) break;
+    s.time = time;
+    s.pos = pos;
+    s.exists = (s.exists | (int)dr.z) & ~collected & used;
+    s.early_term = term;
+  }
+  cum_return[i] = cum;
 }
 
 }  // namespace
@@ -547,6 +796,47 @@ int toued_batch_reset_masked(EnvSpec sp, const int* levels, const uint32_t* agen
   if (n == 0) return 0;
   TOUED_DISPATCH(sp, hipLaunchKernelGGL((k_batch_reset<NMAX, TAB>), dim3(nblk(n)), dim3(256), 0, stream, sp, levels,
                                         agent_keys, W, state, obs_idx, obs_time, n, mask));
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_eval_keys(const uint32_t* agent_keys, int n_agents, int W, int T, uint32_t* chain, hipStream_t stream) {
+  TOUED_REQUIRE(n_agents >= 0 && W >= 1 && T >= 0, "toued_eval_keys: bad sizes N=%d W=%d T=%d", n_agents, W, T);
+  const int n = n_agents * W;
+  if (n == 0 || T == 0) return 0;
+  hipLaunchKernelGGL(k_eval_keys, dim3(nblk(n)), dim3(256), 0, stream, agent_keys, W, T, n,
+                     reinterpret_cast<uint4*>(chain));
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_eval_draws(EnvSpec sp, const int* levels, int n_agents, int W, int T, const uint32_t* chain, uint32_t* draws,
+                     hipStream_t stream) {
+  if (int e = check_spec(sp)) return e;
+  TOUED_REQUIRE(sp.tabular, "toued_eval_draws: tabular envs only");
+  TOUED_REQUIRE(n_agents >= 0 && W >= 1 && T >= 0, "toued_eval_draws: bad sizes N=%d W=%d T=%d", n_agents, W, T);
+  const int n = n_agents * W;
+  const long total = (long)n * T;
+  if (total == 0) return 0;
+  const unsigned g = (unsigned)((total + 255) / 256);
+  TOUED_DISPATCH_NMAX(sp.n_max, true, hipLaunchKernelGGL(k_eval_draws<NMAX>, dim3(g), dim3(256), 0, stream, levels,
+                                                        W, n, total, reinterpret_cast<const uint4*>(chain),
+                                                        reinterpret_cast<uint4*>(draws)));
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_eval_returns(EnvSpec sp, const int* levels, const float* theta, int D, const int* state, int n_agents, int W,
+                       int T, const uint32_t* draws, float* cum_return, hipStream_t stream) {
+  if (int e = check_spec(sp)) return e;
+  TOUED_REQUIRE(sp.tabular, "toued_eval_returns: the linear tabular actor needs a tabular env");
+  TOUED_REQUIRE(n_agents >= 0 && W >= 1 && T >= 0, "toued_eval_returns: bad sizes N=%d W=%d T=%d", n_agents, W, T);
+  TOUED_REQUIRE(D == sp.max_grid * sp.max_grid * (1 << sp.n_max) + 1, "toued_eval_returns: D=%d != obs_dim", D);
+  const int n = n_agents * W;
+  if (n == 0) return 0;
+  TOUED_DISPATCH_NMAX(sp.n_max, true, hipLaunchKernelGGL(k_eval_returns<NMAX>, dim3(nblk(n)), dim3(256), 0, stream, sp,
+                                                        levels, theta, D, state, T, W, n,
+                                                        reinterpret_cast<const uint4*>(draws), cum_return));
   TOUED_CHECK_LAUNCH();
   return 0;
 }

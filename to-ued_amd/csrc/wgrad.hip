@@ -130,9 +130,14 @@ TOUED_DEV void split3_bf16(float x, V& p0, V& p1, V& p2, int e) {
   p2[e] = (__bf16)(r1 - (float)m);
 }
 
-// LDS image of one 32-k A slab piece: [row][4 k-octets of 8 bf16], octet o of row r at slot o ^ ((r >> 2) & 3):
-// the 16 lanes of a fragment read (rows 16i + 0..15, one octet) then cover all 64 banks.
-TOUED_DEV int x6_slot(int row, int oct) { return row * 4 + (oct ^ ((row >> 2) & 3)); }
+// LDS image of one 32-k A slab piece: [row][4 k-octets of 8 bf16], octet o of row r at slot o ^ f((r >> 2) & 3)
+// with f = (0, 2, 3, 1).  A fragment read (lane l: row 16i + (l & 15), octet l >> 4) is a ds_read_b128, which
+// gfx950 serves in the lane groups {0-3, 12-15, 20-27}, {4-11, 16-19, 28-31} (+32): each group holds rows
+// {0-3, 12-15} of one octet and rows {4-11} of the other, and f sends those 16 (row, octet) pairs to 16 distinct
+// bank quads (the former o ^ ((r >> 2) & 3) paired rows 0/4 and 12/8 on one quad: 2-way conflicts on every read).
+// The staging writes (ds_write_b64, 16 contiguous lanes = two whole rows) stay conflict-free under any in-row
+// permutation.
+TOUED_DEV int x6_slot(int row, int oct) { return row * 4 + (oct ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3)); }
 
 // Software pipeline per 32-k slab s (A image `buf` in LDS, B pieces bp in registers):
 //   slab start: load the raw A slab s+1 (9 float4 per thread);
@@ -537,6 +542,8 @@ static bool wgrad_f32_forced() {
   return f;
 }
 
+static int g_reserved_cus = 0;   // toued_set_reserved_cus
+
 static Plan plan(int ra, int rb, long K) {
   Plan p;
   p.nrt = ra <= 16 ? 1 : 17;
@@ -548,6 +555,7 @@ static Plan plan(int ra, int rb, long K) {
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
     cus = 256;
+  cus = cus - g_reserved_cus > cus / 2 ? cus - g_reserved_cus : cus / 2;
   // x6: one workgroup per CU (104 KB LDS), as many K chunks as fill the CUs in one round.  f32 NRT = 17:
   // two workgroups per CU (125 VGPRs, 68 KB LDS each).  NRT = 1 is a bandwidth-bound stream over B: four
   // workgroups per CU keep enough loads in flight.
@@ -564,6 +572,12 @@ static Plan plan(int ra, int rb, long K) {
 }  // namespace
 
 extern "C" {
+
+int toued_set_reserved_cus(int n) {
+  const int prev = g_reserved_cus;
+  g_reserved_cus = n > 0 ? n : 0;
+  return prev;
+}
 
 size_t toued_wgrad_workspace_floats(int ra, int rb, long K) {
   if (ra <= 0 || rb <= 0 || K <= 0) return 0;

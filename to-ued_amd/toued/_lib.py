@@ -45,6 +45,9 @@ _SIGS = {
     "toued_batch_reset": [EnvSpecC, _P, _P, _I, _I, _P, _P, _P, _P],
     "toued_batch_reset_masked": [EnvSpecC, _P, _P, _I, _I, _P, _P, _P, _P, _P],
     "toued_rollout": [EnvSpecC, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "toued_eval_keys": [_P, _I, _I, _I, _P, _P],
+    "toued_eval_draws": [EnvSpecC, _P, _I, _I, _I, _P, _P, _P],
+    "toued_eval_returns": [EnvSpecC, _P, _P, _I, _P, _I, _I, _I, _P, _P, _P],
     "toued_meta_keys": [_P, _I, _I, _P, _P, _P, _P, _P],
     "toued_lpg_inputs": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _L, _L, _P],
     "toued_agent_grad": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P],
@@ -65,6 +68,7 @@ _SIGS = {
     "toued_gru_bwd": [_I, _I, _I, _I, _P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _P, _P, _P, _P, _P,
                       _P, _P],
     "toued_gru_bwd_col_exp": [_I],
+    "toued_set_reserved_cus": [_I],
     "toued_wgrad_bfp_workspace_floats": [_I, _I, _L],
     "toued_wgrad_bfp": [_I, _I, _L, _P, _L, _I, _P, _L, _P, _P, _P, ctypes.c_size_t, _P],
     "toued_gru_bwd_small_work_floats": [_L],

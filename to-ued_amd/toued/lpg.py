@@ -196,9 +196,10 @@ class LPGGRU:
         del Xk
 
     def backward(self, done_all: torch.Tensor, eta: torch.Tensor, y_hat: torch.Tensor, d_pi_hat: torch.Tensor,
-                 d_y_hat: torch.Tensor, X: torch.Tensor, grad: torch.Tensor, timers=None):
+                 d_y_hat: torch.Tensor, X: torch.Tensor, grad: torch.Tensor, timers=None, after_bwd=None):
         """done_all: u8 [K(+1), N, T, W] (first K slots used).  Accumulates d(loss)/d(eta) into ``grad``
-        (all parameters except the embedding MLP, which needs dX3/dX4 -> agent-side kernel)."""
+        (all parameters except the embedding MLP, which needs dX3/dX4 -> agent-side kernel).  ``after_bwd()`` is
+        called right after the recurrent backward kernel is enqueued, before the weight-gradient reductions."""
         R, T, K, M = self.R, self.T, self.K, self.M
         S = self.S
         stride_k = done_all[0].numel()
@@ -210,6 +211,9 @@ class LPGGRU:
                   _lib.ptr(self.CE) if self.bfp else None, _lib.stream_ptr())
         if timers is not None:
             timers.stop(tok)
+        if after_bwd is not None:
+            after_bwd()
+        if timers is not None:
             tok = timers.start("wgrad_gemm")
         lay = self.lay
         F = lay.F

@@ -151,6 +151,7 @@ class MetaGradStep:
         self.ea_cum = None
         self.timers = KernelTimers()
         self.side = torch.cuda.Stream(device=dev)
+        self._ea_draws = None   # eval_agent draws buffer (rollout.eval_draws), reused every step
 
     # ------------------------------------------------------------------ helpers
     def _t(self, k: int) -> Transition:
@@ -239,6 +240,7 @@ class MetaGradStep:
                    ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(self.gstat[k]), st)
             L.call("toued_entropy", N, W, T, D, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(tk.obs_idx),
                    ptr(tk.obs_time), ptr(self.met[k]), 0.0, 0.0, None, None, st)
+        main = torch.cuda.current_stream()
         # ---------------- value critic on the train rollouts (--fix_value_critic), eval rollout, lpg loss
         if hyp.fix_value_critic:
             self.vc_loss.zero_()
@@ -258,13 +260,24 @@ class MetaGradStep:
         if not hyp.fix_value_critic:
             agents.vstep.add_(K + 1)
         # eval_agent (agents/agents.py:98-106): fresh 4-worker reset, eval-length rollout, mean return.
-        # It only reads theta_K and the levels, and its long sequential rollout occupies few CUs, so it
-        # runs on a side stream concurrently with the MFMA-bound backward pass.
-        main = torch.cuda.current_stream()
-        self.side.wait_stream(main)
-        with torch.cuda.stream(self.side):
-            (_, _), ea_state = self.ro.batch_reset(self.keys_ea_reset, agents.levels, hyp.eval_workers)
-            ea_cum = self._eval_rollout(self.keys_ea_roll, self.theta_h[K], agents.levels, ea_state)
+        # It only reads theta_K and the levels; its sequential chains (key chain, then the env chain on the
+        # precomputed draws: rollout.eval_draws / eval_returns_from_draws) hold few CUs (one per 256 eval
+        # workers) for ~5 ms, so they run on a side stream beside the weight-gradient reductions, whose split-K
+        # plans leave those CUs free.  (Beside the recurrent backward instead, whose 64-row workgroups fill exactly
+        # K*R/64/256 rounds of the chip, any CU held pushes that kernel into one more round; beside the
+        # latency-bound agent kernels the key chain slowed them by more than it took.)
+        eval_cus = -(-N * hyp.eval_workers // 256)
+        ea = {}
+
+        def launch_eval():
+            self.side.wait_stream(main)
+            with torch.cuda.stream(self.side):
+                (_, _), ea["state"] = self.ro.batch_reset(self.keys_ea_reset, agents.levels, hyp.eval_workers)
+                self._ea_draws = self.ro.eval_draws(self.keys_ea_roll, agents.levels, hyp.eval_workers,
+                                                    self._ea_draws)
+                ea["cum"] = self.ro.eval_returns_from_draws(self._ea_draws, self.theta_h[K], agents.levels,
+                                                            ea["state"])
+            ea["prev_reserve"] = L.lib().toued_set_reserved_cus(eval_cus)
         # ---------------- reverse: explicit adjoint w.r.t. eta
         a_in = 0
         self.adj_th[a_in].zero_()
@@ -289,7 +302,8 @@ class MetaGradStep:
                    hyp.critic_lr, hyp.agent_target_coeff, hyp.policy_l2_coeff, hyp.target_l2_coeff,
                    ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]), ptr(self.d_pi_hat[k]), ptr(self.d_y_hat[k]), st)
         self.gru.backward(self.traj.done, eta, self.y_hat, self.d_pi_hat, self.d_y_hat, self.X, self.grad,
-                          self.timers)
+                          self.timers, after_bwd=launch_eval)
+        L.lib().toued_set_reserved_cus(ea["prev_reserve"])
         tr = self.traj
         L.call("toued_embed_bwd", N, W, T, D, K, ptr(self.phi_h), self.phi_h[0].numel(), ptr(tr.obs_idx),
                tr.obs_idx[0].numel(), ptr(tr.obs_time), ptr(tr.done), tr.done[0].numel(), ptr(self.gru.dX3),
@@ -301,8 +315,9 @@ class MetaGradStep:
         self._eta(self.grad, "e2_w").add_(emb[145:161].view(16, 1))
         # ---------------- agent state out + metrics
         main.wait_stream(self.side)
+        ea_cum = ea["cum"]
         ea_cum.record_stream(main)
-        ea_state.record_stream(main)
+        ea["state"].record_stream(main)
         agents.theta.copy_(self.theta_h[K])
         agents.phi.copy_(self.phi_h[K])
         inv_wt = 1.0 / (W * T)

@@ -99,6 +99,33 @@ class RolloutWrapper:
                   _lib.ptr(out.reward), _lib.ptr(out.done), _lib.ptr(cum), _lib.stream_ptr())
         return out, state, cum
 
+    def eval_draws(self, agent_keys: torch.Tensor, levels: torch.Tensor, n_workers: int,
+                   buf: torch.Tensor | None = None) -> torch.Tensor:
+        """The state-independent draws of an eval-length returns-only rollout (toued_eval_keys, toued_eval_draws):
+        u32 [T, N*W, 4], consumed by eval_returns_from_draws.  They depend on the keys and levels only, so they can
+        be produced early, beside other work."""
+        N = agent_keys.shape[0]
+        n, T = N * n_workers, self.eval_rollout_len
+        dev = levels.device
+        chain = torch.empty((T, n, 4), dtype=torch.int32, device=dev)
+        if buf is None or buf.shape != (T, n, 4):
+            buf = torch.empty((T, n, 4), dtype=torch.int32, device=dev)
+        st = _lib.stream_ptr()
+        _lib.call("toued_eval_keys", _lib.ptr(agent_keys.contiguous()), N, n_workers, T, _lib.ptr(chain), st)
+        _lib.call("toued_eval_draws", self._c, _lib.ptr(levels), N, n_workers, T, _lib.ptr(chain), _lib.ptr(buf), st)
+        return buf
+
+    def eval_returns_from_draws(self, draws: torch.Tensor, theta: torch.Tensor, levels: torch.Tensor,
+                                state: torch.Tensor) -> torch.Tensor:
+        """eval_returns on draws from eval_draws (same keys, levels and worker count): bit-identical.
+        Returns f32 [N, W]."""
+        N = theta.shape[0]
+        n = state.shape[1]
+        cum = torch.empty((N, n // N), dtype=torch.float32, device=state.device)
+        _lib.call("toued_eval_returns", self._c, _lib.ptr(levels), _lib.ptr(theta), theta.shape[1], _lib.ptr(state),
+                  N, n // N, self.eval_rollout_len, _lib.ptr(draws), _lib.ptr(cum), _lib.stream_ptr())
+        return cum
+
     def eval_returns(self, agent_keys: torch.Tensor, theta: torch.Tensor, levels: torch.Tensor,
                      state: torch.Tensor) -> torch.Tensor:
         """batch_rollout(..., eval=True) when only cum_return is consumed (eval_agent): returns-only

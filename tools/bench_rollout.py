@@ -52,7 +52,14 @@ def main():
     res["eval_rollout_ms"] = timed(lambda: st._eval_rollout(st.keys_ea_roll, st.theta_h[K], ag.levels, ea_state))
     state = ag.state.clone()
     res["train_rollout_ms"] = timed(lambda: ro.batch_rollout(st.keys_ea_roll, st.theta_h[K], ag.levels, state))
+    ew = ea_state.shape[1] // ag.levels.shape[0]
+    res["eval_draws_ms"] = timed(lambda: ro.eval_draws(st.keys_ea_roll, ag.levels, ew))
+    draws = ro.eval_draws(st.keys_ea_roll, ag.levels, ew)
+    res["eval_returns_from_draws_ms"] = timed(lambda: ro.eval_returns_from_draws(draws, st.theta_h[K], ag.levels,
+                                                                                 ea_state))
     cum = st._eval_rollout(st.keys_ea_roll, st.theta_h[K], ag.levels, ea_state)
+    cum3 = ro.eval_returns_from_draws(draws, st.theta_h[K], ag.levels, ea_state)
+    res["three_launch_bit_identical"] = bool(torch.equal(cum, cum3))
     res["eval_mean_return"] = float(cum.mean())
     print(json.dumps(res), flush=True)
 
