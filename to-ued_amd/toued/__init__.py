@@ -7,4 +7,14 @@ streams and torch.distributed; the computation is in the HIP kernels.
 """
 from ._lib import ToUEDError, lib  # noqa: F401
 
-__all__ = ["ToUEDError", "lib"]
+
+def __getattr__(name):
+    # the reference's meta/meta.py entry points, imported lazily (they pull in torch and the rollout machinery)
+    if name in ("create_lpg_train_state", "make_lpg_train_step", "LpgTrainState", "ValueCriticStates"):
+        from . import meta
+        return getattr(meta, name)
+    raise AttributeError(name)
+
+
+__all__ = ["ToUEDError", "lib", "create_lpg_train_state", "make_lpg_train_step", "LpgTrainState",
+           "ValueCriticStates"]

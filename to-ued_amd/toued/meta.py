@@ -383,3 +383,90 @@ def _cat_metrics(parts):
     for k, v in parts[0].items():
         out[k] = _cat_metrics([p[k] for p in parts]) if isinstance(v, dict) else torch.cat([p[k] for p in parts])
     return out
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# The reference's functional surface (meta/meta.py:10-52): create_lpg_train_state / make_lpg_train_step returning
+# train_step(rng, lpg_train_state, agent_states, value_critic_states) -> the same 4-tuple as lpg_meta_grad_train_step
+# (meta/train.py:14-130) and lpg_es_train_step (meta/train.py:133-227).  The device tables are large (144 MB of
+# agent tables per copy at N=512), so the step updates them in place and the returned states alias the inputs.
+
+
+@dataclass
+class LpgTrainState:
+    """flax ``TrainState`` of the LPG (meta/meta.py:21-24): ``params`` is the flat eta in jax tree order
+    (lpg.LPGLayout), ``opt`` the optax Adam state (count, mu, nu); with --use_es ``es`` holds the OpenES strategy and
+    state of ``ESTrainState`` (util/data.py:63-68) once the step has been built."""
+    params: torch.Tensor
+    opt: AdamState | None
+    es: object | None = None
+
+    @property
+    def step(self) -> int:
+        return self.opt.count if self.opt is not None else 0
+
+
+@dataclass
+class ValueCriticStates:
+    """The per-agent value critics (agents/agents.py:70-95): params f32 [N, D], step int32 [N]."""
+    params: torch.Tensor
+    step: torch.Tensor
+
+
+def lpg_hypers_from_args(args, sampler) -> LpgHyperparams:
+    """LpgHyperparams.from_run_args (util/data.py) plus the agent hyperparameters of the level sampler."""
+    ah = sampler.agent_hypers
+    return LpgHyperparams(
+        num_agent_updates=args.num_agent_updates, agent_target_coeff=args.lpg_agent_target_coeff,
+        policy_entropy_coeff=args.lpg_policy_entropy_coeff, target_entropy_coeff=args.lpg_target_entropy_coeff,
+        policy_l2_coeff=args.lpg_policy_l2_coeff, target_l2_coeff=args.lpg_target_l2_coeff, gamma=args.gamma,
+        gae_lambda=args.gae_lambda, actor_lr=ah.actor_learning_rate, critic_lr=ah.critic_learning_rate,
+        max_grad_norm=ah.max_grad_norm, lpg_lr=args.lpg_learning_rate,
+        fix_value_critic=bool(getattr(args, "fix_value_critic", False)))
+
+
+def create_lpg_train_state(rng: torch.Tensor, args) -> LpgTrainState:
+    """meta/meta.py:10-30: flax's init of the LPG from ``rng`` (lpg.flax_init_lpg_params) and a fresh Adam state;
+    with --use_es the OpenES strategy is attached by make_lpg_train_step's first call."""
+    from .lpg import flax_init_lpg_params
+    eta = flax_init_lpg_params(rng, 7 if args.lifetime_conditioning else 5)
+    return LpgTrainState(eta, None if args.use_es else AdamState(eta.numel(), eta.device))
+
+
+def make_lpg_train_step(args, level_sampler, n_agents: int | None = None, world=None, rank_slice=None, impl=None):
+    """meta/meta.py:33-52.  Returns ``train_step(rng, lpg_train_state, agent_states, value_critic_states=None)`` ->
+    ``(lpg_train_state, agent_states, value_critic_states, metrics)``.
+
+    agent_states: agents.AgentBatch of this rank's agents (``rank_slice`` = (lo, hi, n_total) under data
+    parallelism; n_agents defaults to its size).  value_critic_states: ValueCriticStates or None (then the ones
+    inside agent_states are used); ignored by the ES step, as in the reference.  ``impl``: an already built
+    MetaGradStep / ESTrainStep to drive (train.Trainer keeps its instance for timers and buffers)."""
+    n_local = n_agents if n_agents is not None else (args.num_agents if rank_slice is None
+                                                     else rank_slice[1] - rank_slice[0])
+    holder = {} if impl is None else {"step": impl}
+    if args.use_es:
+
+        def es_step(rng, lpg_train_state, agent_states, value_critic_states=None):
+            from .es import ESTrainStep
+            if "step" not in holder:
+                holder["step"] = ESTrainStep(args, level_sampler, n_local, lpg_train_state.params,
+                                             lpg_train_state.params.device, world)
+            lpg_train_state.es = holder["step"].es
+            metrics = holder["step"](rng, agent_states, rank_slice)
+            return lpg_train_state, agent_states, value_critic_states, metrics
+        return es_step
+
+    hyp = lpg_hypers_from_args(args, level_sampler)
+
+    def meta_grad_step(rng, lpg_train_state, agent_states, value_critic_states=None):
+        if "step" not in holder:
+            holder["step"] = MetaGradStep(level_sampler.rollout_manager, n_local, hyp, args.lifetime_conditioning,
+                                          lpg_train_state.params.device, world,
+                                          num_mini_batches=args.num_mini_batches)
+        if value_critic_states is not None:
+            agent_states.vcrit, agent_states.vstep = value_critic_states.params, value_critic_states.step
+        metrics = holder["step"](rng, lpg_train_state.params, lpg_train_state.opt, agent_states, rank_slice)
+        return (lpg_train_state, agent_states, ValueCriticStates(agent_states.vcrit, agent_states.vstep), metrics)
+
+    meta_grad_step.step = holder   # the MetaGradStep instance (timers, buffers) once built
+    return meta_grad_step

@@ -4,7 +4,11 @@ The reference's ``RolloutWrapper`` works on one agent and is vmapped by its
 callers (agents/a2c.py:98, agents/lpg_agent.py:109, meta/train.py:48,
 agents/agents.py:101-105, level_sampler.py:276).  Here the agent axis is
 explicit: every call takes N agent keys, N packed levels and N actor tables,
-and runs one fused HIP launch (csrc/env.hip k_rollout).
+and runs one fused HIP launch (csrc/env.hip k_rollout).  Called with the reference's
+single-agent arguments instead -- one key ``rng`` of shape [2], one level, one actor table
+``[D, 5]`` -- ``batch_reset``/``batch_rollout`` run that one agent and return its results
+without the agent axis, as ``RolloutWrapper.batch_reset(rng, env_params, num_workers)`` and
+``batch_rollout(rng, train_state, env_params, init_obs, init_state)`` do.
 """
 from __future__ import annotations
 
@@ -45,7 +49,10 @@ class RolloutWrapper:
         return self.spec.obs_dim
 
     def batch_reset(self, agent_keys: torch.Tensor, levels: torch.Tensor, num_workers: int | None = None):
-        """rollout.py:38-42 per agent: split(rng, W); vmap(env.reset).  Returns ((idx, time) [N*W], state)."""
+        """rollout.py:38-42 per agent: split(rng, W); vmap(env.reset).  Returns ((idx, time) [N*W], state).
+        A single key [2] and level resets that one agent's W workers (the reference's unvmapped call)."""
+        if agent_keys.dim() == 1:
+            return self.batch_reset(agent_keys.view(1, 2), levels.view(1, -1), num_workers)
         W = self.env_workers if num_workers is None else num_workers
         N = agent_keys.shape[0]
         dev = agent_keys.device
@@ -75,8 +82,15 @@ class RolloutWrapper:
                       inplace_state: bool = False):
         """rollout.py:45-102.  theta: actor tables f32 [N, D, 5].
 
-        Returns (Transition, end_state, cum_return f32 [N, W]).
+        Returns (Transition, end_state, cum_return f32 [N, W]).  With a single key [2] (one level, theta [D, 5]):
+        the reference's single-agent batch_rollout, results without the agent axis (cum_return [W]).
         """
+        if agent_keys.dim() == 1:
+            o = None if out is None else Transition(*(x.unsqueeze(0) for x in (out.obs_idx, out.obs_time, out.action,
+                                                                              out.reward, out.done)))
+            tr, st, cum = self.batch_rollout(agent_keys.view(1, 2), theta.unsqueeze(0), levels.view(1, -1), state,
+                                             eval=eval, out=o, inplace_state=inplace_state)
+            return Transition(tr.obs_idx[0], tr.obs_time[0], tr.action[0], tr.reward[0], tr.done[0]), st, cum[0]
         N = agent_keys.shape[0]
         n = state.shape[1]
         W = n // N

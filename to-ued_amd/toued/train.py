@@ -23,19 +23,9 @@ from . import prng
 from .dist import World, init_from_env
 from .level_sampler import LevelSampler
 from .lpg import flax_init_lpg_params
-from .meta import AdamState, LpgHyperparams, MetaGradStep
+from .meta import (AdamState, LpgTrainState, MetaGradStep, lpg_hypers_from_args,  # noqa: F401 (re-exported)
+                   make_lpg_train_step)
 from .parse_args import parse_args
-
-
-def lpg_hypers_from_args(args, sampler: LevelSampler) -> LpgHyperparams:
-    ah = sampler.agent_hypers
-    return LpgHyperparams(
-        num_agent_updates=args.num_agent_updates, agent_target_coeff=args.lpg_agent_target_coeff,
-        policy_entropy_coeff=args.lpg_policy_entropy_coeff, target_entropy_coeff=args.lpg_target_entropy_coeff,
-        policy_l2_coeff=args.lpg_policy_l2_coeff, target_l2_coeff=args.lpg_target_l2_coeff, gamma=args.gamma,
-        gae_lambda=args.gae_lambda, actor_lr=ah.actor_learning_rate, critic_lr=ah.critic_learning_rate,
-        max_grad_norm=ah.max_grad_norm, lpg_lr=args.lpg_learning_rate,
-        fix_value_critic=bool(getattr(args, "fix_value_critic", False)))
 
 
 def check_supported(args):
@@ -84,15 +74,15 @@ class Trainer:
             self.step_fn = MetaGradStep(self.sampler.rollout_manager, n_local, self.hyp, args.lifetime_conditioning,
                                         self.dev, self.world, num_mini_batches=args.num_mini_batches)
             self.adam = AdamState(self.eta.numel(), self.dev)
+        # the reference's lpg_train_step_fn (train.py:33, meta/meta.py:33-52) driving this instance
+        self.train_state = LpgTrainState(self.eta, None if args.use_es else self.adam)
+        self.train_step = make_lpg_train_step(args, self.sampler, n_local, self.world, sl, impl=self.step_fn)
 
     def meta_step(self):
         """_meta_train_loop (train.py:36-54): LPG update, then level_sampler.sample."""
         ks = prng.split(self.rng, 2)
         self.rng, sub = ks[0].contiguous(), ks[1].contiguous()
-        if self.args.use_es:
-            metrics = self.step_fn(sub, self.agents, self.sl)
-        else:
-            metrics = self.step_fn(sub, self.eta, self.adam, self.agents, self.sl)
+        self.train_state, self.agents, _, metrics = self.train_step(sub, self.train_state, self.agents)
         ks = prng.split(self.rng, 2)
         self.rng, sub = ks[0].contiguous(), ks[1].contiguous()
         self.buffer, self.agents = self.sampler.sample(sub, self.buffer, self.agents, self.sl)
