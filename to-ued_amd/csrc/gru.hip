@@ -116,6 +116,35 @@ TOUED_DEV float tanh_f(float x) {
   return copysignf(t, x);
 }
 
+// The n gate of the split-precision kernels: n = tanh(W_in x + b_in + r * (W_hn h + b_hn)).  The input part
+// ain = W_in x + b_in is one f32 MFMA chain (v_mfma_f32_32x32x2f32, K = 8: x_0..x_{F-1}, 0.., 1) in the gate
+// maths' accumulator layout (lane = row, register q = unit 32 wave + 4 hi + qunit(q)), issued identically by the
+// forward (k_gru_fwd6) and the backward (k_gru_bwd6n), so the backward recomputes n bit for bit from the saved r
+// and W_hn h + b_hn instead of reading a saved n: 1 KiB per column less written by the forward and read by the
+// backward.  wI[kk] = A[i = unit 32 wave + (l & 31)][k = 2 kk + (l >> 5)] = W_in[k][u] (k < F), b_in[u] (k = 7).
+TOUED_DEV void load_win_frags(float (&wI)[4], const float* eta, const EtaOff& o, int F, int wave, int lane) {
+  const int u = 32 * wave + (lane & 31);
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const int k = 2 * kk + (lane >> 5);
+    wI[kk] = k < F ? eta[o.in_w + k * HU + u] : k == 7 ? eta[o.in_b + u] : 0.0f;
+  }
+}
+// B[k = 2 kk + hi][j = row] from this lane's row inputs (xk(k) = x_k for k < F)
+template <typename XK>
+TOUED_DEV floatx16 gate_ain(const float (&wI)[4], int F, int hi, XK xk) {
+  floatx16 a;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) a[q] = 0.0f;
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const int k = 2 * kk + hi;
+    a = mfma32(wI[kk], k < F ? xk(k) : k == 7 ? 1.0f : 0.0f, a);
+  }
+  return a;
+}
+TOUED_DEV float gate_n(float ain, float rg, float hn) { return tanh_r(__builtin_fmaf(rg, hn, ain)); }
+
 // ------------------------------------------------------------------ packing
 // fwdA[(tile*KQF + kq)*64 + lane] = float4 over kk = 4kq..4kq+3 of A[i=l&31][k=2kk+(l>>5)]
 __global__ void k_pack_fwd(const float* __restrict__ eta, EtaOff o, int F, float4* __restrict__ out,
@@ -589,6 +618,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     wh[i] = oo == 0 ? eta[p.o.pi_w + u] : oo < 9 ? eta[p.o.y_w + u * 8 + (oo - 1)] : 0.0f;
   }
   for (int i = tid; i < 4 * HU; i += 512) usc[i] = 1.0f / (A6c[F6_SCALES + i] * HSCALE);   // powers of two: exact
+  float wI[4];
+  load_win_frags(wI, eta, p.o, F, wave, lane);
   {
     uint4* z = reinterpret_cast<uint4*>(&hB[0][0]);
     for (int i = tid; i < 3 * 64 * F6_HP / 8; i += 512) z[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -611,12 +642,12 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     return __builtin_bit_cast(f16x8, x);
   };
   const __amdgpu_buffer_rsrc_t rs_hin = rsrc_of(p.s_hin), rs_r = rsrc_of(p.s_r), rs_z = rsrc_of(p.s_z),
-                               rs_n = rsrc_of(p.s_n), rs_hn = rsrc_of(p.s_hn);
+                               rs_hn = rsrc_of(p.s_hn);
   for (int s = 0; s < T; ++s) {
     const int t = T - 1 - s;
-    floatx16 acc[4][2];
+    floatx16 acc[3][2];   // r, z, W_hn h + b_hn (the n gate's input part is gate_ain, on the VALU)
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
+    for (int g = 0; g < 3; ++g)
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -674,8 +705,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
       for (int q = 0; q < 3; ++q) Aa[g][q] = ldA(fragAug(g, q));
       __builtin_amdgcn_sched_barrier(0);
     }
-    // augmented k-step: B = bf16 pieces of 2^14 [x, 1, 0 ...]; the ni gate's fragments go into Aa[0] once
-    // r's MFMAs are issued
+    // augmented k-step: B = bf16 pieces of 2^14 [x, 1, 0 ...]
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -687,15 +717,12 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     for (int g = 0; g < 3; ++g) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) acc[g][h] = mfma6(Aa[g], Ba[h], acc[g][h]);
-      if (g == 0) {
-#pragma unroll
-        for (int q = 0; q < 3; ++q) Aa[0][q] = ldA(fragAug(3, q));
-      }
     }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) acc[3][h] = mfma6(Aa[0], Ba[h], acc[3][h]);
     __syncthreads();   // every wave done reading hB / xB: the carry and x(t-1) overwrite them in place
     // ---- gate maths (lane = row 32h + col, register q = unit 32 wave + 4 hi + qunit(q))
+    floatx16 ain[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) ain[h] = gate_ain(wI, F, hi, [&](int k) { return xv[h][k < 7 ? k : 6]; });
     const long cbase = (long)t * R;
     const int ub = 32 * wave + 4 * hi;
     const float4* whl = reinterpret_cast<const float4*>(wh + ub * 12);
@@ -716,9 +743,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
         const f16x4 h0 = *reinterpret_cast<const f16x4*>(&hB[0][ho]);
         const f16x4 h1 = *reinterpret_cast<const f16x4*>(&hB[1][ho]);
         const bf16x4 hr = *reinterpret_cast<const bf16x4*>(&hB[2][ho]);
-        float us[4][4];
+        float us[3][4];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
+        for (int g = 0; g < 3; ++g) {
           const float4 v = *reinterpret_cast<const float4*>(&usc[g * HU + ub + 8 * g4]);
           us[g][0] = v.x; us[g][1] = v.y; us[g][2] = v.z; us[g][3] = v.w;
         }
@@ -730,7 +757,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
           const float rg = sigm_r(acc[0][h][q] * us[0][e]);
           const float zg = sigm_r(acc[1][h][q] * us[1][e]);
           const float hn = acc[2][h][q] * us[2][e];
-          const float ng = tanh_r(acc[3][h][q] * us[3][e] + rg * hn);
+          const float ng = gate_n(ain[h][q], rg, hn);
           const float hin = (((float)h0[e] + (float)h1[e]) + (float)hr[e]) * (1.0f / HSCALE);   // exact
           const float hh = (1.0f - zg) * ng + zg * hin;
           split_carry(dn ? 0.0f : hh, n0, n1, nr, e);   // carry h_in(t-1) = where(d_{t-1}, 0, h_out(t))
@@ -739,8 +766,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
             st_u(rs_hin, vbyte, so, hin);
             st_u(rs_r, vbyte, so, rg);
             st_u(rs_z, vbyte, so, zg);
-            st_u(rs_n, vbyte, so, ng);
-            st_u(rs_hn, vbyte, so, hn);
+            st_u(rs_hn, vbyte, so, hn);   // n is recomputed by the backward (gate_n)
           }
           const float rl = fmaxf(hh, 0.0f);
           const float4 w0 = whl[qunit(q) * 3], w1 = whl[qunit(q) * 3 + 1], w2 = whl[qunit(q) * 3 + 2];
@@ -797,6 +823,7 @@ struct BwdArgs {
   float* dX3; float* dX4;   // [K][T][R]
   int8_t* CE;       // [M] (optional, lockstep kernel): column m's cotangent scale exponent for the weight-gradient
                     // reduction (2^CE[m] max over dr, dz, dhn of column m < 2^14; 127 = all zero)
+  int F;            // LPG input width (lockstep kernel: x rows at s_hin + 256 M, n recomputed by gate_n)
 };
 
 // NT row tiles of 32 rows per workgroup.  NT = 2: one workgroup per CU (150 KB LDS, 256 VGPRs), every
@@ -1015,6 +1042,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   __shared__ __attribute__((aligned(8))) float dxp[8 * RBT * 2];   // [wave][row][dx3 | dx4]
   __shared__ __attribute__((aligned(16))) float wsc[HU];          // 2^s of W_g row i (fp16 A scale)
   __shared__ float rmx[8 * RBT];                   // per-wave row maxima of |dr|, |dz|, |dhn| (fp16 B scale)
+  __shared__ float wIs[8 * 4 * 64];                // gate_ain's W_in fragments [wave][kk][lane] (read at each tile)
   // dr in f32 while the memory part streams ([row][unit], pitch DRP), over image slots 1 and 2
   constexpr int DRP = HU + 4;
   static_assert(RBT * DRP * 4 <= 2 * RBT * PP * 2, "dr staging exceeds image slots 1-2");
@@ -1037,6 +1065,13 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     wi34[i] = p.eta[base + f * HU + u];
   }
   for (int i = tid; i < HU; i += 512) wsc[i] = reinterpret_cast<const float*>(p.A6)[B6_SCALES + i];
+  const int F = p.F;
+  {
+    float wI[4];   // n gate input weights (gate_ain), kept in LDS: registers are the bound here
+    load_win_frags(wI, p.eta, p.o, F, wave, lane);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) wIs[(wave * 4 + kk) * 64 + lane] = wI[kk];
+  }
   float wA[5];   // W_heads^T A fragments of unit tile `wave`: A[i = unit][k = head output 2kk + hi]
 #pragma unroll
   for (int kk = 0; kk < 5; ++kk) {
@@ -1049,7 +1084,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) dh[h][q] = 0.0f;
   const __amdgpu_buffer_rsrc_t rs_hin = rsrc_of(p.s_hin), rs_r = rsrc_of(p.s_r), rs_z = rsrc_of(p.s_z),
-                               rs_n = rsrc_of(p.s_n), rs_hn = rsrc_of(p.s_hn), rs_rh = rsrc_of(p.RH);
+                               rs_hn = rsrc_of(p.s_hn), rs_rh = rsrc_of(p.RH);
+  const __amdgpu_buffer_rsrc_t rs_x = rsrc_of(p.s_hin + (size_t)HU * p.M);   // the rows' inputs x [F][M]
   const __amdgpu_buffer_rsrc_t rs_dg[4] = {rsrc_of(p.DG), rsrc_of(p.DG + 1L * HU * p.M),
                                            rsrc_of(p.DG + 2L * HU * p.M), rsrc_of(p.DG + 3L * HU * p.M)};
   const __amdgpu_buffer_rsrc_t rs_yh = rsrc_of(p.y_hat), rs_dyh = rsrc_of(p.d_y_hat), rs_dpi = rsrc_of(p.d_pi_hat),
@@ -1134,25 +1170,38 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     float dz_r[2][16], dhn_r[2][16];
     const int ub = 32 * wave + 4 * hi;               // lane's unit base (register q adds qunit(q))
     const float* wil = wi34 + ub;
-    float va[5][4], vb4[5][4];
-    auto load_q = [&](int h, int g4, float (&v)[5][4]) {
+    float vr[3][4][4];   // three-slot ring: quads i+1 and i+2 in flight while quad i is processed
+    auto load_q = [&](int h, int g4, float (&v)[4][4]) {
       const unsigned vq = (unsigned)((((long)(ub + (col & 3))) * p.M + r0 + RB * h + (col & 28)) * 4);
       const unsigned so = (unsigned)(((long)8 * g4 * p.M + ctr) * 4);
       ld4(rs_hin, vq, so, v[0]);
       ld4(rs_r, vq, so, v[1]);
       ld4(rs_z, vq, so, v[2]);
-      ld4(rs_n, vq, so, v[3]);
-      ld4(rs_hn, vq, so, v[4]);
+      ld4(rs_hn, vq, so, v[3]);
     };
+    // the rows' inputs x(t) as gate_ain's B fragments (lane = row RB h + col, k = 2 kk + hi): n is recomputed.
+    // Tile 0's go out now, tile 1's beside the ring loads of quad 3.
+    float xa[4], xb[4];
+    auto load_x = [&](int h, float (&x)[4]) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int k = 2 * kk + hi;
+        x[kk] = ld_u(rs_x, (unsigned)((RB * h + col) * 4), (unsigned)((((long)(k < F ? k : 0)) * p.M + ctr + r0) * 4));
+      }
+    };
+    load_x(0, xa);
+    floatx16 ain;
     floatx16 hacc;
     float dx3 = 0.0f, dx4 = 0.0f;
     float rmr[2] = {0.0f, 0.0f};   // running row maxima of |dr|
-    load_q(0, 0, va);
+    load_q(0, 0, vr[0]);
+    load_q(0, 1, vr[1]);
 #pragma unroll
     for (int qi = 0; qi < 8; ++qi) {
       const int h = qi >> 2, g4 = qi & 3;
-      float (&v)[5][4] = (qi & 1) ? vb4 : va;
-      if (qi + 1 < 8) load_q((qi + 1) >> 2, (qi + 1) & 3, (qi & 1) ? va : vb4);
+      float (&v)[4][4] = vr[qi % 3];
+      if (qi + 2 < 8) load_q((qi + 2) >> 2, (qi + 2) & 3, vr[(qi + 2) % 3]);
+      if (qi == 3) load_x(1, xb);
       __builtin_amdgcn_sched_barrier(0);
       if (g4 == 0) {
         // head VJP W_heads . hv on MFMA for this row tile (lane = row, register = unit)
@@ -1163,18 +1212,23 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
           const int o = 2 * kk + hi;
           hacc = mfma32(wA[kk], o < 9 ? hv[o * RBT + RB * h + col] : 0.0f, hacc);
         }
+        float wI[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) wI[kk] = wIs[(wave * 4 + kk) * 64 + lane];
+        ain = gate_ain(wI, F, hi, [&](int k) { return h ? xb[k >> 1] : xa[k >> 1]; });
         dx3 = 0.0f;
         dx4 = 0.0f;
       }
       const int row = RB * h + col;
       const unsigned vbo = (unsigned)(((long)ub * p.M + r0 + row) * 4);
 #pragma unroll
-      for (int a = 0; a < 5; ++a) quad_transpose(v[a], lane);
+      for (int a = 0; a < 4; ++a) quad_transpose(v[a], lane);
       float drq[4];
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int q = 4 * g4 + jj;
-        const float hin = v[0][jj], rg = v[1][jj], zg = v[2][jj], ng = v[3][jj], hn = v[4][jj];
+        const float hin = v[0][jj], rg = v[1][jj], zg = v[2][jj], hn = v[3][jj];
+        const float ng = gate_n(ain[q], rg, hn);
         const float hout = (1.0f - zg) * ng + zg * hin;
         const float d = dh[h][q] + (hout > 0.0f ? hacc[q] : 0.0f);
         const float dn_ = d * (1.0f - zg);
@@ -1449,6 +1503,8 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
   p.y_hat = y_hat; p.d_pi_hat = d_pi_hat; p.d_y_hat = d_y_hat;
   p.s_hin = s_hin; p.s_r = s_r; p.s_z = s_z; p.s_n = s_n; p.s_hn = s_hn; p.M = M;
   p.DG = DG; p.RH = RH; p.DH = DH; p.dX3 = dX3; p.dX4 = dX4; p.CE = col_exp;
+  p.F = (p.o.ir_b - p.o.in_w) / HU;   // in_w [F][256] is followed by ir_b in the flat layout (lpg.LPGLayout)
+  TOUED_REQUIRE(p.F >= 1 && p.F <= 7 && p.o.ir_b - p.o.in_w == p.F * HU, "toued_gru_bwd: LPG layout F=%d", p.F);
   if (toued_gru_bwd_col_exp(R))
     hipLaunchKernelGGL(k_gru_bwd6n, dim3(K * (R / (2 * RB))), dim3(512), 0, stream, p);
   else
