@@ -666,7 +666,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
         xv[h][f] = ld_u(rs_X, (unsigned)((RB * h + col) * p.xs_col * 4),
                         (unsigned)((fc * p.xs_f + ((long)t * R + r0) * p.xs_col) * 4));
       }
-    f16x8 A[3][2], B[2][2];
+    // A fragments through a two-k-step ring (A0: even k-steps, A1: odd): each L2 fragment load has a whole k-step
+    // of the wave's MFMAs (plus the partner wave's) to land instead of one gate's
+    f16x8 A0[3][2], A1[3][2], B[2][2];
     auto fragA = [&](int ks, int g, int q) { return ((ks * 8 + wave) * 3 + g) * 2 + q; };
     auto fragAug = [&](int g, int q) { return F6_NFH + (wave * 4 + g) * 3 + q; };
     auto load_B = [&](int ks, int h) {
@@ -677,24 +679,35 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
 #pragma unroll
     for (int g = 0; g < 3; ++g)
 #pragma unroll
-      for (int q = 0; q < 2; ++q) A[g][q] = ldAh(fragA(0, g, q));
+      for (int q = 0; q < 2; ++q) {
+        A0[g][q] = ldAh(fragA(0, g, q));
+        A1[g][q] = ldAh(fragA(1, g, q));
+      }
     load_B(0, 0);
     load_B(0, 1);
-    // (a rolled loop: a full unroll hoists ~300 fragment offsets into SGPRs, which spill)
-#pragma nounroll
-    for (int ks = 0; ks < 15; ++ks) {
+    auto kstep = [&](int ks, f16x8 (&Ar)[3][2], bool reload) {
 #pragma unroll
       for (int g = 0; g < 3; ++g) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          acc[g][h] = mfma3h(A[g], B[h], acc[g][h]);
+          acc[g][h] = mfma3h(Ar[g], B[h], acc[g][h]);
           if (g == 2) load_B(ks + 1, h);
         }
+        if (reload) {
 #pragma unroll
-        for (int q = 0; q < 2; ++q) A[g][q] = ldAh(fragA(ks + 1, g, q));
+          for (int q = 0; q < 2; ++q) Ar[g][q] = ldAh(fragA(ks + 2, g, q));
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
+    };
+    // (a rolled loop over k-step pairs: a full unroll hoists ~300 fragment offsets into SGPRs, which spill)
+#pragma nounroll
+    for (int kp = 0; kp < 7; ++kp) {
+      kstep(2 * kp, A0, true);
+      kstep(2 * kp + 1, A1, true);
     }
+    kstep(14, A0, false);
+    f16x8 (&A)[3][2] = A1;   // k-step 15
     // last carry k-step; each gate's augmented fragments (three bf16 pieces) load behind its MFMAs
     bf16x8 Aa[3][3], Ba[2][3];
 #pragma unroll
