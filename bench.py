@@ -46,11 +46,18 @@ HBM_PEAK_GBS = 8000.0
 SPLIT_PRODUCTS = {"gru_fwd": (16 * 3 + 6) / 17, "gru_bwd": 3.0}
 GRU_FWD_FLOP_PER_ELEM = {5: 406080, 7: 409152}    # per (agent, worker, t)
 GRU_BWD_FLOP_PER_ELEM = 2 * 256 * 768              # dh_prev = dG . W_h^T per (k, agent, worker, t)
-# algorithmic HBM bytes per element: forward saves h_in, r, z, n, W_hn h + b_hn (5 x 256 f32) and
-# reads its inputs/writes its heads (F + 1 + 9 floats); backward reads those five saves and writes DG (4 x 256),
-# relu(h_out) (256) and DH (9), reading the head cotangents and y_hat (1 + 8 + 8) and writing dX3/dX4 (2)
-GRU_FWD_BYTES_PER_ELEM = {F: 4 * (5 * 256 + F + 1 + 9) for F in (5, 7)}
-GRU_BWD_BYTES_PER_ELEM = 4 * (5 * 256 + 5 * 256 + 9 + 17 + 2)
+# algorithmic HBM bytes per element: forward saves h_in, r, z, W_hn h + b_hn (4 x 256 f32; n is
+# recomputed by the backward) and reads its inputs/writes its heads (F + 1 + 9 floats); backward reads those four
+# saves and the inputs x (F), writes DG (4 x 256), relu(h_out) (256) and DH (9), reading the head cotangents and
+# y_hat (1 + 8 + 8) and writing dX3/dX4 (2)
+GRU_FWD_BYTES_PER_ELEM = {F: 4 * (4 * 256 + F + 1 + 9) for F in (5, 7)}
+GRU_BWD_BYTES_PER_ELEM = {F: 4 * (4 * 256 + F + 5 * 256 + 9 + 17 + 2) for F in (5, 7)}
+# main weight-gradient reduction [h_in; x; 1] (256 + F + 1 rows) x [dr; dz; dhn] (768 rows) over M columns: f32-equiv
+# FLOP 2 * rows * 768 per column, issued as 3 fp16 products (block-floating-point pairs); algorithmic bytes = both
+# operands once (the A rows are re-read by 4 column tiles through L2)
+WGRAD_PRODUCTS = 3.0
+# train rollout: 34 B per agent-env-step (14 written: idx, time, action, reward, done; 20 read: the actor row)
+ROLLOUT_BYTES_PER_STEP = 34
 
 
 # device kernel behind each timed region, as rocprofv3 names it (prof_summary.short)
@@ -289,7 +296,7 @@ def main():
     # the roofline bound is whichever roof sets the longer minimum time (bytes / 8 TB/s vs the bf16 MFMA work
     # the f32-accurate split issues / 2.5 PF/s)
     work = {"gru_fwd": (R * T * GRU_FWD_FLOP_PER_ELEM[F], R * T * GRU_FWD_BYTES_PER_ELEM[F]),
-            "gru_bwd": (K * R * T * GRU_BWD_FLOP_PER_ELEM, K * R * T * GRU_BWD_BYTES_PER_ELEM)}
+            "gru_bwd": (K * R * T * GRU_BWD_FLOP_PER_ELEM, K * R * T * GRU_BWD_BYTES_PER_ELEM[F])}
     cand = [(n, ksum[n][2], ksum[n][1]) for n in work if n in ksum]
     dom, _, mean_ms = max(cand, key=lambda c: c[1])
     flop, nbytes = work[dom]
@@ -307,21 +314,44 @@ def main():
                      "mean_ms": round(mean_ms, 4), "min_ms_hbm": round(t_hbm * 1e3, 3),
                      "min_ms_mfma": round(t_mfma * 1e3, 3), "flop_per_launch_f32": flop,
                      "f32_equiv_tflops": round(flop / sec / 1e12, 1), "f32_mfma_peak": MFMA_F32_PEAK_TFLOPS})
+    # secondary roofline entries: the weight-gradient reduction (MFMA) and the train rollout (HBM by its bytes; in
+    # practice a per-step dependent chain of threefry blocks on the VALU)
+    secondary = {}
+    M = K * R * T
+    if "wgrad_main" in ksum:
+        wsec = ksum["wgrad_main"][1] * 1e-3
+        wflop = 2.0 * (256 + F + 1) * 768 * M
+        wbytes = 4.0 * (256 + F + 1 + 768) * M
+        secondary["wgrad"] = {"bound": "mfma", "kernel": "k_wgrad_h3 (+ rowmax, chunk reduce)",
+                              "achieved": round(WGRAD_PRODUCTS * wflop / wsec / 1e12, 1),
+                              "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s (16-bit issued)",
+                              "frac": round(WGRAD_PRODUCTS * wflop / (MFMA_BF16_PEAK_TFLOPS * 1e12) / wsec, 4),
+                              "hbm_gbs": round(wbytes / wsec / 1e9, 1), "mean_ms": round(wsec * 1e3, 4),
+                              "traffic": pmc_traffic("k_wgrad_h3")[0]}
+    if "rollout" in ksum:
+        rsec = ksum["rollout"][1] * 1e-3
+        rsteps = R * T
+        secondary["rollout"] = {"bound": "valu (threefry chain); hbm by bytes", "kernel": "k_rollout (train)",
+                                "achieved": round(rsteps * ROLLOUT_BYTES_PER_STEP / rsec / 1e9, 1),
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": round(rsteps * ROLLOUT_BYTES_PER_STEP / rsec / 1e9 / HBM_PEAK_GBS, 4),
+                                "agent_env_steps_per_sec": round(rsteps / rsec, 1), "mean_ms": round(rsec * 1e3, 4)}
     out = {
         "metric": "agent-env-steps/sec (inner rollout) at num_agents=512; meta-updates/sec",
         "value": round(value, 1), "unit": "agent-env-steps/sec", "n_gpus": n_gpus, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "mfma_precision": "f32-class: GRU recurrent products (forward carry, backward gate passes) on power-of-two-"
-                          "scaled fp16 pairs (3 fp16 MFMA products, pieces to 2^-22 relative), the input k-step and the "
-                          "weight-gradient reduction on the exact 3-piece bf16 split (6 products); f32 accumulate",
+                          "scaled fp16 pairs (3 fp16 MFMA products, pieces to 2^-22 relative), the weight-gradient "
+                          "reduction on block-floating-point fp16 pairs (3 products), the input k-step on the exact "
+                          "3-piece bf16 split (6 products), the n gate's input part on f32 MFMA; f32 accumulate",
         "data": "synthetic (procedurally generated levels)",
         "meta_updates_per_sec": round(a.steps / dt, 3),
         "config": {"workload": f"C2 LPG meta-gradient env_mode={a.env_mode} num_agents={N_total} "
                                f"num_mini_batches=1 W={W} T={T} K={K} score_function=random",
                    "num_agents": N_total, "agents_per_gpu": a.agents_per_gpu, "env_workers": W,
                    "train_rollout_len": T, "num_agent_updates": K, "parallelism": f"dp{n_gpus} (agent axis)"},
-        "roofline": roofline, "kernels": kern,
+        "roofline": roofline, "roofline_secondary": secondary, "kernels": kern,
         "metrics": {"lpg_agent_return": float(metrics["lpg_agent_return"].mean()),
                     "lpg_loss": float(metrics["lpg_loss"].mean())},
     }

@@ -226,12 +226,15 @@ class LPGGRU:
         st = _lib.stream_ptr()
         _lib.call("toued_gru_bwd_small", M, _lib.ptr(self.A), _lib.ptr(DG), _lib.ptr(self.RH), _lib.ptr(self.DH),
                   _lib.ptr(self.GI), ws, wn, st)
+        tok_main = timers.start("wgrad_main") if timers is not None else None
         if self.bfp:
             _lib.call("toued_wgrad_bfp", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, H, _lib.ptr(DG), M,
                       _lib.ptr(self.CE), _lib.ptr(G), ws, wn, st)
         else:
             _lib.call("toued_wgrad", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, _lib.ptr(DG), M, _lib.ptr(G), ws, wn,
                       st)
+        if tok_main is not None:
+            timers.stop(tok_main)
         lay.view(grad, "hr_w").add_(G[0:H, 0:H])
         lay.view(grad, "hz_w").add_(G[0:H, H:2 * H])
         lay.view(grad, "hn_w").add_(G[0:H, 2 * H:3 * H])
