@@ -731,7 +731,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) acc[g][h] = mfma6(Aa[g], Ba[h], acc[g][h]);
     }
-    __syncthreads();   // every wave done reading hB / xB: the carry and x(t-1) overwrite them in place
+    lds_barrier();   // every wave done reading hB / xB: the carry and x(t-1) overwrite them in place
     // ---- gate maths (lane = row 32h + col, register q = unit 32 wave + 4 hi + qunit(q))
     floatx16 ain[2];
 #pragma unroll
@@ -798,7 +798,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
         if (hi == 0) hp[(wave * 9 + oo) * 64 + row] = hp_loc[oo] + o;
       }
     }
-    __syncthreads();   // head partials, the carry and x(t-1) visible
+    lds_barrier();   // head partials, the carry and x(t-1) visible
     for (int i = tid; i < 9 * 64; i += 512) {
       const int oo = i >> 6, c = i & 63;
       float v = oo == 0 ? bpi : eta[p.o.y_b + oo - 1];
@@ -806,7 +806,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
       for (int gq = 0; gq < 8; ++gq) v += hp[(gq * 9 + oo) * 64 + c];
       hout[i] = v;
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < 64) {
       const long ob = (long)t * R + r0 + tid;
       p.pi_hat[ob] = hout[tid];
@@ -1037,6 +1037,19 @@ __global__ void __launch_bounds__(512, NT == 1 ? 4 : 1) k_gru_bwd(BwdArgs p) {
 }
 
 
+#ifdef BWD_STAMPS
+// timing instrumentation (tools/bwd_stamps.py, built by tools/build_variant.py gru.hip BWD_STAMPS=1): wave 0 lane 0
+// of workgroups < 64 records s_memtime at 8 points of every step
+__device__ unsigned long long g_bwd_stamps[64 * 32 * 8];
+#define BWD_STAMP(ph)                                                                                  \
+  do {                                                                                                 \
+    if (blockIdx.x < 64 && tid == 0 && t < 32)                                                         \
+      g_bwd_stamps[(blockIdx.x * 32 + t) * 8 + (ph)] = __builtin_amdgcn_s_memtime();                   \
+  } while (0)
+#else
+#define BWD_STAMP(ph) do {} while (0)
+#endif
+
 // Backward in lockstep (k_gru_bwd6n): one 512-thread workgroup per (k, 64 rows), both 32-row tiles in
 // every wave, so each pre-split W_g fragment (L2) feeds both tiles: half the fragment traffic of the two-group
 // kernel, which was the vector-memory bottleneck once the contraction moved to the bf16 matrix cores.  Wave w
@@ -1176,8 +1189,10 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   };
   for (int t = 0; t < T; ++t) {
     const long ctr = ((long)k * T + t) * R;
+    BWD_STAMP(0);
     head_cot(t);
-    __syncthreads();
+    lds_barrier();
+    BWD_STAMP(1);
     // ---- memory part: the eight unit quads (two row tiles x four) as a software pipeline, quad i+1's five
     // 16-byte loads in flight while quad i is transposed and processed (twice the bytes in flight per wave)
     float dz_r[2][16], dhn_r[2][16];
@@ -1271,6 +1286,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+    BWD_STAMP(2);
     // row maxima of |dr|, |dz|, |dhn| over this wave's units (the fp16 B scale of the three passes)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1280,7 +1296,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       m = fmaxf(m, __shfl_xor(m, 32));
       if (hi == 0) rmx[wave * RBT + RB * h + col] = m;
     }
-    __syncthreads();   // dr staged, row maxima visible
+    lds_barrier();   // dr staged, row maxima visible
+    BWD_STAMP(3);
     // row scale 2^t (t = 14 - e, max_u max(|dr|, |dz|, |dhn|) < 2^e, clamped to [-40, 40]): the three passes
     // accumulate in the frame 2^(s_i + t_row), unscaled exactly (powers of two) after the hn pass
     float bs[2];
@@ -1323,20 +1340,21 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         *reinterpret_cast<f16x4*>(&dgB[0][row * PP + ub + 8 * g4]) = x0;
         store_dg(0, row, g4, v4);
       }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4)
         *reinterpret_cast<f16x4*>(&dgB[1][(RB * h + col) * PP + ub + 8 * g4]) = x1h[h][g4];
-    __syncthreads();
+    lds_barrier();
     // ---- contraction: dr, then dz, then dhn (scaled fp16 pairs) through the one image
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[h][q] = 0.0f;
+    BWD_STAMP(4);
     contract_h(0);
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -1345,9 +1363,10 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         put4h(RB * h + col, ub + 8 * g4, v4, bs[h]);
         store_dg(1, RB * h + col, g4, v4);
       }
-    __syncthreads();
+    lds_barrier();
+    BWD_STAMP(5);
     contract_h(1);
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -1356,7 +1375,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         put4h(RB * h + col, ub + 8 * g4, v4, bs[h]);
         store_dg(2, RB * h + col, g4, v4);
       }
-    __syncthreads();
+    lds_barrier();
+    BWD_STAMP(6);
     contract_h(2);
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
@@ -1385,7 +1405,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) dh[h][q] = dn ? 0.0f : dh[h][q] + acc[h][q];
     }
-    __syncthreads();   // hv, dxp and the image are rewritten next step
+    BWD_STAMP(7);
+    lds_barrier();   // hv, dxp and the image are rewritten next step
   }
 }
 
@@ -1525,6 +1546,12 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
   TOUED_CHECK_LAUNCH();
   return 0;
 }
+
+#ifdef BWD_STAMPS
+int toued_dbg_bwd_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bwd_stamps), sizeof(g_bwd_stamps)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 size_t toued_gru_bwd_small_work_floats(long M) {
   return std::max(toued_wgrad_workspace_floats(8, HU, M), toued_wgrad_workspace_floats(9, HU + 1, M));

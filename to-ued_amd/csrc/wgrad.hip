@@ -258,7 +258,7 @@ __global__ void __launch_bounds__(64 * X6_NW, 1) k_wgrad_x6(const float* __restr
       __builtin_amdgcn_sched_barrier(0);
       if (i + 1 < 17) { a[0] = an[0]; a[1] = an[1]; a[2] = an[2]; }
     }
-    __syncthreads();
+    lds_barrier();
   };
 
   bf16x8 bpa[X6_BT][3], bpb[X6_BT][3];
@@ -466,7 +466,7 @@ __global__ void __launch_bounds__(64 * X6_NW, 1) k_wgrad_h3(const float* __restr
       __builtin_amdgcn_sched_barrier(0);
       if (i + 1 < 17) { a[0] = an[0]; a[1] = an[1]; }
     }
-    __syncthreads();
+    lds_barrier();
   };
 
   f16x8 bpa[X6_BT][2], bpb[X6_BT][2];
