@@ -340,6 +340,19 @@ __global__ void __launch_bounds__(256) k_wgrad_rowmax(const float* __restrict__ 
   if ((threadIdx.x & 63) == 0) atomicMax(&bits[blockIdx.y], __float_as_int(m));
 }
 
+#ifdef WG_STAMPS
+// timing instrumentation (tools/wgrad_stamps.py): lane 0 of each wave of workgroups < 64 records s_memtime at the
+// start of each of the first 64 slabs, after tile 7, before and after the slab barrier
+__device__ unsigned long long g_wg_stamps[64 * 4 * 64 * 4];
+#define WG_STAMP(s, ph)                                                                                 \
+  do {                                                                                                  \
+    if (blockIdx.x < 64 && lane == 0 && (s) < 64)                                                       \
+      g_wg_stamps[((blockIdx.x * 4 + wave) * 64 + (s)) * 4 + (ph)] = __builtin_amdgcn_s_memtime();      \
+  } while (0)
+#else
+#define WG_STAMP(s, ph) do {} while (0)
+#endif
+
 __global__ void __launch_bounds__(64 * X6_NW, 1) k_wgrad_h3(const float* __restrict__ A, long lda, int ra,
                                                              int a_unit_rows, const int* __restrict__ rowmax_bits,
                                                              const float* __restrict__ B, long ldb, int rb,
@@ -428,6 +441,7 @@ __global__ void __launch_bounds__(64 * X6_NW, 1) k_wgrad_h3(const float* __restr
     for (int t = 0; t < X6_BT; ++t) acc[i][t] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
 
   auto slab = [&](int s, f16x8 (&bp)[X6_BT][2], f16x8 (&bpn)[X6_BT][2]) {
+    WG_STAMP(s, 0);
     const int buf = s & 1;
     load_a(s + 1 < nslab ? s + 1 : s);
     const f16x8* a0p = As[buf][0];
@@ -454,6 +468,7 @@ __global__ void __launch_bounds__(64 * X6_NW, 1) k_wgrad_h3(const float* __restr
       }
       if (i < 2 * X6_BT) split_b(bpn, i >> 1, i & 1);
       if (i == 2 * X6_BT) issue_b(s + 2 < nslab ? s + 2 : nslab - 1);
+      if (i == 8) WG_STAMP(s, 1);
       if (i >= 8) write_a(buf ^ 1, i - 8);
       if (i + 1 < 17) {
         __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // next tile's fragment reads first
@@ -466,7 +481,9 @@ __global__ void __launch_bounds__(64 * X6_NW, 1) k_wgrad_h3(const float* __restr
       __builtin_amdgcn_sched_barrier(0);
       if (i + 1 < 17) { a[0] = an[0]; a[1] = an[1]; }
     }
+    WG_STAMP(s, 2);
     lds_barrier();
+    WG_STAMP(s, 3);
   };
 
   f16x8 bpa[X6_BT][2], bpb[X6_BT][2];
@@ -572,6 +589,12 @@ static Plan plan(int ra, int rb, long K) {
 }  // namespace
 
 extern "C" {
+
+#ifdef WG_STAMPS
+int toued_dbg_wgrad_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wg_stamps), sizeof(g_wg_stamps)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 int toued_set_reserved_cus(int n) {
   const int prev = g_reserved_cus;
