@@ -315,6 +315,15 @@ TOUED_DEV void split2_f16(float y, V& p0, V& p1, int e) {
   p0[e] = h;
   p1[e] = (_Float16)(y - (float)h);
 }
+// the same pieces of y = x * s (s a power of two: the product is exact) in two VALU instructions, each a
+// v_fma_mixlo_f16: h = fp16(x s), l = fp16(fma(x, s, -h)) with h read back as f16 -- the f32 product, the f32 of h
+// and the subtraction of the plain form cost three more, and beside one wave's MFMAs the VALU issue is the bound
+template <typename V>
+TOUED_DEV void split2_f16s(float x, float s, V& p0, V& p1, int e) {
+  const _Float16 h = (_Float16)__builtin_fmaf(x, s, 0.0f);
+  p0[e] = h;
+  p1[e] = (_Float16)__builtin_fmaf(x, s, -(float)h);
+}
 
 // exponent e with 2^e > |x| >= 2^(e-1) (frexp), for the scale 2^(14 - e)
 TOUED_DEV int scale_exp_of(float mx) {
@@ -414,14 +423,17 @@ __global__ void __launch_bounds__(64 * X6_NW, 1) k_wgrad_h3(const float* __restr
       ast[j] = *reinterpret_cast<const float4*>(A + (long)row * lda + kb + 32L * s + 4 * (i & 7));
     }
   };
+  // this thread's staging rows are the same in every slab: their scales live in registers (an LDS read per round
+  // would sit on the in-order LDS counter in front of the fragment reads)
+  float asr[X6_NS];
   auto write_a = [&](int buf, int j) {
     const int i = a_index(j);
     const int row = i >> 3, kq = i & 7;
     const int slot = x6_slot(row, kq >> 1);
-    const float s = asc[row];
+    const float s = asr[j];
     f16x4 p0, p1;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) split2_f16(f4(ast[j], e) * s, p0, p1, e);
+    for (int e = 0; e < 4; ++e) split2_f16s(f4(ast[j], e), s, p0, p1, e);
     reinterpret_cast<f16x4*>(&As[buf][0][slot])[kq & 1] = p0;
     reinterpret_cast<f16x4*>(&As[buf][1][slot])[kq & 1] = p1;
   };
@@ -432,7 +444,7 @@ __global__ void __launch_bounds__(64 * X6_NW, 1) k_wgrad_h3(const float* __restr
   };
   auto split_b = [&](f16x8 (&dst)[X6_BT][2], int t, int half) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) split2_f16(f4(bq[t][half], e) * bsc, dst[t][0], dst[t][1], 4 * half + e);
+    for (int e = 0; e < 4; ++e) split2_f16s(f4(bq[t][half], e), bsc, dst[t][0], dst[t][1], 4 * half + e);
   };
   floatx4 acc[17][X6_BT];
 #pragma unroll
@@ -446,17 +458,19 @@ __global__ void __launch_bounds__(64 * X6_NW, 1) k_wgrad_h3(const float* __restr
     load_a(s + 1 < nslab ? s + 1 : s);
     const f16x8* a0p = As[buf][0];
     const f16x8* a1p = As[buf][1];
-    f16x8 a[2];
+    // A fragments two tiles ahead (the LDS reads of tile i + 2 go out with tile i's MFMAs)
+    f16x8 a[2], an[2];
     {
-      const int slot = x6_slot(q16, oct);
+      const int slot = x6_slot(q16, oct), slot1 = x6_slot(16 + q16, oct);
       a[0] = a0p[slot]; a[1] = a1p[slot];
+      an[0] = a0p[slot1]; an[1] = a1p[slot1];
     }
 #pragma unroll
     for (int i = 0; i < 17; ++i) {
-      f16x8 an[2];
-      if (i + 1 < 17) {
-        const int slot = x6_slot(16 * (i + 1) + q16, oct);
-        an[0] = a0p[slot]; an[1] = a1p[slot];
+      f16x8 ann[2];
+      if (i + 2 < 17) {
+        const int slot = x6_slot(16 * (i + 2) + q16, oct);
+        ann[0] = a0p[slot]; ann[1] = a1p[slot];
       }
 #pragma unroll
       for (int t = 0; t < X6_BT; ++t) {
@@ -470,8 +484,8 @@ __global__ void __launch_bounds__(64 * X6_NW, 1) k_wgrad_h3(const float* __restr
       if (i == 2 * X6_BT) issue_b(s + 2 < nslab ? s + 2 : nslab - 1);
       if (i == 8) WG_STAMP(s, 1);
       if (i >= 8) write_a(buf ^ 1, i - 8);
-      if (i + 1 < 17) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // next tile's fragment reads first
+      if (i + 2 < 17) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // the fragment reads of tile i + 2 first
       }
 #pragma unroll
       for (int m = 0; m < 3 * X6_BT; ++m) {
@@ -480,6 +494,7 @@ __global__ void __launch_bounds__(64 * X6_NW, 1) k_wgrad_h3(const float* __restr
       }
       __builtin_amdgcn_sched_barrier(0);
       if (i + 1 < 17) { a[0] = an[0]; a[1] = an[1]; }
+      if (i + 2 < 17) { an[0] = ann[0]; an[1] = ann[1]; }
     }
     WG_STAMP(s, 2);
     lds_barrier();
@@ -487,6 +502,8 @@ __global__ void __launch_bounds__(64 * X6_NW, 1) k_wgrad_h3(const float* __restr
   };
 
   f16x8 bpa[X6_BT][2], bpb[X6_BT][2];
+#pragma unroll
+  for (int j = 0; j < X6_NS; ++j) asr[j] = asc[a_index(j) >> 3];
   if (nslab > 0) {
     load_a(0);
     issue_b(0);
