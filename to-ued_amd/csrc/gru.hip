@@ -94,13 +94,13 @@ TOUED_DEV void quad_transpose(float* a, int lane) {
 
 // A VALU write to the data VGPRs of a preceding >8-byte VMEM store needs wait states that this compiler
 // does not always insert for buffer-store builtins on gfx950 (observed: the first dword of some 16-byte
-// stores replaced by the next value written to its register).  The s_nop after the store provides them
-// and, being volatile asm, keeps the scheduler from moving a write of those registers above it.
+// stores replaced by the next value written to its register).  The s_nop after the store provides them; the
+// data is an operand of the asm, so its registers stay allocated (no write to them is scheduled) until then.
 TOUED_DEV void st4(__amdgpu_buffer_rsrc_t r, unsigned vbyte, unsigned soff, const float* v) {
   u32x4 x;
   x.x = __float_as_uint(v[0]); x.y = __float_as_uint(v[1]); x.z = __float_as_uint(v[2]); x.w = __float_as_uint(v[3]);
   __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)vbyte, (int)soff, 0);
-  asm volatile("s_nop 1" ::: "memory");
+  asm volatile("s_nop 1" ::"v"(x) : "memory");
 }
 
 TOUED_DEV float sigm(float x) { return 1.0f / (1.0f + __expf(-x)); }
@@ -1198,7 +1198,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     float dz_r[2][16], dhn_r[2][16];
     const int ub = 32 * wave + 4 * hi;               // lane's unit base (register q adds qunit(q))
     const float* wil = wi34 + ub;
-    float vr[3][4][4];   // three-slot ring: quads i+1 and i+2 in flight while quad i is processed
+    constexpr int NR = 3;
+    float vr[NR][4][4];   // NR-slot ring: quads i+1 .. i+NR-1 in flight while quad i is processed (NR = 2: 10.11 ms)
     auto load_q = [&](int h, int g4, float (&v)[4][4]) {
       const unsigned vq = (unsigned)((((long)(ub + (col & 3))) * p.M + r0 + RB * h + (col & 28)) * 4);
       const unsigned so = (unsigned)(((long)8 * g4 * p.M + ctr) * 4);
@@ -1206,6 +1207,15 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       ld4(rs_r, vq, so, v[1]);
       ld4(rs_z, vq, so, v[2]);
       ld4(rs_hn, vq, so, v[3]);
+    };
+    // four units ub + 8 g4 .. +3 of this lane's row RB h + col (register quad g4 of tile h): per-unit dword
+    // stores, lane = row (128-byte segments).  (Transposed back to 16-byte stores of four rows, as the loads are,
+    // they measured no faster: 9.82-10.0 ms against 9.75-9.88.)
+    auto st_q = [&](__amdgpu_buffer_rsrc_t rs, int h, int g4, const float (&v)[4]) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        st_u(rs, (unsigned)(((long)ub * p.M + r0 + RB * h + col) * 4),
+             (unsigned)(((long)qunit(4 * g4 + e) * p.M + ctr) * 4), v[e]);
     };
     // the rows' inputs x(t) as gate_ain's B fragments (lane = row RB h + col, k = 2 kk + hi): n is recomputed.
     // Tile 0's go out now, tile 1's beside the ring loads of quad 3.
@@ -1222,13 +1232,13 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     floatx16 hacc;
     float dx3 = 0.0f, dx4 = 0.0f;
     float rmr[2] = {0.0f, 0.0f};   // running row maxima of |dr|
-    load_q(0, 0, vr[0]);
-    load_q(0, 1, vr[1]);
+#pragma unroll
+    for (int qi = 0; qi < NR - 1; ++qi) load_q(qi >> 2, qi & 3, vr[qi]);
 #pragma unroll
     for (int qi = 0; qi < 8; ++qi) {
       const int h = qi >> 2, g4 = qi & 3;
-      float (&v)[4][4] = vr[qi % 3];
-      if (qi + 2 < 8) load_q((qi + 2) >> 2, (qi + 2) & 3, vr[(qi + 2) % 3]);
+      float (&v)[4][4] = vr[qi % NR];
+      if (qi + NR - 1 < 8) load_q((qi + NR - 1) >> 2, (qi + NR - 1) & 3, vr[(qi + NR - 1) % NR]);
       if (qi == 3) load_x(1, xb);
       __builtin_amdgcn_sched_barrier(0);
       if (g4 == 0) {
@@ -1248,10 +1258,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         dx4 = 0.0f;
       }
       const int row = RB * h + col;
-      const unsigned vbo = (unsigned)(((long)ub * p.M + r0 + row) * 4);
 #pragma unroll
       for (int a = 0; a < 4; ++a) quad_transpose(v[a], lane);
-      float drq[4];
+      float drq[4], rhq[4], dnq[4];
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int q = 4 * g4 + jj;
@@ -1265,17 +1274,18 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         const float dhn = dnp * rg;
         const float drp = dnp * hn * rg * (1.0f - rg);
         const float dzp = dz * zg * (1.0f - zg);
-        dh[h][q] = d * zg;   // direct path; the W_h^T contraction is added below
+        dh[h][q] = d * zg;   // direct path; the W_h^T contraction accumulates onto it below
         drq[jj] = drp;
         dz_r[h][q] = dzp;
         dhn_r[h][q] = dhn;
         const int qu = qunit(q);
         dx3 += drp * wil[0 * HU + qu] + dzp * wil[1 * HU + qu] + dnp * wil[2 * HU + qu];
         dx4 += drp * wil[3 * HU + qu] + dzp * wil[4 * HU + qu] + dnp * wil[5 * HU + qu];
-        const unsigned so1 = (unsigned)(((long)qu * p.M + ctr) * 4);
-        st_u(rs_rh, vbo, so1, fmaxf(hout, 0.0f));
-        st_u(rs_dg[3], vbo, so1, dnp);   // dr, dz, dhn leave during the contraction phase (HBM idle there)
+        rhq[jj] = fmaxf(hout, 0.0f);
+        dnq[jj] = dnp;
       }
+      st_q(rs_rh, h, g4, rhq);
+      st_q(rs_dg[3], h, g4, dnq);   // dr, dz and dhn leave beside the contraction passes
       *reinterpret_cast<float4*>(&drs[row * DRP + ub + 8 * g4]) = make_float4(drq[0], drq[1], drq[2], drq[3]);
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) rmr[h] = fmaxf(rmr[h], fabsf(drq[jj]));
@@ -1316,14 +1326,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       bs[h] = ldexpf(1.0f, sc);
       if (p.CE && wave == 0 && hi == 0) p.CE[ctr + r0 + RB * h + col] = (int8_t)ce;
     }
-    // a lane's four units ub + 8 g4 .. +3 of batch row `row` of gate cotangent g to DG (lane = row: 128-byte
-    // segments), issued beside the contraction's MFMAs where the memory pipe is otherwise idle
-    auto store_dg = [&](int g, int row, int g4, const float (&v)[4]) {
-      const unsigned vb = (unsigned)(((long)ub * p.M + r0 + row) * 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        st_u(rs_dg[g], vb, (unsigned)(((long)qunit(4 * g4 + e) * p.M + ctr) * 4), v[e]);
-    };
+    // a lane's four units ub + 8 g4 .. +3 of batch row `row` of gate cotangent g to DG, issued beside the
+    // contraction's MFMAs where the memory pipe is otherwise idle
+    auto store_dg = [&](int g, int row, int g4, const float (&v)[4]) { st_q(rs_dg[g], row >= RB, g4, v); };
     // dr -> fp16 pieces: x0 straight into slot 0, x1 held until every lane has read its staged f32 values
     // (slot 1 overlaps the staging)
     f16x4 x1h[2][4];
@@ -1347,11 +1352,18 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       for (int g4 = 0; g4 < 4; ++g4)
         *reinterpret_cast<f16x4*>(&dgB[1][(RB * h + col) * PP + ub + 8 * g4]) = x1h[h][g4];
     lds_barrier();
-    // ---- contraction: dr, then dz, then dhn (scaled fp16 pairs) through the one image
+    // ---- contraction: dr, then dz, then dhn (scaled fp16 pairs) through the one image, accumulated onto the
+    // direct path dh (taken into the accumulator frame 2^(s_i + t_row), exact: powers of two), so dh's registers
+    // are free while the contraction's fragments are live
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const float4 w4 = *reinterpret_cast<const float4*>(&wsc[ub + 8 * g4]);
+      const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
-      for (int q = 0; q < 16; ++q) acc[h][q] = 0.0f;
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[h][4 * g4 + e] = dh[h][4 * g4 + e] * (wv[e] * bs[h]);
+    }
     BWD_STAMP(4);
     contract_h(0);
     lds_barrier();
@@ -1403,7 +1415,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     for (int h = 0; h < 2; ++h) {
       const bool dn = __builtin_amdgcn_raw_buffer_load_b8(rs_done, w_[h], (int)(((long)a_[h] * T + t) * W), 0) != 0;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) dh[h][q] = dn ? 0.0f : dh[h][q] + acc[h][q];
+      for (int q = 0; q < 16; ++q) dh[h][q] = dn ? 0.0f : acc[h][q];
     }
     BWD_STAMP(7);
     lds_barrier();   // hv, dxp and the image are rewritten next step

@@ -10,7 +10,6 @@ from __future__ import annotations
 
 import argparse
 import json
-import os
 import sys
 from pathlib import Path
 
@@ -75,7 +74,6 @@ def main():
                    L.ptr(o.dX4), L.ptr(o.CE) if o.bfp else None, L.stream_ptr())
         ms = timed(bwd)
         res["gru_bwd_ms"] = round(ms, 3)
-        res["stagger"] = (os.environ.get("TOUED_BWD_STAGGER_US"), os.environ.get("TOUED_BWD_STAGGER_MODE"))
         res["gru_bwd_tflops"] = round(K * R * T * 393216 / (ms * 1e-3) / 1e12, 1)
     print(json.dumps(res), flush=True)
 
