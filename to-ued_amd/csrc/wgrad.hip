@@ -27,6 +27,7 @@
 #include "common.h"
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
@@ -352,28 +353,34 @@ __global__ void __launch_bounds__(256) k_wgrad_rowmax(const float* __restrict__ 
 #ifdef WG_STAMPS
 // timing instrumentation (tools/wgrad_stamps.py): lane 0 of each wave of workgroups < 64 records s_memtime at the
 // start of each of the first 64 slabs, after tile 7, before and after the slab barrier
-__device__ unsigned long long g_wg_stamps[64 * 4 * 64 * 4];
+__device__ unsigned long long g_wg_stamps[64 * 8 * 64 * 4];
 #define WG_STAMP(s, ph)                                                                                 \
   do {                                                                                                  \
     if (blockIdx.x < 64 && lane == 0 && (s) < 64)                                                       \
-      g_wg_stamps[((blockIdx.x * 4 + wave) * 64 + (s)) * 4 + (ph)] = __builtin_amdgcn_s_memtime();      \
+      g_wg_stamps[((blockIdx.x * 8 + wave) * 64 + (s)) * 4 + (ph)] = __builtin_amdgcn_s_memtime();      \
   } while (0)
 #else
 #define WG_STAMP(s, ph) do {} while (0)
 #endif
 
-__global__ void __launch_bounds__(64 * X6_NW, 1) k_wgrad_h3(const float* __restrict__ A, long lda, int ra,
-                                                             int a_unit_rows, const int* __restrict__ rowmax_bits,
-                                                             const float* __restrict__ B, long ldb, int rb,
-                                                             const int8_t* __restrict__ colexp, long K, long kchunk,
-                                                             float* __restrict__ part) {
-  constexpr int NT = 64 * X6_NW;
-  const int G = gridDim.x, ncol = (rb + X6_CT - 1) / X6_CT;
+// NW waves per workgroup, BT B tiles of 16 rows per wave: <4, 3> one wave per SIMD (acc 17 x 3, 512-register
+// budget), <8, 2> two waves per SIMD (acc 17 x 2 in 256 registers) so that one wave's waits are the other's issue.
+template <int NW, int BT>
+__global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict__ A, long lda, int ra,
+                                                        int a_unit_rows, const int* __restrict__ rowmax_bits,
+                                                        const float* __restrict__ B, long ldb, int rb,
+                                                        const int8_t* __restrict__ colexp, long K, long kchunk,
+                                                        float* __restrict__ part) {
+  constexpr int NT = 64 * NW;
+  constexpr int CT = 16 * BT * NW;                          // B rows per workgroup
+  constexpr int NS = (X6_AQ + NT - 1) / NT;                 // A staging rounds per thread
+  static_assert(NS <= 17 && 2 * BT < 17 - NS, "side-work schedule: B splits, B issue, then the staging rounds");
+  const int G = gridDim.x, ncol = (rb + CT - 1) / CT;
   const int xcd = blockIdx.x & 7;
   const int L = xcd * (G >> 3) + (xcd < (G & 7) ? xcd : (G & 7)) + (blockIdx.x >> 3);
   __shared__ f16x8 As[2][2][X6_RA * 4];    // [buffer][piece][slot]: 69,632 B
   __shared__ float asc[X6_RA];             // 2^s_i of A row i
-  __shared__ int cred[X6_NW];
+  __shared__ int cred[NW];
   const int tid = threadIdx.x, lane = tid & 63, q16 = lane & 15, oct = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ct = L % ncol, sc = L / ncol;
@@ -400,129 +407,153 @@ __global__ void __launch_bounds__(64 * X6_NW, 1) k_wgrad_h3(const float* __restr
   __syncthreads();
   int cexp = cred[0];
 #pragma unroll
-  for (int w = 1; w < X6_NW; ++w) cexp = min(cexp, cred[w]);
+  for (int w = 1; w < NW; ++w) cexp = min(cexp, cred[w]);
   if (cexp == 127) cexp = 0;
   const float bsc = ldexpf(1.0f, cexp);
-  const float4* Bp[X6_BT];
-  int brow[X6_BT];
+  // B tile t through its own (wave-uniform) descriptor at the tile's first row and the chunk's first column, with
+  // 32-bit lane offsets (rows past rb read row rb - 1: they only feed C rows that are never written out).  A
+  // fragment's 8 k of lane octet o are k-quads o and o + 4 of the slab (both operands permuted alike: the sum is
+  // over all 32), so each B load instruction reads 64 contiguous bytes of each of its 16 rows.
+  __amdgpu_buffer_rsrc_t rsB[BT];
+  unsigned boff[BT];
+  int brow[BT];
 #pragma unroll
-  for (int t = 0; t < X6_BT; ++t) {
-    brow[t] = ct * X6_CT + 16 * (X6_BT * wave + t) + q16;
-    Bp[t] = reinterpret_cast<const float4*>(B + (long)(brow[t] < rb ? brow[t] : 0) * ldb + kb) + 2 * oct;
+  for (int t = 0; t < BT; ++t) {
+    const int tb = ct * CT + 16 * (BT * wave + t);
+    const int tbc = tb < rb ? tb : rb - 1;
+    brow[t] = tb + q16;
+    const int rr = brow[t] < rb ? brow[t] : rb - 1;
+    rsB[t] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B + (long)tbc * ldb + kb), 0, -1, 0x00020000);
+    boff[t] = (unsigned)(((long)(rr - tbc) * ldb + 4 * oct) * 4);
   }
-  float4 ast[X6_NS];
+  float4 ast[NS];
   auto a_index = [&](int j) {
     const int i = tid + NT * j;
-    return j < X6_NS - 1 || i < X6_AQ ? i : i - NT;
+    return j < NS - 1 || i < X6_AQ ? i : i - NT;
   };
+  // A through a buffer descriptor: per round one 32-bit lane offset (row, k-quad), the slab's column in the scalar
+  // offset (64-bit row pointers per round, loop-invariant, were spilled and reloaded every slab)
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A), 0, -1, 0x00020000);
+  unsigned avo[NS];
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    const int i = a_index(j);
+    const int row = (i >> 3) < ra ? (i >> 3) : ra - 1;
+    avo[j] = (unsigned)(((long)row * lda + 4 * (i & 7)) * 4);
+  }
   auto load_a = [&](int s) {
 #pragma unroll
-    for (int j = 0; j < X6_NS; ++j) {
-      const int i = a_index(j);
-      const int row = (i >> 3) < ra ? (i >> 3) : ra - 1;
-      ast[j] = *reinterpret_cast<const float4*>(A + (long)row * lda + kb + 32L * s + 4 * (i & 7));
+    for (int j = 0; j < NS; ++j) {
+      const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)avo[j], (int)((kb + 32L * s) * 4), 0);
+      ast[j] = make_float4(__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w));
     }
   };
   // this thread's staging rows are the same in every slab: their scales live in registers (an LDS read per round
   // would sit on the in-order LDS counter in front of the fragment reads)
-  float asr[X6_NS];
+  float asr[NS];
   auto write_a = [&](int buf, int j) {
     const int i = a_index(j);
     const int row = i >> 3, kq = i & 7;
-    const int slot = x6_slot(row, kq >> 1);
+    const int slot = x6_slot(row, kq & 3);
     const float s = asr[j];
     f16x4 p0, p1;
 #pragma unroll
     for (int e = 0; e < 4; ++e) split2_f16s(f4(ast[j], e), s, p0, p1, e);
-    reinterpret_cast<f16x4*>(&As[buf][0][slot])[kq & 1] = p0;
-    reinterpret_cast<f16x4*>(&As[buf][1][slot])[kq & 1] = p1;
+    reinterpret_cast<f16x4*>(&As[buf][0][slot])[kq >> 2] = p0;
+    reinterpret_cast<f16x4*>(&As[buf][1][slot])[kq >> 2] = p1;
   };
-  float4 bq[X6_BT][2];
+  float4 bq[BT][2];
   auto issue_b = [&](int s) {
 #pragma unroll
-    for (int t = 0; t < X6_BT; ++t) { bq[t][0] = Bp[t][8 * s]; bq[t][1] = Bp[t][8 * s + 1]; }
+    for (int t = 0; t < BT; ++t)
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsB[t], (int)boff[t], 128 * s + 64 * hf, 0);
+        bq[t][hf] = make_float4(__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w));
+      }
   };
-  auto split_b = [&](f16x8 (&dst)[X6_BT][2], int t, int half) {
+  auto split_b = [&](f16x8 (&dst)[BT][2], int t, int half) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) split2_f16s(f4(bq[t][half], e), bsc, dst[t][0], dst[t][1], 4 * half + e);
   };
-  floatx4 acc[17][X6_BT];
+  floatx4 acc[17][BT];
 #pragma unroll
   for (int i = 0; i < 17; ++i)
 #pragma unroll
-    for (int t = 0; t < X6_BT; ++t) acc[i][t] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int t = 0; t < BT; ++t) acc[i][t] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
 
-  auto slab = [&](int s, f16x8 (&bp)[X6_BT][2], f16x8 (&bpn)[X6_BT][2]) {
+  auto slab = [&](int s, f16x8 (&bp)[BT][2], f16x8 (&bpn)[BT][2]) {
     WG_STAMP(s, 0);
     const int buf = s & 1;
     load_a(s + 1 < nslab ? s + 1 : s);
     const f16x8* a0p = As[buf][0];
     const f16x8* a1p = As[buf][1];
     // A fragments two tiles ahead (the LDS reads of tile i + 2 go out with tile i's MFMAs)
-    f16x8 a[2], an[2];
-    {
-      const int slot = x6_slot(q16, oct), slot1 = x6_slot(16 + q16, oct);
-      a[0] = a0p[slot]; a[1] = a1p[slot];
-      an[0] = a0p[slot1]; an[1] = a1p[slot1];
+    // A fragments LA tiles ahead through an (LA + 1)-slot ring (the LDS reads of tile i + LA go out with tile i's
+    // MFMAs): two ahead with one wave per SIMD, one ahead with two (the partner wave covers the rest; registers)
+    constexpr int LA = NW == 4 ? 2 : 1;
+    f16x8 fr[LA + 1][2];
+#pragma unroll
+    for (int d = 0; d < LA; ++d) {
+      const int slot = x6_slot(16 * d + q16, oct);
+      fr[d][0] = a0p[slot]; fr[d][1] = a1p[slot];
     }
 #pragma unroll
     for (int i = 0; i < 17; ++i) {
-      f16x8 ann[2];
-      if (i + 2 < 17) {
-        const int slot = x6_slot(16 * (i + 2) + q16, oct);
-        ann[0] = a0p[slot]; ann[1] = a1p[slot];
+      if (i + LA < 17) {
+        const int slot = x6_slot(16 * (i + LA) + q16, oct);
+        fr[(i + LA) % (LA + 1)][0] = a0p[slot]; fr[(i + LA) % (LA + 1)][1] = a1p[slot];
       }
+      const f16x8(&a)[2] = fr[i % (LA + 1)];
 #pragma unroll
-      for (int t = 0; t < X6_BT; ++t) {
+      for (int t = 0; t < BT; ++t) {
         floatx4 c = acc[i][t];
         c = mfma_h(a[1], bp[t][0], c);
         c = mfma_h(a[0], bp[t][1], c);
         c = mfma_h(a[0], bp[t][0], c);
         acc[i][t] = c;
       }
-      if (i < 2 * X6_BT) split_b(bpn, i >> 1, i & 1);
-      if (i == 2 * X6_BT) issue_b(s + 2 < nslab ? s + 2 : nslab - 1);
+      if (i < 2 * BT) split_b(bpn, i >> 1, i & 1);
+      if (i == 2 * BT) issue_b(s + 2 < nslab ? s + 2 : nslab - 1);
       if (i == 8) WG_STAMP(s, 1);
-      if (i >= 8) write_a(buf ^ 1, i - 8);
-      if (i + 2 < 17) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // the fragment reads of tile i + 2 first
+      if (i >= 17 - NS) write_a(buf ^ 1, i - (17 - NS));
+      if (i + LA < 17) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // the fragment reads of tile i + LA first
       }
 #pragma unroll
-      for (int m = 0; m < 3 * X6_BT; ++m) {
+      for (int m = 0; m < 3 * BT; ++m) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
         __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);   // side-work VALU
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (i + 1 < 17) { a[0] = an[0]; a[1] = an[1]; }
-      if (i + 2 < 17) { an[0] = ann[0]; an[1] = ann[1]; }
     }
     WG_STAMP(s, 2);
     lds_barrier();
     WG_STAMP(s, 3);
   };
 
-  f16x8 bpa[X6_BT][2], bpb[X6_BT][2];
+  f16x8 bpa[BT][2], bpb[BT][2];
 #pragma unroll
-  for (int j = 0; j < X6_NS; ++j) asr[j] = asc[a_index(j) >> 3];
+  for (int j = 0; j < NS; ++j) asr[j] = asc[a_index(j) >> 3];
   if (nslab > 0) {
     load_a(0);
     issue_b(0);
 #pragma unroll
-    for (int j = 0; j < X6_NS; ++j) write_a(0, j);
+    for (int j = 0; j < NS; ++j) write_a(0, j);
 #pragma unroll
-    for (int t = 0; t < X6_BT; ++t) { split_b(bpa, t, 0); split_b(bpa, t, 1); }
+    for (int t = 0; t < BT; ++t) { split_b(bpa, t, 0); split_b(bpa, t, 1); }
     issue_b(nslab > 1 ? 1 : 0);
   }
   __syncthreads();
   for (int s = 0; s < nslab; ++s) {
     slab(s, bpa, bpb);
 #pragma unroll
-    for (int t = 0; t < X6_BT; ++t)
+    for (int t = 0; t < BT; ++t)
 #pragma unroll
       for (int pc = 0; pc < 2; ++pc) bpa[t][pc] = bpb[t][pc];
   }
   // D map: lane l, reg r -> C[16i + 4 oct + r][brow]; unscale by 2^-(s_row + c) (two exact steps)
-  const int rbp = ncol * X6_CT;
+  const int rbp = ncol * CT;
   float* out = part + (long)sc * X6_RA * rbp;
   const float ib = ldexpf(1.0f, -cexp);
 #pragma unroll
@@ -531,7 +562,7 @@ __global__ void __launch_bounds__(64 * X6_NW, 1) k_wgrad_h3(const float* __restr
     for (int r = 0; r < 4; ++r) {
       const float ia = 1.0f / asc[16 * i + 4 * oct + r];
 #pragma unroll
-      for (int t = 0; t < X6_BT; ++t) out[(long)(16 * i + 4 * oct + r) * rbp + brow[t]] = (acc[i][t][r] * ia) * ib;
+      for (int t = 0; t < BT; ++t) out[(long)(16 * i + 4 * oct + r) * rbp + brow[t]] = (acc[i][t][r] * ia) * ib;
     }
 }
 
@@ -659,10 +690,41 @@ int toued_wgrad(int ra, int rb, long K, const float* A, long lda, const float* B
 
 // Main LPG weight-gradient reduction on block-floating-point fp16 pairs (k_wgrad_h3): rows [0, a_unit_rows) of A
 // must be bounded by 1 in magnitude; col_exp[m] is B column m's scale exponent (127 = zero column).
+// k_wgrad_h3<8, 2> (two waves per SIMD) unless TOUED_WGRAD_NW4=1 selects <4, 3> (one wave per SIMD, comparison
+// runs): 4.59-4.67 ms against 4.75-4.88 at the C2 shape, per-slab stamps 23.4 against 29.8 cycles per B row
+static bool wgrad_h8() {
+  static const bool f = [] {
+    const char* e = getenv("TOUED_WGRAD_NW4");
+    return !(e && e[0] == '1');
+  }();
+  return f;
+}
+
+// the k_wgrad_h3 variant's plan: B rows per workgroup, column tiles and K chunks (one workgroup per CU)
+static Plan plan_bfp(int ra, int rb, long K) {
+  Plan p = plan(ra > 16 ? ra : 17, rb, K);
+  p.ct = wgrad_h8() ? 16 * 2 * 8 : X6_CT;
+  p.ncol = (rb + p.ct - 1) / p.ct;
+  int cus = 256;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+    cus = 256;
+  cus = cus - g_reserved_cus > cus / 2 ? cus - g_reserved_cus : cus / 2;
+  int S = cus / p.ncol;
+  if (S < 1) S = 1;
+  const long slabs = K / 32;
+  if (S > slabs) S = (int)(slabs > 0 ? slabs : 1);
+  p.kchunk = ((slabs + S - 1) / S) * 32;
+  p.S = (int)((K + p.kchunk - 1) / p.kchunk);
+  if (p.S < 1) p.S = 1;
+  return p;
+}
+
 size_t toued_wgrad_bfp_workspace_floats(int ra, int rb, long K) {
   if (ra <= 0 || rb <= 0 || K <= 0) return 0;
-  Plan p = plan(ra > 16 ? ra : 17, rb, K);
-  return (size_t)p.S * 17 * 16 * p.ncol * X6_CT + X6_RA;
+  const Plan p = plan_bfp(ra, rb, K);
+  return (size_t)p.S * 17 * 16 * p.ncol * p.ct + X6_RA;
 }
 
 int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit_rows, const float* B, long ldb,
@@ -671,13 +733,13 @@ int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit
                 "toued_wgrad_bfp: ra=%d (17..%d) rb=%d a_unit_rows=%d", ra, X6_RA, rb, a_unit_rows);
   TOUED_REQUIRE(K > 0 && K % 32 == 0, "toued_wgrad_bfp: K=%ld must be a positive multiple of 32", K);
   TOUED_REQUIRE(lda % 4 == 0 && ldb % 4 == 0, "toued_wgrad_bfp: lda=%ld ldb=%ld must be multiples of 4", lda, ldb);
+  TOUED_REQUIRE((double)ra * lda * 4.0 < 4294967295.0, "toued_wgrad_bfp: A (%d rows x %ld) exceeds the 4 GiB buffer range",
+                ra, lda);
   TOUED_REQUIRE(A && B && C && col_exp, "toued_wgrad_bfp: null operand");
   TOUED_REQUIRE((reinterpret_cast<uintptr_t>(col_exp) & 15) == 0, "toued_wgrad_bfp: col_exp must be 16-byte aligned");
-  Plan p = plan(ra, rb, K);
-  p.ct = X6_CT;
-  p.ncol = (rb + X6_CT - 1) / X6_CT;
+  const Plan p = plan_bfp(ra, rb, K);
   TOUED_REQUIRE(p.kchunk % 16 == 0, "toued_wgrad_bfp: chunk %ld", p.kchunk);
-  const size_t need = (size_t)p.S * 17 * 16 * p.ncol * X6_CT;
+  const size_t need = (size_t)p.S * 17 * 16 * p.ncol * p.ct;
   TOUED_REQUIRE(work && work_floats >= need + X6_RA, "toued_wgrad_bfp: workspace of %zu floats needed (got %zu)",
                 need + X6_RA, work_floats);
   int* bits = reinterpret_cast<int*>(work + need);
@@ -688,11 +750,15 @@ int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit
     hipLaunchKernelGGL(k_wgrad_rowmax, dim3((unsigned)((K + kper - 1) / kper), nmeas), dim3(256), 0, stream, A, lda,
                        a_unit_rows, K, kper, bits);
   }
-  hipLaunchKernelGGL(k_wgrad_h3, dim3(p.ncol * p.S), dim3(64 * X6_NW), 0, stream, A, lda, ra, a_unit_rows, bits, B,
-                     ldb, rb, col_exp, K, p.kchunk, work);
+  if (wgrad_h8())
+    hipLaunchKernelGGL((k_wgrad_h3<8, 2>), dim3(p.ncol * p.S), dim3(512), 0, stream, A, lda, ra, a_unit_rows, bits, B,
+                       ldb, rb, col_exp, K, p.kchunk, work);
+  else
+    hipLaunchKernelGGL((k_wgrad_h3<X6_NW, X6_BT>), dim3(p.ncol * p.S), dim3(64 * X6_NW), 0, stream, A, lda, ra,
+                       a_unit_rows, bits, B, ldb, rb, col_exp, K, p.kchunk, work);
   const long n = (long)ra * rb;
   hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, work, p.S, 17 * 16,
-                     p.ncol * X6_CT, ra, rb, C);
+                     p.ncol * p.ct, ra, rb, C);
   TOUED_CHECK_LAUNCH();
   return 0;
 }

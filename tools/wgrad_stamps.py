@@ -30,15 +30,19 @@ def main():
         L.call("toued_wgrad_bfp", 262, 768, M, L.ptr(A), M, 256, L.ptr(B), M, L.ptr(CE), L.ptr(C), L.ptr(wb),
                wb.numel(), L.stream_ptr())
     torch.cuda.synchronize()
-    buf = np.zeros(64 * 4 * 64 * 4, np.uint64)
+    buf = np.zeros(64 * 8 * 64 * 4, np.uint64)
     fn = L.lib().toued_dbg_wgrad_stamps
     fn.argtypes = [ctypes.c_void_p]
     assert fn(buf.ctypes.data) == 0
-    st = buf.reshape(64, 4, 64, 4).astype(np.int64)[:, :, 1:63]
-    res = {"tiles 0-7": float((st[..., 1] - st[..., 0]).mean()), "tiles 8-16": float((st[..., 2] - st[..., 1]).mean()),
+    st = buf.reshape(64, 8, 64, 4).astype(np.int64)
+    nw = 8 if st[:, 4:].any() else 4                  # k_wgrad_h3<8, 2> (default) or <4, 3> (TOUED_WGRAD_NW4=1)
+    st = st[:, :nw, 1:63]
+    mfma = 17 * (2 if nw == 8 else 3) * 3               # MFMAs per wave and slab
+    res = {"waves": nw, "tiles 0-7": float((st[..., 1] - st[..., 0]).mean()),
+           "tiles 8-16": float((st[..., 2] - st[..., 1]).mean()),
            "barrier": float((st[..., 3] - st[..., 2]).mean()),
            "slab": float((st[:, :, 1:, 0] - st[:, :, :-1, 0]).mean()),
-           "ideal MFMA (153 x 16)": 153 * 16}
+           "ideal MFMA issue per SIMD (x 16 cycles)": mfma * 16 * nw // 4}
     print(json.dumps({k: round(v) for k, v in res.items()}), flush=True)
 
 
