@@ -70,9 +70,11 @@ def pmc_traffic(kernel: str):
     calibration factors).  (None, None) when no summary covers the kernel."""
     for d in sorted((ROOT / "profiles").glob("*/pmc_traffic.json"), reverse=True):
         try:
-            k = json.loads(d.read_text())["kernels"].get(kernel)
+            ks = json.loads(d.read_text())["kernels"]
         except (OSError, ValueError, KeyError):
             continue
+        # the kernel by name, or its (single) template instance: "k_wgrad_h3" -> "k_wgrad_h3<8, 2>"
+        k = ks.get(kernel) or next((v for n, v in ks.items() if n.startswith(kernel + "<")), None)
         if k:
             return k["hbm_bytes_per_launch"], str(d.relative_to(ROOT))
     return None, None
