@@ -65,6 +65,19 @@ TOUED_DEV int next_pos(const LV& lev, int pos, int action) {
 }
 
 // the same on the level's wall bitmask held in registers (wl = lev[L_WALLS .. +7])
+// One actor-table row (5 floats, 20-byte rows: 4-byte aligned) as a 16-byte and a 4-byte buffer load instead of five
+// dword gathers: per row one cache-line lookup per instruction instead of five (the candidate-row gathers of the
+// rollouts are bound by those lookups: 64 lanes, 64 different rows).  `off` = byte offset of the row in `theta`.
+typedef unsigned row_u32x4 __attribute__((ext_vector_type(4)));
+TOUED_DEV void load_row5(__amdgpu_buffer_rsrc_t rs, unsigned off, float (&r)[5]) {
+  const row_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
+  r[0] = __uint_as_float(x.x); r[1] = __uint_as_float(x.y); r[2] = __uint_as_float(x.z); r[3] = __uint_as_float(x.w);
+  r[4] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)off + 16, 0, 0));
+}
+TOUED_DEV __amdgpu_buffer_rsrc_t theta_rsrc(const float* theta) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(theta), 0, -1 /* 4 GiB: host-checked */, 0x00020000);
+}
+
 TOUED_DEV int next_pos_r(int g, const uint32_t (&wl)[8], int pos, int action) {
   const int top = pos < g, bottom = pos >= g * (g - 1);
   const int left = (pos % g) == 0, right = (pos % g) == g - 1;
@@ -467,6 +480,8 @@ __global__ void __launch_bounds__(256) k_rollout(EnvSpec sp, const int* __restri
   const int w = i - a * W;
   const LevR lev = lev_regs(levels + (size_t)a * LEVEL_WORDS);
   const float* tab = theta + (size_t)a * D * 5;
+  const __amdgpu_buffer_rsrc_t rs_t = theta_rsrc(theta);
+  const unsigned tab_off = (unsigned)((size_t)a * D * 20);
   float last[5];
 #pragma unroll
   for (int j = 0; j < 5; ++j) last[j] = tab[(size_t)(D - 1) * 5 + j];
@@ -533,8 +548,7 @@ __global__ void __launch_bounds__(256) k_rollout(EnvSpec sp, const int* __restri
         for (int o = 0; o < NMAX; ++o)
           if (((s.exists >> o) & 1) && objpos[o] == p) col |= 1 << o;
         cidx[a] = p + G2 * ((s.exists | resp) & ~col & used);
-#pragma unroll
-        for (int j = 0; j < 5; ++j) crow[a][j] = tab[(size_t)cidx[a] * 5 + j];
+        load_row5(rs_t, tab_off + (unsigned)cidx[a] * 20u, crow[a]);
       }
     }
     const StepKeys kn = keys_of(kc.rng);      // next step's keys while the gathers are in flight
@@ -641,6 +655,8 @@ __global__ void __launch_bounds__(256) k_eval_returns(EnvSpec sp, const int* __r
   const int a = i / W;
   const LevR lev = lev_regs(levels + (size_t)a * LEVEL_WORDS);
   const float* tab = theta + (size_t)a * D * 5;
+  const __amdgpu_buffer_rsrc_t rs_t = theta_rsrc(theta);
+  const unsigned tab_off = (unsigned)((size_t)a * D * 20);
   float last[5];
 #pragma unroll
   for (int j = 0; j < 5; ++j) last[j] = tab[(size_t)(D - 1) * 5 + j];
@@ -683,8 +699,7 @@ __global__ void __launch_bounds__(256) k_eval_returns(EnvSpec sp, const int* __r
       cpos[act] = p;
       cex[act] = col;
       const int ci = p + G2 * ((s.exists | (int)dr.z) & ~col & used);
-#pragma unroll
-      for (int j = 0; j < 5; ++j) crow[act][j] = tab[(size_t)ci * 5 + j];
+      load_row5(rs_t, tab_off + (unsigned)ci * 20u, crow[act]);
     }
     float p[5];
     actor_probs5_row(row, last, s.time, p);
@@ -832,6 +847,8 @@ int toued_eval_returns(EnvSpec sp, const int* levels, const float* theta, int D,
   TOUED_REQUIRE(sp.tabular, "toued_eval_returns: the linear tabular actor needs a tabular env");
   TOUED_REQUIRE(n_agents >= 0 && W >= 1 && T >= 0, "toued_eval_returns: bad sizes N=%d W=%d T=%d", n_agents, W, T);
   TOUED_REQUIRE(D == sp.max_grid * sp.max_grid * (1 << sp.n_max) + 1, "toued_eval_returns: D=%d != obs_dim", D);
+  TOUED_REQUIRE((double)n_agents * D * 20.0 < 4294967295.0, "toued_eval_returns: actor tables (%d x %d rows) exceed 4 GiB",
+                n_agents, D);
   const int n = n_agents * W;
   if (n == 0) return 0;
   TOUED_DISPATCH_NMAX(sp.n_max, true, hipLaunchKernelGGL(k_eval_returns<NMAX>, dim3(nblk(n)), dim3(256), 0, stream, sp,
@@ -848,6 +865,8 @@ int toued_rollout(EnvSpec sp, const int* levels, const float* theta, int D, cons
   TOUED_REQUIRE(n_agents >= 0 && W >= 1 && T >= 0, "toued_rollout: bad sizes N=%d W=%d T=%d", n_agents, W, T);
   TOUED_REQUIRE(sp.tabular, "toued_rollout: the linear tabular actor needs a tabular env");
   TOUED_REQUIRE(D == sp.max_grid * sp.max_grid * (1 << sp.n_max) + 1, "toued_rollout: D=%d != obs_dim", D);
+  TOUED_REQUIRE((double)n_agents * D * 20.0 < 4294967295.0, "toued_rollout: actor tables (%d x %d rows) exceed 4 GiB",
+                n_agents, D);
   TOUED_REQUIRE(traj_idx || cum_return, "toued_rollout: returns-only mode needs cum_return");
   const int n = n_agents * W;
   if (n == 0) return 0;
