@@ -1149,10 +1149,14 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
                                                           (int)((((ks * 8 + wave) * 3 + g) * 3 + q) * 1024), 0);
     return __builtin_bit_cast(f16x8, x);
   };
+#ifndef BWD_RD
+#define BWD_RD 4
+#endif
   auto contract_h = [&](int g) {
-    f16x8 ring[2][2], B[2][2];
+    constexpr int RD = BWD_RD;                    // A-fragment ring depth (k-steps in flight from L2)
+    f16x8 ring[RD][2], B[2][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < RD; ++i)
 #pragma unroll
       for (int q = 0; q < 2; ++q) ring[i][q] = ldAh(i, g, q);
     auto ldB = [&](int ks, int h) {
@@ -1162,22 +1166,26 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     };
     ldB(0, 0);
     ldB(0, 1);
-    auto kstep = [&](int ks, bool reload) {
+    auto kstep = [&](int ks, f16x8 (&Ar)[2], bool reload) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        acc[h] = mfma3h(ring[ks & 1], B[h], acc[h]);
+        acc[h] = mfma3h(Ar, B[h], acc[h]);
         if (ks + 1 < 16) ldB(ks + 1, h);
       }
       if (reload) {
 #pragma unroll
-        for (int q = 0; q < 2; ++q) ring[ks & 1][q] = ldAh(ks + 2, g, q);
+        for (int q = 0; q < 2; ++q) Ar[q] = ldAh(ks + RD, g, q);
       }
       __builtin_amdgcn_sched_barrier(0);
     };
-#pragma unroll 2
-    for (int ks = 0; ks < 14; ++ks) kstep(ks, true);
-    kstep(14, false);
-    kstep(15, false);
+    // whole groups of RD k-steps that all refill their slot (slots named statically), then the tail
+    constexpr int NG = (16 - RD) / RD;
+#pragma nounroll
+    for (int gi = 0; gi < NG; ++gi)
+#pragma unroll
+      for (int j = 0; j < RD; ++j) kstep(gi * RD + j, ring[j], true);
+#pragma unroll
+    for (int ks = NG * RD; ks < 16; ++ks) kstep(ks, ring[ks % RD], ks + RD < 16);
   };
   // scaled fp16 pieces of the four units u0 .. u0 + 3 of row `row` into image slots 0, 1
   auto put4h = [&](int row, int u0, const float (&v)[4], float sc) {
