@@ -29,6 +29,7 @@
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
+
 namespace {
 
 TOUED_DEV floatx4 mfma16(float a, float b, floatx4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
