@@ -155,6 +155,10 @@ TOUED_DEV floatx16 gate_ain(const float (&wI)[4], int F, int hi, XK xk) {
 }
 TOUED_DEV float gate_n(float ain, float rg, float hn) { return tanh_r(__builtin_fmaf(rg, hn, ain)); }
 
+// 1/x for a power of two x = 2^k (normal, -126 <= k <= 126): exact, by the exponent field (an IEEE division costs
+// ten VALU instructions)
+TOUED_DEV float inv_pow2(float x) { return __int_as_float((254 << 23) - __float_as_int(x)); }
+
 // ------------------------------------------------------------------ packing
 // fwdA[(tile*KQF + kq)*64 + lane] = float4 over kk = 4kq..4kq+3 of A[i=l&31][k=2kk+(l>>5)]
 __global__ void k_pack_fwd(const float* __restrict__ eta, EtaOff o, int F, float4* __restrict__ out,
@@ -1415,7 +1419,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[h][4 * g4 + e] *= 1.0f / (wv[e] * bs[h]);
+        for (int e = 0; e < 4; ++e) acc[h][4 * g4 + e] *= inv_pow2(wv[e] * bs[h]);
     }
     if (tid < RBT) {
       float s3 = 0.0f, s4 = 0.0f;
