@@ -164,9 +164,13 @@ class LPGGRU:
         self.dX3 = torch.empty((K, T, R), dtype=f32, device=dev)
         self.dX4 = torch.empty((K, T, R), dtype=f32, device=dev)
         # weight-gradient reductions (csrc/wgrad.hip): outputs and the per-K-chunk partial-sum workspace
-        self.G = torch.empty((H + lay.F + 1, 3 * H), dtype=f32, device=dev)
+        # G and GI share one buffer so that their scatter into the flat gradient is one gather + one index_add
+        ng, ngi = (H + lay.F + 1) * 3 * H, 8 * H + 9 * (H + 1)
+        self._ggi = torch.empty(ng + ngi, dtype=f32, device=dev)
+        self.G = self._ggi[:ng].view(H + lay.F + 1, 3 * H)
         # the backward's small products: [8][256] ([X; 1; 0] . dn^T) then [9][257] (DH . [relu(h_out); 1]^T)
-        self.GI = torch.empty(8 * H + 9 * (H + 1), dtype=f32, device=dev)
+        self.GI = self._ggi[ng:]
+        self._scatter = None   # (src, dst) index pairs of the weight-gradient blocks into eta's flat layout
         # per-column cotangent exponents from the lockstep backward -> the block-floating-point fp16 reduction
         # (toued_wgrad_bfp, 3 products); else (or TOUED_WGRAD_X6=1) the bf16-triple reduction (toued_wgrad)
         self.bfp = bool(L.toued_gru_bwd_col_exp(R)) and os.environ.get("TOUED_WGRAD_X6") != "1" and \
@@ -176,6 +180,27 @@ class LPGGRU:
                    int(L.toued_wgrad_bfp_workspace_floats(H + lay.F + 1, 3 * H, M)),
                    int(L.toued_gru_bwd_small_work_floats(M)))
         self.wg_work = torch.empty(max(need, 1), dtype=f32, device=dev)
+
+    def _scatter_indices(self, dev):
+        """(src into G|GI, dst into eta) for the blocks the backward accumulates, the same element pairs as the
+        per-parameter views: hr_w <- G[0:H, 0:H], ..., heads <- GI[8H:] viewed [9][H+1] transposed."""
+        lay, F = self.lay, self.lay.F
+        ng = (H + F + 1) * 3 * H
+        Gi = torch.arange(ng).view(H + F + 1, 3 * H)
+        GIi = ng + torch.arange(8 * H + 9 * (H + 1))
+        Gn = GIi[:8 * H].view(8, H)
+        heads = GIi[8 * H:].view(9, H + 1).t()
+        blocks = [("hr_w", Gi[0:H, 0:H]), ("hz_w", Gi[0:H, H:2 * H]), ("hn_w", Gi[0:H, 2 * H:3 * H]),
+                  ("ir_w", Gi[H:H + F, 0:H]), ("iz_w", Gi[H:H + F, H:2 * H]), ("ir_b", Gi[H + F, 0:H]),
+                  ("iz_b", Gi[H + F, H:2 * H]), ("hn_b", Gi[H + F, 2 * H:3 * H]), ("in_w", Gn[0:F]), ("in_b", Gn[F]),
+                  ("pi_w", heads[0:H, 0:1]), ("y_w", heads[0:H, 1:9]), ("pi_b", heads[H, 0:1]), ("y_b", heads[H, 1:9])]
+        src, dst = [], []
+        for name, t in blocks:
+            n = int(np.prod(lay.shapes[name]))
+            assert t.numel() == n, (name, t.shape, lay.shapes[name])
+            src.append(t.reshape(-1))
+            dst.append(lay.offsets[name] + torch.arange(n))
+        return torch.cat(src).to(dev), torch.cat(dst).to(dev)
 
     def pack(self, eta: torch.Tensor):
         _lib.call("toued_gru_pack", _lib.ptr(eta), self.lay.c_offsets, self.lay.F, _lib.ptr(self.fwdA),
@@ -235,21 +260,11 @@ class LPGGRU:
                       st)
         if tok_main is not None:
             timers.stop(tok_main)
-        lay.view(grad, "hr_w").add_(G[0:H, 0:H])
-        lay.view(grad, "hz_w").add_(G[0:H, H:2 * H])
-        lay.view(grad, "hn_w").add_(G[0:H, 2 * H:3 * H])
-        lay.view(grad, "ir_w").add_(G[H:H + F, 0:H])
-        lay.view(grad, "iz_w").add_(G[H:H + F, H:2 * H])
-        lay.view(grad, "ir_b").add_(G[H + F, 0:H])
-        lay.view(grad, "iz_b").add_(G[H + F, H:2 * H])
-        lay.view(grad, "hn_b").add_(G[H + F, 2 * H:3 * H])
-        Gn = self.GI[:8 * H].view(8, H)
-        lay.view(grad, "in_w").add_(Gn[0:F])
-        lay.view(grad, "in_b").add_(Gn[F])
-        heads = self.GI[8 * H:].view(9, H + 1).t()                        # [257, 9]
-        lay.view(grad, "pi_w").add_(heads[0:H, 0:1])
-        lay.view(grad, "y_w").add_(heads[0:H, 1:9])
-        lay.view(grad, "pi_b").add_(heads[H, 0:1])
-        lay.view(grad, "y_b").add_(heads[H, 1:9])
+        # every block of G (dW_h, dW_i, biases) and GI (dW_in, b_in, head kernels and biases) into eta's layout:
+        # one gather + one index_add over precomputed indices (each target element once) instead of 14 launches
+        if self._scatter is None:
+            self._scatter = self._scatter_indices(grad.device)
+        src, dst = self._scatter
+        grad.index_add_(0, dst, self._ggi[src])
         if timers is not None:
             timers.stop(tok)

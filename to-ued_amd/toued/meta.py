@@ -309,10 +309,10 @@ class MetaGradStep:
                tr.obs_idx[0].numel(), ptr(tr.obs_time), ptr(tr.done), tr.done[0].numel(), ptr(self.gru.dX3),
                ptr(self.gru.dX4), T * R, ptr(e1w), ptr(e1b), ptr(e2w), ptr(self.embed_partial), self.embed_blocks, st)
         emb = self.embed_partial.sum(dim=0)
-        self._eta(self.grad, "e1_b").add_(emb[0:16])
-        self._eta(self.grad, "e1_w").add_(emb[16:144].view(8, 16))
-        self._eta(self.grad, "e2_b").add_(emb[144:145])
-        self._eta(self.grad, "e2_w").add_(emb[145:161].view(16, 1))
+        # e1_b, e1_w, e2_b, e2_w are contiguous in eta in the partials' order: one add
+        o = self.lay.offsets["e1_b"]
+        assert self.lay.offsets["e2_w"] + 16 == o + 161
+        self.grad[o:o + 161].add_(emb[0:161])
         # ---------------- agent state out + metrics
         main.wait_stream(self.side)
         ea_cum = ea["cum"]
