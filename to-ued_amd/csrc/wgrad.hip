@@ -514,8 +514,12 @@ __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict
         c = mfma_h(a[0], bp[t][0], c);
         acc[i][t] = c;
       }
-      if (i < 2 * BT) split_b(bpn, i >> 1, i & 1);
-      if (i == 2 * BT) issue_b(s + 2 < nslab ? s + 2 : nslab - 1);
+      // all of the next slab's B splits in the first tile, the loads of the slab after next in the second: those
+      // loads get 16 tiles to land instead of 13 (the kernel waits on its B stream: 4.62-4.66 vs 4.70-4.73 ms)
+      if (i == 0)
+#pragma unroll
+        for (int t = 0; t < BT; ++t) { split_b(bpn, t, 0); split_b(bpn, t, 1); }
+      if (i == 1) issue_b(s + 2 < nslab ? s + 2 : nslab - 1);
       if (i == 8) WG_STAMP(s, 1);
       if (i >= 17 - NS) write_a(buf ^ 1, i - (17 - NS));
       if (i + LA < 17) {
