@@ -158,6 +158,14 @@ TOUED_DEV float gate_n(float ain, float rg, float hn) { return tanh_r(__builtin_
 // 1/x for a power of two x = 2^k (normal, -126 <= k <= 126): exact, by the exponent field (an IEEE division costs
 // ten VALU instructions)
 TOUED_DEV float inv_pow2(float x) { return __int_as_float((254 << 23) - __float_as_int(x)); }
+// the lane id derived afresh where it is used (volatile: never hoisted): a lane-dependent LDS address kept
+// live across a long loop body gets spilled, and its reload's wait drains every outstanding buffer access
+// (vmcnt counts the stores too)
+TOUED_DEV int lane_now() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
 
 // ------------------------------------------------------------------ packing
 // fwdA[(tile*KQF + kq)*64 + lane] = float4 over kk = 4kq..4kq+3 of A[i=l&31][k=2kk+(l>>5)]
@@ -1173,10 +1181,10 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     for (int i = 0; i < RD; ++i)
 #pragma unroll
       for (int q = 0; q < 2; ++q) ring[i][q] = ldAh(i, g, q);
+    const int ln = lane_now(), bl = (ln & 31) * PP + 8 * (ln >> 5);
     auto ldB = [&](int ks, int h) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
-        B[h][q] = *reinterpret_cast<const f16x8*>(&dgB[q][(RB * h + col) * PP + 16 * ks + 8 * hi]);
+      for (int q = 0; q < 2; ++q) B[h][q] = *reinterpret_cast<const f16x8*>(&dgB[q][bl + RB * h * PP + 16 * ks]);
     };
     ldB(0, 0);
     ldB(0, 1);
@@ -1377,9 +1385,10 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     // ---- contraction: dr, then dz, then dhn (scaled fp16 pairs) through the one image, accumulated onto the
     // direct path dh (taken into the accumulator frame 2^(s_i + t_row), exact: powers of two), so dh's registers
     // are free while the contraction's fragments are live
+    const int ubn = 32 * wave + 4 * (lane_now() >> 5);
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
-      const float4 w4 = *reinterpret_cast<const float4*>(&wsc[ub + 8 * g4]);
+      const float4 w4 = *reinterpret_cast<const float4*>(&wsc[ubn + 8 * g4]);
       const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
       for (int h = 0; h < 2; ++h)
