@@ -1091,6 +1091,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   __shared__ __attribute__((aligned(16))) float wsc[HU];          // 2^s of W_g row i (fp16 A scale)
   __shared__ float rmx[8 * RBT];                   // per-wave row maxima of |dr|, |dz|, |dhn| (fp16 B scale)
   __shared__ float wIs[8 * 4 * 64];                // gate_ain's W_in fragments [wave][kk][lane] (read at each tile)
+  __shared__ float wAs[8 * 5 * 64];                // W_heads^T A fragments [wave][kk][lane] (read at each tile)
+  __shared__ int dns[RBT];                         // done flags of the step's rows (loaded with the head cotangents)
   // dr in f32 while the memory part streams ([row][unit], pitch DRP), over image slots 1 and 2
   constexpr int DRP = HU + 4;
   static_assert(RBT * DRP * 4 <= 2 * RBT * PP * 2, "dr staging exceeds image slots 1-2");
@@ -1101,12 +1103,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   const int k = blockIdx.x / nb;
   const int r0 = (blockIdx.x - k * nb) * RBT;
   const int R = p.R, T = p.T, W = p.W;
-  int a_[2], w_[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    a_[h] = (r0 + RB * h) / W;
-    w_[h] = r0 + RB * h + col - a_[h] * W;
-  }
   for (int i = tid; i < 2 * 3 * HU; i += 512) {
     const int f = 3 + i / (3 * HU), g = (i / HU) % 3, u = i % HU;
     const int base = g == 0 ? p.o.ir_w : g == 1 ? p.o.iz_w : p.o.in_w;
@@ -1120,11 +1116,11 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) wIs[(wave * 4 + kk) * 64 + lane] = wI[kk];
   }
-  float wA[5];   // W_heads^T A fragments of unit tile `wave`: A[i = unit][k = head output 2kk + hi]
+  // W_heads^T A fragments of unit tile `wave`: A[i = unit][k = head output 2kk + hi]
 #pragma unroll
   for (int kk = 0; kk < 5; ++kk) {
     const int o = 2 * kk + hi, u = 32 * wave + col;
-    wA[kk] = o < 9 ? (o == 0 ? p.eta[p.o.pi_w + u] : p.eta[p.o.y_w + u * 8 + (o - 1)]) : 0.0f;
+    wAs[(wave * 5 + kk) * 64 + lane] = o < 9 ? (o == 0 ? p.eta[p.o.pi_w + u] : p.eta[p.o.y_w + u * 8 + (o - 1)]) : 0.0f;
   }
   float dh[2][16];
 #pragma unroll
@@ -1139,25 +1135,31 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   const __amdgpu_buffer_rsrc_t rs_yh = rsrc_of(p.y_hat), rs_dyh = rsrc_of(p.d_y_hat), rs_dpi = rsrc_of(p.d_pi_hat),
                                rs_DH = rsrc_of(p.DH), rs_dx3 = rsrc_of(p.dX3), rs_dx4 = rsrc_of(p.dX4),
                                rs_done = rsrc_of(reinterpret_cast<const float*>(p.done + (long)k * p.done_stride_k));
-  const unsigned vrow = (unsigned)tid * 4;   // row offset of the per-row work (tid < RBT)
   // head cotangents of step t (softmax VJP of y_hat, d pi_hat) -> hv, DH
   auto head_cot = [&](int t) {
     if (tid < RBT) {
+      const int tl = lane_now();   // == tid (wave 0)
+      const unsigned vrw = (unsigned)tl * 4;
       const long o = ((long)k * T + t) * R + r0;
       float yh[8], dy[8], s = 0.0f;
       for (int j = 0; j < 8; ++j) {
         const unsigned so = (unsigned)((((long)k * T * 8 + (long)t * 8 + j) * R + r0) * 4);
-        yh[j] = ld_u(rs_yh, vrow, so);
-        dy[j] = ld_u(rs_dyh, vrow, so);
+        yh[j] = ld_u(rs_yh, vrw, so);
+        dy[j] = ld_u(rs_dyh, vrw, so);
         s += yh[j] * dy[j];
       }
-      const float dpi = ld_u(rs_dpi, vrow, (unsigned)(o * 4));
-      hv[tid] = dpi;
-      st_u(rs_DH, vrow, (unsigned)(o * 4), dpi);
+      const float dpi = ld_u(rs_dpi, vrw, (unsigned)(o * 4));
+      {
+        // the row's done flag, read at the carry: loaded here, with nothing behind it to drain
+        const int rw = r0 + tl, a = rw / W;
+        dns[tl] = __builtin_amdgcn_raw_buffer_load_b8(rs_done, (a * T + t) * W + rw - a * W, 0, 0);
+      }
+      hv[tl] = dpi;
+      st_u(rs_DH, vrw, (unsigned)(o * 4), dpi);
       for (int j = 0; j < 8; ++j) {
         const float v = yh[j] * (dy[j] - s);
-        hv[(j + 1) * RBT + tid] = v;
-        st_u(rs_DH, vrow, (unsigned)(((long)(j + 1) * p.M + o) * 4), v);
+        hv[(j + 1) * RBT + tl] = v;
+        st_u(rs_DH, vrw, (unsigned)(((long)(j + 1) * p.M + o) * 4), v);
       }
     }
   };
@@ -1227,7 +1229,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     // 16-byte loads in flight while quad i is transposed and processed (twice the bytes in flight per wave)
     float dz_r[2][16], dhn_r[2][16];
     const int ub = 32 * wave + 4 * hi;               // lane's unit base (register q adds qunit(q))
-    const float* wil = wi34 + ub;
+    // LDS addresses below are re-derived from lane_now() where used (see lane_now)
+    auto ubn = [&] { return 32 * wave + 4 * (lane_now() >> 5); };
+    auto rown = [&](int h) { return RB * h + (lane_now() & 31); };
     constexpr int NR = 3;
     float vr[NR][4][4];   // NR-slot ring: quads i+1 .. i+NR-1 in flight while quad i is processed (NR = 2: 10.11 ms)
     auto load_q = [&](int h, int g4, float (&v)[4][4]) {
@@ -1253,8 +1257,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     auto load_x = [&](int h, float (&x)[4]) {
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
-        const int k = 2 * kk + hi;
-        x[kk] = ld_u(rs_x, (unsigned)((RB * h + col) * 4), (unsigned)((((long)(k < F ? k : 0)) * p.M + ctr + r0) * 4));
+        const int ln = lane_now(), k = 2 * kk + (ln >> 5);
+        // k (lane-dependent) goes in the VGPR offset: a lane-dependent soffset compiles to a waterfall loop
+        x[kk] = ld_u(rs_x, (unsigned)((((long)(k < F ? k : 0)) * p.M + RB * h + (ln & 31)) * 4), (unsigned)((ctr + r0) * 4));
       }
     };
     load_x(0, xa);
@@ -1277,8 +1282,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         for (int q = 0; q < 16; ++q) hacc[q] = 0.0f;
 #pragma unroll
         for (int kk = 0; kk < 5; ++kk) {
-          const int o = 2 * kk + hi;
-          hacc = mfma32(wA[kk], o < 9 ? hv[o * RBT + RB * h + col] : 0.0f, hacc);
+          const int ln = lane_now(), o = 2 * kk + (ln >> 5);
+          hacc = mfma32(wAs[(wave * 5 + kk) * 64 + ln], o < 9 ? hv[o * RBT + RB * h + (ln & 31)] : 0.0f, hacc);
         }
         float wI[4];
 #pragma unroll
@@ -1287,9 +1292,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         dx3 = 0.0f;
         dx4 = 0.0f;
       }
-      const int row = RB * h + col;
 #pragma unroll
       for (int a = 0; a < 4; ++a) quad_transpose(v[a], lane);
+      const float* wil = wi34 + ubn();
       float drq[4], rhq[4], dnq[4];
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
@@ -1316,13 +1321,14 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       }
       st_q(rs_rh, h, g4, rhq);
       st_q(rs_dg[3], h, g4, dnq);   // dr, dz and dhn leave beside the contraction passes
-      *reinterpret_cast<float4*>(&drs[row * DRP + ub + 8 * g4]) = make_float4(drq[0], drq[1], drq[2], drq[3]);
+      *reinterpret_cast<float4*>(&drs[rown(h) * DRP + ubn() + 8 * g4]) = make_float4(drq[0], drq[1], drq[2], drq[3]);
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) rmr[h] = fmaxf(rmr[h], fabsf(drq[jj]));
       if (g4 == 3) {
         // lanes l and l + 32 hold the same row: fold the halves, one float2 per (wave, row)
         const float f3 = dx3 + __shfl_xor(dx3, 32), f4 = dx4 + __shfl_xor(dx4, 32);
-        if (hi == 0) *reinterpret_cast<float2*>(dxp + (wave * RBT + row) * 2) = make_float2(f3, f4);
+        const int ln = lane_now();
+        if (ln < 32) *reinterpret_cast<float2*>(dxp + (wave * RBT + RB * h + ln) * 2) = make_float2(f3, f4);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -1334,7 +1340,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) m = fmaxf(m, fmaxf(fabsf(dz_r[h][q]), fabsf(dhn_r[h][q])));
       m = fmaxf(m, __shfl_xor(m, 32));
-      if (hi == 0) rmx[wave * RBT + RB * h + col] = m;
+      const int ln = lane_now();
+      if (ln < 32) rmx[wave * RBT + RB * h + ln] = m;
     }
     lds_barrier();   // dr staged, row maxima visible
     BWD_STAMP(3);
@@ -1344,8 +1351,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       float m = 0.0f;
+      const int cl = lane_now() & 31;
 #pragma unroll
-      for (int w8 = 0; w8 < 8; ++w8) m = fmaxf(m, rmx[w8 * RBT + RB * h + col]);
+      for (int w8 = 0; w8 < 8; ++w8) m = fmaxf(m, rmx[w8 * RBT + RB * h + cl]);
       int sc = 0, ce = 127;
       if (m > 0.0f && m <= 3.0e38f) {
         int e;
@@ -1354,7 +1362,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         ce = min(126, max(-126, 14 - e));
       }
       bs[h] = ldexpf(1.0f, sc);
-      if (p.CE && wave == 0 && hi == 0) p.CE[ctr + r0 + RB * h + col] = (int8_t)ce;
+      if (p.CE && wave == 0 && lane_now() < 32) p.CE[ctr + r0 + rown(h)] = (int8_t)ce;
     }
     // a lane's four units ub + 8 g4 .. +3 of batch row `row` of gate cotangent g to DG, issued beside the
     // contraction's MFMAs where the memory pipe is otherwise idle
@@ -1366,29 +1374,29 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
-        const int row = RB * h + col;
-        const float4 v = *reinterpret_cast<const float4*>(&drs[row * DRP + ub + 8 * g4]);
+        const int row = rown(h), un = ubn();
+        const float4 v = *reinterpret_cast<const float4*>(&drs[row * DRP + un + 8 * g4]);
         const float v4[4] = {v.x, v.y, v.z, v.w};
         f16x4 x0;
 #pragma unroll
         for (int e = 0; e < 4; ++e) split2h(v4[e] * bs[h], x0, x1h[h][g4], e);
-        *reinterpret_cast<f16x4*>(&dgB[0][row * PP + ub + 8 * g4]) = x0;
-        store_dg(0, row, g4, v4);
+        *reinterpret_cast<f16x4*>(&dgB[0][row * PP + un + 8 * g4]) = x0;
+        store_dg(0, RB * h, g4, v4);
       }
     lds_barrier();
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4)
-        *reinterpret_cast<f16x4*>(&dgB[1][(RB * h + col) * PP + ub + 8 * g4]) = x1h[h][g4];
+        *reinterpret_cast<f16x4*>(&dgB[1][rown(h) * PP + ubn() + 8 * g4]) = x1h[h][g4];
     lds_barrier();
     // ---- contraction: dr, then dz, then dhn (scaled fp16 pairs) through the one image, accumulated onto the
     // direct path dh (taken into the accumulator frame 2^(s_i + t_row), exact: powers of two), so dh's registers
     // are free while the contraction's fragments are live
-    const int ubn = 32 * wave + 4 * (lane_now() >> 5);
+    const int un0 = ubn();
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
-      const float4 w4 = *reinterpret_cast<const float4*>(&wsc[ubn + 8 * g4]);
+      const float4 w4 = *reinterpret_cast<const float4*>(&wsc[un0 + 8 * g4]);
       const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
       for (int h = 0; h < 2; ++h)
@@ -1403,8 +1411,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const float v4[4] = {dz_r[h][4 * g4], dz_r[h][4 * g4 + 1], dz_r[h][4 * g4 + 2], dz_r[h][4 * g4 + 3]};
-        put4h(RB * h + col, ub + 8 * g4, v4, bs[h]);
-        store_dg(1, RB * h + col, g4, v4);
+        put4h(rown(h), ubn() + 8 * g4, v4, bs[h]);
+        store_dg(1, RB * h, g4, v4);
       }
     lds_barrier();
     BWD_STAMP(5);
@@ -1415,15 +1423,15 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const float v4[4] = {dhn_r[h][4 * g4], dhn_r[h][4 * g4 + 1], dhn_r[h][4 * g4 + 2], dhn_r[h][4 * g4 + 3]};
-        put4h(RB * h + col, ub + 8 * g4, v4, bs[h]);
-        store_dg(2, RB * h + col, g4, v4);
+        put4h(rown(h), ubn() + 8 * g4, v4, bs[h]);
+        store_dg(2, RB * h, g4, v4);
       }
     lds_barrier();
     BWD_STAMP(6);
     contract_h(2);
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
-      const float4 w4 = *reinterpret_cast<const float4*>(&wsc[ub + 8 * g4]);
+      const float4 w4 = *reinterpret_cast<const float4*>(&wsc[32 * wave + 4 * (lane_now() >> 5) + 8 * g4]);
       const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
       for (int h = 0; h < 2; ++h)
@@ -1431,20 +1439,21 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         for (int e = 0; e < 4; ++e) acc[h][4 * g4 + e] *= inv_pow2(wv[e] * bs[h]);
     }
     if (tid < RBT) {
+      const int tl = lane_now();   // == tid (wave 0)
       float s3 = 0.0f, s4 = 0.0f;
 #pragma unroll
       for (int w8 = 0; w8 < 8; ++w8) {
-        const float2 v = *reinterpret_cast<const float2*>(dxp + (w8 * RBT + tid) * 2);
+        const float2 v = *reinterpret_cast<const float2*>(dxp + (w8 * RBT + tl) * 2);
         s3 += v.x;
         s4 += v.y;
       }
-      st_u(rs_dx3, vrow, (unsigned)((ctr + r0) * 4), s3);
-      st_u(rs_dx4, vrow, (unsigned)((ctr + r0) * 4), s4);
+      st_u(rs_dx3, (unsigned)tl * 4, (unsigned)((ctr + r0) * 4), s3);
+      st_u(rs_dx4, (unsigned)tl * 4, (unsigned)((ctr + r0) * 4), s4);
     }
     // carry to h_out(t+1): h_in(t) = where(d_t, 0, h_out(t+1))
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const bool dn = __builtin_amdgcn_raw_buffer_load_b8(rs_done, w_[h], (int)(((long)a_[h] * T + t) * W), 0) != 0;
+      const bool dn = dns[RB * h + (lane_now() & 31)] != 0;
 #pragma unroll
       for (int q = 0; q < 16; ++q) dh[h][q] = dn ? 0.0f : acc[h][q];
     }
