@@ -621,6 +621,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   __shared__ __attribute__((aligned(16))) float usc[4 * HU];          // accumulator unscale 2^-(s + 14) [gate][unit]
   __shared__ float hp[8 * 9 * 64];      // head partials [wave][output][row]
   __shared__ float hout[9 * 64];
+  __shared__ float wIs[8 * 4 * 64];     // gate_ain's W_in fragments [wave][kk][lane] (registers are the bound)
   const int tid = threadIdx.x, lane = tid & 63, hi = lane >> 5, col = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r0 = blockIdx.x * 64;
@@ -640,8 +641,12 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     wh[i] = oo == 0 ? eta[p.o.pi_w + u] : oo < 9 ? eta[p.o.y_w + u * 8 + (oo - 1)] : 0.0f;
   }
   for (int i = tid; i < 4 * HU; i += 512) usc[i] = 1.0f / (A6c[F6_SCALES + i] * HSCALE);   // powers of two: exact
-  float wI[4];
-  load_win_frags(wI, eta, p.o, F, wave, lane);
+  {
+    float wI[4];
+    load_win_frags(wI, eta, p.o, F, wave, lane);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) wIs[(wave * 4 + kk) * 64 + lane] = wI[kk];
+  }
   {
     uint4* z = reinterpret_cast<uint4*>(&hB[0][0]);
     for (int i = tid; i < 3 * 64 * F6_HP / 8; i += 512) z[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -756,6 +761,21 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     lds_barrier();   // every wave done reading hB / xB: the carry and x(t-1) overwrite them in place
     // ---- gate maths (lane = row 32h + col, register q = unit 32 wave + 4 hi + qunit(q))
     floatx16 ain[2];
+    // done flags d_{t-1} of the lane's two rows, issued before the saves so their wait drains nothing else
+    // (lane offset re-derived here: a spilled copy's reload would wait on every outstanding access)
+    bool dnf[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      dnf[h] = (t >= 1) ? __builtin_amdgcn_raw_buffer_load_b8(
+                              rs_done, lane_now() & 31, (int)(((long)a_[h] * T + (t - 1)) * W + r0 + RB * h - a_[h] * W),
+                              0) != 0
+                        : false;
+    float wI[4];
+    {
+      const int ln = lane_now();
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) wI[kk] = wIs[(wave * 4 + kk) * 64 + ln];
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) ain[h] = gate_ain(wI, F, hi, [&](int k) { return xv[h][k < 7 ? k : 6]; });
     const long cbase = (long)t * R;
@@ -764,9 +784,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int row = RB * h + col;
-      const bool dn = (t >= 1) ? __builtin_amdgcn_raw_buffer_load_b8(rs_done, w_[h],
-                                                                       (int)(((long)a_[h] * T + (t - 1)) * W), 0) != 0
-                               : false;
+      const bool dn = dnf[h];
       const unsigned vbyte = (unsigned)(((long)ub * p.M + r0 + row) * 4);
       float hp_loc[9];
 #pragma unroll
@@ -821,7 +839,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
       }
     }
     lds_barrier();   // head partials, the carry and x(t-1) visible
-    for (int i = tid; i < 9 * 64; i += 512) {
+    for (int i = 64 * wave + lane_now(); i < 9 * 64; i += 512) {
       const int oo = i >> 6, c = i & 63;
       float v = oo == 0 ? bpi : eta[p.o.y_b + oo - 1];
 #pragma unroll
@@ -830,14 +848,15 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     }
     lds_barrier();
     if (tid < 64) {
-      const long ob = (long)t * R + r0 + tid;
-      p.pi_hat[ob] = hout[tid];
+      const int tl = lane_now();   // == tid (wave 0)
+      const long ob = (long)t * R + r0 + tl;
+      p.pi_hat[ob] = hout[tl];
       float m = -__builtin_inff();
-      for (int j = 0; j < 8; ++j) m = fmaxf(m, hout[(j + 1) * 64 + tid]);
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, hout[(j + 1) * 64 + tl]);
       float e[8], ssum = 0.0f;
-      for (int j = 0; j < 8; ++j) { e[j] = __expf(hout[(j + 1) * 64 + tid] - m); ssum += e[j]; }
+      for (int j = 0; j < 8; ++j) { e[j] = __expf(hout[(j + 1) * 64 + tl] - m); ssum += e[j]; }
       const float inv = 1.0f / ssum;
-      for (int j = 0; j < 8; ++j) p.y_hat[((long)t * 8 + j) * R + r0 + tid] = e[j] * inv;
+      for (int j = 0; j < 8; ++j) p.y_hat[((long)t * 8 + j) * R + r0 + tl] = e[j] * inv;
     }
   }
 }
