@@ -57,6 +57,20 @@ def test_wgrad_strided_rows_and_determinism():
     assert torch.equal(C, C2)
 
 
+def test_wgrad_small_strided_rows_and_determinism():
+    # ra <= 16 (the register-ring stream): row pitches past K, a partial last column tile, a ragged slab count
+    from toued import _lib as L
+    ra, rb, K, lda, ldb = 9, 257, 32 * 411, 32 * 411 + 36, 32 * 411 + 8
+    C, ref, mag, (Ab, Bb, work) = run(ra, rb, K, lda, ldb, seed=5)
+    err = (C.double() - ref).abs()
+    assert (err <= 2e-6 * math.sqrt(K) * mag).all()
+    C2 = torch.empty_like(C)
+    L.call("toued_wgrad", ra, rb, K, L.ptr(Ab), lda, L.ptr(Bb), ldb, L.ptr(C2), L.ptr(work), work.numel(),
+           L.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(C, C2)
+
+
 def test_wgrad_empty_k_and_errors():
     from toued import _lib as L
     C = torch.full((3, 5), 7.0, device="cuda")

@@ -1159,22 +1159,27 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     if (tid < RBT) {
       const int tl = lane_now();   // == tid (wave 0)
       const unsigned vrw = (unsigned)tl * 4;
-      const long o = ((long)k * T + t) * R + r0;
-      float yh[8], dy[8], s = 0.0f;
-      for (int j = 0; j < 8; ++j) {
-        const unsigned so = (unsigned)((((long)k * T * 8 + (long)t * 8 + j) * R + r0) * 4);
-        yh[j] = ld_u(rs_yh, vrw, so);
-        dy[j] = ld_u(rs_dyh, vrw, so);
-        s += yh[j] * dy[j];
-      }
-      const float dpi = ld_u(rs_dpi, vrw, (unsigned)(o * 4));
+      int dnv;
       {
         // the row's done flag, read at the carry: loaded here, with nothing behind it to drain
         const int rw = r0 + tl, a = rw / W;
-        dns[tl] = __builtin_amdgcn_raw_buffer_load_b8(rs_done, (a * T + t) * W + rw - a * W, 0, 0);
+        dnv = __builtin_amdgcn_raw_buffer_load_b8(rs_done, (a * T + t) * W + rw - a * W, 0, 0);
       }
+      const long o = ((long)k * T + t) * R + r0;
+      float yh[8], dy[8], s = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {   // all 17 loads in flight at once (the other waves wait at the barrier)
+        const unsigned so = (unsigned)((((long)k * T * 8 + (long)t * 8 + j) * R + r0) * 4);
+        yh[j] = ld_u(rs_yh, vrw, so);
+        dy[j] = ld_u(rs_dyh, vrw, so);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += yh[j] * dy[j];
+      const float dpi = ld_u(rs_dpi, vrw, (unsigned)(o * 4));
+      dns[tl] = dnv;
       hv[tl] = dpi;
       st_u(rs_DH, vrw, (unsigned)(o * 4), dpi);
+#pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float v = yh[j] * (dy[j] - s);
         hv[(j + 1) * RBT + tl] = v;
