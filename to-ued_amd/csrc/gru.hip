@@ -102,17 +102,6 @@ TOUED_DEV void quad_transpose(float* a, int lane) {
   if (b0) { a[0] = r0; a[2] = r1; } else { a[1] = r0; a[3] = r1; }
 }
 
-// A VALU write to the data VGPRs of a preceding >8-byte VMEM store needs wait states that this compiler
-// does not always insert for buffer-store builtins on gfx950 (observed: the first dword of some 16-byte
-// stores replaced by the next value written to its register).  The s_nop after the store provides them; the
-// data is an operand of the asm, so its registers stay allocated (no write to them is scheduled) until then.
-TOUED_DEV void st4(__amdgpu_buffer_rsrc_t r, unsigned vbyte, unsigned soff, const float* v) {
-  u32x4 x;
-  x.x = __float_as_uint(v[0]); x.y = __float_as_uint(v[1]); x.z = __float_as_uint(v[2]); x.w = __float_as_uint(v[3]);
-  __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)vbyte, (int)soff, 0);
-  asm volatile("s_nop 1" ::"v"(x) : "memory");
-}
-
 TOUED_DEV float sigm(float x) { return 1.0f / (1.0f + __expf(-x)); }
 // v_rcp_f32 (1 ulp) instead of the IEEE division sequence: the forward's gate maths is on the critical path
 TOUED_DEV float sigm_r(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
@@ -221,9 +210,12 @@ __global__ void k_pack_bwd(const float* __restrict__ eta, EtaOff o, float4* __re
 #define B6_SCALES (B6_NF * 256)            // float offset of the per-input-unit scales 2^s of W_z, W_hn [256]
 #define B6_FLOATS (B6_SCALES + HU)
 // One k-major LDS buffer ([unit][row], pitch RB*NT + 1; h^T in the forward, a gate cotangent in the
-// backward) of NT row tiles out to its row-major
-// [unit][M] array: lane l stores 4 consecutive rows (4*(l & 7) ..) of unit 32*wave + 8i + (l >> 3),
-// so every wave instruction writes 8 units x 128 contiguous bytes; the LDS reads are conflict-free.
+// backward) of NT row tiles out to its row-major [unit][M] array: per instruction lane l stores row
+// RB*h + (l & 31) of unit 32*wave + 2i + (l >> 5), so every wave instruction writes 2 units x 128
+// contiguous bytes; the LDS reads (consecutive rows of a unit) are conflict-free.  Dword stores: a VALU write to
+// the data VGPRs of a preceding 16-byte buffer store needs wait states that hipcc does not insert when the store
+// has an SGPR soffset (observed on gfx950: the first dword of some 16-byte stores replaced by the next value
+// written to its register); dword stores carry no such hazard.
 template <int NT>
 TOUED_DEV void store_gate_lds(const float* buf, __amdgpu_buffer_rsrc_t rs, long M, long col0, int wave, int lane) {
   constexpr int LDT = RB * NT + 1;
@@ -231,11 +223,9 @@ TOUED_DEV void store_gate_lds(const float* buf, __amdgpu_buffer_rsrc_t rs, long 
 #pragma unroll
   for (int h = 0; h < NT; ++h) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int unit = 32 * wave + 8 * i + (lane >> 3), r = RB * h + 4 * (lane & 7);
-      const float* src = buf + unit * LDT + r;
-      const float v[4] = {src[0], src[1], src[2], src[3]};
-      st4(rs, (unsigned)(((long)unit * M + r) * 4), so, v);
+    for (int i = 0; i < 16; ++i) {
+      const int unit = 32 * wave + 2 * i + (lane >> 5), r = RB * h + (lane & 31);
+      st_u(rs, (unsigned)(((long)unit * M + r) * 4), so, buf[unit * LDT + r]);
     }
   }
 }

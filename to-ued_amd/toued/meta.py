@@ -87,6 +87,23 @@ class KernelTimers:
         self.events = {}
 
 
+def local_mini_batches(n_local: int, num_agents: int, num_mini_batches: int) -> int:
+    """This rank's sequential chunk count for ``--num_mini_batches``.
+
+    The reference checks the split globally: mini_batch_vmap reshapes all num_agents into num_mini_batches
+    equal batches (util/jax.py:25-41), each of num_agents / num_mini_batches agents.  Chunking is a memory bound
+    (the summed meta-gradient is the same), so each rank runs its n_local agents as the fewest equal chunks no
+    larger than that batch: the smallest divisor of n_local that is >= ceil(n_local / batch)."""
+    if num_mini_batches < 1 or num_agents % num_mini_batches:
+        raise ValueError(f"num_agents={num_agents} does not split into num_mini_batches={num_mini_batches} equal "
+                         "mini-batches (util/jax.py:25-41 reshapes them)")
+    if n_local < 1:
+        raise ValueError(f"this rank holds {n_local} agents")
+    batch = num_agents // num_mini_batches
+    need = -(-n_local // batch)
+    return next(d for d in range(need, n_local + 1) if n_local % d == 0)
+
+
 class MetaGradStep:
     """``n_agents`` is the agents per call (this rank's); with ``num_mini_batches`` > 1 they run as that many
     sequential chunks of n_agents / num_mini_batches (util/jax.py:25-41 mini_batch_vmap: chunk i holds agents
@@ -94,13 +111,10 @@ class MetaGradStep:
     The per-chunk buffers (GRU saves etc.) are sized for one chunk."""
 
     def __init__(self, rollout: RolloutWrapper, n_agents: int, hyp: LpgHyperparams, lifetime_conditioning: bool,
-                 device=None, world=None, num_mini_batches: int = 1):
-        if num_mini_batches < 1 or n_agents % num_mini_batches:
-            raise ValueError(f"this rank's {n_agents} agents do not split into num_mini_batches={num_mini_batches} "
-                             "equal chunks")
+                 device=None, world=None, num_mini_batches: int = 1, num_agents_global: int | None = None):
         self.n_total_local = n_agents
-        self.n_chunks = num_mini_batches
-        n_agents //= num_mini_batches
+        self.n_chunks = local_mini_batches(n_agents, num_agents_global or n_agents, num_mini_batches)
+        n_agents //= self.n_chunks
         self.ro = rollout
         self.N = n_agents
         self.W = rollout.env_workers
@@ -301,9 +315,15 @@ class MetaGradStep:
                    ptr(self.G_ph[k]), ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]), ptr(self.coef), hyp.actor_lr,
                    hyp.critic_lr, hyp.agent_target_coeff, hyp.policy_l2_coeff, hyp.target_l2_coeff,
                    ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]), ptr(self.d_pi_hat[k]), ptr(self.d_y_hat[k]), st)
-        self.gru.backward(self.traj.done, eta, self.y_hat, self.d_pi_hat, self.d_y_hat, self.X, self.grad,
-                          self.timers, after_bwd=launch_eval)
-        L.lib().toued_set_reserved_cus(ea["prev_reserve"])
+        try:
+            self.gru.backward(self.traj.done, eta, self.y_hat, self.d_pi_hat, self.d_y_hat, self.X, self.grad,
+                              self.timers, after_bwd=launch_eval)
+        finally:
+            # the CU reservation is process-global split-K planning state: restore it whatever happened
+            if "prev_reserve" in ea:
+                L.lib().toued_set_reserved_cus(ea["prev_reserve"])
+        if "cum" not in ea:
+            raise RuntimeError("MetaGradStep: the GRU backward returned without launching eval_agent")
         tr = self.traj
         L.call("toued_embed_bwd", N, W, T, D, K, ptr(self.phi_h), self.phi_h[0].numel(), ptr(tr.obs_idx),
                tr.obs_idx[0].numel(), ptr(tr.obs_time), ptr(tr.done), tr.done[0].numel(), ptr(self.gru.dX3),
@@ -462,7 +482,7 @@ def make_lpg_train_step(args, level_sampler, n_agents: int | None = None, world=
         if "step" not in holder:
             holder["step"] = MetaGradStep(level_sampler.rollout_manager, n_local, hyp, args.lifetime_conditioning,
                                           lpg_train_state.params.device, world,
-                                          num_mini_batches=args.num_mini_batches)
+                                          num_mini_batches=args.num_mini_batches, num_agents_global=args.num_agents)
         if value_critic_states is not None:
             agent_states.vcrit, agent_states.vstep = value_critic_states.params, value_critic_states.step
         metrics = holder["step"](rng, lpg_train_state.params, lpg_train_state.opt, agent_states, rank_slice)

@@ -72,7 +72,8 @@ class Trainer:
         else:
             self.hyp = lpg_hypers_from_args(args, self.sampler)
             self.step_fn = MetaGradStep(self.sampler.rollout_manager, n_local, self.hyp, args.lifetime_conditioning,
-                                        self.dev, self.world, num_mini_batches=args.num_mini_batches)
+                                        self.dev, self.world, num_mini_batches=args.num_mini_batches,
+                                        num_agents_global=args.num_agents)
             self.adam = AdamState(self.eta.numel(), self.dev)
         # the reference's lpg_train_step_fn (train.py:33, meta/meta.py:33-52) driving this instance
         self.train_state = LpgTrainState(self.eta, None if args.use_es else self.adam)
@@ -147,3 +148,7 @@ def save_final_checkpoints(ckpt_dir: str, tr: "Trainer", steps: int):
     buf = tr.buffer_init if init else tr.buffer
     if buf is not None:
         save_checkpoint(ckpt_dir, level_buffer_state_dict(buf, tr.sampler.spec), steps, prefix="buffer_")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
