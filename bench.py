@@ -89,6 +89,9 @@ def parse():
     ap.add_argument("--agents_per_gpu", type=int, default=512)
     ap.add_argument("--lifetime_conditioning", action="store_true")
     ap.add_argument("--no_cpu_baseline", action="store_true")
+    ap.add_argument("--workloads", default="c3,c4",
+                    help="secondary BASELINE configs measured after the headline at N=1 (comma list of c3, c4; "
+                         "'none' to skip): each gets its own value, roofline and cpu_baseline under 'workloads'")
     ap.add_argument("--cpu_agents", type=int, default=0, help="agents in the CPU sample (0 = auto-size to ~15 s)")
     ap.add_argument("--launcher_selftest", action="store_true",
                     help="test hook: run the multi-rank launch, barrier and max-over-ranks timing on gloo/CPU with "
@@ -244,6 +247,252 @@ def cpp_rollout_baseline(env_mode: str, n_agents: int = 512, target_s: float = 5
                                       f"rollouts of {n_agents} agents x W={W} x T={T}, env_mode={env_mode}; {dt:.1f} s"}
 
 
+# ---------------------------------------------------------------------------------------------- C3 / C4 workloads
+def _sync_time(fn, n):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(n):
+        out = fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / n, out
+
+
+def _hbm_roofline(name, nbytes, mean_ms, note=None, traffic_kernel=None):
+    sec = mean_ms * 1e-3
+    r = {"bound": "hbm", "kernel": name, "achieved": round(nbytes / sec / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(nbytes / sec / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_launch": int(nbytes), "mean_ms": round(mean_ms, 4)}
+    if traffic_kernel:
+        r["traffic"], r["traffic_source"] = pmc_traffic(traffic_kernel)
+    if note:
+        r["note"] = note
+    return r
+
+
+def workload_c3(a, cpu: bool):
+    """BASELINE C3, GROOVE: --score_function alg_regret --env_mode all_shortlife, 512 agents.  The reference scores
+    every agent's level on every meta-step (level_sampler.py:176-181: _compute_algorithmic_regret for all agents,
+    the non-terminated scores then masked out), so its meta-step = the LPG meta-gradient step + one regret round
+    (a fresh A2C antagonist per agent trained for max_lifetime = 250 updates of W x T, agents/a2c.py:79-125, plus the
+    two eval_agent rollouts, level_sampler.py:293-329).  This build scores only terminated agents (the same outputs);
+    the regret round is timed with every agent terminated, so t_meta + t_regret is the reference-equivalent step.
+    value = inner-rollout agent-env-steps (N W T K of the LPG updates + N U W T of the antagonists) / that time."""
+    from toued.env import L_LIFETIME
+    from toued.meta import KernelTimers
+    from toued.parse_args import parse_args
+    from toued.train import Trainer
+    N = a.agents_per_gpu
+    args = parse_args(["--env_mode", "all_shortlife", "--num_agents", str(N), "--num_mini_batches", "1",
+                       "--score_function", "alg_regret"])
+    tr = Trainer(args)
+    W, T, K = args.env_workers, args.train_rollout_len, args.num_agent_updates
+    U = tr.sampler.max_lifetime
+    tr.meta_step()                                    # warm: graph capture, code objects
+    t_meta, _ = _sync_time(lambda: tr.step_fn(tr.rng, tr.eta, tr.adam, tr.agents), max(1, a.steps))
+
+    def regret_round():
+        tr.agents.step = tr.agents.levels[:, L_LIFETIME].clone()     # every agent terminated: all are scored
+        tr.buffer, tr.agents = tr.sampler.sample(tr.rng, tr.buffer, tr.agents)
+    regret_round()
+    t_regret, _ = _sync_time(regret_round, max(1, a.steps))
+    # per-kernel launch durations of the antagonists' update chain: one eager round with HIP events (the graph
+    # replays the same two kernels per update)
+    trn = tr.sampler.a2c_trainer()
+    trn.timers = KernelTimers()
+    trn.timers.enabled = True
+    regret_round()
+    torch.cuda.synchronize()
+    ks = trn.timers.summary()
+    trn.timers = None
+    D = tr.sampler.obs_dim
+    roll_ms, upd_ms = ks["a2c_rollout"][1], ks["a2c_update"][1]
+    steps_launch = N * W * T
+    traj_bytes = N * ((T + 1) * W * 8 + T * W * 6)
+    upd_bytes = traj_bytes + N * D * 6 * 4 * 2
+    rollout_rf = _hbm_roofline("k_rollout (A2C antagonist train rollout)", steps_launch * ROLLOUT_BYTES_PER_STEP,
+                               roll_ms, "bound in practice by its dependent threefry VALU chain (~12 blocks per step)")
+    update_rf = _hbm_roofline("k_a2c_update (fused GAE + actor/critic gradients + clip + SGD, tables in LDS)",
+                              upd_bytes, upd_ms)
+    dom = rollout_rf if roll_ms >= upd_ms else update_rf
+    a2c_steps = N * U * W * T
+    meta_steps = N * W * T * K
+    t_ref = t_meta + t_regret
+    out = {"workload": f"C3 GROOVE alg_regret env_mode=all_shortlife num_agents={N} W={W} T={T} K={K} "
+                       f"antagonist updates U={U} (reference-equivalent meta-step: LPG meta-gradient + regret round "
+                       f"scoring every agent)",
+           "value": round((meta_steps + a2c_steps) / t_ref, 1), "unit": "agent-env-steps/sec",
+           "ms_per_step": round(t_ref * 1e3, 3), "meta_updates_per_sec": round(1.0 / t_ref, 3),
+           "lpg_meta_step_ms": round(t_meta * 1e3, 3), "regret_round_ms": round(t_regret * 1e3, 3),
+           "regret_round_agent_env_steps_per_sec": round(a2c_steps / t_regret, 1),
+           "amortized_meta_step_ms": round((t_meta + t_regret * K / U) * 1e3, 3),
+           "roofline": dom, "roofline_secondary": {"a2c_rollout": rollout_rf, "a2c_update": update_rf},
+           "kernels": {k: {"launches": v[0], "mean_ms": round(v[1], 4)} for k, v in ks.items()}}
+    out["cpu_baseline"] = c3_cpu_baseline(args, tr.sampler) if cpu else None
+    del tr
+    torch.cuda.empty_cache()
+    return out
+
+
+def c3_cpu_baseline(args, sampler, target_s: float = 12.0):
+    """C3's regret round on the host (C++ rollout/GAE/A2C): the C++/OpenMP restatement (oracle/cpu)
+    of n antagonists x U = max_lifetime A2C updates (rollout + GAE + actor/critic update, the A2C update checked
+    against the float64 oracle in tests/test_oracle_cpu.py) plus the two eval_agent rollouts per agent (returns
+    only, eval length), n sized to ~target_s.  agent-env-steps/sec of the A2C updates, comparable with the GPU's
+    regret_round_agent_env_steps_per_sec."""
+    import ctypes
+    import numpy as np
+
+    from oracle import cpu
+    from oracle import jaxrand as jr
+    from oracle import levels as olv
+    from oracle import rollout as oro
+    mode = args.env_mode
+    spec = olv.env_spec(mode)
+    W, T, D = args.env_workers, args.train_rollout_len, spec.obs_dim
+    U, Lr = sampler.max_lifetime, sampler.max_rollout_len
+    L = cpu.lib()
+    P = lambda x: x.ctypes.data_as(ctypes.c_void_p)
+
+    def run(n, updates):
+        p, lt = olv.reset_env_params(jr.split(jr.PRNGKey(0), n), mode)
+        lt = np.full_like(lt, 10 ** 6)
+        lev = np.ascontiguousarray(olv.pack_levels(p, lt, spec))
+        rs = np.random.RandomState(0)
+        theta = (rs.randn(n, D, 5) * 0.05).astype(np.float32)
+        vc = (rs.randn(n, D) * 0.05).astype(np.float32)
+        step = np.zeros(n, np.int32)
+        loss = np.zeros((n, 2), np.float32)
+
+        def soa(st, nw):
+            s_ = np.zeros((12, n * nw), np.int32)
+            s_[0], s_[1], s_[3] = st["time"], st["pos"], st["early_term"]
+            s_[2] = np.sum(st["obj_existss"] * (1 << np.arange(spec.max_n_objs))[None, :], axis=1)
+            s_[4:4 + spec.max_n_objs] = st["obj_poss"].T
+            return s_
+        state = soa(oro.batch_reset(spec, jr.split(jr.PRNGKey(1), n), p, W), W)
+        idx = np.zeros((n, T + 1, W), np.int32)
+        tm = np.zeros_like(idx)
+        act = np.zeros((n, T, W), np.uint8)
+        rew = np.zeros((n, T, W), np.float32)
+        dn = np.zeros_like(act)
+        ev_state = soa(oro.batch_reset(spec, jr.split(jr.PRNGKey(2), n), p, 64), 64)
+        cum = np.zeros(n * 64, np.float32)
+        t0 = time.perf_counter()
+        for u in range(updates):
+            keys = np.ascontiguousarray(jr.split(jr.PRNGKey(100 + u), n))
+            L.toued_cpu_rollout(spec.max_grid_size, spec.max_n_objs, spec.max_n_obj_types, int(spec.tabular), P(lev),
+                                P(theta), D, P(keys), P(state), T, W, n, P(idx), P(tm), P(act), P(rew), P(dn), None)
+            L.toued_cpu_a2c_update(P(theta), P(vc), P(step), P(lev), D, P(idx), P(tm), P(act), P(rew), P(dn), T, W, n,
+                                   0.99, 0.95, 0.01, 40.0, 4.0, 0.5, P(loss))
+        for e in range(2):     # eval_agent of the LPG actor and of the trained antagonist: 64 workers x eval length
+            keys = np.ascontiguousarray(jr.split(jr.PRNGKey(7 + e), n))
+            st_e = ev_state.copy()
+            L.toued_cpu_rollout(spec.max_grid_size, spec.max_n_objs, spec.max_n_obj_types, int(spec.tabular), P(lev),
+                                P(theta), D, P(keys), P(st_e), Lr, 64, n, None, None, None, None, None, P(cum))
+        return time.perf_counter() - t0
+
+    n = 8
+    for _ in range(3):       # size n to ~target_s (the parallel efficiency grows with n: re-measure)
+        dt = run(n, U)
+        if dt >= 0.5 * target_s or n >= 512:
+            break
+        n = int(max(8, min(512, round(n * target_s / max(dt, 1e-3)))))
+    return {"value": round(n * U * W * T / dt, 1), "unit": "agent-env-steps/sec", "cores": cpu.threads(),
+            "kind": "port",
+            "sample": f"C++/OpenMP restatement (oracle/cpu) of the regret round: {n} antagonists x U={U} A2C updates "
+                      f"(rollout + GAE + actor/critic update, W={W}, T={T}) + 2 eval rollouts (64 workers x {Lr} "
+                      f"steps) each, env_mode={mode}; {dt:.1f} s"}
+
+
+def workload_c4(a, cpu: bool):
+    """BASELINE C4, TA-LPG: --use_es --lifetime_conditioning --env_mode all_vrandlife, 512 agents -> 1024 OpenES
+    candidates (antithetic pairs), each trained with its own LPG for max_lifetime = 250 updates (meta/meta.py:35-37),
+    then eval_agent fitness, pair ranks and the OpenES tell (meta/train.py:133-227).  value = candidates x U x W x T
+    inner-rollout agent-env-steps per ES step / ES-step time.  The dominant kernel is the per-candidate LPG GRU forward
+    (k_gru_fwd6<false>, 16-bit MFMA on the f32-accurate split)."""
+    from toued.parse_args import parse_args
+    from toued.train import Trainer
+    N = a.agents_per_gpu
+    args = parse_args(["--env_mode", "all_vrandlife", "--num_agents", str(N), "--num_mini_batches", "1", "--use_es",
+                       "--lifetime_conditioning", "--lpg_learning_rate", "0.01"])
+    tr = Trainer(args)
+    st = tr.step_fn
+    W, T, U, C, F = st.W, st.T, st.K, st.C, st.F
+    tr.meta_step()
+    st.timers.enabled = True
+    st.timers.reset()
+    t_es, m = _sync_time(tr.meta_step, max(1, a.steps // 2))
+    ks = st.timers.summary()
+    st.timers.enabled = False
+    R = C * W
+    flop = R * T * GRU_FWD_FLOP_PER_ELEM[F]
+    g_ms = ks["gru_fwd_multi"][1]
+    t_mfma = SPLIT_PRODUCTS["gru_fwd"] * flop / (MFMA_BF16_PEAK_TFLOPS * 1e12)
+    rf = {"bound": "mfma", "kernel": "k_gru_fwd6<false> (per-candidate LPG GRU forward)",
+          "achieved": round(SPLIT_PRODUCTS["gru_fwd"] * flop / (g_ms * 1e-3) / 1e12, 1), "peak": MFMA_BF16_PEAK_TFLOPS,
+          "unit": "TFLOP/s (16-bit issued)", "frac": round(t_mfma / (g_ms * 1e-3), 4), "mean_ms": round(g_ms, 4),
+          "flop_per_launch_f32": flop, "f32_equiv_tflops": round(flop / (g_ms * 1e-3) / 1e12, 1)}
+    roll_ms = ks["rollout"][1]
+    rollout_rf = _hbm_roofline("k_rollout (candidates' train rollout)", R * T * ROLLOUT_BYTES_PER_STEP, roll_ms,
+                               "bound in practice by its dependent threefry VALU chain")
+    steps = C * U * W * T
+    out = {"workload": f"C4 TA-LPG OpenES env_mode=all_vrandlife lifetime_conditioning num_agents={N} candidates={C} "
+                       f"W={W} T={T} updates per candidate U={U}",
+           "value": round(steps / t_es, 1), "unit": "agent-env-steps/sec", "ms_per_step": round(t_es * 1e3, 3),
+           "meta_updates_per_sec": round(1.0 / t_es, 3), "roofline": rf,
+           "roofline_secondary": {"rollout": rollout_rf},
+           "kernels": {k: {"launches": v[0], "mean_ms": round(v[1], 4), "total_ms_per_step": round(v[2], 3)}
+                       for k, v in ks.items()},
+           "fitness_mean": float(m["fitness"]["mean"])}
+    out["cpu_baseline"] = c4_cpu_baseline(args, tr.sampler) if cpu else None
+    del tr
+    torch.cuda.empty_cache()
+    return out
+
+
+def c4_cpu_baseline(args, sampler, target_s: float = 12.0):
+    """C4 on the host (a subset of candidates, extrapolated and labelled): the oracle restatement
+    (numpy rollout + torch-CPU float32 LPG forward and agent update, oracle/meta.py lpg_agent_step) of one candidate's
+    lifetime-conditioned LPG updates, as many as fit ~target_s; agent-env-steps/sec of that one candidate's updates.
+    The rate per candidate is what a full ES step (1024 candidates x 250 updates) would run at, serially."""
+    import numpy as np
+
+    from oracle import jaxrand as jr
+    from oracle import levels as olv
+    from oracle import lpg as olpg
+    from oracle import meta as ometa
+    from oracle import rollout as oro
+    mode = args.env_mode
+    spec = olv.env_spec(mode)
+    W, T, D = args.env_workers, args.train_rollout_len, spec.obs_dim
+    p, lt = olv.reset_env_params(jr.split(jr.PRNGKey(0), 1), mode)
+    eta = torch.from_numpy(olpg.init_params(0, 7).astype(np.float32))
+    rs = np.random.RandomState(0)
+    theta = torch.from_numpy((rs.randn(D, 5) * 0.1).astype(np.float32))
+    phi = torch.from_numpy((rs.randn(D, 8) * 0.1).astype(np.float32))
+    hyp = ometa.Hypers(lifetime_conditioning=True)
+    st = oro.batch_reset(spec, jr.split(jr.PRNGKey(1), 1), p, W)
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < target_s and n < sampler.max_lifetime:
+        tr, st, _ = oro.batch_rollout(spec, jr.split(jr.PRNGKey(10 + n), 1), theta.numpy()[None], p, st, T)
+        traj = {k: v[0] for k, v in tr.items()}
+        traj["action"] = traj["action"].astype(np.int64)
+        traj["done"] = traj["done"].astype(bool)
+        th = theta.clone().requires_grad_()
+        ph = phi.clone().requires_grad_()
+        th, ph, _, _, _ = ometa.lpg_agent_step(th, ph, n, int(lt[0]), eta, traj, hyp)
+        theta, phi = th.detach(), ph.detach()
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n * W * T / dt, 1), "unit": "agent-env-steps/sec", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle restatement (numpy rollout + torch-CPU f32 lifetime-conditioned LPG forward + agent "
+                      f"update) of ONE candidate's first {n} of {sampler.max_lifetime} updates (W={W}, T={T}), "
+                      f"env_mode={mode}; {dt:.1f} s; a full ES step is 1024 such candidates x "
+                      f"{sampler.max_lifetime} updates (extrapolated: {1024 * sampler.max_lifetime * W * T / (n * W * T / dt):.0f} s)"}
+
+
 def main():
     a = parse()
     ws = int(os.environ.get("WORLD_SIZE", "1"))
@@ -362,6 +611,17 @@ def main():
             out["cpu_baseline"] = cpu_baseline(a.env_mode, a.lifetime_conditioning, a.cpu_agents)
         else:
             out["cpu_baseline"] = None
+    wl = [w for w in a.workloads.split(",") if w and w != "none"]
+    if wl and n_gpus == 1:
+        del tr, step
+        torch.cuda.empty_cache()
+        out["workloads"] = {}
+        for w in wl:
+            fn = {"c3": workload_c3, "c4": workload_c4}[w]
+            t0w = time.perf_counter()
+            out["workloads"][w.upper()] = fn(a, not a.no_cpu_baseline)
+            out["workloads"][w.upper()]["wall_s"] = round(time.perf_counter() - t0w, 1)
+    if world.rank == 0:
         print(json.dumps(out), flush=True)
     if world.active:
         import torch.distributed as dist

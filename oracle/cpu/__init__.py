@@ -1,4 +1,4 @@
-"""C++/OpenMP CPU restatement of the rollout + GAE (test infrastructure and the bench's second CPU baseline).
+"""C++/OpenMP CPU restatement of the rollout + GAE + A2C update (test infrastructure and the bench's CPU baselines).
 
 build() compiles rollout_cpu.cpp with g++ -O3 -fopenmp -ffp-contract=off into librollout_cpu.so next to it;
 lib() loads it (building on demand).  Only tests/, bench.py's cpu_baseline and __graft_entry__ use it.
@@ -31,6 +31,7 @@ def lib():
         P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
         L.toued_cpu_rollout.argtypes = [I, I, I, I, P, P, I, P, P, I, I, I, P, P, P, P, P, P]
         L.toued_cpu_gae.argtypes = [P, I, P, P, P, P, I, I, I, F, F, P, P]
+        L.toued_cpu_a2c_update.argtypes = [P, P, P, P, I, P, P, P, P, P, I, I, I, F, F, F, F, F, F, P]
         L.toued_cpu_threads.argtypes = []
         _lib = L
     return _lib

@@ -15,6 +15,7 @@
 // int32[12][n] layout of the device (fields time, pos, exists bitmask, early_term, obj_poss[8]).
 // Built by oracle/cpu/__init__.py (g++ -O3 -fopenmp -ffp-contract=off); never linked by the product.
 #include <math.h>
+#include <cmath>
 #include <stdint.h>
 #include <string.h>
 #include <omp.h>
@@ -335,6 +336,101 @@ int toued_cpu_gae(const float* vcrit, int D, const int* traj_idx, const int* tra
       target[(size_t)i * T + t] = g + vv;
       vn = vv;
     }
+  }
+  return 0;
+}
+
+// a2c_agent_train_step (agents/a2c.py:19-76) for N agents over one rollout in the layout above, as oracle/a2c.py
+// restates it, with closed-form gradients of the linear tables (one OpenMP thread per agent):
+//   critic: V = vcrit[idx] + 0.001 t vcrit[D-1]; GAE per worker; loss mean_w mean_t (target - V)^2
+//           -> dL/dV_{w,t} = -2 (target - V) / (W T) for t < T (the bootstrap V_T is stop-gradient);
+//   actor:  per worker -mean_t log(pi_a + 1e-8) * mean_t adv_n (the [T] x [T,1] broadcast) minus
+//           entropy_coeff * (-mean_t sum_b q_b log q_b), q = pi + 1e-8, adv_n normalised over the agent's [W, T];
+//           d/dl_c through the softmax: p_c (g_c - sum_b g_b p_b) with g_b the loss's derivative w.r.t. p_b;
+//   optax clip_by_global_norm (each table's own norm) -> SGD; the update is discarded past the lifetime
+//   (a2c.py:82-86).  theta [N][D][5], vcrit [N][D], step [N] updated in place; loss [N][2] (actor, critic).
+int toued_cpu_a2c_update(float* theta, float* vcrit, int* step, const int* levels, int D, const int* traj_idx,
+                         const int* traj_time, const uint8_t* traj_action, const float* traj_reward,
+                         const uint8_t* traj_done, int T, int W, int N, float gamma, float lam, float entropy_coeff,
+                         float actor_lr, float critic_lr, float max_norm, float* loss) {
+  const float EPS = 1e-8f;
+#pragma omp parallel for schedule(dynamic)
+  for (int a = 0; a < N; ++a) {
+    float* th = theta + (size_t)a * D * 5;
+    float* vc = vcrit + (size_t)a * D;
+    std::vector<float> ga((size_t)D * 5, 0.0f), gc(D, 0.0f), adv((size_t)W * T), tgt((size_t)W * T), vv((size_t)W * T);
+    double asum = 0.0, closs = 0.0;
+    for (int w = 0; w < W; ++w) {
+      const size_t bo = (size_t)a * (T + 1) * W + w, bt = (size_t)a * T * W + w;
+      auto V = [&](int t) { return vc[traj_idx[bo + (size_t)t * W]] + (float)traj_time[bo + (size_t)t * W] * 0.001f * vc[D - 1]; };
+      float g = 0.0f, vn = V(T);
+      for (int t = T - 1; t >= 0; --t) {
+        const float v = V(t), nd = traj_done[bt + (size_t)t * W] ? 0.0f : 1.0f;
+        const float delta = traj_reward[bt + (size_t)t * W] + (gamma * vn * nd - v);
+        g = delta + gamma * lam * nd * g;
+        adv[(size_t)w * T + t] = g;
+        tgt[(size_t)w * T + t] = g + v;
+        vv[(size_t)w * T + t] = v;
+        vn = v;
+      }
+    }
+    const double inv = 1.0 / ((double)W * T);
+    for (size_t i = 0; i < (size_t)W * T; ++i) asum += adv[i];
+    const double mean = asum * inv;
+    double var = 0.0;
+    for (size_t i = 0; i < (size_t)W * T; ++i) var += (adv[i] - mean) * (adv[i] - mean);
+    const float sd = (float)std::sqrt(var * inv) + EPS;
+    double aloss = 0.0;
+    for (int w = 0; w < W; ++w) {
+      const size_t bo = (size_t)a * (T + 1) * W + w, bt = (size_t)a * T * W + w;
+      double abar = 0.0, lsum = 0.0, ent = 0.0;
+      for (int t = 0; t < T; ++t) abar += ((double)adv[(size_t)w * T + t] - mean) / sd;
+      abar /= T;
+      for (int t = 0; t < T; ++t) {
+        const int idx = traj_idx[bo + (size_t)t * W], tm = traj_time[bo + (size_t)t * W];
+        const int act = traj_action[bt + (size_t)t * W];
+        const float c = (float)tm * 0.001f;
+        // critic
+        const float dv = -2.0f * (tgt[(size_t)w * T + t] - vv[(size_t)w * T + t]) * (float)inv;
+        closs += (double)(tgt[(size_t)w * T + t] - vv[(size_t)w * T + t]) * (tgt[(size_t)w * T + t] - vv[(size_t)w * T + t]);
+        gc[idx] += dv;
+        gc[D - 1] += dv * c;
+        // actor
+        float l[5], p[5], m = -INFINITY, s = 0.0f;
+        for (int j = 0; j < 5; ++j) { l[j] = th[(size_t)idx * 5 + j] + c * th[(size_t)(D - 1) * 5 + j]; m = std::max(m, l[j]); }
+        for (int j = 0; j < 5; ++j) { p[j] = std::exp(l[j] - m); s += p[j]; }
+        float gp[5], dot = 0.0f;
+        for (int j = 0; j < 5; ++j) {
+          p[j] /= s;
+          const float q = p[j] + EPS, lq = std::log(q);
+          ent -= (double)q * lq;
+          gp[j] = entropy_coeff * (lq + 1.0f) * (float)inv;
+        }
+        lsum += std::log(p[act] + EPS);
+        gp[act] += -(float)abar / (T * (p[act] + EPS)) / W;
+        for (int j = 0; j < 5; ++j) dot += gp[j] * p[j];
+        for (int j = 0; j < 5; ++j) {
+          const float gl = p[j] * (gp[j] - dot);
+          ga[(size_t)idx * 5 + j] += gl;
+          ga[(size_t)(D - 1) * 5 + j] += gl * c;
+        }
+      }
+      aloss += -(lsum / T) * abar - entropy_coeff * (ent / T);
+    }
+    if (loss) {
+      loss[2 * a] = (float)(aloss / W);
+      loss[2 * a + 1] = (float)(closs * inv);
+    }
+    const int lifetime = levels[(size_t)a * LW + 5];
+    if (step[a] + 1 > lifetime) continue;            // discarded update (a2c.py:82-86)
+    double na = 0.0, nc = 0.0;
+    for (float g : ga) na += (double)g * g;
+    for (float g : gc) nc += (double)g * g;
+    // optax: where(norm < max_norm, g, g / norm * max_norm)
+    const float fa = (float)std::sqrt(na), fc = (float)std::sqrt(nc);
+    for (size_t i = 0; i < ga.size(); ++i) th[i] -= actor_lr * (fa < max_norm ? ga[i] : ga[i] / fa * max_norm);
+    for (int i = 0; i < D; ++i) vc[i] -= critic_lr * (fc < max_norm ? gc[i] : gc[i] / fc * max_norm);
+    step[a] += 1;
   }
   return 0;
 }

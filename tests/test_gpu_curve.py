@@ -17,6 +17,11 @@ Every meta-step of the GPU run is replayed by the oracle from the GPU's state be
 Starting point: flax init of eta from lpg_rng and the initial levels/agents, bit-exact / within 1e-6.
 With TOUED_CURVE_OUT=<path> the per-step curve (GPU and oracle values) is written there as JSON.
 
+The tabular lifetime (2500) is never reached in 10 x K=5 updates, so the plain curve's sample() only re-checks
+"nothing changed".  The extra case (seed 0, life0=7) overrides agent 0's level lifetime to 7 on both sides (device
+level word, oracle level): its updates past step 7 are discarded (lpg_agent.py:77-80), it terminates, and sample()
+regenerates its level, agent and env state inside the curve (the override re-applied to each new level of agent 0).
+
 Small agent count (N=4) so that the float64 oracle replays a step in seconds; the per-step
 checks are size-independent.
 """
@@ -47,8 +52,8 @@ def _tr(traj, k, a):
             "done": traj.done[k, a].T.astype(bool)}
 
 
-@pytest.mark.parametrize("seed", [0, 1, 2])
-def test_meta_return_curve_certified(seed):
+@pytest.mark.parametrize("seed,life0", [(0, None), (1, None), (2, None), (0, 7)])
+def test_meta_return_curve_certified(seed, life0):
     from test_gpu_env import _state_np
     from toued import prng
     from toued.parse_args import parse_args
@@ -71,6 +76,14 @@ def test_meta_return_curve_certified(seed):
     assert np.array_equal(tr.agents.theta.cpu().numpy(), th) and np.array_equal(tr.agents.vcrit.cpu().numpy(),
                                                                                    vc.reshape(N, -1))
     assert np.array_equal(prng.to_uint32_numpy(tr.rng), rng)
+    from toued.env import L_LIFETIME
+
+    def override_life0():
+        tr.agents.levels[0, L_LIFETIME] = life0
+        lv[1][0] = life0
+    if life0:
+        override_life0()
+    resampled = 0
     curve = []
     for s in range(S):
         ag = tr.agents
@@ -168,6 +181,12 @@ def test_meta_return_curve_certified(seed):
         assert np.array_equal(tr.agents.theta.cpu().numpy(), th)
         assert np.array_equal(tr.agents.vcrit.cpu().numpy(), vc.reshape(N, -1))
         assert np.array_equal(tr.agents.step.cpu().numpy(), stp)
+        post2 = _state_np(tr.agents.state, spec)
+        for kname in ("time", "pos", "obj_existss", "early_term", "obj_poss"):
+            np.testing.assert_array_equal(post2[kname], st[kname], err_msg=kname)
+        if life0 and term[0]:
+            resampled += 1
+            override_life0()
         curve.append({"meta_step": s, "lpg_agent_return": float(ret_gpu.mean()),
                       "lpg_agent_return_oracle": float(ret_ref.mean()),
                       "lpg_agent_return_oracle_own_tables": float(ret_own.mean()),
@@ -175,7 +194,9 @@ def test_meta_return_curve_certified(seed):
                       "meta_grad_rel_l2": float(err), "relu_kinks_taken_from_device": kinks,
                       "meta_grad_rel_l2_float64_relu": float(err_nomask), "terminated": int(term.sum())})
         print(json.dumps({"seed": seed, **curve[-1]}), flush=True)
-    _CURVES[seed] = curve
+    if life0:
+        assert resampled >= 2      # lifetime 7 at 5 updates per meta-step: terminated every second step
+    _CURVES[seed if life0 is None else f"{seed}_life0_{life0}"] = curve
     out = os.environ.get("TOUED_CURVE_OUT")
     if out:
         with open(out, "w") as f:

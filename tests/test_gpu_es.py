@@ -3,10 +3,15 @@
   * OpenES ask (normal noise, antithetic reorder, sharded rows): bit-exact vs oracle/es.py
   * OpenES tell (population dot + Adam): within 1e-5 relative of the float64 oracle
   * per-candidate LPG forward (toued_gru_fwd_multi): each candidate's rows match the float64
-    oracle GRU with that candidate's parameters (same tolerance as the shared-eta forward test)
-  * one ES step with K=1 agent updates: rollouts bit-exact, each candidate's updated agent within
-    float32 tolerance of oracle/meta.py lpg_agent_step under its own LPG, fitness within 1e-5 of
-    oracle eval_agent on the device's trained actor, pair ranks / winners consistent
+    oracle GRU with that candidate's parameters within 5e-6 absolute (the shared-eta forward's bound)
+  * one ES step with K=1 agent update: each candidate's updated agent (on the device's trajectory) within
+    float32 tolerance of oracle/meta.py lpg_agent_step under its own LPG, fitness within 1e-5 of oracle
+    eval_agent on the device's trained actor, pair ranks / winners consistent
+  * one ES step with K=3 agent updates (test_es_step_k3_matches_oracle): ask bit-exact, every candidate's
+    K rollouts regenerated bit-exactly by oracle/rollout.py from the oracle's own key chain
+    (meta/train.py:160-200, lpg_agent.py:107) and the device's theta_k, the K chained float64 agent updates
+    within 2e-5, the agent metrics within 2e-5, fitness within 1e-5, and the in-step rank -> tell -> mean
+    within 1e-5 of oracle/es.tell (meta/train.py:203-217)
 """
 import numpy as np
 import pytest
@@ -18,6 +23,7 @@ from oracle import jaxrand as jr
 from oracle import levels as olv
 from oracle import lpg as olpg
 from oracle import meta as ometa
+from oracle import rollout as oro
 
 pytestmark = pytest.mark.gpu
 
@@ -100,13 +106,14 @@ def test_gru_fwd_multi_per_candidate():
         hs = torch.relu(torch.stack(outs, 1))
         pi_ref = (hs @ P["pi_w"] + P["pi_b"])[..., 0]
         y_ref = torch.softmax(hs @ P["y_w"] + P["y_b"], -1)
-        np.testing.assert_allclose(pi_hat[:, c * W:(c + 1) * W].cpu().numpy().T, pi_ref.numpy(), atol=1e-4,
-                                   rtol=1e-4)
+        np.testing.assert_allclose(pi_hat[:, c * W:(c + 1) * W].cpu().numpy().T, pi_ref.numpy(), atol=5e-6, rtol=0)
         np.testing.assert_allclose(y_hat[:, :, c * W:(c + 1) * W].cpu().numpy().transpose(2, 0, 1), y_ref.numpy(),
-                                   atol=1e-5, rtol=1e-4)
+                                   atol=5e-6, rtol=0)
 
 
 def test_es_step_k1_matches_oracle():
+    """K = 1: the device's one trajectory per candidate is fed to the oracle update (the K = 3 test below also
+    regenerates the rollouts)."""
     from toued import prng
     from toued.es import ESTrainStep
     from toued.level_sampler import LevelSampler
@@ -167,3 +174,121 @@ def test_es_step_k1_matches_oracle():
     winners = np.where(fg, np.arange(N) * 2, np.arange(N) * 2 + 1)
     assert np.array_equal(agents.theta.cpu().numpy(), theta_dev[winners])
     assert float(m["fitness"]["max"]) == pytest.approx(float(f.max()))
+
+
+def certify_es_step(args, smp, step, rng, pre, metrics, p_lv):
+    """Every stage of one lpg_es_train_step (meta/train.py:133-227) against the oracle, from the device state
+    before it (pre: es mean/m/v/n/lrate/sigma, the agents' theta/phi/step/env state/packed levels; p_lv: the
+    oracle's EnvParams of those levels, checked against the packed ones) and the
+    step's trace (ESTrainStep.trace): ask bit-exact; every candidate's K rollouts regenerated bit-exactly from
+    the oracle's own key chain (:160-200, lpg_agent.py:107) and the device's theta_k; the K chained float64 agent
+    updates under each candidate's LPG and the agent metrics within 2e-5; fitness = eval_agent within 1e-5;
+    winners; the rank -> tell -> mean within 1e-5 of oracle/es.tell.  Returns (fitness, oracle fitness)."""
+    from test_gpu_env import _state_np
+    from oracle.levels import L_LIFETIME
+    mode = args.env_mode
+    N, C, W, T, K = step.N, step.C, step.W, step.T, step.K
+    assert len(step.trace) == K
+    x = step.x.cpu().numpy()
+    lev = pre["levels"]
+    r1, sub = jr.split(rng, 2)
+    np.testing.assert_array_equal(x, oes.ask(sub, pre["mean"], np.float32(pre["sigma"]), C))
+    _, sub2 = jr.split(r1, 2)
+    ck2 = jr.split(jr.split(sub2, C), 2)
+    fit_keys, tk = ck2[:, 0], ck2[:, 1]
+    spec = olv.env_spec(mode)
+    p2 = {kk: np.repeat(v, 2, axis=0) for kk, v in p_lv.items()}
+    st_rep = torch.from_numpy(pre["state"]).view(12, N, W).repeat_interleave(2, dim=1).reshape(12, C * W)
+    ost = _state_np(st_rep, spec)
+    trajs = []
+    for k in range(K):
+        s2 = jr.split(tk, 2)
+        tk, rk = s2[:, 0], s2[:, 1]
+        th_k = step.trace[k]["theta"].cpu().numpy()
+        otr, ost, _ = oro.batch_rollout(spec, rk, th_k, p2, ost, T)
+        tr = step.trace[k]["traj"]
+        for name, got in (("idx", tr.obs_idx), ("time", tr.obs_time), ("action", tr.action), ("reward", tr.reward),
+                          ("done", tr.done)):
+            g = got.cpu().numpy()
+            np.testing.assert_array_equal(g, otr[name].transpose(0, 2, 1).astype(g.dtype), err_msg=f"rollout {k} {name}")
+        trajs.append({"idx": otr["idx"], "time": otr["time"], "action": otr["action"].astype(np.int64),
+                      "reward": otr["reward"], "done": otr["done"].astype(bool)})
+    hyp = ometa.Hypers(lifetime_conditioning=step.F == 7)
+    th_dev, ph_dev = step.theta[K % 2].cpu().numpy(), step.phi[K % 2].cpu().numpy()
+    steps_ref = []
+    for c in range(C):
+        a = c // 2
+        eta_c = torch.tensor(x[c], dtype=torch.float64)
+        th = torch.tensor(pre["theta"][a], dtype=torch.float64, requires_grad=True)
+        ph = torch.tensor(pre["phi"][a], dtype=torch.float64, requires_grad=True)
+        s = int(pre["step"][a])
+        mets = []
+        for k in range(K):
+            tr_c = {kk: v[c] for kk, v in trajs[k].items()}
+            th, ph, s, mk, _ = ometa.lpg_agent_step(th, ph, s, int(lev[a, L_LIFETIME]), eta_c, tr_c, hyp)
+            th, ph = th.detach().requires_grad_(), ph.detach().requires_grad_()
+            pe = ometa.entropy(torch.softmax(ometa.linear_logits(th, tr_c["idx"][:, :-1], tr_c["time"][:, :-1]), -1))
+            ce = ometa.entropy(torch.softmax(ometa.linear_logits(ph, tr_c["idx"][:, :-1], tr_c["time"][:, :-1]), -1))
+            mets.append({**{kk: float(v) for kk, v in mk.items()}, "policy_entropy": float(pe),
+                         "critic_entropy": float(ce)})
+        steps_ref.append(s)
+        np.testing.assert_allclose(th_dev[c], th.detach().numpy(), rtol=2e-5, atol=2e-5, err_msg=f"theta {c}")
+        np.testing.assert_allclose(ph_dev[c], ph.detach().numpy(), rtol=2e-5, atol=2e-5, err_msg=f"phi {c}")
+        for key in ("critic_loss", "policy_l2", "critic_l2", "policy_entropy", "critic_entropy"):
+            ref = np.mean([mm[key] for mm in mets])
+            np.testing.assert_allclose(float(metrics["lpg_agent"][key][c]), ref, rtol=2e-5, atol=1e-7, err_msg=key)
+    fit_ref = oag.eval_agent(spec, fit_keys, p2, th_dev, W, step.sampler.max_rollout_len)
+    f = step.fitness.cpu().numpy()
+    np.testing.assert_allclose(f, fit_ref, atol=1e-5)
+    rank, fg = oes.pair_rank(f)
+    winners = np.where(fg, np.arange(N) * 2, np.arange(N) * 2 + 1)
+    assert float(metrics["fitness"]["mean"]) == pytest.approx(float(f.mean()), rel=1e-6, abs=1e-9)
+    st = {"mean": pre["mean"].astype(np.float64), "m": pre["m"].astype(np.float64), "v": pre["v"].astype(np.float64),
+          "n": pre["n"], "lrate": pre["lrate"], "sigma": pre["sigma"], "lrate_decay": args.es_lrate_decay,
+          "lrate_limit": args.es_lrate_limit, "sigma_decay": args.es_sigma_decay, "sigma_limit": args.es_sigma_limit}
+    st = oes.tell(x, rank, st, args.lpg_opt.lower())
+    got = step.es.mean.cpu().numpy()
+    np.testing.assert_allclose(got, st["mean"], rtol=1e-5, atol=1e-7 * max(1.0, np.abs(st["mean"]).max()))
+    assert float(step.es.sigma) == pytest.approx(st["sigma"], abs=1e-7)
+    return f, fit_ref, winners, np.array(steps_ref)[winners], th_dev[winners], ph_dev[winners], ost
+
+
+def es_pre(step, agents):
+    es = step.es
+    return {"mean": es.mean.cpu().numpy(), "m": es.m.cpu().numpy(), "v": es.v.cpu().numpy(), "n": es.n,
+            "lrate": float(es.lrate), "sigma": float(es.sigma), "theta": agents.theta.cpu().numpy(),
+            "phi": agents.phi.cpu().numpy(), "step": agents.step.cpu().numpy(), "state": agents.state.cpu().numpy(),
+            "levels": agents.levels.cpu().numpy()}
+
+
+def test_es_step_k3_matches_oracle():
+    """lpg_es_train_step (meta/train.py:133-227) with K = 3 agent updates per candidate at N = 2 (4 candidates),
+    all_vrandlife with lifetime conditioning, every stage against the oracle from the oracle's own key chain
+    (certify_es_step); the kept agents are the pair winners' trained tables."""
+    from toued import prng
+    from toued.es import ESTrainStep
+    from toued.level_sampler import LevelSampler
+    from toued.lpg import LPGLayout
+    from toued.parse_args import parse_args
+    mode, N, K = "all_vrandlife", 2, 3
+    args = parse_args(["--env_mode", mode, "--num_agents", str(N), "--num_mini_batches", "1", "--use_es",
+                       "--lifetime_conditioning", "--lpg_learning_rate", "0.01"])
+    smp = LevelSampler(args)
+    buf = smp.initialize_buffer(prng.PRNGKey(0, "cuda"))
+    _, agents = smp.initial_sample(prng.PRNGKey(1, "cuda"), buf, N, False)
+    agents.theta.mul_(20.0)
+    agents.phi.mul_(20.0)
+    step = ESTrainStep(args, smp, N, torch.zeros(LPGLayout(7).size, device="cuda"), "cuda", None,
+                       num_agent_updates=K)
+    step.es.mean.copy_(torch.from_numpy(np.random.RandomState(5).randn(step.es.nd).astype(np.float32) * 0.05))
+    pre = es_pre(step, agents)
+    spec = olv.env_spec(mode)
+    p_lv, lt = olv.reset_env_params(jr.split(jr.split(jr.PRNGKey(1), 2)[1], N), mode)
+    assert np.array_equal(olv.pack_levels(p_lv, lt, spec), pre["levels"])
+    step.trace = []
+    rng = jr.PRNGKey(11)
+    m = step(dk(rng), agents)
+    torch.cuda.synchronize()
+    _, _, winners, steps_w, th_w, ph_w, _ = certify_es_step(args, smp, step, rng, pre, m, p_lv)
+    assert np.array_equal(agents.theta.cpu().numpy(), th_w) and np.array_equal(agents.phi.cpu().numpy(), ph_w)
+    assert np.array_equal(agents.step.cpu().numpy(), steps_w)

@@ -139,6 +139,40 @@ def test_a2c_graph_replay_matches_eager_and_lifetime_discard():
     torch.testing.assert_close(vc_g, vc_e, rtol=1e-5, atol=1e-6)
 
 
+def test_a2c_c1_tabular_n8_matches_oracle():
+    """BASELINE config C1: the A2C-only inner loop (train_a2c_agent, agents/a2c.py:79-125) on env_mode=tabular
+    (the defined manual dispatch over the five LPG tabular levels, D = 5409 padded) with num_agents = 8 and the
+    mode's agent hyperparameters (configs.py:322-325 via get_agent_hypers).  Five updates, every update's
+    rollout bit-exact from the oracle's own key chain (a2c.py:97) and the carried env state, every parameter
+    change within 2e-5 of float64 autograd (oracle/a2c.py); the step counters and lifetime discard likewise."""
+    from toued.a2c import A2CHyperparams, A2CTrainer
+    from toued.env import get_agent_hypers
+    mode, N, W, T, U = "tabular", 8, 64, 20, 5
+    ro, levels, p, lt, theta, vcrit, state, D = _a2c_setup(mode, N, W, T, seed=21)
+    spec = olv.env_spec(mode)
+    assert D == spec.obs_dim and D > 5000
+    ah = get_agent_hypers(mode)
+    st0 = state.cpu().numpy()
+    rng = jr.split(jr.PRNGKey(23), N)
+    inputs = (theta.clone(), vcrit.clone(), state.clone())
+    tr = A2CTrainer(ro, A2CHyperparams(), _ahyp(mode))
+    tr.record = []
+    step = torch.zeros(N, dtype=torch.int32, device="cuda")
+    tr.train(dk(rng), theta, vcrit, step, levels, state, U)
+    assert len(tr.record) == U
+    # the production path (graph-replayed update chain) gives the recorded eager chain's tables bit for bit
+    th_g, vc_g, st_g = inputs
+    step_g = torch.zeros(N, dtype=torch.int32, device="cuda")
+    A2CTrainer(ro, A2CHyperparams(), _ahyp(mode)).train(dk(rng), th_g, vc_g, step_g, levels, st_g, U)
+    assert torch.equal(th_g, theta) and torch.equal(vc_g, vcrit) and torch.equal(st_g, state)
+    assert step.cpu().tolist() == step_g.cpu().tolist()
+    ost = _a2c_follow(spec, p, lt, tr.record, rng, _ost(st0, spec.max_n_objs),
+                      lrs=(ah["actor_learning_rate"], ah["critic_learning_rate"], ah["max_grad_norm"]))
+    from test_gpu_env import _assert_state
+    _assert_state(state, ost, spec)
+    assert torch.equal(theta, tr.record[-1]["theta_out"])
+
+
 @pytest.mark.parametrize("mode", ["mazes", "dense"])
 def test_regret_untrained_matches_oracle(mode):
     """max_lifetime = 0: regret = eval(fresh A2C actor) - eval(LPG actor) — checks the key
@@ -174,7 +208,7 @@ def test_regret_untrained_matches_oracle(mode):
     np.testing.assert_allclose(got, r_a2c - r_lpg, atol=1e-5, rtol=0)
 
 
-def _a2c_follow(spec, p, lt, rec, keys_tr, ost, tol=2e-5):
+def _a2c_follow(spec, p, lt, rec, keys_tr, ost, tol=2e-5, lrs=(40.0, 4.0, 0.5)):
     """Replays a recorded A2C chain (A2CTrainer.record) on the oracle: every update's rollout bit-exact from
     the device's starting tables and the oracle's own key chain (a2c.py:97 rng, _rng = split(rng)) and carried
     env state; every update's parameter change within `tol` relative L2 of the float64 autograd oracle
@@ -199,7 +233,7 @@ def _a2c_follow(spec, p, lt, rec, keys_tr, ost, tol=2e-5):
                     "reward": rew[a].T.copy(), "done": dn[a].T.astype(bool)}
             t_ref, v_ref, s_ref, _, _ = oa2c.a2c_step(
                 torch.from_numpy(th0[a].astype(np.float64)), torch.from_numpy(vc0[a][:, None].astype(np.float64)),
-                int(st0[a]), int(lt[a]), traj, hyp, 40.0, 4.0, 0.5)
+                int(st0[a]), int(lt[a]), traj, hyp, *lrs)
             assert int(st1[a]) == s_ref, (u, a)
             dt_ref, dv_ref = t_ref.numpy() - th0[a], v_ref.numpy()[:, 0] - vc0[a]
             dt, dv = th1[a].astype(np.float64) - th0[a], vc1[a].astype(np.float64) - vc0[a]

@@ -44,6 +44,9 @@ class A2CTrainer:
         # test hook: a list here makes train() run eagerly and append, after every update, the actor/critic
         # tables it started from, the rollout it ran and the tables it produced (tests/test_gpu_plr.py)
         self.record = None
+        # optional toued.meta.KernelTimers: while enabled, train() runs eagerly and times each rollout ("a2c_rollout")
+        # and update ("a2c_update") launch with HIP events on the launching stream (bench.py's C3 roofline)
+        self.timers = None
 
     def _alloc(self, n, D, W, T, U, dev):
         key = (n, D, W, T, U, str(dev))
@@ -75,12 +78,17 @@ class A2CTrainer:
         lr_a, lr_c, mn = self.ah.actor_learning_rate, self.ah.critic_learning_rate, self.ah.max_grad_norm
         fits = bool(L.lib().toued_a2c_update_fits(W, T, D))
         fused = fits if self.fused is None else (self.fused and fits)
+        tm = self.timers if self.timers is not None and self.timers.enabled else None
         for u in range(U):
             if record is not None:
                 before = (b["theta"].clone(), b["vcrit"].clone(), b["step"].clone())
+            tok = tm.start("a2c_rollout") if tm is not None else None
             L.call("toued_rollout", self.ro._c, L.ptr(b["levels"]), L.ptr(b["theta"]), D, L.ptr(b["chain"][u]),
                    L.ptr(b["state"]), n, W, T, L.ptr(tr.obs_idx), L.ptr(tr.obs_time), L.ptr(tr.action),
                    L.ptr(tr.reward), L.ptr(tr.done), None, st)
+            if tm is not None:
+                tm.stop(tok)
+                tok = tm.start("a2c_update")
             if fused:   # gradient tables in LDS, grad + clip + SGD in one kernel
                 L.call("toued_a2c_update", n, W, T, D, L.ptr(b["theta"]), L.ptr(b["vcrit"]), L.ptr(tr.obs_idx),
                        L.ptr(tr.obs_time), L.ptr(tr.action), L.ptr(tr.reward), L.ptr(tr.done), self.hyp.gamma,
@@ -93,6 +101,8 @@ class A2CTrainer:
                        st)
                 L.call("toued_a2c_apply", n, D, L.ptr(b["theta"]), L.ptr(b["vcrit"]), L.ptr(b["Ga"]), L.ptr(b["Gv"]),
                        lr_a, lr_c, mn, L.ptr(b["step"]), L.ptr(b["levels"]), st)
+            if tm is not None:
+                tm.stop(tok)
             if record is not None:
                 record.append({"theta": before[0], "vcrit": before[1], "step": before[2],
                                "traj": Transition(tr.obs_idx.clone(), tr.obs_time.clone(), tr.action.clone(), tr.reward.clone(),
@@ -113,7 +123,7 @@ class A2CTrainer:
         for name, src in (("rng", rng), ("theta", theta), ("vcrit", vcrit.reshape(n, D)), ("step", step),
                           ("levels", levels), ("state", state)):
             b[name].copy_(src)
-        if self.record is not None:
+        if self.record is not None or (self.timers is not None and self.timers.enabled):
             self._updates(b, n, D, W, T, U, self.record)
         elif self.use_graph and U > 0:
             if self._graph is None:

@@ -147,6 +147,12 @@ class ESTrainStep:
         self.pi_hat = z(T, R)
         self.y_hat = z(T, _Y, R)
         self.fitness = None
+        # test hook: a list receives, per agent update k, the candidates' (theta_k, phi_k, env state before the
+        # rollout, trajectory k) as device clones (tests/test_gpu_es.py regenerates every rollout from them)
+        self.trace = None
+        # HIP-event timing of the per-update launches (bench.py's C4 roofline); disabled by default
+        from .meta import KernelTimers
+        self.timers = KernelTimers()
 
     def _eta(self, name):
         o = self.lay.offsets[name]
@@ -186,12 +192,21 @@ class ESTrainStep:
         # ---- train_lpg_agent for K = max_lifetime updates (agents/lpg_agent.py:88-140)
         for k in range(K):
             th, ph = self.theta[cur], self.phi[cur]
+            if self.trace is not None:
+                rec = {"theta": th.clone(), "phi": ph.clone(), "state": state.clone(), "step": step.clone()}
+            tok = self.timers.start("rollout")
             self.ro.batch_rollout(chain[k], th, levels, state, out=tr, inplace_state=True)
+            self.timers.stop(tok)
+            if self.trace is not None:
+                rec["traj"] = Transition(*(x.clone() for x in tr))
+                self.trace.append(rec)
             L.call("toued_lpg_inputs", C, W, T, D, self.F, ptr(th), ptr(ph), ptr(tr.obs_idx), ptr(tr.obs_time),
                    ptr(tr.action), ptr(tr.reward), ptr(tr.done), ptr(e1w), ptr(e1b), ptr(e2w), ptr(e2b), ptr(step),
                    ptr(levels), ptr(self.X), T * R, 1, nd, st)
+            tok = self.timers.start("gru_fwd_multi")
             L.call("toued_gru_fwd_multi", R, T, W, self.F, W, ptr(self.X), T * R, 1, ptr(tr.done), ptr(self.fwdA),
                    ptr(self.x), nd, self.lay.c_offsets, ptr(self.pi_hat), ptr(self.y_hat), st)
+            self.timers.stop(tok)
             self.G_th.zero_()
             self.G_ph.zero_()
             L.call("toued_agent_grad", C, W, T, D, ptr(th), ptr(ph), ptr(tr.obs_idx), ptr(tr.obs_time),
