@@ -188,12 +188,20 @@ def test_gru_forward_matches_oracle():
 def test_gru_backward_matches_autograd(N, W, gscale, wscale):
     """LPG GRU VJP (toued_gru_bwd + the weight-gradient GEMMs over the saved m-major operands) vs float64
     torch autograd of the same GRU + heads: every GRU / head parameter gradient and the input cotangents
-    dX3, dX4 within 1e-5 relative L2 (achieved 1e-7..2e-6; one dropped fp16 piece costs ~5e-4).  R = 128 runs the lockstep split-precision kernel, R = 96 (not a
+    dX3, dX4 within 1e-5 relative L2 (achieved 1e-7..2e-6; one dropped fp16 piece costs ~5e-4).
+
+    relu kinks: the heads read relu(h_out) (models/lpg.py:81), whose derivative jumps at 0.  Where |h_out| is
+    within float32 rounding of 0 the device and float64 may take different branches; at wscale 4 or 1e-3 ONE such
+    flip in 393k elements moves the recurrent-fed gradients by 1e-3 relative (tools/gru_seed_sweep.py: 6 of 450
+    seeded inputs, each with exactly one flip at |h| <= 1.4e-6, reruns bit-identical, 2e-6 with the device's branch
+    -- this was the "intermittent" round-2 failure: the eta perturbation was unseeded then).  So the float64
+    reference takes the device's relu decisions, every differing decision must lie within 5e-6 of the kink (the
+    forward's own tolerance), and the flips are counted.  R = 128 runs the lockstep split-precision kernel, R = 96 (not a
     multiple of 64) the f32 kernel.  gscale multiplies the head cotangents (the backward's per-row fp16
     scales must follow them over 24 decades), wscale the recurrent weights W_hr, W_hz, W_hn (the per-unit
     weight scales of the forward and backward packs).  (At wscale 16 the gates saturate and the f32-MFMA kernel
     itself misses 1e-4 against float64: 1 - n^2 loses its digits in f32.)"""
-    from toued.lpg import LPGGRU, LPGLayout, init_lpg_params
+    from toued.lpg import LPGLayout, init_lpg_params
     T, K, F = 6, 2, 5
     R = N * W
     lay = LPGLayout(F)
@@ -202,24 +210,62 @@ def test_gru_backward_matches_autograd(N, W, gscale, wscale):
     eta += torch.randn_like(eta) * 0.05
     for name in ("hr_w", "hz_w", "hn_w"):
         lay.view(eta, name).mul_(wscale)
-    gru = LPGGRU(lay, R, T, K, W, "cuda")
-    gru.pack(eta)
     rs = np.random.RandomState(1)
     xs = rs.randn(F, K, T, R).astype(np.float32)
+    done = (rs.rand(K, N, T, W) < 0.15).astype(np.uint8)
+    d_pi = (rs.randn(K, T, R) * gscale).astype(np.float32)
+    d_y = (rs.randn(K, T, 8, R) * gscale).astype(np.float32)
+    errs, flips = _gru_bwd_case(N, W, T, K, F, eta, xs, done, d_pi, d_y)
+    tol = 1e-5 if R % 64 == 0 else 1e-4     # the f32-MFMA fallback (R % 64 != 0) keeps the f32 bound
+    bad = {k: v for k, v in errs.items() if not v < tol}
+    assert not bad, errs
+
+
+@pytest.mark.parametrize("seed,wscale", [(129, 4.0), (104, 1e-3)])
+def test_gru_backward_relu_kink_inputs(seed, wscale):
+    """The inputs of tools/gru_seed_sweep.py seeds that flip one relu decision (|h_out| 5.4e-7 at wscale 4,
+    5.1e-8 at wscale 1e-3; recurrent-fed gradients 2.9e-3 / 5.1e-3 off the float64 branch): with the device's
+    branch the backward is within 1e-5, and the flip sits inside the kink band."""
+    from toued.lpg import LPGLayout, init_lpg_params
+    N, W, T, K, F = 2, 64, 6, 2, 5
+    R = N * W
+    lay = LPGLayout(F)
+    eta0 = init_lpg_params(5, F)
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    eta = eta0.clone() + (torch.randn(eta0.shape, generator=g) * 0.05).cuda()
+    for name in ("hr_w", "hz_w", "hn_w"):
+        lay.view(eta, name).mul_(wscale)
+    rs = np.random.RandomState(100000 + seed)
+    xs = rs.randn(F, K, T, R).astype(np.float32)
+    done = (rs.rand(K, N, T, W) < 0.15).astype(np.uint8)
+    d_pi = rs.randn(K, T, R).astype(np.float32)
+    d_y = rs.randn(K, T, 8, R).astype(np.float32)
+    errs, flips = _gru_bwd_case(N, W, T, K, F, eta, xs, done, d_pi, d_y)
+    assert len(flips) >= 1
+    assert max(errs.values()) < 1e-5, errs
+
+
+def _gru_bwd_case(N, W, T, K, F, eta, xs, done, d_pi, d_y):
+    """forward + backward + weight gradients on the device; float64 autograd with the device's relu branches;
+    relative L2 errors per parameter and of dX3/dX4, and |h_out| of every relu decision taken from the device."""
+    from toued.lpg import LPGGRU, LPGLayout
+    R = N * W
+    lay = LPGLayout(F)
+    gru = LPGGRU(lay, R, T, K, W, "cuda")
+    gru.pack(eta)
     gru.X.copy_(torch.from_numpy(xs))
     X = gru.X
-    done = (rs.rand(K, N, T, W) < 0.15).astype(np.uint8)
     done_t = torch.from_numpy(done).cuda()
     pi_hat = torch.zeros(K, T, R, device="cuda")
     y_hat = torch.zeros(K, T, 8, R, device="cuda")
     for k in range(K):
         gru.forward(k, X, done_t[k], eta, pi_hat, y_hat)
-    d_pi = torch.from_numpy((rs.randn(K, T, R) * gscale).astype(np.float32)).cuda()
-    d_y = torch.from_numpy((rs.randn(K, T, 8, R) * gscale).astype(np.float32)).cuda()
     grad = torch.zeros(lay.size, device="cuda")
-    gru.backward(done_t, eta, y_hat, d_pi, d_y, X, grad)
+    gru.backward(done_t, eta, y_hat, torch.from_numpy(d_pi).cuda(), torch.from_numpy(d_y).cuda(), X, grad)
     torch.cuda.synchronize()
-    # float64 autograd oracle
+    # float64 autograd oracle, relu branches from the device (RH = relu(h_out) rows [256][M], column (k, t, r))
+    relu_dev = (gru.RH[:256] > 0).cpu().numpy().reshape(256, K, T, R)
+    flips = []
     flat = torch.tensor(eta.cpu().numpy(), dtype=torch.float64, requires_grad=True)
     P = olpg.unflatten(flat, F)
     x = torch.tensor(xs, dtype=torch.float64, requires_grad=True)       # [F, K, T, R]
@@ -237,11 +283,15 @@ def test_gru_backward_matches_autograd(N, W, gscale, wscale):
             ng = torch.tanh(xt @ P["in_w"] + P["in_b"] + rg * (h @ P["hn_w"] + P["hn_b"]))
             h = (1 - zg) * ng + zg * h
             outs[t] = h
-        hs = torch.relu(torch.stack(outs, 1))                              # [R, T, 256]
+        hst = torch.stack(outs, 1)                                         # [R, T, 256]
+        mk = torch.from_numpy(relu_dev[:, k].transpose(2, 1, 0).copy())    # [R, T, 256]
+        hv = hst.detach().numpy()
+        flips.extend(np.abs(hv[mk.numpy() != (hv > 0)]).tolist())
+        hs = torch.where(mk, hst, torch.zeros_like(hst))
         pi_ref = (hs @ P["pi_w"] + P["pi_b"])[..., 0]                      # [R, T]
         y_ref = torch.softmax(hs @ P["y_w"] + P["y_b"], -1)                # [R, T, 8]
-        dpi = torch.tensor(d_pi[k].cpu().numpy().T, dtype=torch.float64)
-        dy = torch.tensor(d_y[k].cpu().numpy().transpose(2, 0, 1), dtype=torch.float64)
+        dpi = torch.tensor(d_pi[k].T, dtype=torch.float64)
+        dy = torch.tensor(d_y[k].transpose(2, 0, 1), dtype=torch.float64)
         loss = loss + (pi_ref * dpi).sum() + (y_ref * dy).sum()
     loss.backward()
     g_ref = flat.grad.numpy()
@@ -256,10 +306,10 @@ def test_gru_backward_matches_autograd(N, W, gscale, wscale):
     for f, dX in ((3, gru.dX3), (4, gru.dX4)):
         got = dX.cpu().numpy()
         errs[f"dX{f}"] = np.linalg.norm(got - gx[f]) / np.linalg.norm(gx[f])
-    print("gru backward relative L2 errors:", {k: f"{v:.2e}" for k, v in errs.items()})
-    tol = 1e-5 if R % 64 == 0 else 1e-4     # the f32-MFMA fallback (R % 64 != 0) keeps the f32 bound
-    bad = {k: v for k, v in errs.items() if not v < tol}
-    assert not bad, errs
+    print("gru backward relative L2 errors:", {k: f"{v:.2e}" for k, v in errs.items()},
+          f"relu decisions taken from the device: {len(flips)} (max |h_out| {max(flips, default=0.0):.1e})")
+    assert all(f < 5e-6 for f in flips), flips
+    return errs, flips
 
 
 def test_gru_backward_repeat_bit_identical():

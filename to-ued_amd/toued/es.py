@@ -198,7 +198,8 @@ class ESTrainStep:
             self.ro.batch_rollout(chain[k], th, levels, state, out=tr, inplace_state=True)
             self.timers.stop(tok)
             if self.trace is not None:
-                rec["traj"] = Transition(*(x.clone() for x in tr))
+                rec["traj"] = Transition(tr.obs_idx.clone(), tr.obs_time.clone(), tr.action.clone(), tr.reward.clone(),
+                                         tr.done.clone())
                 self.trace.append(rec)
             L.call("toued_lpg_inputs", C, W, T, D, self.F, ptr(th), ptr(ph), ptr(tr.obs_idx), ptr(tr.obs_time),
                    ptr(tr.action), ptr(tr.reward), ptr(tr.done), ptr(e1w), ptr(e1b), ptr(e2w), ptr(e2b), ptr(step),

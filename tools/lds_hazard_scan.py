@@ -2,7 +2,13 @@
 DESIGN.md section 7: a VALU instruction that overwrites a VGPR a preceding ds_write / buffer_store still reads as data
 within `--window` instructions, and an s_barrier not preceded by `s_waitcnt lgkmcnt(0)` since the last LDS access.
 
-    python tools/lds_hazard_scan.py to-ued_amd/csrc/gru.hip k_gru_bwd6n [--window 4]
+    python tools/lds_hazard_scan.py to-ued_amd/csrc/gru.hip k_gru_bwd6n [--window 4] [--wide]
+
+--wide restricts the store check to stores with a data operand of more than 8 bytes (ds_write_b96/b128,
+buffer/global_store_dwordx3/x4; ds_write2_b64 reads two 8-byte operands) -- the stores whose data VGPRs a VALU write may not follow without wait states
+(the gfx950 16-byte buffer-store loss in DESIGN.md section 7) -- and flags every VALU write to those VGPRs in the
+next --window instructions (hipcc overwrites the data VGPRs of dword and b64 stores 1-3 instructions later as a
+matter of course, which the hardware tolerates).
 """
 import argparse
 import re
@@ -26,6 +32,7 @@ def main():
     ap.add_argument("src")
     ap.add_argument("kernel")
     ap.add_argument("--window", type=int, default=4)
+    ap.add_argument("--wide", action="store_true", help="only stores of more than 8 bytes of data")
     a = ap.parse_args()
     src = Path(a.src)
     out = Path("/tmp") / (src.stem + "_scan.s")
@@ -52,6 +59,9 @@ def main():
                 print(f"{name[:60]}: #{n} s_barrier with LDS accesses not waited for")
                 bad += 1
             if op.startswith(("ds_write", "buffer_store", "global_store")):
+                wide = op.endswith(("b96", "b128", "dwordx3", "dwordx4"))
+                if a.wide and not wide:
+                    continue
                 ops = [x.strip() for x in t[len(op):].split(",")]
                 data = set()
                 for x in (ops[1:] if op.startswith("ds_write") else ops[:1]):
