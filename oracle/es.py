@@ -10,7 +10,8 @@ PRNG known-answer vectors):
               grad = 1/(P sigma) * noise^T fitness'; optimiser step; lrate = max(lrate*decay, limit);
               sigma = max(sigma*decay, limit)
   Adam:       m = (1-b1) g + b1 m; v = (1-b2) g^2 + b2 v; mhat = m/(1-b1^(n+1)); vhat = v/(1-b2^(n+1));
-              mean -= lrate * mhat / (sqrt(vhat) + eps); b1 = .99, b2 = .999, eps = 1e-8
+              mean -= lrate * mhat / (sqrt(vhat) + eps); b1 = .99, b2 = .999, eps = 1e-8 as float32 values (the
+              OptParams leaves are traced as f32 arrays: 1 - b2 = 0.00099998713, not 0.001)
 meta/train.py:152-158 reorders the population so candidates 2i and 2i+1 are z_i and -z_i;
 meta/train.py:199-206 rank per antithetic pair.
 """
@@ -42,15 +43,26 @@ def pair_rank(fitness):
 def tell(x, rank_fitness, state: dict, opt="adam"):
     """state: mean, sigma, m, v, n, lrate, lrate_decay, lrate_limit, sigma_decay, sigma_limit.
     Returns the new state (float64 accumulation of the population dot)."""
+    return opt_step(grad(x, rank_fitness, state), state, opt)
+
+
+def grad(x, rank_fitness, state):
+    """the OpenES gradient 1/(P sigma) noise^T (-rank fitness) (maximize), float64"""
     P = x.shape[0]
     mean = state["mean"].astype(np.float64)
     sigma = float(state["sigma"])
     fit = -np.asarray(rank_fitness, np.float64)
     noise = (x.astype(np.float64) - mean) / sigma
-    g = (1.0 / (P * sigma)) * (noise.T @ fit)
+    return (1.0 / (P * sigma)) * (noise.T @ fit)
+
+
+def opt_step(g, state: dict, opt="adam"):
+    """the optimiser step on the mean and the lrate / sigma decay, given the gradient g"""
+    mean = state["mean"].astype(np.float64)
     s = dict(state)
     if opt == "adam":
-        b1, b2, eps = 0.99, 0.999, 1e-8
+        # evosax's OptParams (beta_1 .99, beta_2 .999, eps 1e-8) reach the jitted tell as float32 leaves
+        b1, b2, eps = float(np.float32(0.99)), float(np.float32(0.999)), float(np.float32(1e-8))
         m = (1 - b1) * g + b1 * state["m"]
         v = (1 - b2) * g * g + b2 * state["v"]
         mhat = m / (1 - b1 ** (state["n"] + 1))

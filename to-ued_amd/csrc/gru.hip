@@ -603,6 +603,19 @@ TOUED_DEV floatx16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx16 c)
   return c;
 }
 
+#ifdef FWD_STAMPS
+// timing instrumentation (tools/fwd_stamps.py, built by tools/build_variant.py gru.hip FWD_STAMPS=1): thread 0 of
+// workgroups < 64 records s_memtime at 6 points of every step of the SAVE instance
+__device__ unsigned long long g_fwd_stamps[64 * 32 * 6];
+#define FWD_STAMP(ph)                                                                                  \
+  do {                                                                                                 \
+    if (SAVE && blockIdx.x < 64 && tid == 0 && s < 32)                                                 \
+      g_fwd_stamps[(blockIdx.x * 32 + s) * 6 + (ph)] = __builtin_amdgcn_s_memtime();                   \
+  } while (0)
+#else
+#define FWD_STAMP(ph) do {} while (0)
+#endif
+
 template <bool SAVE>
 __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   // carry image [row][unit]: slots 0, 1 the fp16 pieces of 2^14 h (MFMA B operand), slot 2 the bf16 residual
@@ -662,6 +675,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
                                rs_hn = rsrc_of(p.s_hn);
   for (int s = 0; s < T; ++s) {
     const int t = T - 1 - s;
+    FWD_STAMP(0);
     floatx16 acc[3][2];   // r, z, W_hn h + b_hn (the n gate's input part is gate_ain, on the VALU)
 #pragma unroll
     for (int g = 0; g < 3; ++g)
@@ -748,7 +762,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) acc[g][h] = mfma6(Aa[g], Ba[h], acc[g][h]);
     }
+    FWD_STAMP(1);
     lds_barrier();   // every wave done reading hB / xB: the carry and x(t-1) overwrite them in place
+    FWD_STAMP(2);
     // ---- gate maths (lane = row 32h + col, register q = unit 32 wave + 4 hi + qunit(q))
     floatx16 ain[2];
     // done flags d_{t-1} of the lane's two rows, issued before the saves so their wait drains nothing else
@@ -828,7 +844,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
         if (hi == 0) hp[(wave * 9 + oo) * 64 + row] = hp_loc[oo] + o;
       }
     }
+    FWD_STAMP(3);
     lds_barrier();   // head partials, the carry and x(t-1) visible
+    FWD_STAMP(4);
     for (int i = 64 * wave + lane_now(); i < 9 * 64; i += 512) {
       const int oo = i >> 6, c = i & 63;
       float v = oo == 0 ? bpi : eta[p.o.y_b + oo - 1];
@@ -848,6 +866,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
       const float inv = 1.0f / ssum;
       for (int j = 0; j < 8; ++j) p.y_hat[((long)t * 8 + j) * R + r0 + tl] = e[j] * inv;
     }
+    FWD_STAMP(5);
   }
 }
 
@@ -1612,6 +1631,12 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
   TOUED_CHECK_LAUNCH();
   return 0;
 }
+
+#ifdef FWD_STAMPS
+int toued_dbg_fwd_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd_stamps), sizeof(g_fwd_stamps)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 #ifdef BWD_STAMPS
 int toued_dbg_bwd_stamps(unsigned long long* host) {

@@ -1,0 +1,53 @@
+"""Per-phase timing of k_gru_fwd6<true> from in-kernel s_memtime stamps (a FWD_STAMPS=1 variant library):
+
+    python tools/build_variant.py gru.hip FWD_STAMPS=1
+    TOUED_LIB=to-ued_amd/exp/libtoued_FWD_STAMPS_1.so python tools/fwd_stamps.py
+
+Runs the C2-shape forward (512 agents x 64 workers, T = 20) and prints, for the first 64 workgroups, the mean
+shader-clock cycles of each phase of a step: contraction issue (16 fp16 carry k-steps + the augmented k-step),
+the barrier behind it (MFMA drain + wave skew), gate maths + saves + head partials, the head barrier, the head
+reduction + softmax tail; and the whole step."""
+import ctypes
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "to-ued_amd"))
+import torch  # noqa: E402
+
+
+def main():
+    from toued import _lib
+    from toued.lpg import LPGGRU, LPGLayout, init_lpg_params
+    N, W, T, K, F = 512, 64, 20, 1, 5
+    R = N * W
+    lay = LPGLayout(F)
+    eta = init_lpg_params(0, F)
+    gru = LPGGRU(lay, R, T, K, W, "cuda")
+    gru.pack(eta)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    gru.X.copy_(torch.randn(gru.X.shape, generator=g, device="cuda"))
+    done = (torch.rand((K, N, T, W), generator=g, device="cuda") < 0.05).to(torch.uint8)
+    pi_hat = torch.zeros(K, T, R, device="cuda")
+    y_hat = torch.zeros(K, T, 8, R, device="cuda")
+    for _ in range(3):
+        gru.forward(0, gru.X, done[0], eta, pi_hat, y_hat)
+    torch.cuda.synchronize()
+    buf = np.zeros(64 * 32 * 6, np.uint64)
+    fn = _lib.lib().toued_dbg_fwd_stamps
+    fn.argtypes = [ctypes.c_void_p]
+    assert fn(buf.ctypes.data) == 0
+    st = buf.reshape(64, 32, 6)[:, :T].astype(np.int64)
+    ph = np.diff(st, axis=2)
+    names = ["contraction issue", "barrier (MFMA drain)", "gate maths + saves + head partials", "head barrier",
+             "head reduce + softmax"]
+    res = {n: float(ph[:, :, i].mean()) for i, n in enumerate(names)}
+    res["step total"] = float((st[:, 1:, 0] - st[:, :-1, 0]).mean())
+    print(json.dumps({k: round(v) for k, v in res.items()}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -59,6 +59,12 @@ def main():
         w = csv.DictWriter(f, fieldnames=list(rows[0]))
         w.writeheader()
         w.writerows(rows)
+    if (src / "ks_wl" / "run_results.db").exists():      # the C3 / C4 workloads' kernel trace (bench.py --workloads)
+        wl = kernel_stats(src / "ks_wl" / "run_results.db")
+        with open(dst / "kernel_stats_workloads.csv", "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=list(wl[0]))
+            w.writeheader()
+            w.writerows(wl)
     cf = pmc(src / "calib_fetch" / "run_results.db", "FETCH_SIZE")
     cw = pmc(src / "calib_write" / "run_results.db", "WRITE_SIZE")
     # factor = true bytes / (counter kB * 1024)

@@ -13,13 +13,16 @@ export TMPDIR=/tmp
 hipcc -O3 --offload-arch=gfx950 "$R/tools/calib_fetch.hip" -o /tmp/calib_fetch 2>/dev/null
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv rocpd -d "$OUT/ks" -o run -- python3 "$R/bench.py" --steps 3 --warmup 2 \
-    --no_cpu_baseline > "$OUT/ks.log" 2>&1
+    --no_cpu_baseline --workloads none > "$OUT/ks.log" 2>&1
 echo "kernel-trace done"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv rocpd -d "$OUT/ks_wl" -o run -- python3 "$R/bench.py" --steps 2 \
+    --warmup 1 --no_cpu_baseline --workloads c3,c4 > "$OUT/ks_wl.log" 2>&1
+echo "workloads kernel-trace done"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run -- python3 "$R/bench.py" \
-    --steps 1 --warmup 1 --no_cpu_baseline > "$OUT/pmc_fetch.log" 2>&1
+    --steps 1 --warmup 1 --no_cpu_baseline --workloads none > "$OUT/pmc_fetch.log" 2>&1
 echo "fetch pass done"
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run -- python3 "$R/bench.py" \
-    --steps 1 --warmup 1 --no_cpu_baseline > "$OUT/pmc_write.log" 2>&1
+    --steps 1 --warmup 1 --no_cpu_baseline --workloads none > "$OUT/pmc_write.log" 2>&1
 echo "write pass done"
 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/calib_fetch" -o run -- /tmp/calib_fetch \
     > "$OUT/calib_fetch.log" 2>&1
