@@ -65,8 +65,13 @@ def opt_step(g, state: dict, opt="adam"):
         b1, b2, eps = float(np.float32(0.99)), float(np.float32(0.999)), float(np.float32(1e-8))
         m = (1 - b1) * g + b1 * state["m"]
         v = (1 - b2) * g * g + b2 * state["v"]
-        mhat = m / (1 - b1 ** (state["n"] + 1))
-        vhat = v / (1 - b2 ** (state["n"] + 1))
+        # the bias corrections as evosax's jitted f32 computes them: 1 - b2^(n+1) cancels (0.005 at n = 4), so its
+        # float32 rounding (~1e-5 relative) shows in every update
+        n1 = np.float32(state["n"] + 1)
+        bc1 = float(np.float32(1.0) - np.float32(b1) ** n1)
+        bc2 = float(np.float32(1.0) - np.float32(b2) ** n1)
+        mhat = m / bc1
+        vhat = v / bc2
         s["mean"] = mean - state["lrate"] * mhat / (np.sqrt(vhat) + eps)
         s["m"], s["v"] = m, v
     else:

@@ -9,8 +9,8 @@
     eval_agent on the device's trained actor, pair ranks / winners consistent
   * one ES step with K=3 agent updates (test_es_step_k3_matches_oracle): ask bit-exact, every candidate's
     K rollouts regenerated bit-exactly by oracle/rollout.py from the oracle's own key chain
-    (meta/train.py:160-200, lpg_agent.py:107) and the device's theta_k, the K chained float64 agent updates
-    within 2e-5, the agent metrics within 2e-5, fitness within 1e-5, and the in-step rank -> tell: the
+    (meta/train.py:160-200, lpg_agent.py:107) and the device's theta_k, each agent update and the K chained
+    float64 agent updates within 2e-5, the agent metrics within 2e-5, fitness within 1e-5, and the in-step rank -> tell: the
     population gradient within 1e-6 relative L2, the Adam step on it within f32 rounding (meta/train.py:203-217)
 """
 import numpy as np
@@ -176,13 +176,14 @@ def test_es_step_k1_matches_oracle():
     assert float(m["fitness"]["max"]) == pytest.approx(float(f.max()))
 
 
-def certify_es_step(args, smp, step, rng, pre, metrics, p_lv):
+def certify_es_step(args, smp, step, rng, pre, metrics, p_lv, chained=False):
     """Every stage of one lpg_es_train_step (meta/train.py:133-227) against the oracle, from the device state
     before it (pre: es mean/m/v/n/lrate/sigma, the agents' theta/phi/step/env state/packed levels; p_lv: the
     oracle's EnvParams of those levels, checked against the packed ones) and the
     step's trace (ESTrainStep.trace): ask bit-exact; every candidate's K rollouts regenerated bit-exactly from
-    the oracle's own key chain (:160-200, lpg_agent.py:107) and the device's theta_k; the K chained float64 agent
-    updates under each candidate's LPG and the agent metrics within 2e-5; fitness = eval_agent within 1e-5;
+    the oracle's own key chain (:160-200, lpg_agent.py:107) and the device's theta_k; each of the K agent updates
+    (from the device's tables before it) within 2e-5 relative L2 of the float64 update under the candidate's LPG,
+    and the agent metrics within 2e-5; fitness = eval_agent within 1e-5;
     winners; the rank -> tell -> mean within 1e-5 of oracle/es.tell.  Returns (fitness, oracle fitness)."""
     from test_gpu_env import _state_np
     from oracle.levels import L_LIFETIME
@@ -215,25 +216,45 @@ def certify_es_step(args, smp, step, rng, pre, metrics, p_lv):
                       "reward": otr["reward"], "done": otr["done"].astype(bool)})
     hyp = ometa.Hypers(lifetime_conditioning=step.F == 7)
     th_dev, ph_dev = step.theta[K % 2].cpu().numpy(), step.phi[K % 2].cpu().numpy()
+    # every update from the device's tables before it (trace): the parameter change within 2e-5 relative L2 of the
+    # float64 update under the candidate's LPG (per update, as _a2c_follow: chained over K updates at the actor
+    # lr 40 the float32 rounding of one update is amplified into the next one's inputs)
+    th_k = [r["theta"].cpu().numpy() for r in step.trace] + [th_dev]
+    ph_k = [r["phi"].cpu().numpy() for r in step.trace] + [ph_dev]
+    st_k = [r["step"].cpu().numpy() for r in step.trace]
     steps_ref = []
     for c in range(C):
         a = c // 2
         eta_c = torch.tensor(x[c], dtype=torch.float64)
-        th = torch.tensor(pre["theta"][a], dtype=torch.float64, requires_grad=True)
-        ph = torch.tensor(pre["phi"][a], dtype=torch.float64, requires_grad=True)
         s = int(pre["step"][a])
         mets = []
         for k in range(K):
+            assert int(st_k[k][c]) == s, (c, k)
             tr_c = {kk: v[c] for kk, v in trajs[k].items()}
-            th, ph, s, mk, _ = ometa.lpg_agent_step(th, ph, s, int(lev[a, L_LIFETIME]), eta_c, tr_c, hyp)
-            th, ph = th.detach().requires_grad_(), ph.detach().requires_grad_()
-            pe = ometa.entropy(torch.softmax(ometa.linear_logits(th, tr_c["idx"][:, :-1], tr_c["time"][:, :-1]), -1))
-            ce = ometa.entropy(torch.softmax(ometa.linear_logits(ph, tr_c["idx"][:, :-1], tr_c["time"][:, :-1]), -1))
+            th = torch.tensor(th_k[k][c], dtype=torch.float64, requires_grad=True)
+            ph = torch.tensor(ph_k[k][c], dtype=torch.float64, requires_grad=True)
+            th1, ph1, s, mk, _ = ometa.lpg_agent_step(th, ph, s, int(lev[a, L_LIFETIME]), eta_c, tr_c, hyp)
+            for got0, got1, ref1, nm in ((th_k[k][c], th_k[k + 1][c], th1, "theta"), (ph_k[k][c], ph_k[k + 1][c], ph1, "phi")):
+                d_ref = ref1.detach().numpy() - got0
+                d_dev = got1.astype(np.float64) - got0
+                assert np.linalg.norm(d_dev - d_ref) <= 2e-5 * np.linalg.norm(d_ref) + 1e-7, (nm, c, k)
+            t1 = torch.tensor(th_k[k + 1][c], dtype=torch.float64)
+            p1 = torch.tensor(ph_k[k + 1][c], dtype=torch.float64)
+            pe = ometa.entropy(torch.softmax(ometa.linear_logits(t1, tr_c["idx"][:, :-1], tr_c["time"][:, :-1]), -1))
+            ce = ometa.entropy(torch.softmax(ometa.linear_logits(p1, tr_c["idx"][:, :-1], tr_c["time"][:, :-1]), -1))
             mets.append({**{kk: float(v) for kk, v in mk.items()}, "policy_entropy": float(pe),
                          "critic_entropy": float(ce)})
         steps_ref.append(s)
-        np.testing.assert_allclose(th_dev[c], th.detach().numpy(), rtol=2e-5, atol=2e-5, err_msg=f"theta {c}")
-        np.testing.assert_allclose(ph_dev[c], ph.detach().numpy(), rtol=2e-5, atol=2e-5, err_msg=f"phi {c}")
+        if chained:   # and the K updates chained in float64 from the tables before the step, within 2e-5
+            th = torch.tensor(pre["theta"][a], dtype=torch.float64, requires_grad=True)
+            ph = torch.tensor(pre["phi"][a], dtype=torch.float64, requires_grad=True)
+            s2 = int(pre["step"][a])
+            for k in range(K):
+                tr_c = {kk: v[c] for kk, v in trajs[k].items()}
+                th, ph, s2, _, _ = ometa.lpg_agent_step(th, ph, s2, int(lev[a, L_LIFETIME]), eta_c, tr_c, hyp)
+                th, ph = th.detach().requires_grad_(), ph.detach().requires_grad_()
+            np.testing.assert_allclose(th_dev[c], th.detach().numpy(), rtol=2e-5, atol=2e-5, err_msg=f"theta {c}")
+            np.testing.assert_allclose(ph_dev[c], ph.detach().numpy(), rtol=2e-5, atol=2e-5, err_msg=f"phi {c}")
         for key in ("critic_loss", "policy_l2", "critic_l2", "policy_entropy", "critic_entropy"):
             ref = np.mean([mm[key] for mm in mets])
             np.testing.assert_allclose(float(metrics["lpg_agent"][key][c]), ref, rtol=2e-5, atol=1e-7, err_msg=key)
@@ -296,6 +317,6 @@ def test_es_step_k3_matches_oracle():
     rng = jr.PRNGKey(11)
     m = step(dk(rng), agents)
     torch.cuda.synchronize()
-    _, _, winners, steps_w, th_w, ph_w, _ = certify_es_step(args, smp, step, rng, pre, m, p_lv)
+    _, _, winners, steps_w, th_w, ph_w, _ = certify_es_step(args, smp, step, rng, pre, m, p_lv, chained=True)
     assert np.array_equal(agents.theta.cpu().numpy(), th_w) and np.array_equal(agents.phi.cpu().numpy(), ph_w)
     assert np.array_equal(agents.step.cpu().numpy(), steps_w)
