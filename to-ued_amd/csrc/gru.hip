@@ -37,9 +37,6 @@ extern "C" int toued_wgrad(int ra, int rb, long K, const float* A, long lda, con
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 #define HU 256          // GRU width (lpg_gru_width)
-#ifndef PINGPONG_DEFAULT_OFF
-#define PINGPONG_DEFAULT_OFF 1   // while k_gru_bwd6p is validated: TOUED_GRU_BWD=6p selects it
-#endif
 #define RB 32           // batch rows per workgroup
 #define LDH 33          // padded LDS row length
 #define NAUG 8          // augmented K rows: x (F <= 7) + bias row
@@ -1498,444 +1495,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   }
 }
 
-// Backward with two row groups in ping-pong (k_gru_bwd6p).  One 512-thread workgroup per (k, 64 rows) as in
-// k_gru_bwd6n, but the rows form two independent 32-row groups of four waves (group g = waves 4g .. 4g + 3; wave
-// 4g + j owns units [64 j, 64 j + 64) of rows 32 g .. 32 g + 31) that run half a time step apart: while one group
-// is in its memory part (saved-activation loads, gate maths, cotangent stores: load latency and VALU) the other
-// runs the three contraction passes of its previous step (MFMA).  Waves j and 4 + j share a SIMD, so each SIMD
-// holds one wave of each role and overlaps them.  Half-step hs = 0 .. 2T: group g is in the memory part of step
-// (hs - g) / 2 when hs - g is even, else in the contraction of step (hs - 1 - g) / 2; five sub-phases separated by
-// workgroup barriers (every wave executes all five whatever its role):
-//            memory role                                  contraction role
-//   P1   quads 0, 1 (x, ring prologue)                 accumulator init from dh, dr pass
-//   P2   quads 2, 3                                     dz -> image, DG[1] stores
-//   P3   quads 4, 5                                     dz pass
-//   P4   quads 6, 7, row maxima -> LDS                  dhn -> image, DG[2] stores
-//   P5   row scale, dr: f32 staging -> fp16 pieces,     dhn pass, unscale, dX3/dX4, carry, head cotangents of the
-//        DG[0] stores                                   group's next step
-// The dr staging needs no second barrier: a wave's f32 values of row r (64 units) sit in exactly the 2 x 128 bytes
-// of image slots 0 and 1 that its own fp16 pieces of row r occupy, and the wave reads all of them before writing.
-// The head cotangents and done flags are double-buffered by step parity (written one half-step ahead).
-// Precision, outputs and their layouts are k_gru_bwd6n's.
-#ifdef BWDP_STAMPS
-// timing instrumentation (tools/bwd_stamps.py --pingpong, built by tools/build_variant.py gru.hip BWDP_STAMPS=1):
-// thread 0 (group 0) of workgroups < 64 records s_memtime at the start of each of the five sub-phases of every
-// half-step and at its end
-__device__ unsigned long long g_bwdp_stamps[64 * 48 * 6];
-#define BWDP_STAMP(ph)                                                                                 \
-  do {                                                                                                 \
-    if (blockIdx.x < 64 && tid == 0 && hs < 48)                                                        \
-      g_bwdp_stamps[(blockIdx.x * 48 + hs) * 6 + (ph)] = __builtin_amdgcn_s_memtime();                 \
-  } while (0)
-#else
-#define BWDP_STAMP(ph) do {} while (0)
-#endif
-
-__global__ void __launch_bounds__(512, 1) k_gru_bwd6p(BwdArgs p) {
-  constexpr int RG = RB;                           // rows per group
-  constexpr int PP = HU + 8;                       // piece image row pitch (fp16 elements): 528 B
-  constexpr int SLOT = RG * PP;                    // one piece slot of a group's image
-  __shared__ __attribute__((aligned(16))) _Float16 img[2][2 * SLOT];   // [group][slot 0 (x0) | slot 1 (x1)]
-  __shared__ float wi34[2 * 3 * HU];
-  __shared__ float hv[2][2][9 * RG];               // [group][step parity][output][row]
-  __shared__ __attribute__((aligned(8))) float dxp[8 * RG * 2];   // [wave][row][dx3 | dx4]
-  __shared__ __attribute__((aligned(16))) float wsc[HU];          // 2^s of W_g row i (fp16 A scale)
-  __shared__ float rmx[8 * RG];                    // [wave][row] max over the wave's units of |dr|, |dz|, |dhn|
-  __shared__ float wIs[8 * 4 * 64];                // gate_ain's W_in fragments [unit tile][kk][lane]
-  __shared__ float wAs[8 * 5 * 64];                // W_heads^T A fragments [unit tile][kk][lane]
-  __shared__ int dns[2][2][RG];                    // done flags [group][step parity][row]
-  const int tid = threadIdx.x, lane = tid & 63, hi = lane >> 5, col = lane & 31;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-#ifndef BWDP_GMAP
-#define BWDP_GMAP 0
-#endif
-  // group of a wave: waves 0-3 | 4-7 (GMAP 0) or even | odd (GMAP 1)
-  const int gq = BWDP_GMAP ? (wave & 1) : (wave >> 2), wg = BWDP_GMAP ? (wave >> 1) : (wave & 3);
-  const int nb = p.R / (2 * RG);
-  const int k = blockIdx.x / nb;
-  const int r0 = (blockIdx.x - k * nb) * (2 * RG);
-  const int rg0 = r0 + RG * gq;                    // the group's first row
-  const int R = p.R, T = p.T, W = p.W, F = p.F;
-  for (int i = tid; i < 2 * 3 * HU; i += 512) {
-    const int f = 3 + i / (3 * HU), g = (i / HU) % 3, u = i % HU;
-    const int base = g == 0 ? p.o.ir_w : g == 1 ? p.o.iz_w : p.o.in_w;
-    wi34[i] = p.eta[base + f * HU + u];
-  }
-  for (int i = tid; i < HU; i += 512) wsc[i] = reinterpret_cast<const float*>(p.A6)[B6_SCALES + i];
-  {
-    float wI[4];   // unit tile `wave` (eight waves fill the eight tiles)
-    load_win_frags(wI, p.eta, p.o, F, wave, lane);
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) wIs[(wave * 4 + kk) * 64 + lane] = wI[kk];
-  }
-#pragma unroll
-  for (int kk = 0; kk < 5; ++kk) {
-    const int o = 2 * kk + hi, u = 32 * wave + col;
-    wAs[(wave * 5 + kk) * 64 + lane] = o < 9 ? (o == 0 ? p.eta[p.o.pi_w + u] : p.eta[p.o.y_w + u * 8 + (o - 1)]) : 0.0f;
-  }
-  float dh[2][16];          // [unit tile of the wave][register]: the carried cotangent of h_out
-#pragma unroll
-  for (int u2 = 0; u2 < 2; ++u2)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) dh[u2][q] = 0.0f;
-  float dz_r[2][16], dhn_r[2][16];
-  float bs = 1.0f;          // the lane's row scale 2^t of the step in flight (memory part -> contraction)
-  const __amdgpu_buffer_rsrc_t rs_hin = rsrc_of(p.s_hin), rs_r = rsrc_of(p.s_r), rs_z = rsrc_of(p.s_z),
-                               rs_hn = rsrc_of(p.s_hn), rs_rh = rsrc_of(p.RH);
-  const __amdgpu_buffer_rsrc_t rs_x = rsrc_of(p.s_hin + (size_t)HU * p.M);
-  const __amdgpu_buffer_rsrc_t rs_dg[4] = {rsrc_of(p.DG), rsrc_of(p.DG + 1L * HU * p.M),
-                                           rsrc_of(p.DG + 2L * HU * p.M), rsrc_of(p.DG + 3L * HU * p.M)};
-  const __amdgpu_buffer_rsrc_t rs_yh = rsrc_of(p.y_hat), rs_dyh = rsrc_of(p.d_y_hat), rs_dpi = rsrc_of(p.d_pi_hat),
-                               rs_DH = rsrc_of(p.DH), rs_dx3 = rsrc_of(p.dX3), rs_dx4 = rsrc_of(p.dX4),
-                               rs_done = rsrc_of(reinterpret_cast<const float*>(p.done + (long)k * p.done_stride_k));
-  const __amdgpu_buffer_rsrc_t rs_A = rsrc_of(reinterpret_cast<const float*>(p.A6));
-  const unsigned vA = (unsigned)lane * 16;
-  _Float16* gimg = img[gq];
-  // head cotangents (softmax VJP of y_hat, d pi_hat) and done flags of the group's rows at step t -> hv, dns, DH
-  auto head_cot = [&](int t) {
-    if (wg == 0 && lane < RG) {
-      const int tl = lane_now();   // == lane
-      const unsigned vrw = (unsigned)tl * 4;
-      const int rw = rg0 + tl, a = rw / W;
-      const int dnv = __builtin_amdgcn_raw_buffer_load_b8(rs_done, (a * T + t) * W + rw - a * W, 0, 0);
-      const long o = ((long)k * T + t) * R + rg0;
-      float yh[8], dy[8], s = 0.0f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const unsigned so = (unsigned)((((long)k * T * 8 + (long)t * 8 + j) * R + rg0) * 4);
-        yh[j] = ld_u(rs_yh, vrw, so);
-        dy[j] = ld_u(rs_dyh, vrw, so);
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s += yh[j] * dy[j];
-      const float dpi = ld_u(rs_dpi, vrw, (unsigned)(o * 4));
-      float* h = hv[gq][t & 1];
-      dns[gq][t & 1][tl] = dnv;
-      h[tl] = dpi;
-      st_u(rs_DH, vrw, (unsigned)(o * 4), dpi);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float v = yh[j] * (dy[j] - s);
-        h[(j + 1) * RG + tl] = v;
-        st_u(rs_DH, vrw, (unsigned)(((long)(j + 1) * p.M + o) * 4), v);
-      }
-    }
-  };
-  // a lane's four units ub(u2) + 8 g4 .. +3 of its row: per-unit dword stores (lane = row: 128-byte rows)
-  auto st_q = [&](__amdgpu_buffer_rsrc_t rs, long ctr, int u2, int g4, const float (&v)[4]) {
-    const int ln = lane_now();   // lane-dependent offsets re-derived at use (a hoisted copy would be spilled)
-    const unsigned vb = (unsigned)(((long)(64 * wg + 32 * u2 + 4 * (ln >> 5)) * p.M + rg0 + (ln & 31)) * 4);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) st_u(rs, vb, (unsigned)(((long)qunit(4 * g4 + e) * p.M + ctr) * 4), v[e]);
-  };
-  // fp16 pieces of the lane's units ub(u2) + 8 g4 .. +3 (row `col`) in the frame bs into the group's image
-  auto put4h = [&](int u2, int g4, const float (&v)[4]) {
-    f16x4 x0, x1;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) split2h(v[e] * bs, x0, x1, e);
-    const int off = u2 * SLOT + (lane_now() & 31) * PP + 64 * wg + 4 * (lane_now() >> 5) + 8 * g4;
-    *reinterpret_cast<f16x4*>(&gimg[off]) = x0;
-    *reinterpret_cast<f16x4*>(&gimg[off + 32]) = x1;
-  };
-  // one gate pass of the contraction: dh_prev[unit][row] += sum_c W_g[unit][c] dg_g[c][row] for the wave's two
-  // unit tiles, B = the group's cotangent image (two fp16 pieces), A fragments through a 2-k-step ring from L2
-  floatx16 acc[2];
-  auto ldAh = [&](int ks, int ut, int g, int q) {
-    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs_A, (int)vA, (int)((((ks * 8 + ut) * 3 + g) * 3 + q) * 1024),
-                                                          0);
-    return __builtin_bit_cast(f16x8, x);
-  };
-#ifndef BWDP_RD
-#define BWDP_RD 4
-#endif
-  auto contract = [&](int g) {
-    constexpr int RD = BWDP_RD;                   // A-fragment ring depth (k-steps in flight from L2)
-    f16x8 ring[RD][2][2], Bf[2][2];
-#pragma unroll
-    for (int i = 0; i < RD; ++i)
-#pragma unroll
-      for (int u2 = 0; u2 < 2; ++u2)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) ring[i][u2][q] = ldAh(i, 2 * wg + u2, g, q);
-    auto ldB = [&](int ks, f16x8 (&b)[2]) {
-      // units 16 ks + 8 hi .. +7: wave ks >> 2's segment of slot (ks >> 1) & 1, x0 at +16 (ks & 1), x1 32 later
-      const int bl = ((ks >> 1) & 1) * SLOT + (lane_now() & 31) * PP + 64 * (ks >> 2) + 16 * (ks & 1) +
-                     8 * (lane_now() >> 5);
-#pragma unroll
-      for (int q = 0; q < 2; ++q) b[q] = *reinterpret_cast<const f16x8*>(&gimg[bl + 32 * q]);
-    };
-    ldB(0, Bf[0]);
-    auto kstep = [&](int ks, f16x8 (&Ar)[2][2], f16x8 (&Bc)[2], f16x8 (&Bn)[2], bool reload) {
-      if (ks + 1 < 16) ldB(ks + 1, Bn);
-#pragma unroll
-      for (int u2 = 0; u2 < 2; ++u2) acc[u2] = mfma3h(Ar[u2], Bc, acc[u2]);
-      if (reload) {
-#pragma unroll
-        for (int u2 = 0; u2 < 2; ++u2)
-#pragma unroll
-          for (int q = 0; q < 2; ++q) Ar[u2][q] = ldAh(ks + RD, 2 * wg + u2, g, q);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    // whole groups of RD k-steps that all refill their slot (slots named statically), then the tail
-    constexpr int NG = (16 - RD) / RD;
-#pragma nounroll
-    for (int gi = 0; gi < NG; ++gi)
-#pragma unroll
-      for (int j = 0; j < RD; ++j) kstep(gi * RD + j, ring[j], Bf[j & 1], Bf[(j + 1) & 1], true);
-#pragma unroll
-    for (int ks = NG * RD; ks < 16; ++ks) kstep(ks, ring[ks % RD], Bf[ks & 1], Bf[(ks + 1) & 1], ks + RD < 16);
-  };
-  head_cot(0);
-  lds_barrier();
-  for (int hs = 0; hs <= 2 * T; ++hs) {
-    const bool mem = ((hs - gq) & 1) == 0;
-    BWDP_STAMP(0);
-    if (mem) {
-      // ======================== memory part of step t
-      const int t = (hs - gq) >> 1;
-      const bool act = t >= 0 && t < T;
-      const long ctr = ((long)k * T + t) * R;
-      const float* hvp = hv[gq][t & 1];
-#ifndef BWDP_NR
-#define BWDP_NR 2
-#endif
-      constexpr int NR = BWDP_NR;
-      float vr[NR][4][4];   // NR-slot ring: quads i+1 .. i+NR-1 in flight while quad i is processed
-      auto load_q = [&](int qi, float (&v)[4][4]) {
-        const int u2 = qi >> 2, g4 = qi & 3, ln = lane_now();
-        const unsigned vq = (unsigned)((((long)(64 * wg + 32 * u2 + 4 * (ln >> 5) + (ln & 3))) * p.M + rg0 + (ln & 28)) * 4);
-        const unsigned so = (unsigned)(((long)8 * g4 * p.M + ctr) * 4);
-        ld4(rs_hin, vq, so, v[0]);
-        ld4(rs_r, vq, so, v[1]);
-        ld4(rs_z, vq, so, v[2]);
-        ld4(rs_hn, vq, so, v[3]);
-      };
-      float xa[4];
-      floatx16 ain, hacc;
-      float dx3 = 0.0f, dx4 = 0.0f, rmr = 0.0f;
-      auto quad = [&](int qi) {
-        const int u2 = qi >> 2, g4 = qi & 3, utg = 2 * wg + u2;
-        float (&v)[4][4] = vr[qi % NR];
-        if (qi + NR - 1 < 8) load_q(qi + NR - 1, vr[(qi + NR - 1) % NR]);
-        __builtin_amdgcn_sched_barrier(0);
-        if (g4 == 0) {
-          // head VJP W_heads . hv on MFMA for unit tile utg (lane = row, register = unit)
-#pragma unroll
-          for (int q = 0; q < 16; ++q) hacc[q] = 0.0f;
-#pragma unroll
-          for (int kk = 0; kk < 5; ++kk) {
-            const int ln = lane_now(), o = 2 * kk + (ln >> 5);
-            hacc = mfma32(wAs[(utg * 5 + kk) * 64 + ln], o < 9 ? hvp[o * RG + (ln & 31)] : 0.0f, hacc);
-          }
-          float wI[4];
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk) wI[kk] = wIs[(utg * 4 + kk) * 64 + lane_now()];
-          ain = gate_ain(wI, F, hi, [&](int kx) { return xa[kx >> 1]; });
-        }
-#pragma unroll
-        for (int a = 0; a < 4; ++a) quad_transpose(v[a], lane);
-        const float* wil = wi34 + 64 * wg + 32 * u2 + 4 * (lane_now() >> 5);
-        float drq[4], rhq[4], dnq[4];
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int q = 4 * g4 + jj;
-          const float hin = v[0][jj], rg = v[1][jj], zg = v[2][jj], hn = v[3][jj];
-          const float ng = gate_n(ain[q], rg, hn);
-          const float hout = (1.0f - zg) * ng + zg * hin;
-          const float d = dh[u2][q] + (hout > 0.0f ? hacc[q] : 0.0f);
-          const float dn_ = d * (1.0f - zg);
-          const float dz = d * (hin - ng);
-          const float dnp = dn_ * (1.0f - ng * ng);
-          const float dhn = dnp * rg;
-          const float drp = dnp * hn * rg * (1.0f - rg);
-          const float dzp = dz * zg * (1.0f - zg);
-          dh[u2][q] = d * zg;   // direct path; the W_h^T contraction accumulates onto it
-          drq[jj] = drp;
-          dz_r[u2][q] = dzp;
-          dhn_r[u2][q] = dhn;
-          const int qu = qunit(q);
-          dx3 += drp * wil[0 * HU + qu] + dzp * wil[1 * HU + qu] + dnp * wil[2 * HU + qu];
-          dx4 += drp * wil[3 * HU + qu] + dzp * wil[4 * HU + qu] + dnp * wil[5 * HU + qu];
-          rhq[jj] = fmaxf(hout, 0.0f);
-          dnq[jj] = dnp;
-          rmr = fmaxf(rmr, fabsf(drp));
-        }
-        st_q(rs_rh, ctr, u2, g4, rhq);
-        st_q(rs_dg[3], ctr, u2, g4, dnq);
-        // dr in f32 in the wave's own 128-byte segment of image slot u2, row `col` (units 32 u2 .. 32 u2 + 31 of
-        // the wave's 64): the bytes its fp16 pieces of that row take in P5
-        float* seg = reinterpret_cast<float*>(&gimg[u2 * SLOT + (lane_now() & 31) * PP + 64 * wg]);
-        *reinterpret_cast<float4*>(seg + 4 * (lane_now() >> 5) + 8 * g4) = make_float4(drq[0], drq[1], drq[2], drq[3]);
-        if (qi == 7) {
-          // lanes l and l + 32 hold the same row: fold the halves, one float2 per (wave, row)
-          const float f3 = dx3 + __shfl_xor(dx3, 32), f4 = dx4 + __shfl_xor(dx4, 32);
-          const int ln = lane_now();
-          if (ln < 32) *reinterpret_cast<float2*>(dxp + ((4 * gq + wg) * RG + ln) * 2) = make_float2(f3, f4);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      };
-      // P1
-      if (act) {
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const int ln = lane_now(), kx = 2 * kk + (ln >> 5);
-          xa[kk] = ld_u(rs_x, (unsigned)((((long)(kx < F ? kx : 0)) * p.M + RG * gq + (ln & 31)) * 4),
-                        (unsigned)((ctr + r0) * 4));
-        }
-#pragma unroll
-        for (int qi = 0; qi < NR - 1; ++qi) load_q(qi, vr[qi]);
-        quad(0);
-        quad(1);
-      }
-      lds_barrier();
-      BWDP_STAMP(1);
-      // P2
-      if (act) { quad(2); quad(3); }
-      lds_barrier();
-      BWDP_STAMP(2);
-      // P3
-      if (act) { quad(4); quad(5); }
-      lds_barrier();
-      BWDP_STAMP(3);
-      // P4
-      if (act) {
-        quad(6);
-        quad(7);
-        float m = rmr;
-#pragma unroll
-        for (int u2 = 0; u2 < 2; ++u2)
-#pragma unroll
-          for (int q = 0; q < 16; ++q) m = fmaxf(m, fmaxf(fabsf(dz_r[u2][q]), fabsf(dhn_r[u2][q])));
-        m = fmaxf(m, __shfl_xor(m, 32));
-        const int ln = lane_now();
-        if (ln < 32) rmx[(4 * gq + wg) * RG + ln] = m;
-      }
-      lds_barrier();
-      BWDP_STAMP(4);
-      // P5: row scale 2^t (t = 14 - e, max_u max(|dr|, |dz|, |dhn|) < 2^e, clamped to [-40, 40]) from the
-      // group's four waves; dr from its f32 staging to fp16 pieces in place (all reads, then all writes)
-      if (act) {
-        const int row = lane_now() & 31;
-        float m = 0.0f;
-#pragma unroll
-        for (int w4 = 0; w4 < 4; ++w4) m = fmaxf(m, rmx[(4 * gq + w4) * RG + row]);
-        int sc = 0, ce = 127;
-        if (m > 0.0f && m <= 3.0e38f) {
-          int e;
-          frexpf(m, &e);
-          sc = min(40, max(-40, 14 - e));
-          ce = min(126, max(-126, 14 - e));
-        }
-        bs = ldexpf(1.0f, sc);
-        if (p.CE && wg == 0 && lane_now() < 32) p.CE[ctr + rg0 + row] = (int8_t)ce;
-#pragma unroll
-        for (int u2 = 0; u2 < 2; ++u2) {
-          // the wave's segment of slot u2 holds this row's 32 staged f32 values and receives their pieces
-          float4 st[4];
-          const float* seg = reinterpret_cast<const float*>(&gimg[u2 * SLOT + row * PP + 64 * wg]);
-#pragma unroll
-          for (int g4 = 0; g4 < 4; ++g4) st[g4] = *reinterpret_cast<const float4*>(seg + 4 * (lane_now() >> 5) + 8 * g4);
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every staged value read before any piece is written
-#pragma unroll
-          for (int g4 = 0; g4 < 4; ++g4) {
-            const float v4[4] = {st[g4].x, st[g4].y, st[g4].z, st[g4].w};
-            put4h(u2, g4, v4);
-            st_q(rs_dg[0], ctr, u2, g4, v4);
-          }
-        }
-      }
-      lds_barrier();
-      BWDP_STAMP(5);
-    } else {
-      // ======================== contraction of step t: dr, then dz, then dhn (scaled fp16 pairs) through the
-      // group's image, accumulated onto the direct path dh in the frame 2^(s_i + t_row) (exact: powers of two)
-      const int t = (hs - 1 - gq) >> 1;
-      const bool act = t >= 0 && t < T;
-      const long ctr = ((long)k * T + t) * R;
-      // P1
-      if (act) {
-#pragma unroll
-        for (int u2 = 0; u2 < 2; ++u2)
-#pragma unroll
-          for (int g4 = 0; g4 < 4; ++g4) {
-            const float4 w4 = *reinterpret_cast<const float4*>(&wsc[64 * wg + 32 * u2 + 4 * (lane_now() >> 5) + 8 * g4]);
-            const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[u2][4 * g4 + e] = dh[u2][4 * g4 + e] * (wv[e] * bs);
-          }
-        contract(0);
-      }
-      lds_barrier();
-      BWDP_STAMP(1);
-      // P2
-      if (act) {
-#pragma unroll
-        for (int u2 = 0; u2 < 2; ++u2)
-#pragma unroll
-          for (int g4 = 0; g4 < 4; ++g4) {
-            const float v4[4] = {dz_r[u2][4 * g4], dz_r[u2][4 * g4 + 1], dz_r[u2][4 * g4 + 2], dz_r[u2][4 * g4 + 3]};
-            put4h(u2, g4, v4);
-            st_q(rs_dg[1], ctr, u2, g4, v4);
-          }
-      }
-      lds_barrier();
-      BWDP_STAMP(2);
-      // P3
-      if (act) contract(1);
-      lds_barrier();
-      BWDP_STAMP(3);
-      // P4
-      if (act) {
-#pragma unroll
-        for (int u2 = 0; u2 < 2; ++u2)
-#pragma unroll
-          for (int g4 = 0; g4 < 4; ++g4) {
-            const float v4[4] = {dhn_r[u2][4 * g4], dhn_r[u2][4 * g4 + 1], dhn_r[u2][4 * g4 + 2], dhn_r[u2][4 * g4 + 3]};
-            put4h(u2, g4, v4);
-            st_q(rs_dg[2], ctr, u2, g4, v4);
-          }
-      }
-      lds_barrier();
-      BWDP_STAMP(4);
-      // P5
-      if (act) {
-        contract(2);
-#pragma unroll
-        for (int u2 = 0; u2 < 2; ++u2)
-#pragma unroll
-          for (int g4 = 0; g4 < 4; ++g4) {
-            const float4 w4 = *reinterpret_cast<const float4*>(&wsc[64 * wg + 32 * u2 + 4 * (lane_now() >> 5) + 8 * g4]);
-            const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[u2][4 * g4 + e] *= inv_pow2(wv[e] * bs);
-          }
-        if (wg == 0 && lane < RG) {
-          const int tl = lane_now();   // == lane
-          float s3 = 0.0f, s4 = 0.0f;
-#pragma unroll
-          for (int w4 = 0; w4 < 4; ++w4) {
-            const float2 v = *reinterpret_cast<const float2*>(dxp + ((4 * gq + w4) * RG + tl) * 2);
-            s3 += v.x;
-            s4 += v.y;
-          }
-          st_u(rs_dx3, (unsigned)tl * 4, (unsigned)((ctr + rg0) * 4), s3);
-          st_u(rs_dx4, (unsigned)tl * 4, (unsigned)((ctr + rg0) * 4), s4);
-        }
-        // carry to h_out(t+1): h_in(t) = where(d_t, 0, h_out(t+1))
-        const bool dn = dns[gq][t & 1][lane_now() & 31] != 0;
-#pragma unroll
-        for (int u2 = 0; u2 < 2; ++u2)
-#pragma unroll
-          for (int q = 0; q < 16; ++q) dh[u2][q] = dn ? 0.0f : acc[u2][q];
-        if (t + 1 < T) head_cot(t + 1);
-      }
-      lds_barrier();
-      BWDP_STAMP(5);
-    }
-  }
-}
-
 }  // namespace
 
 extern "C" {
@@ -1970,16 +1529,6 @@ static bool gru_f32_forced() {
   static const bool f = [] {
     const char* e = getenv("TOUED_GRU_F32");
     return e && e[0] == '1';
-  }();
-  return f;
-}
-
-// the split-precision backward's variant: the two-row-group ping-pong k_gru_bwd6p unless TOUED_GRU_BWD=6n (the
-// lockstep k_gru_bwd6n; same outputs within rounding)
-static bool gru_bwd_pingpong() {
-  static const bool f = [] {
-    const char* e = getenv("TOUED_GRU_BWD");
-    return !(e && strcmp(e, "6n") == 0) && !(e == nullptr && PINGPONG_DEFAULT_OFF);
   }();
   return f;
 }
@@ -2075,12 +1624,8 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
   p.DG = DG; p.RH = RH; p.DH = DH; p.dX3 = dX3; p.dX4 = dX4; p.CE = col_exp;
   p.F = (p.o.ir_b - p.o.in_w) / HU;   // in_w [F][256] is followed by ir_b in the flat layout (lpg.LPGLayout)
   TOUED_REQUIRE(p.F >= 1 && p.F <= 7 && p.o.ir_b - p.o.in_w == p.F * HU, "toued_gru_bwd: LPG layout F=%d", p.F);
-  if (toued_gru_bwd_col_exp(R)) {
-    if (gru_bwd_pingpong())
-      hipLaunchKernelGGL(k_gru_bwd6p, dim3(K * (R / (2 * RB))), dim3(512), 0, stream, p);
-    else
-      hipLaunchKernelGGL(k_gru_bwd6n, dim3(K * (R / (2 * RB))), dim3(512), 0, stream, p);
-  }
+  if (toued_gru_bwd_col_exp(R))
+    hipLaunchKernelGGL(k_gru_bwd6n, dim3(K * (R / (2 * RB))), dim3(512), 0, stream, p);
   else
     hipLaunchKernelGGL(k_gru_bwd<1>, dim3(K * (R / RB)), dim3(512), 0, stream, p);
   TOUED_CHECK_LAUNCH();
@@ -2090,12 +1635,6 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
 #ifdef FWD_STAMPS
 int toued_dbg_fwd_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd_stamps), sizeof(g_fwd_stamps)) == hipSuccess ? 0 : 1;
-}
-#endif
-
-#ifdef BWDP_STAMPS
-int toued_dbg_bwdp_stamps(unsigned long long* host) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bwdp_stamps), sizeof(g_bwdp_stamps)) == hipSuccess ? 0 : 1;
 }
 #endif
 

@@ -44,20 +44,6 @@ def main():
     for _ in range(2):
         gru.backward(done, eta, y_hat, d_pi, d_y, gru.X, grad)
     torch.cuda.synchronize()
-    if "--pingpong" in sys.argv:   # k_gru_bwd6p (BWDP_STAMPS=1 library, TOUED_GRU_BWD=6p)
-        buf = np.zeros(64 * 48 * 6, np.uint64)
-        fn = _lib.lib().toued_dbg_bwdp_stamps
-        fn.argtypes = [ctypes.c_void_p]
-        assert fn(buf.ctypes.data) == 0
-        st = buf.reshape(64, 48, 6)[:, :2 * T + 1].astype(np.int64)
-        ph = np.diff(st, axis=2)                               # five sub-phases per half-step (group 0's view)
-        res = {}
-        for role, sl in (("mem", slice(0, 2 * T, 2)), ("contr", slice(1, 2 * T, 2))):
-            for i in range(5):
-                res[f"{role} P{i + 1}"] = float(ph[:, sl, i].mean())
-        res["half-step"] = float((st[:, 1:2 * T, 0] - st[:, 0:2 * T - 1, 0]).mean())
-        print(json.dumps({k: round(v) for k, v in res.items()}), flush=True)
-        return
     buf = np.zeros(64 * 32 * 8, np.uint64)
     fn = _lib.lib().toued_dbg_bwd_stamps
     fn.argtypes = [ctypes.c_void_p]
