@@ -38,3 +38,4 @@ for (k, n), v in sorted(agg.items()):
     print(f"{k:34s} {n:28s} {sum(v)/len(v):.6g}  (n={len(v)})")
 PY
 cat "$OUT/summary.txt"
+find "$OUT" -name "*.db" -delete

@@ -29,4 +29,7 @@ timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/calib_fetch
 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/calib_write" -o run -- /tmp/calib_fetch \
     > "$OUT/calib_write.log" 2>&1
 echo "calibration done"
-find "$OUT" -name "*.csv" | head -50
+# summarise on the box (kernel_stats*.csv, pmc_traffic.json) and drop the databases: gpurun copies back <= 64 MiB
+python3 "$R/tools/prof_summary.py" "$OUT" "$R/gpurun_out/prof_${TAG}_summary" && find "$OUT" -name "*.db" -delete
+find "$OUT" -name "*kernel_trace.csv" -delete
+ls -la "$R/gpurun_out/prof_${TAG}_summary"
