@@ -296,7 +296,7 @@ def workload_c3(a, cpu: bool):
     regret_round()
     t_regret, _ = _sync_time(regret_round, max(1, a.steps))
     # per-kernel launch durations of the antagonists' update chain: one eager round with HIP events (the graph
-    # replays the same two kernels per update)
+    # replays the same launches)
     trn = tr.sampler.a2c_trainer()
     trn.timers = KernelTimers()
     trn.timers.enabled = True
@@ -305,15 +305,30 @@ def workload_c3(a, cpu: bool):
     ks = trn.timers.summary()
     trn.timers = None
     D = tr.sampler.obs_dim
-    roll_ms, upd_ms = ks["a2c_rollout"][1], ks["a2c_update"][1]
     steps_launch = N * W * T
-    traj_bytes = N * ((T + 1) * W * 8 + T * W * 6)
-    upd_bytes = traj_bytes + N * D * 6 * 4 * 2
-    rollout_rf = _hbm_roofline("k_rollout (A2C antagonist train rollout)", steps_launch * ROLLOUT_BYTES_PER_STEP,
-                               roll_ms, "bound in practice by its dependent threefry VALU chain (~12 blocks per step)")
-    update_rf = _hbm_roofline("k_a2c_update (fused GAE + actor/critic gradients + clip + SGD, tables in LDS)",
-                              upd_bytes, upd_ms)
-    dom = rollout_rf if roll_ms >= upd_ms else update_rf
+    if "a2c_chain" in ks:
+        # toued_a2c_chain: DRAW_CHUNK updates per launch.  Algorithmic bytes per agent-env-step: its draws (16 B),
+        # the chosen actor row (20 B) and the V(obs) gather (4 B); the trajectory never leaves LDS
+        from toued.a2c import DRAW_CHUNK
+        upl = min(U, DRAW_CHUNK)
+        chain_ms = ks["a2c_chain"][1]
+        dom = _hbm_roofline("k_a2c_chain (A2C antagonist: env chain + fused update, %d updates per launch)" % upl,
+                            steps_launch * upl * 40, chain_ms,
+                            "latency-bound: per update a T-step dependent env chain, then the LDS sort/segment update")
+        draws_rf = _hbm_roofline("k_eval_keys + k_eval_draws (state-independent draws of %d updates)" % upl,
+                                 steps_launch * upl * 32, ks["a2c_draws"][1], "threefry VALU-bound")
+        secondary = {"a2c_chain": dom, "a2c_draws": draws_rf,
+                     "per_update_ms": round((chain_ms + ks["a2c_draws"][1]) / upl, 4)}
+    else:
+        roll_ms, upd_ms = ks["a2c_rollout"][1], ks["a2c_update"][1]
+        traj_bytes = N * ((T + 1) * W * 8 + T * W * 6)
+        upd_bytes = traj_bytes + N * D * 6 * 4 * 2
+        rollout_rf = _hbm_roofline("k_rollout (A2C antagonist train rollout)", steps_launch * ROLLOUT_BYTES_PER_STEP,
+                                   roll_ms, "bound in practice by its dependent threefry VALU chain (~12 blocks per step)")
+        update_rf = _hbm_roofline("k_a2c_update (fused GAE + actor/critic gradients + clip + SGD, tables in LDS)",
+                                  upd_bytes, upd_ms)
+        dom = rollout_rf if roll_ms >= upd_ms else update_rf
+        secondary = {"a2c_rollout": rollout_rf, "a2c_update": update_rf}
     a2c_steps = N * U * W * T
     meta_steps = N * W * T * K
     t_ref = t_meta + t_regret
@@ -325,7 +340,7 @@ def workload_c3(a, cpu: bool):
            "lpg_meta_step_ms": round(t_meta * 1e3, 3), "regret_round_ms": round(t_regret * 1e3, 3),
            "regret_round_agent_env_steps_per_sec": round(a2c_steps / t_regret, 1),
            "amortized_meta_step_ms": round((t_meta + t_regret * K / U) * 1e3, 3),
-           "roofline": dom, "roofline_secondary": {"a2c_rollout": rollout_rf, "a2c_update": update_rf},
+           "roofline": dom, "roofline_secondary": secondary,
            "kernels": {k: {"launches": v[0], "mean_ms": round(v[1], 4)} for k, v in ks.items()}}
     out["cpu_baseline"] = c3_cpu_baseline(args, tr.sampler) if cpu else None
     del tr
@@ -421,7 +436,8 @@ def workload_c4(a, cpu: bool):
     tr.meta_step()
     st.timers.enabled = True
     st.timers.reset()
-    t_es, m = _sync_time(tr.meta_step, max(1, a.steps // 2))
+    n_es = max(1, a.steps // 2)
+    t_es, m = _sync_time(tr.meta_step, n_es)
     ks = st.timers.summary()
     st.timers.enabled = False
     R = C * W
@@ -441,8 +457,8 @@ def workload_c4(a, cpu: bool):
            "value": round(steps / t_es, 1), "unit": "agent-env-steps/sec", "ms_per_step": round(t_es * 1e3, 3),
            "meta_updates_per_sec": round(1.0 / t_es, 3), "roofline": rf,
            "roofline_secondary": {"rollout": rollout_rf},
-           "kernels": {k: {"launches": v[0], "mean_ms": round(v[1], 4), "total_ms_per_step": round(v[2], 3)}
-                       for k, v in ks.items()},
+           "kernels": {k: {"launches_per_step": v[0] // n_es, "mean_ms": round(v[1], 4),
+                           "total_ms_per_step": round(v[2] / n_es, 3)} for k, v in ks.items()},
            "fitness_mean": float(m["fitness"]["mean"])}
     out["cpu_baseline"] = c4_cpu_baseline(args, tr.sampler) if cpu else None
     del tr

@@ -99,6 +99,16 @@ int toued_rollout(EnvSpec spec, const int* levels, const float* theta, int D, co
 /* The same returns-only rollout (eval_agent, agents/agents.py:98-106 over rollout.py:45-102) in three launches,
  * bit-identical: the per-worker key chain (chain: uint32[T][n][4], n = n_agents*W), every state-independent draw of
  * every step in parallel (draws: uint32[T][n][4]), then the env chain on those draws (`state` read only). */
+/* RolloutWrapper.batch_rollout (environments/rollout.py:45-102) in three launches, bit-identical to toued_rollout:
+ * the state-independent draws of U batches of train rollouts at once (keys [U][n_agents][2]; chain scratch and draws
+ * out u32x4 [T][U * n_agents * W]), then each batch's env chain on its draws (draws = the batch's first worker at
+ * step 0, dstride u32x4 elements between steps).  The A2C antagonist's U = max_lifetime update rollouts
+ * (agents/a2c.py:79-125) draw everything up front this way. */
+int toued_rollout_draws(EnvSpec spec, const int* levels, const uint32_t* keys, int n_agents, int U, int W, int T,
+                        uint32_t* chain, uint32_t* draws, hipStream_t stream);
+int toued_rollout_env(EnvSpec spec, const int* levels, const float* theta, int D, int* state, int n_agents, int W, int T,
+                      const uint32_t* draws, long dstride, int* traj_idx, int* traj_time, uint8_t* traj_action,
+                      float* traj_reward, uint8_t* traj_done, float* cum_return, hipStream_t stream);
 int toued_eval_keys(const uint32_t* agent_keys, int n_agents, int W, int T, uint32_t* chain, hipStream_t stream);
 int toued_eval_draws(EnvSpec spec, const int* levels, int n_agents, int W, int T, const uint32_t* chain,
                      uint32_t* draws, hipStream_t stream);
@@ -147,6 +157,15 @@ int toued_a2c_update(int N, int W, int T, int D, float* theta, float* vcrit, con
                      const uint8_t* tact, const float* trew, const uint8_t* tdone, float gamma, float lam,
                      float ent_coef, float lr_a, float lr_c, float max_norm, int* step, const int* levels,
                      float* loss_out, hipStream_t stream);
+/* train_a2c_agent's whole scan (a2c.py:79-125) in one launch: U updates (rollout + fused update) of N antagonists,
+ * one workgroup each, on the state-independent draws toued_rollout_draws made for the U update keys (toued_key_chain
+ * of the agents' rng): draws [T][dstride] uint32x4, update u's worker i at column u*N*W + i.  theta/vcrit/step/state
+ * updated in place, loss_out[N][2] accumulated.  Bit-identical, update by update, to toued_rollout_env +
+ * toued_a2c_update.  Tabular envs, sizes where toued_a2c_chain_fits(W, T, D) is 1 (W <= 256, W*T <= 2048). */
+int toued_a2c_chain_fits(int W, int T, int D);
+int toued_a2c_chain(EnvSpec spec, const int* levels, int N, int W, int T, int D, int U, float* theta, float* vcrit,
+                    int* state, const uint32_t* draws, long dstride, float gamma, float lam, float ent_coef, float lr_a,
+                    float lr_c, float max_norm, int* step, float* loss_out, hipStream_t stream);
 /* --fix_value_critic: one update of the meta-gradient value critics vcrit [N][D] on a trajectory (meta/train.py:61-81
  * with the discarded `.replace` fixed): critic loss mean_w mean_t (target - V)^2 on stop-gradient GAE targets,
  * clip_by_global_norm + SGD (lr, max_norm), vstep[i] += 1; loss_out[i][1] += the loss before the update.

@@ -181,3 +181,50 @@ def test_eval_returns_three_launches(mode, N, W):
         _, _, ocum = oro.batch_rollout(spec, jr.split(jr.PRNGKey(33), N), theta, p, _state_np(st0, spec),
                                        rw.eval_rollout_len)
         np.testing.assert_array_equal(got.cpu().numpy(), ocum)
+
+
+@pytest.mark.parametrize("mode,N,W", [("dense", 3, 64), ("tabular", 2, 64), ("all_shortlife", 5, 32), ("mazes", 2, 64),
+                                      ("debug", 3, 16)])
+def test_train_rollout_three_launches(mode, N, W):
+    """The train rollouts as draws (toued_rollout_draws, U batches at once: the A2C update chain's form) + env chain
+    (toued_rollout_env) are bit-identical to the single-kernel toued_rollout: every batch's trajectory, end state and
+    cum_return, batches rolled one after another from the carried state, on peaked and uniform actors; the
+    production batch_rollout (split path) likewise."""
+    from toued import _lib
+    from toued.rollout import RolloutWrapper, Transition
+    keys = jr.split(jr.PRNGKey(41), N)
+    spec, p, lt, packed = oracle_levels(mode, keys)
+    T = 20
+    rw = RolloutWrapper(mode, T, env_workers=W)
+    lev = torch.from_numpy(packed).cuda()
+    (_, _), st0 = rw.batch_reset(dev_keys(jr.split(jr.PRNGKey(42), N)), lev)
+    U = 3
+    ukeys = dev_keys(jr.split(jr.PRNGKey(43), U * N)).view(U, N, 2).contiguous()
+    for scale in (3.0, 0.0):
+        th = torch.from_numpy((np.random.RandomState(4).randn(N, spec.obs_dim, 5) * scale).astype(np.float32)).cuda()
+        draws = rw.train_draws(ukeys, lev, W)
+        s_ref, s_got = st0.clone(), st0.clone()
+        for u in range(U):
+            def buf():
+                return Transition(torch.zeros((N, T + 1, W), dtype=torch.int32, device="cuda"),
+                                  torch.zeros((N, T + 1, W), dtype=torch.int32, device="cuda"),
+                                  torch.zeros((N, T, W), dtype=torch.uint8, device="cuda"),
+                                  torch.zeros((N, T, W), dtype=torch.float32, device="cuda"),
+                                  torch.zeros((N, T, W), dtype=torch.uint8, device="cuda"))
+            ref, got = buf(), buf()
+            c_ref = torch.zeros((N, W), device="cuda")
+            c_got = torch.zeros((N, W), device="cuda")
+            _lib.call("toued_rollout", rw._c, _lib.ptr(lev), _lib.ptr(th), spec.obs_dim, _lib.ptr(ukeys[u]),
+                      _lib.ptr(s_ref), N, W, T, _lib.ptr(ref.obs_idx), _lib.ptr(ref.obs_time), _lib.ptr(ref.action),
+                      _lib.ptr(ref.reward), _lib.ptr(ref.done), _lib.ptr(c_ref), _lib.stream_ptr())
+            rw.rollout_from_draws(draws, u, th, lev, s_got, got, c_got)
+            for name in ("obs_idx", "obs_time", "action", "reward", "done"):
+                assert torch.equal(getattr(got, name), getattr(ref, name)), (scale, u, name)
+            assert torch.equal(s_got, s_ref) and torch.equal(c_got, c_ref), (scale, u)
+        # the production path (batch_rollout's default split path) on batch 0's keys
+        o, s2, c2 = rw.batch_rollout(ukeys[0], th, lev, st0)
+        ref0, s0r, c0r = buf(), st0.clone(), torch.zeros((N, W), device="cuda")
+        _lib.call("toued_rollout", rw._c, _lib.ptr(lev), _lib.ptr(th), spec.obs_dim, _lib.ptr(ukeys[0]),
+                  _lib.ptr(s0r), N, W, T, _lib.ptr(ref0.obs_idx), _lib.ptr(ref0.obs_time), _lib.ptr(ref0.action),
+                  _lib.ptr(ref0.reward), _lib.ptr(ref0.done), _lib.ptr(c0r), _lib.stream_ptr())
+        assert torch.equal(o.action, ref0.action) and torch.equal(s2, s0r) and torch.equal(c2, c0r)

@@ -82,7 +82,9 @@ def test_a2c_update_matches_oracle(fused):
     spec = olv.env_spec(mode)
     th0, vc0, st0 = theta.cpu().numpy(), vcrit.cpu().numpy(), state.cpu().numpy()
     rng = jr.split(jr.PRNGKey(9), N)
-    tr = A2CTrainer(ro, A2CHyperparams(), _ahyp(mode), use_graph=False, fused=fused)
+    # one launch per update (the chain kernel keeps its trajectories in LDS; its parity with this path:
+    # test_a2c_chain_matches_launch_per_update)
+    tr = A2CTrainer(ro, A2CHyperparams(), _ahyp(mode), use_graph=False, fused=fused, chain=False)
     step = torch.zeros(N, dtype=torch.int32, device="cuda")
     loss = tr.train(dk(rng), theta, vcrit, step, levels, state, 1).cpu().numpy()
     b = tr._bufs["tr"]
@@ -137,6 +139,30 @@ def test_a2c_graph_replay_matches_eager_and_lifetime_discard():
     assert torch.equal(s_e, s_g)
     torch.testing.assert_close(th_g, th_e, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(vc_g, vc_e, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("mode,W,U", [("dense", 64, 40), ("all_shortlife", 32, 7), ("mazes", 64, 33)])
+def test_a2c_chain_matches_launch_per_update(mode, W, U):
+    """toued_a2c_chain (the whole update chain in one kernel per 32 updates, trajectories in LDS) against one
+    toued_rollout_env + one toued_a2c_update launch per update: actor/critic tables, env state, step counters (with
+    lifetime discards) and losses bit-identical, over several draw chunks and a partial last chunk."""
+    from toued.a2c import A2CHyperparams, A2CTrainer
+    from toued.env import L_LIFETIME
+    N, T = 4, 20
+    ro, levels, p, lt, theta, vcrit, state, D = _a2c_setup(mode, N, W, T, seed=31)
+    levels[:, L_LIFETIME] = torch.tensor([1, U // 2, 1000, U - 1], dtype=torch.int32, device="cuda")
+    rng = dk(jr.split(jr.PRNGKey(37), N))
+    outs = []
+    for chain in (False, True):
+        th, vc, st = theta.clone(), vcrit.clone(), state.clone()
+        step = torch.zeros(N, dtype=torch.int32, device="cuda")
+        tr = A2CTrainer(ro, A2CHyperparams(), _ahyp(mode), use_graph=False, chain=chain)
+        assert tr.use_chain(W, T, D) == chain
+        loss = tr.train(rng, th, vc, step, levels, st, U)
+        outs.append((th, vc, st, step, loss))
+    for x, y, name in zip(outs[0], outs[1], ("theta", "vcrit", "state", "step", "loss")):
+        assert torch.equal(x, y), name
+    assert outs[1][3].cpu().tolist() == [1, U // 2, U, U - 1]
 
 
 def test_a2c_c1_tabular_n8_matches_oracle():

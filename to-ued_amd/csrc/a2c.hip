@@ -13,7 +13,7 @@
 //                (W*T <= 2048; grad + apply, which scatter with float atomics, are the fallback above that)
 //
 // Trajectory layout as the rollout kernel writes it: idx/time [N][T+1][W], act/done/rew [N][T][W].
-#include "common.h"
+#include "env_dev.h"
 
 #define EPSF 1e-8f
 
@@ -47,7 +47,10 @@ struct A2CStage {
   float* adv;   // [W*T] GAE advantages, worker-major
   float* dv;    // [W*T] target - V
   float* abar;  // [W] mean_t normalised advantage
-  __host__ __device__ static size_t floats(int W, int T) { return 3 * (size_t)(T + 1) * W + 4 * (size_t)W * T + W; }
+  uint8_t* act; // [T][W] action
+  __host__ __device__ static size_t floats(int W, int T) {
+    return 3 * (size_t)(T + 1) * W + 4 * (size_t)W * T + W + ((size_t)W * T + 3) / 4;
+  }
   TOUED_DEV void carve(float* base, int W, int T) {
     const int NO = (T + 1) * W, NS = T * W;
     vt = base;
@@ -58,18 +61,17 @@ struct A2CStage {
     adv = nd + NS;
     dv = adv + NS;
     abar = dv + NS;
+    act = reinterpret_cast<uint8_t*>(abar + W);
   }
 };
 
-// Latency structure: the agent's whole trajectory (obs rows and times, rewards, dones) is staged into LDS with
-// coalesced loads, V(obs) gathered for every observation at once, and only then the per-worker GAE scans run
-// out of LDS -- a handful of dependent memory round trips per update instead of two per time step.  Returns the
-// critic loss mean((target - V)^2) (a2c.py:29-37); fills adv/dv/abar (a2c.py:43 normalisation, the [T,T]
-// broadcast's mean_t factor).  Ends with a barrier.
-TOUED_DEV float a2c_stage(const A2CStage& S, int a, int W, int T, int D, const float* __restrict__ v,
-                          const int* __restrict__ tidx, const int* __restrict__ ttime,
-                          const float* __restrict__ trew, const uint8_t* __restrict__ tdone, float gamma, float lam,
-                          float* red) {
+// Latency structure: the agent's whole trajectory (obs rows and times, actions, rewards, dones) is staged into LDS
+// with coalesced loads, V(obs) gathered for every observation at once, and only then the per-worker GAE scans run
+// out of LDS -- a handful of dependent memory round trips per update instead of two per time step.  Ends with a
+// barrier.
+TOUED_DEV void a2c_load(const A2CStage& S, int a, int W, int T, int D, const float* __restrict__ v,
+                        const int* __restrict__ tidx, const int* __restrict__ ttime, const uint8_t* __restrict__ tact,
+                        const float* __restrict__ trew, const uint8_t* __restrict__ tdone) {
   const int NO = (T + 1) * W, NS = T * W, tid = threadIdx.x;
   const float vlast = v[D - 1];
   const size_t tb = (size_t)a * (T + 1) * W;
@@ -84,8 +86,15 @@ TOUED_DEV float a2c_stage(const A2CStage& S, int a, int W, int T, int D, const f
   for (int i = tid; i < NS; i += blockDim.x) {
     S.rw[i] = trew[sb + i];
     S.nd[i] = tdone[sb + i] ? 0.0f : 1.0f;
+    if (tact) S.act[i] = tact[sb + i];
   }
   __syncthreads();
+}
+
+// GAE on the staged trajectory.  Returns the critic loss mean((target - V)^2) (a2c.py:29-37); fills adv/dv/abar
+// (a2c.py:43 normalisation, the [T,T] broadcast's mean_t factor).  Ends with a barrier.
+TOUED_DEV float a2c_gae(const A2CStage& S, int W, int T, float gamma, float lam, float* red) {
+  const int tid = threadIdx.x;
   // per-worker GAE (reverse scan over T, util/metrics.py:17-38)
   float s_adv = 0.0f, s_cl = 0.0f;
   for (int w = tid; w < W; w += blockDim.x) {
@@ -127,12 +136,11 @@ TOUED_DEV float a2c_stage(const A2CStage& S, int a, int W, int T, int D, const f
 // the entropy bonus of pi + 1e-8, a2c.py:52-63), critic row cotangent (returned), the row, the time coefficient
 // and this sample's actor-loss term.
 TOUED_DEV float a2c_sample(const A2CStage& S, int i, int W, int T, const float* __restrict__ th,
-                           const float* lastA, const uint8_t* __restrict__ tact, size_t sb, float ent_coef,
-                           float inv_n, float* d, int& idx, float& c, float& al) {
+                           const float* lastA, float ent_coef, float inv_n, float* d, int& idx, float& c, float& al) {
   const int t = i / W, w = i - t * W;
   idx = S.ix[i];
   c = S.cc[i];
-  const int act = tact[sb + (size_t)t * W + w];
+  const int act = S.act[i];
   float l[5], p[5], m = -__builtin_inff();
 #pragma unroll
   for (int j = 0; j < 5; ++j) { l[j] = th[(size_t)idx * 5 + j] + c * lastA[j]; m = fmaxf(m, l[j]); }
@@ -188,7 +196,8 @@ __global__ void __launch_bounds__(256) k_a2c_grad(int W, int T, int D, const flo
   A2CStage S;
   S.carve(lds, W, T);
   const int a = blockIdx.x, tid = threadIdx.x;
-  const float closs = a2c_stage(S, a, W, T, D, vcrit + (size_t)a * D, tidx, ttime, trew, tdone, gamma, lam, red);
+  a2c_load(S, a, W, T, D, vcrit + (size_t)a * D, tidx, ttime, tact, trew, tdone);
+  const float closs = a2c_gae(S, W, T, gamma, lam, red);
   const float* th = theta + (size_t)a * D * 5;
   float* ga = Ga + (size_t)a * D * 5;
   float* gv = Gv + (size_t)a * D;
@@ -196,12 +205,11 @@ __global__ void __launch_bounds__(256) k_a2c_grad(int W, int T, int D, const flo
 #pragma unroll
   for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
   const float inv_n = 1.0f / (float)(W * T);
-  const size_t sb = (size_t)a * T * W;
   float accA[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, accV = 0.0f, s_al = 0.0f;
   for (int i = tid; i < W * T; i += blockDim.x) {
     float d[5], c, al;
     int idx;
-    const float dvv = a2c_sample(S, i, W, T, th, lastA, tact, sb, ent_coef, inv_n, d, idx, c, al);
+    const float dvv = a2c_sample(S, i, W, T, th, lastA, ent_coef, inv_n, d, idx, c, al);
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
       atomicAdd(&ga[(size_t)idx * 5 + j], d[j]);
@@ -270,68 +278,119 @@ __global__ void __launch_bounds__(256) k_a2c_apply(int D, float* __restrict__ th
 #define A2C_SORT_MAX 2048
 #define A2C_NV 6
 
-// bitonic sort of 2048 keys with 256 threads: wave w owns keys [512 w, 512 w + 512), so every stage with partner
-// distance j < 512 needs only a wave barrier; the three stages with j >= 512 take workgroup barriers.
-TOUED_DEV void a2c_cmp_swap(uint32_t* key, int i, int j, int k) {
-  const int ij = i | j;
-  const uint32_t x = key[i], y = key[ij];
-  if ((x > y) == ((i & k) == 0)) { key[i] = y; key[ij] = x; }
+// bitonic sort of the 2048 keys in LDS with 256 threads, in registers: wave w holds keys [512 w, 512 w + 512), lane l
+// the eight keys 512 w + 8 l + r (two 16-byte LDS reads).  Stages with partner distance j < 8 are compare-selects
+// between a lane's own registers, 8 <= j <= 256 exchange registers between lanes (lane distance j / 8, one shuffle per
+// key), and the three stages with j >= 512 exchange whole halves through LDS between waves.  Every element keeps
+// min or max of itself and its partner i ^ j: min when (i & j == 0) == ascending, ascending = (i & k == 0).
+// Begins and ends with a workgroup barrier; the sorted keys are back in `key`.
+template <int K, int J>
+TOUED_DEV void a2c_bitonic_stage(uint32_t (&x)[8], uint32_t* key, int lane, int wv) {
+  if constexpr (J < 8) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      if ((r & J) == 0) {
+        const int i = 512 * wv + 8 * lane + r;
+        const bool asc = (i & K) == 0;
+        const uint32_t a = x[r], b = x[r | J];
+        const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+        x[r] = asc ? lo : hi;
+        x[r | J] = asc ? hi : lo;
+      }
+    }
+  } else if constexpr (J <= 256) {
+    const bool lowpos = (lane & (J / 8)) == 0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int i = 512 * wv + 8 * lane + r;
+      const bool asc = (i & K) == 0;
+      const uint32_t p = (uint32_t)__shfl_xor((int)x[r], J / 8, 64);
+      const uint32_t lo = x[r] < p ? x[r] : p, hi = x[r] < p ? p : x[r];
+      x[r] = lowpos == asc ? lo : hi;
+    }
+  } else {
+    uint4* kv = reinterpret_cast<uint4*>(key);
+    const int me = (512 * wv + 8 * lane) / 4, pa = (512 * (wv ^ (J / 512)) + 8 * lane) / 4;
+    kv[me] = make_uint4(x[0], x[1], x[2], x[3]);
+    kv[me + 1] = make_uint4(x[4], x[5], x[6], x[7]);
+    __syncthreads();
+    const uint4 p0 = kv[pa], p1 = kv[pa + 1];
+    const uint32_t p[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+    const bool lowpos = (wv & (J / 512)) == 0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int i = 512 * wv + 8 * lane + r;
+      const bool asc = (i & K) == 0;
+      const uint32_t lo = x[r] < p[r] ? x[r] : p[r], hi = x[r] < p[r] ? p[r] : x[r];
+      x[r] = lowpos == asc ? lo : hi;
+    }
+    __syncthreads();   // every partner read before the next stage's writes
+  }
+}
+
+template <int K, int J>
+TOUED_DEV void a2c_bitonic_merge(uint32_t (&x)[8], uint32_t* key, int lane, int wv) {
+  a2c_bitonic_stage<K, J>(x, key, lane, wv);
+  if constexpr (J > 1) a2c_bitonic_merge<K, J / 2>(x, key, lane, wv);
+}
+
+template <int K>
+TOUED_DEV void a2c_bitonic_levels(uint32_t (&x)[8], uint32_t* key, int lane, int wv) {
+  a2c_bitonic_merge<K, K / 2>(x, key, lane, wv);
+  if constexpr (K < 2048) a2c_bitonic_levels<2 * K>(x, key, lane, wv);
 }
 
 TOUED_DEV void a2c_sort2048(uint32_t* key, int tid) {
   const int lane = tid & 63, wv = tid >> 6;
-  for (int k = 2; k <= 2048; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const int lj = 31 - __builtin_clz(j);
-      if (j >= 512) {
-        __syncthreads();
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {       // 1024 pairs over 256 threads
-          const int pr = tid + 256 * h;
-          a2c_cmp_swap(key, ((pr >> lj) << (lj + 1)) | (pr & (j - 1)), j, k);
-        }
-        __syncthreads();
-      } else {
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {       // this wave's 256 pairs
-          const int pr = lane + 64 * h;
-          a2c_cmp_swap(key, 512 * wv + (((pr >> lj) << (lj + 1)) | (pr & (j - 1))), j, k);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
-    }
-  }
+  __syncthreads();
+  uint4* kv = reinterpret_cast<uint4*>(key);
+  const int me = (512 * wv + 8 * lane) / 4;
+  const uint4 a = kv[me], b = kv[me + 1];
+  uint32_t x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  a2c_bitonic_levels<2>(x, key, lane, wv);
+  kv[me] = make_uint4(x[0], x[1], x[2], x[3]);
+  kv[me + 1] = make_uint4(x[4], x[5], x[6], x[7]);
   __syncthreads();
 }
 
-// CRITIC_ONLY: the meta-gradient value critic's own update (meta/train.py:61-81 with the reference's discarded
-// `.replace` fixed, --fix_value_critic): the same critic loss and SGD, no actor, no lifetime discard, `step` is
-// the value critic's TrainState step.
+#ifdef A2C_STAMPS
+// timing instrumentation (tools/a2c_stamps.py, built by tools/build_variant.py a2c.hip A2C_STAMPS=1): thread 0 of
+// workgroups < 512 records s_memtime at 7 points of the (last) launch (k_a2c_chain: of its last update, plus the end of
+// the env phase in slot 7)
+__device__ unsigned long long g_a2c_stamps[512 * 8];
+#define A2C_STAMP(ph)                                                                                  \
+  do {                                                                                                 \
+    if (blockIdx.x < 512 && tid == 0) g_a2c_stamps[blockIdx.x * 8 + (ph)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define A2C_STAMP(ph) do {} while (0)
+#endif
+
+// LDS scalars of one fused update
+struct A2CShared {
+  float red[8];
+  float tot[A2C_NV];
+  int has_last;
+};
+
+// The fused update on a staged trajectory after its GAE (closs = the critic loss): per-sample row vectors, the sort,
+// segmented sums, norms, clip + SGD of the touched rows, the step counter and the losses.  sh.has_last must be 0 on
+// entry (the caller clears it before a barrier).  CRITIC_ONLY: the meta-gradient value critic's own update
+// (meta/train.py:61-81 with the reference's discarded `.replace` fixed, --fix_value_critic): the same critic loss
+// and SGD, no actor, no lifetime discard, `step` is the value critic's TrainState step.
 template <bool CRITIC_ONLY>
-__global__ void __launch_bounds__(256) k_a2c_update(int W, int T, int D, float* __restrict__ theta,
-                                                    float* __restrict__ vcrit, const int* __restrict__ tidx,
-                                                    const int* __restrict__ ttime, const uint8_t* __restrict__ tact,
-                                                    const float* __restrict__ trew, const uint8_t* __restrict__ tdone,
-                                                    float gamma, float lam, float ent_coef, float lr_a, float lr_c,
-                                                    float max_norm, int* __restrict__ step,
-                                                    const int* __restrict__ levels, float* __restrict__ loss_out) {
+TOUED_DEV void a2c_update_body(const A2CStage& S, uint32_t* key, float* vec, A2CShared& sh, float closs, int a, int W,
+                               int T, int D, float* __restrict__ theta, float* __restrict__ vcrit, float ent_coef,
+                               float lr_a, float lr_c, float max_norm, int* __restrict__ step,
+                               const int* __restrict__ levels, float* __restrict__ loss_out) {
   constexpr int NV = A2C_NV, CH = A2C_SORT_MAX / 256;
   constexpr uint32_t NONE = 0xFFFFFFFFu, SMASK = 2047u;
-  extern __shared__ float lds[];
-  __shared__ float red[8];
-  __shared__ float tot[NV];
-  __shared__ int has_last;
-  const int a = blockIdx.x, tid = threadIdx.x, TW = W * T;
-  A2CStage S;
-  S.carve(lds, W, T);
-  uint32_t* key = reinterpret_cast<uint32_t*>(lds + A2CStage::floats(W, T));   // [2048]
-  float* vec = reinterpret_cast<float*>(key + A2C_SORT_MAX);                    // [W*T][6]
+  const int tid = threadIdx.x, TW = W * T;
+  float* red = sh.red;
+  float* tot = sh.tot;
+  int& has_last = sh.has_last;
   float* v = vcrit + (size_t)a * D;
   float* th = CRITIC_ONLY ? nullptr : theta + (size_t)a * D * 5;
-  if (tid == 0) has_last = 0;
-  const float closs = a2c_stage(S, a, W, T, D, v, tidx, ttime, trew, tdone, gamma, lam, red);
   // 1) per-sample row vectors -> LDS, sort keys, time-row partial sums, actor loss
   float lastA[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
   if (!CRITIC_ONLY) {
@@ -339,7 +398,6 @@ __global__ void __launch_bounds__(256) k_a2c_update(int W, int T, int D, float* 
     for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
   }
   const float inv_n = 1.0f / (float)TW;
-  const size_t sb = (size_t)a * T * W;
   float part[NV] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, s_al = 0.0f;
   for (int sl = tid; sl < A2C_SORT_MAX; sl += 256) {
     uint32_t kk = NONE;
@@ -352,7 +410,7 @@ __global__ void __launch_bounds__(256) k_a2c_update(int W, int T, int D, float* 
         c = S.cc[sl];
         dvv = -2.0f * S.dv[w * T + t] * inv_n;
       } else {
-        dvv = a2c_sample(S, sl, W, T, th, lastA, tact, sb, ent_coef, inv_n, d, idx, c, al);
+        dvv = a2c_sample(S, sl, W, T, th, lastA, ent_coef, inv_n, d, idx, c, al);
       }
       kk = ((uint32_t)idx << 11) | (uint32_t)sl;
 #pragma unroll
@@ -370,8 +428,10 @@ __global__ void __launch_bounds__(256) k_a2c_update(int W, int T, int D, float* 
     if (tid == 0) tot[j] = r;
   }
   const float al = block_sum(s_al, red) * inv_n;
+  A2C_STAMP(2);
   // 2) sort by (row, sample)
   a2c_sort2048(key, tid);
+  A2C_STAMP(3);
   // 3) segmented sums: thread t sums the runs of its CH sorted entries [CH t, CH t + CH); a run continuing a
   //    segment begun in an earlier chunk leaves its partial in the vector slot of the chunk's first entry; after
   //    a barrier each segment's owner adds those in chunk order.  The final row sum goes to the vector slot of
@@ -437,12 +497,14 @@ __global__ void __launch_bounds__(256) k_a2c_update(int W, int T, int D, float* 
     for (int j = 0; j < 5; ++j) na2 += tot[j] * tot[j];
     nc2 += tot[5] * tot[5];
   }
+  A2C_STAMP(4);
   // 4) clip_by_global_norm + SGD (models/optim.py:5-11), discarded past the lifetime (a2c.py:71-75)
   const float gna = sqrtf(block_sum(na2, red));
   const float gnc = sqrtf(block_sum(nc2, red));
   const int st = step[a];
   const bool applied = CRITIC_ONLY || (st + 1) <= levels[(size_t)a * LEVEL_WORDS + L_LIFETIME];
   const bool clip_a = !(gna < max_norm), clip_c = !(gnc < max_norm);
+  A2C_STAMP(5);
   auto apply_row = [&](int r, const float* g) {
     if (!CRITIC_ONLY) {
 #pragma unroll
@@ -467,6 +529,103 @@ __global__ void __launch_bounds__(256) k_a2c_update(int W, int T, int D, float* 
     loss_out[a * 2 + 0] += al;
     loss_out[a * 2 + 1] += closs;
   }
+  A2C_STAMP(6);
+}
+
+template <bool CRITIC_ONLY>
+__global__ void __launch_bounds__(256) k_a2c_update(int W, int T, int D, float* __restrict__ theta,
+                                                    float* __restrict__ vcrit, const int* __restrict__ tidx,
+                                                    const int* __restrict__ ttime, const uint8_t* __restrict__ tact,
+                                                    const float* __restrict__ trew, const uint8_t* __restrict__ tdone,
+                                                    float gamma, float lam, float ent_coef, float lr_a, float lr_c,
+                                                    float max_norm, int* __restrict__ step,
+                                                    const int* __restrict__ levels, float* __restrict__ loss_out) {
+  extern __shared__ float lds[];
+  __shared__ A2CShared sh;
+  const int a = blockIdx.x, tid = threadIdx.x;
+  A2CStage S;
+  S.carve(lds, W, T);
+  uint32_t* key = reinterpret_cast<uint32_t*>(lds + A2CStage::floats(W, T));   // [2048]
+  float* vec = reinterpret_cast<float*>(key + A2C_SORT_MAX);                    // [W*T][6]
+  if (tid == 0) sh.has_last = 0;
+  A2C_STAMP(0);
+  a2c_load(S, a, W, T, D, vcrit + (size_t)a * D, tidx, ttime, CRITIC_ONLY ? nullptr : tact, trew, tdone);
+  const float closs = a2c_gae(S, W, T, gamma, lam, sh.red);
+  A2C_STAMP(1);
+  a2c_update_body<CRITIC_ONLY>(S, key, vec, sh, closs, a, W, T, D, theta, vcrit, ent_coef, lr_a, lr_c, max_norm, step,
+                               levels, loss_out);
+}
+
+// ---------------------------------------------------------------------------- the A2C chain in one kernel
+// train_a2c_agent's scan (a2c.py:79-125) for one antagonist per 256-thread workgroup, U updates in one launch: per
+// update the env chain of the W workers (threads 0..W-1, state in registers across updates, on the precomputed
+// state-independent draws of toued_rollout_draws: [T][U x n] uint32x4, update u's worker i at column u*n + i)
+// writes the trajectory straight into the LDS stage, then the fused update (the same code as k_a2c_update) runs on
+// it and rewrites the touched rows of the agent's actor/critic tables.  The tables stay in global memory (an
+// obs_dim = 3201 table pair is 77 KB; two workgroups share a CU's LDS), read back by the next rollout after the
+// workgroup barrier.  Bit-identical to toued_rollout_env + toued_a2c_update per update
+// (tests/test_gpu_plr.py::test_a2c_chain_matches_launch_per_update).
+template <int NMAX>
+__global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __restrict__ levels, int W, int T, int D,
+                                                   int U, float* __restrict__ theta, float* __restrict__ vcrit,
+                                                   int* __restrict__ state, const uint4* __restrict__ draws,
+                                                   long dstride, float gamma, float lam, float ent_coef, float lr_a,
+                                                   float lr_c, float max_norm, int* __restrict__ step,
+                                                   float* __restrict__ loss_out) {
+  extern __shared__ float lds[];
+  __shared__ A2CShared sh;
+  const int a = blockIdx.x, tid = threadIdx.x, n = (int)gridDim.x * W;
+  A2CStage S;
+  S.carve(lds, W, T);
+  uint32_t* key = reinterpret_cast<uint32_t*>(lds + A2CStage::floats(W, T));   // [2048]
+  float* vec = reinterpret_cast<float*>(key + A2C_SORT_MAX);                    // [W*T][6]
+  const float* tab = theta + (size_t)a * D * 5;
+  const float* v = vcrit + (size_t)a * D;
+  const bool env = tid < W;
+  const int i = a * W + tid;
+  TrainWorker<NMAX> wk;
+  if (env) wk.init(sp, levels, a, theta, D, state, n, i);
+  for (int u = 0; u < U; ++u) {
+    if (tid == 0) sh.has_last = 0;
+    if (u == U - 1) A2C_STAMP(0);
+    if (env) {
+      wk.load_rows(tab, D);
+      const draw4* dr = reinterpret_cast<const draw4*>(draws) + (size_t)u * n + i;
+      draw4 dr0 = {0u, 0u, 0u, 0u};
+      if (T > 0) dr0 = dr[0];
+      draw4 dr1 = dr0;
+      if (T > 1) dr1 = dr[dstride];
+      for (int t = 0; t < T; ++t) {
+        const draw4 d = dr0;
+        dr0 = dr1;
+        if (t + 2 < T) dr1 = dr[(size_t)(t + 2) * dstride];
+        int oi, ot, action;
+        float rew;
+        bool done;
+        wk.step(sp, tab, d, oi, ot, action, rew, done);
+        S.ix[t * W + tid] = oi;
+        S.cc[t * W + tid] = (float)ot * 0.001f;
+        S.act[t * W + tid] = (uint8_t)action;
+        S.rw[t * W + tid] = rew;
+        S.nd[t * W + tid] = done ? 0.0f : 1.0f;
+      }
+      S.ix[T * W + tid] = wk.idx;
+      S.cc[T * W + tid] = (float)wk.s.time * 0.001f;
+    }
+    if (u == U - 1) A2C_STAMP(7);
+    __syncthreads();
+    {   // V(obs) for every observation (a2c_load's gather)
+      const float vlast = v[D - 1];
+      for (int j = tid; j < (T + 1) * W; j += blockDim.x) S.vt[j] = v[S.ix[j]] + S.cc[j] * vlast;
+    }
+    __syncthreads();
+    const float closs = a2c_gae(S, W, T, gamma, lam, sh.red);
+    if (u == U - 1) A2C_STAMP(1);
+    a2c_update_body<false>(S, key, vec, sh, closs, a, W, T, D, theta, vcrit, ent_coef, lr_a, lr_c, max_norm, step,
+                           levels, loss_out);
+    __syncthreads();   // the rewritten rows and the step counter before the next rollout reads them
+  }
+  if (env) store_state<NMAX>(state, n, i, wk.s);
 }
 
 static size_t a2c_update_lds(int W, int T) {
@@ -474,6 +633,12 @@ static size_t a2c_update_lds(int W, int T) {
 }
 
 extern "C" {
+
+#ifdef A2C_STAMPS
+int toued_dbg_a2c_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_a2c_stamps), sizeof(g_a2c_stamps)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 int toued_key_chain(const uint32_t* keys, int n, int U, uint32_t* out, hipStream_t stream) {
   TOUED_REQUIRE(n >= 0 && U >= 0, "toued_key_chain: bad sizes");
@@ -521,6 +686,50 @@ int toued_a2c_update(int N, int W, int T, int D, float* theta, float* vcrit, con
   }
   hipLaunchKernelGGL(k_a2c_update<false>, dim3(N), dim3(256), lds, stream, W, T, D, theta, vcrit, tidx, ttime, tact,
                      trew, tdone, gamma, lam, ent_coef, lr_a, lr_c, max_norm, step, levels, loss_out);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+// 1 when toued_a2c_chain supports these sizes: the fused update's and W <= 256 workers (one per thread)
+int toued_a2c_chain_fits(int W, int T, int D) { return W <= 256 && toued_a2c_update_fits(W, T, D) ? 1 : 0; }
+
+// U A2C updates (rollout + fused update each) of N antagonists in one launch: theta [N][D][5], vcrit [N][D], step
+// [N], state [S_FIELDS][N*W] updated in place, loss_out [N][2] accumulated; draws = toued_rollout_draws' output for
+// U batches ([T][dstride] uint32x4, update u's worker i at column u*N*W + i)
+int toued_a2c_chain(EnvSpec sp, const int* levels, int N, int W, int T, int D, int U, float* theta, float* vcrit,
+                    int* state, const uint32_t* draws, long dstride, float gamma, float lam, float ent_coef, float lr_a,
+                    float lr_c, float max_norm, int* step, float* loss_out, hipStream_t stream) {
+  TOUED_REQUIRE(sp.tabular && sp.n_max >= 1 && sp.n_max <= 5 && sp.max_grid >= 1 && sp.max_grid * sp.max_grid <= 256,
+                "toued_a2c_chain: tabular env spec required");
+  TOUED_REQUIRE(N >= 0 && U >= 0 && toued_a2c_chain_fits(W, T, D), "toued_a2c_chain: N=%d U=%d W=%d T=%d D=%d unsupported",
+                N, U, W, T, D);
+  TOUED_REQUIRE(D == sp.max_grid * sp.max_grid * (1 << sp.n_max) + 1, "toued_a2c_chain: D=%d != obs_dim", D);
+  TOUED_REQUIRE((double)N * D * 20.0 < 4294967295.0, "toued_a2c_chain: actor tables (%d x %d rows) exceed 4 GiB", N, D);
+  TOUED_REQUIRE(dstride >= (long)U * N * W, "toued_a2c_chain: draw stride %ld < %ld", dstride, (long)U * N * W);
+  if (N == 0 || U == 0) return 0;
+  const size_t lds = a2c_update_lds(W, T);
+  static bool attr_set[6] = {false, false, false, false, false, false};
+#define TOUED_A2C_CHAIN_CASE(NM)                                                                                     \
+  case NM: {                                                                                                          \
+    if (!attr_set[NM]) {                                                                                              \
+      TOUED_REQUIRE(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_a2c_chain<NM>),                              \
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) == hipSuccess,        \
+                    "toued_a2c_chain: cannot raise the dynamic LDS limit");                                           \
+      attr_set[NM] = true;                                                                                            \
+    }                                                                                                                 \
+    hipLaunchKernelGGL(k_a2c_chain<NM>, dim3(N), dim3(256), lds, stream, sp, levels, W, T, D, U, theta, vcrit, state, \
+                       reinterpret_cast<const uint4*>(draws), dstride, gamma, lam, ent_coef, lr_a, lr_c, max_norm,    \
+                       step, loss_out);                                                                               \
+  } break;
+  switch (sp.n_max) {
+    TOUED_A2C_CHAIN_CASE(1)
+    TOUED_A2C_CHAIN_CASE(2)
+    TOUED_A2C_CHAIN_CASE(3)
+    TOUED_A2C_CHAIN_CASE(4)
+    TOUED_A2C_CHAIN_CASE(5)
+    default: break;
+  }
+#undef TOUED_A2C_CHAIN_CASE
   TOUED_CHECK_LAUNCH();
   return 0;
 }

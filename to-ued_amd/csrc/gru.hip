@@ -605,11 +605,11 @@ TOUED_DEV floatx16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx16 c)
 
 #ifdef FWD_STAMPS
 // timing instrumentation (tools/fwd_stamps.py, built by tools/build_variant.py gru.hip FWD_STAMPS=1): thread 0 of
-// workgroups < 64 records s_memtime at 6 points of every step of the SAVE instance
+// workgroups < 64 records s_memtime at 6 points of every step (of the last launch of either instance)
 __device__ unsigned long long g_fwd_stamps[64 * 32 * 6];
 #define FWD_STAMP(ph)                                                                                  \
   do {                                                                                                 \
-    if (SAVE && blockIdx.x < 64 && tid == 0 && s < 32)                                                 \
+    if (blockIdx.x < 64 && tid == 0 && s < 32)                                                         \
       g_fwd_stamps[(blockIdx.x * 32 + s) * 6 + (ph)] = __builtin_amdgcn_s_memtime();                   \
   } while (0)
 #else

@@ -46,6 +46,8 @@ _SIGS = {
     "toued_batch_reset_masked": [EnvSpecC, _P, _P, _I, _I, _P, _P, _P, _P, _P],
     "toued_rollout": [EnvSpecC, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "toued_eval_keys": [_P, _I, _I, _I, _P, _P],
+    "toued_rollout_draws": [EnvSpecC, _P, _P, _I, _I, _I, _I, _P, _P, _P],
+    "toued_rollout_env": [EnvSpecC, _P, _P, _I, _P, _I, _I, _I, _P, _L, _P, _P, _P, _P, _P, _P, _P],
     "toued_eval_draws": [EnvSpecC, _P, _I, _I, _I, _P, _P, _P],
     "toued_eval_returns": [EnvSpecC, _P, _P, _I, _P, _I, _I, _I, _P, _P, _P],
     "toued_meta_keys": [_P, _I, _I, _P, _P, _P, _P, _P],
@@ -80,6 +82,8 @@ _SIGS = {
     "toued_a2c_apply": [_I, _I, _P, _P, _P, _P, _F, _F, _F, _P, _P, _P],
     "toued_a2c_update_fits": [_I, _I, _I],
     "toued_a2c_update": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _F, _P, _P, _P, _P],
+    "toued_a2c_chain_fits": [_I, _I, _I],
+    "toued_a2c_chain": [EnvSpecC, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _P, _P, _P],
     "toued_gru_pack_fwd_multi": [_P, _L, _I, _P, _I, _P, _P],
     "toued_gru_fwd_multi": [_I, _I, _I, _I, _I, _P, _L, _L, _P, _P, _P, _L, _P, _P, _P, _P],
     "toued_es_ask": [_P, _L, _L, _L, _L, _P, _F, _P, _P],

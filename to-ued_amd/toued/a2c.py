@@ -11,6 +11,7 @@ hundreds of small launches per regret evaluation cost one graph launch.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -18,7 +19,11 @@ import torch
 from . import _lib
 from .agents import AgentHyperparams
 from .env import LEVEL_WORDS
-from .rollout import RolloutWrapper, Transition
+from .rollout import RolloutWrapper, Transition, split_rollouts
+
+
+# updates whose rollout draws are produced by one toued_rollout_draws call (32 x N x W x T x 16 B of scratch)
+DRAW_CHUNK = 32
 
 
 @dataclass
@@ -31,13 +36,16 @@ class A2CHyperparams:
 
 class A2CTrainer:
     def __init__(self, ro: RolloutWrapper, hyp: A2CHyperparams, agent_hypers: AgentHyperparams,
-                 use_graph: bool = True, fused: bool | None = None):
+                 use_graph: bool = True, fused: bool | None = None, chain: bool | None = None):
         agent_hypers.check_supported()
         self.ro = ro
         self.hyp = hyp
         self.ah = agent_hypers
         self.use_graph = use_graph
         self.fused = fused          # None: the LDS-fused update whenever it fits (toued_a2c_update_fits)
+        # None: the whole update chain in one kernel per DRAW_CHUNK updates (toued_a2c_chain) whenever it fits and
+        # the rollouts are split (unless TOUED_A2C_CHAIN=0); False: one rollout + one update launch per update
+        self.chain = chain
         self._bufs = None
         self._graph = None
         self._graph_key = None
@@ -59,6 +67,9 @@ class A2CTrainer:
                              z(n, T, W, dt=torch.uint8), z(n, T, W), z(n, T, W, dt=torch.uint8)),
             "Ga": z(n, D, 5), "Gv": z(n, D), "loss": z(n, 2),
             "chain": z(U, n, 2, dt=torch.int32),
+            # rollout draws of DRAW_CHUNK updates (split_rollouts): key-chain scratch and draws [T][chunk * n * W][4]
+            "dbuf": (z(T, min(U, DRAW_CHUNK) * n * W, 4, dt=torch.int32), z(T, min(U, DRAW_CHUNK) * n * W, 4,
+                                                                               dt=torch.int32)),
             # graph-static inputs
             "rng": z(n, 2, dt=torch.int32), "theta": z(n, D, 5), "vcrit": z(n, D),
             "step": z(n, dt=torch.int32), "levels": z(n, LEVEL_WORDS, dt=torch.int32),
@@ -67,6 +78,35 @@ class A2CTrainer:
         self._graph = None
         return self._bufs
 
+    def use_chain(self, W, T, D) -> bool:
+        if self.chain is False or os.environ.get("TOUED_A2C_CHAIN") == "0" or not split_rollouts():
+            return False
+        if self.fused is False:
+            return False
+        return bool(_lib.lib().toued_a2c_chain_fits(W, T, D))
+
+    def _chain_updates(self, b, n, D, W, T, U, tm):
+        """All U updates as toued_a2c_chain launches of DRAW_CHUNK updates each, every chunk on its precomputed draws."""
+        L = _lib
+        st = L.stream_ptr()
+        lr_a, lr_c, mn = self.ah.actor_learning_rate, self.ah.critic_learning_rate, self.ah.max_grad_norm
+        ch = min(U, DRAW_CHUNK)
+        for u in range(0, U, ch):
+            m = min(ch, U - u)
+            tok = tm.start("a2c_draws") if tm is not None else None
+            keys = b["chain"][u:u + m]
+            if m < ch:      # the last chunk: its unused key rows are never rolled
+                keys = torch.cat([keys, b["chain"][:ch - m]])
+            draws = self.ro.train_draws(keys, b["levels"], W, b["dbuf"])
+            if tm is not None:
+                tm.stop(tok)
+                tok = tm.start("a2c_chain")
+            L.call("toued_a2c_chain", self.ro._c, L.ptr(b["levels"]), n, W, T, D, m, L.ptr(b["theta"]),
+                   L.ptr(b["vcrit"]), L.ptr(b["state"]), L.ptr(draws), draws.shape[1], self.hyp.gamma,
+                   self.hyp.gae_lambda, self.hyp.entropy_coeff, lr_a, lr_c, mn, L.ptr(b["step"]), L.ptr(b["loss"]), st)
+            if tm is not None:
+                tm.stop(tok)
+
     def _updates(self, b, n, D, W, T, U, record=None):
         L = _lib
         st = L.stream_ptr()
@@ -74,18 +114,38 @@ class A2CTrainer:
         if U == 0:
             return
         L.call("toued_key_chain", L.ptr(b["rng"]), n, U, L.ptr(b["chain"]), st)
+        tm = self.timers if self.timers is not None and self.timers.enabled else None
+        if record is None and self.use_chain(W, T, D):
+            self._chain_updates(b, n, D, W, T, U, tm)
+            return
         tr = b["tr"]
         lr_a, lr_c, mn = self.ah.actor_learning_rate, self.ah.critic_learning_rate, self.ah.max_grad_norm
         fits = bool(L.lib().toued_a2c_update_fits(W, T, D))
         fused = fits if self.fused is None else (self.fused and fits)
-        tm = self.timers if self.timers is not None and self.timers.enabled else None
+        split = split_rollouts()
+        draws, d0 = None, 0
         for u in range(U):
             if record is not None:
                 before = (b["theta"].clone(), b["vcrit"].clone(), b["step"].clone())
+            if split and (draws is None or u - d0 >= DRAW_CHUNK):
+                # every state-independent draw of the next DRAW_CHUNK updates' rollouts at once (their keys are the
+                # update key chain): U x N x W independent key chains instead of one dependent chain per update
+                d0 = u
+                tok = tm.start("a2c_draws") if tm is not None else None
+                ch = min(U, DRAW_CHUNK)
+                keys = b["chain"][u:u + ch]
+                if keys.shape[0] < ch:      # the last chunk: its unused key rows are never rolled
+                    keys = torch.cat([keys, b["chain"][:ch - keys.shape[0]]])
+                draws = self.ro.train_draws(keys, b["levels"], W, b["dbuf"])
+                if tm is not None:
+                    tm.stop(tok)
             tok = tm.start("a2c_rollout") if tm is not None else None
-            L.call("toued_rollout", self.ro._c, L.ptr(b["levels"]), L.ptr(b["theta"]), D, L.ptr(b["chain"][u]),
-                   L.ptr(b["state"]), n, W, T, L.ptr(tr.obs_idx), L.ptr(tr.obs_time), L.ptr(tr.action),
-                   L.ptr(tr.reward), L.ptr(tr.done), None, st)
+            if split:
+                self.ro.rollout_from_draws(draws, u - d0, b["theta"], b["levels"], b["state"], tr)
+            else:
+                L.call("toued_rollout", self.ro._c, L.ptr(b["levels"]), L.ptr(b["theta"]), D, L.ptr(b["chain"][u]),
+                       L.ptr(b["state"]), n, W, T, L.ptr(tr.obs_idx), L.ptr(tr.obs_time), L.ptr(tr.action),
+                       L.ptr(tr.reward), L.ptr(tr.done), None, st)
             if tm is not None:
                 tm.stop(tok)
                 tok = tm.start("a2c_update")

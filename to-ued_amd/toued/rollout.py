@@ -12,6 +12,8 @@ without the agent axis, as ``RolloutWrapper.batch_reset(rng, env_params, num_wor
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 
 import torch
@@ -32,6 +34,12 @@ class Transition:
     action: torch.Tensor
     reward: torch.Tensor
     done: torch.Tensor
+
+
+def split_rollouts() -> bool:
+    """Train rollouts as draws + env chain (toued_rollout_draws / toued_rollout_env) unless TOUED_ROLLOUT_FUSED=1
+    (the single-kernel toued_rollout; bit-identical)."""
+    return os.environ.get("TOUED_ROLLOUT_FUSED") != "1"
 
 
 class RolloutWrapper:
@@ -108,10 +116,53 @@ class RolloutWrapper:
                 torch.empty((N, T, W), dtype=torch.uint8, device=dev),
             )
         cum = torch.empty((N, W), dtype=torch.float32, device=dev)
-        _lib.call("toued_rollout", self._c, _lib.ptr(levels), _lib.ptr(theta), D, _lib.ptr(agent_keys.contiguous()),
-                  _lib.ptr(state), N, W, T, _lib.ptr(out.obs_idx), _lib.ptr(out.obs_time), _lib.ptr(out.action),
-                  _lib.ptr(out.reward), _lib.ptr(out.done), _lib.ptr(cum), _lib.stream_ptr())
+        if eval or not split_rollouts():
+            _lib.call("toued_rollout", self._c, _lib.ptr(levels), _lib.ptr(theta), D,
+                      _lib.ptr(agent_keys.contiguous()), _lib.ptr(state), N, W, T, _lib.ptr(out.obs_idx),
+                      _lib.ptr(out.obs_time), _lib.ptr(out.action), _lib.ptr(out.reward), _lib.ptr(out.done),
+                      _lib.ptr(cum), _lib.stream_ptr())
+            return out, state, cum
+        draws = self.train_draws(agent_keys.view(1, N, 2), levels, W)
+        self.rollout_from_draws(draws, 0, theta, levels, state, out, cum)
         return out, state, cum
+
+    def train_draws(self, keys: torch.Tensor, levels: torch.Tensor, n_workers: int,
+                    bufs: tuple[torch.Tensor, torch.Tensor] | None = None) -> torch.Tensor:
+        """The state-independent draws of U batches of train rollouts (toued_rollout_draws): keys [U, N, 2] (batch u's
+        rollout keys), levels [N, words].  Returns u32 [T, U * N * W, 4]: in ``bufs`` = (chain scratch, draws), each
+        at least [T, U * N * W, 4] (the step stride is theirs), or in a buffer of this wrapper reused by the next
+        call of the same shape."""
+        U, N = keys.shape[0], keys.shape[1]
+        T, W = self.train_rollout_len, n_workers
+        n = U * N * W
+        if bufs is not None:
+            chain, draws = bufs
+            if chain.shape[0] < T or chain.shape[1] < n or draws.shape != chain.shape:
+                raise ValueError(f"train_draws: buffers {tuple(chain.shape)} for T={T}, {n} workers")
+            n = chain.shape[1]
+        else:
+            key = (T, n, str(levels.device))
+            if getattr(self, "_draw_bufs", None) is None or self._draw_bufs[0] != key:
+                self._draw_bufs = (key, torch.empty((T, n, 4), dtype=torch.int32, device=levels.device),
+                                   torch.empty((T, n, 4), dtype=torch.int32, device=levels.device))
+            _, chain, draws = self._draw_bufs
+        if n != U * N * W:
+            raise ValueError("train_draws: the buffers' worker stride must equal U * N * W")
+        _lib.call("toued_rollout_draws", self._c, _lib.ptr(levels), _lib.ptr(keys.contiguous()), N, U, W, T,
+                  _lib.ptr(chain), _lib.ptr(draws), _lib.stream_ptr())
+        return draws
+
+    def rollout_from_draws(self, draws: torch.Tensor, u: int, theta: torch.Tensor, levels: torch.Tensor,
+                           state: torch.Tensor, out: Transition, cum: torch.Tensor | None = None):
+        """Batch u of train_draws' rollouts (toued_rollout_env): trajectories into ``out``, ``state`` advanced in place;
+        bit-identical to toued_rollout with the same keys."""
+        N = theta.shape[0]
+        n = state.shape[1]
+        T = self.train_rollout_len
+        _lib.call("toued_rollout_env", self._c, _lib.ptr(levels), _lib.ptr(theta), theta.shape[1], _lib.ptr(state), N,
+                  n // N, T, _lib.ptr(draws) + 16 * u * n, draws.shape[1], _lib.ptr(out.obs_idx),
+                  _lib.ptr(out.obs_time), _lib.ptr(out.action), _lib.ptr(out.reward), _lib.ptr(out.done),
+                  _lib.ptr(cum) if cum is not None else None, _lib.stream_ptr())
 
     def eval_draws(self, agent_keys: torch.Tensor, levels: torch.Tensor, n_workers: int,
                    buf: torch.Tensor | None = None) -> torch.Tensor:

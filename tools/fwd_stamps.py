@@ -3,10 +3,11 @@
     python tools/build_variant.py gru.hip FWD_STAMPS=1
     TOUED_LIB=to-ued_amd/exp/libtoued_FWD_STAMPS_1.so python tools/fwd_stamps.py
 
-Runs the C2-shape forward (512 agents x 64 workers, T = 20) and prints, for the first 64 workgroups, the mean
-shader-clock cycles of each phase of a step: contraction issue (16 fp16 carry k-steps + the augmented k-step),
-the barrier behind it (MFMA drain + wave skew), gate maths + saves + head partials, the head barrier, the head
-reduction + softmax tail; and the whole step."""
+Runs the C2-shape forward (512 agents x 64 workers, T = 20; with --multi the C4 per-candidate forward: 1024
+candidates x 64 workers, F = 7, no saves) and prints, for the first 64 workgroups, the mean shader-clock cycles of
+each phase of a step: contraction issue (16 fp16 carry k-steps + the augmented k-step), the barrier behind it (MFMA
+drain + wave skew), gate maths + saves + head partials, the head barrier, the head reduction + softmax tail; and the
+whole step."""
 import ctypes
 import json
 import sys
@@ -22,19 +23,35 @@ import torch  # noqa: E402
 def main():
     from toued import _lib
     from toued.lpg import LPGGRU, LPGLayout, init_lpg_params
-    N, W, T, K, F = 512, 64, 20, 1, 5
+    multi = "--multi" in sys.argv
+    N, W, T, K, F = (1024, 64, 20, 1, 7) if multi else (512, 64, 20, 1, 5)
     R = N * W
     lay = LPGLayout(F)
     eta = init_lpg_params(0, F)
-    gru = LPGGRU(lay, R, T, K, W, "cuda")
-    gru.pack(eta)
     g = torch.Generator(device="cuda").manual_seed(0)
-    gru.X.copy_(torch.randn(gru.X.shape, generator=g, device="cuda"))
-    done = (torch.rand((K, N, T, W), generator=g, device="cuda") < 0.05).to(torch.uint8)
-    pi_hat = torch.zeros(K, T, R, device="cuda")
-    y_hat = torch.zeros(K, T, 8, R, device="cuda")
-    for _ in range(3):
-        gru.forward(0, gru.X, done[0], eta, pi_hat, y_hat)
+    if multi:
+        L = _lib
+        nd = lay.size
+        x = (eta.reshape(1, nd) + 0.01 * torch.randn((N, nd), generator=g, device="cuda")).contiguous()
+        fwdA = torch.zeros((N, L.lib().toued_gru_packed_floats(2)), device="cuda")
+        X = torch.randn((F, T, R), generator=g, device="cuda")
+        done = (torch.rand((N, T, W), generator=g, device="cuda") < 0.05).to(torch.uint8)
+        pi_hat = torch.zeros(T, R, device="cuda")
+        y_hat = torch.zeros(T, 8, R, device="cuda")
+        st = L.stream_ptr()
+        L.call("toued_gru_pack_fwd_multi", L.ptr(x), nd, N, lay.c_offsets, F, L.ptr(fwdA), st)
+        for _ in range(3):
+            L.call("toued_gru_fwd_multi", R, T, W, F, W, L.ptr(X), T * R, 1, L.ptr(done), L.ptr(fwdA), L.ptr(x), nd,
+                   lay.c_offsets, L.ptr(pi_hat), L.ptr(y_hat), st)
+    else:
+        gru = LPGGRU(lay, R, T, K, W, "cuda")
+        gru.pack(eta)
+        gru.X.copy_(torch.randn(gru.X.shape, generator=g, device="cuda"))
+        done = (torch.rand((K, N, T, W), generator=g, device="cuda") < 0.05).to(torch.uint8)
+        pi_hat = torch.zeros(K, T, R, device="cuda")
+        y_hat = torch.zeros(K, T, 8, R, device="cuda")
+        for _ in range(3):
+            gru.forward(0, gru.X, done[0], eta, pi_hat, y_hat)
     torch.cuda.synchronize()
     buf = np.zeros(64 * 32 * 6, np.uint64)
     fn = _lib.lib().toued_dbg_fwd_stamps
