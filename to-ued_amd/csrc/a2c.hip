@@ -15,6 +15,9 @@
 // Trajectory layout as the rollout kernel writes it: idx/time [N][T+1][W], act/done/rew [N][T][W].
 #include "env_dev.h"
 
+#include <cstdlib>
+#include <cstring>
+
 #define EPSF 1e-8f
 
 namespace {
@@ -35,6 +38,27 @@ TOUED_DEV float block_sum(float v, float* red) {
   float s = 0.0f;
   for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
   return s;
+}
+
+// Block-wide sums of N values at once (256-thread blocks, red >= 4 N floats): one barrier pair instead of N; the
+// same summation order as N block_sum calls.
+template <int N>
+TOUED_DEV void block_sum_n(float (&v)[N], float* red) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) v[j] = wave_sum(v[j]);
+  const int wv = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) red[wv * N + j] = v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    float s = 0.0f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i * N + j];
+    v[j] = s;
+  }
 }
 
 // Staged trajectory of one agent in LDS and the quantities every sample's gradient needs.
@@ -115,8 +139,10 @@ TOUED_DEV float a2c_gae(const A2CStage& S, int W, int T, float gamma, float lam,
     s_cl += cl / (float)T;
   }
   const float n = (float)(W * T);
-  const float mean = block_sum(s_adv, red) / n;
-  const float closs = block_sum(s_cl, red) / (float)W;
+  float ms[2] = {s_adv, s_cl};
+  block_sum_n<2>(ms, red);
+  const float mean = ms[0] / n;
+  const float closs = ms[1] / (float)W;
   float s_var = 0.0f;
   for (int i = tid; i < W * T; i += blockDim.x) {
     const float d = S.adv[i] - mean;
@@ -135,15 +161,14 @@ TOUED_DEV float a2c_gae(const A2CStage& S, int W, int T, float gamma, float lam,
 // Sample i = t*W + w of the staged agent: actor row cotangent d[5] (policy term through the [T,T] broadcast plus
 // the entropy bonus of pi + 1e-8, a2c.py:52-63), critic row cotangent (returned), the row, the time coefficient
 // and this sample's actor-loss term.
-TOUED_DEV float a2c_sample(const A2CStage& S, int i, int W, int T, const float* __restrict__ th,
-                           const float* lastA, float ent_coef, float inv_n, float* d, int& idx, float& c, float& al) {
+TOUED_DEV float a2c_sample(const A2CStage& S, int i, int W, int T, const float* thr, const float* lastA, float ent_coef,
+                           float inv_n, float* d, float& c, float& al) {
   const int t = i / W, w = i - t * W;
-  idx = S.ix[i];
   c = S.cc[i];
   const int act = S.act[i];
   float l[5], p[5], m = -__builtin_inff();
 #pragma unroll
-  for (int j = 0; j < 5; ++j) { l[j] = th[(size_t)idx * 5 + j] + c * lastA[j]; m = fmaxf(m, l[j]); }
+  for (int j = 0; j < 5; ++j) { l[j] = thr[j] + c * lastA[j]; m = fmaxf(m, l[j]); }
   float z = 0.0f;
 #pragma unroll
   for (int j = 0; j < 5; ++j) { p[j] = __expf(l[j] - m); z += p[j]; }
@@ -207,9 +232,11 @@ __global__ void __launch_bounds__(256) k_a2c_grad(int W, int T, int D, const flo
   const float inv_n = 1.0f / (float)(W * T);
   float accA[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, accV = 0.0f, s_al = 0.0f;
   for (int i = tid; i < W * T; i += blockDim.x) {
-    float d[5], c, al;
-    int idx;
-    const float dvv = a2c_sample(S, i, W, T, th, lastA, ent_coef, inv_n, d, idx, c, al);
+    float d[5], c, al, thr[5];
+    const int idx = S.ix[i];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) thr[j] = th[(size_t)idx * 5 + j];
+    const float dvv = a2c_sample(S, i, W, T, thr, lastA, ent_coef, inv_n, d, c, al);
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
       atomicAdd(&ga[(size_t)idx * 5 + j], d[j]);
@@ -368,9 +395,11 @@ __device__ unsigned long long g_a2c_stamps[512 * 8];
 
 // LDS scalars of one fused update
 struct A2CShared {
-  float red[8];
+  float red[4 * (A2C_NV + 1)];
   float tot[A2C_NV];
   int has_last;
+  int scan_a[4];              // the segmented scan's per-wave totals
+  float scan_b[4][A2C_NV];
 };
 
 // The fused update on a staged trajectory after its GAE (closs = the critic loss): per-sample row vectors, the sort,
@@ -391,106 +420,168 @@ TOUED_DEV void a2c_update_body(const A2CStage& S, uint32_t* key, float* vec, A2C
   int& has_last = sh.has_last;
   float* v = vcrit + (size_t)a * D;
   float* th = CRITIC_ONLY ? nullptr : theta + (size_t)a * D * 5;
-  // 1) per-sample row vectors -> LDS, sort keys, time-row partial sums, actor loss
+  // 1) per-sample row vectors -> LDS, sort keys, time-row partial sums, actor loss.  Thread t's samples
+  //    sl = t + 256 h: their actor rows are gathered up front (eight independent loads in flight, not one per sample)
+  const int lane = tid & 63, wv = tid >> 6;
   float lastA[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
   if (!CRITIC_ONLY) {
 #pragma unroll
     for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
   }
   const float inv_n = 1.0f / (float)TW;
-  float part[NV] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, s_al = 0.0f;
-  for (int sl = tid; sl < A2C_SORT_MAX; sl += 256) {
+  int sidx[CH];
+  float trow[CH][5];
+#pragma unroll
+  for (int h = 0; h < CH; ++h) {
+    const int sl = tid + 256 * h;
+    sidx[h] = sl < TW ? S.ix[sl] : 0;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) trow[h][j] = (!CRITIC_ONLY && sl < TW) ? th[(size_t)sidx[h] * 5 + j] : 0.0f;
+  }
+  float acc[NV + 1] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};   // time-row partials [NV], actor loss
+#pragma unroll
+  for (int h = 0; h < CH; ++h) {
+    const int sl = tid + 256 * h;
     uint32_t kk = NONE;
     if (sl < TW) {
       float d[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, c, al = 0.0f, dvv;
-      int idx;
+      const int idx = sidx[h];
       if (CRITIC_ONLY) {
         const int t = sl / W, w = sl - t * W;
-        idx = S.ix[sl];
         c = S.cc[sl];
         dvv = -2.0f * S.dv[w * T + t] * inv_n;
       } else {
-        dvv = a2c_sample(S, sl, W, T, th, lastA, ent_coef, inv_n, d, idx, c, al);
+        dvv = a2c_sample(S, sl, W, T, trow[h], lastA, ent_coef, inv_n, d, c, al);
       }
       kk = ((uint32_t)idx << 11) | (uint32_t)sl;
 #pragma unroll
-      for (int j = 0; j < 5; ++j) { vec[sl * NV + j] = d[j]; part[j] += c * d[j]; }
+      for (int j = 0; j < 5; ++j) { vec[sl * NV + j] = d[j]; acc[j] += c * d[j]; }
       vec[sl * NV + 5] = dvv;
-      part[5] += c * dvv;
-      s_al += al;
+      acc[5] += c * dvv;
+      acc[NV] += al;
       if (idx == D - 1) has_last = 1;
     }
     key[sl] = kk;
   }
+  block_sum_n<NV + 1>(acc, red);
+  if (tid == 0) {
 #pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    const float r = block_sum(part[j], red);
-    if (tid == 0) tot[j] = r;
+    for (int j = 0; j < NV; ++j) tot[j] = acc[j];
   }
-  const float al = block_sum(s_al, red) * inv_n;
+  const float al = acc[NV] * inv_n;
   A2C_STAMP(2);
   // 2) sort by (row, sample)
   a2c_sort2048(key, tid);
   A2C_STAMP(3);
-  // 3) segmented sums: thread t sums the runs of its CH sorted entries [CH t, CH t + CH); a run continuing a
-  //    segment begun in an earlier chunk leaves its partial in the vector slot of the chunk's first entry; after
-  //    a barrier each segment's owner adds those in chunk order.  The final row sum goes to the vector slot of
-  //    the segment's first sample (read only by its owner) and its square into the norm partials.
-  float na2 = 0.0f, nc2 = 0.0f;
-  auto emit = [&](uint32_t row, uint32_t first, float (&sum)[NV]) {
-    if ((int)row == D - 1) {
+  // 3) segmented row sums, deterministic (a fixed combination tree).  Thread t owns the sorted entries
+  //    [CH t, CH t + CH) as runs of equal rows.  The part of a segment lying in earlier chunks (the carry) reaches the
+  //    chunk where the segment ends through a segmented scan over the 256 chunks: carry_t = a_t carry_{t-1} + b_t,
+  //    b_t = the sum of chunk t's last run, a_t = 1 iff chunk t is one run continuing chunk t-1's segment.  Each
+  //    segment's sum goes to the vector slot of its LAST entry; that entry's thread applies it.
+  auto rowof = [](uint32_t k) { return k == NONE ? NONE : (k >> 11); };
+  uint32_t kc[CH];
+  {
+    const uint4* kv = reinterpret_cast<const uint4*>(key) + 2 * tid;
+    const uint4 x0 = kv[0], x1 = kv[1];
+    kc[0] = x0.x; kc[1] = x0.y; kc[2] = x0.z; kc[3] = x0.w;
+    kc[4] = x1.x; kc[5] = x1.y; kc[6] = x1.z; kc[7] = x1.w;
+  }
+  const uint32_t prow = tid == 0 ? NONE : rowof(key[CH * tid - 1]);
+  const uint32_t nrow = tid == 255 ? NONE : rowof(key[CH * tid + CH]);
+  uint32_t endm = 0u;   // bit e: a segment ends at entry e
 #pragma unroll
-      for (int j = 0; j < NV; ++j) sum[j] += tot[j];
-    }
-    float* slot = vec + (size_t)(first & SMASK) * NV;
+  for (int e = 0; e < CH; ++e) {
+    const uint32_t r = rowof(kc[e]);
+    const uint32_t rn = e < CH - 1 ? rowof(kc[e + 1]) : nrow;
+    if (r != NONE && rn != r) endm |= 1u << e;
+  }
+  // pass 1: the last run's sum b_t and a_t
+  float sb[NV] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  const uint32_t r0 = rowof(kc[0]);
+  int sa = (r0 != NONE && prow == r0) ? 1 : 0;
+  {
+    uint32_t lr = r0;
 #pragma unroll
-    for (int j = 0; j < NV; ++j) slot[j] = sum[j];
+    for (int e = 0; e < CH; ++e) {
+      const uint32_t r = rowof(kc[e]);
+      if (r != lr) {
+        sa = 0;
+        lr = r;
 #pragma unroll
-    for (int j = 0; j < 5; ++j) na2 += sum[j] * sum[j];
-    nc2 += sum[5] * sum[5];
-  };
-  const int i0 = CH * tid, i1 = min(i0 + CH, TW);
-  float run[NV];
-  uint32_t run_row = NONE, run_first = NONE, pend_row = NONE, pend_first = NONE;
-  bool run_owned = false;
-  for (int e = i0; e <= i1; ++e) {
-    const uint32_t ke = e < i1 ? key[e] : NONE;
-    const uint32_t row = ke == NONE ? NONE : ke >> 11;
-    if (row != run_row && run_row != NONE) {
-      const bool cont_next = e == i1 && e < TW && key[e] != NONE && (key[e] >> 11) == run_row;
-      if (!run_owned) {
-        float* slot = vec + (size_t)(key[i0] & SMASK) * NV;
+        for (int j = 0; j < NV; ++j) sb[j] = 0.0f;
+      }
+      if (r != NONE) {
+        const float* ve = vec + (size_t)(kc[e] & SMASK) * NV;
 #pragma unroll
-        for (int j = 0; j < NV; ++j) slot[j] = run[j];
-      } else if (cont_next) {
-        pend_row = run_row;
-        pend_first = run_first;
-      } else {
-        emit(run_row, run_first, run);
+        for (int j = 0; j < NV; ++j) sb[j] += ve[j];
       }
     }
-    if (ke == NONE || e >= i1) break;
-    if (row != run_row) {
-      run_row = row;
-      run_first = ke;
-      run_owned = e == 0 || (key[e - 1] >> 11) != row;
+  }
+  // inclusive scan of (a, b) within the wave, then across the four waves
 #pragma unroll
-      for (int j = 0; j < NV; ++j) run[j] = 0.0f;
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const int oa = __shfl_up(sa, dd, 64);
+    float ob[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) ob[j] = __shfl_up(sb[j], dd, 64);
+    if (lane >= dd && sa) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) sb[j] = ob[j] + sb[j];
+      sa = oa;
     }
-    const float* ve = vec + (size_t)(ke & SMASK) * NV;
+  }
+  if (lane == 63) {
+    sh.scan_a[wv] = sa;
 #pragma unroll
-    for (int j = 0; j < NV; ++j) run[j] += ve[j];
+    for (int j = 0; j < NV; ++j) sh.scan_b[wv][j] = sb[j];
   }
   __syncthreads();
-  if (pend_row != NONE) {
-    for (int c = tid + 1; CH * c < TW; ++c) {
-      const uint32_t kc = key[CH * c];
-      if (kc == NONE || (kc >> 11) != pend_row) break;
-      const float* slot = vec + (size_t)(kc & SMASK) * NV;
+  float pb[NV] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};   // carry at the end of wave wv - 1
+  for (int w2 = 0; w2 < wv; ++w2) {
+    const bool cont = w2 > 0 && sh.scan_a[w2];
 #pragma unroll
-      for (int j = 0; j < NV; ++j) run[j] += slot[j];
+    for (int j = 0; j < NV; ++j) pb[j] = cont ? pb[j] + sh.scan_b[w2][j] : sh.scan_b[w2][j];
+  }
+  float cin[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const float x = (wv > 0 && sa) ? pb[j] + sb[j] : sb[j];   // carry at the end of this chunk
+    cin[j] = __shfl_up(x, 1, 64);
+    if (lane == 0) cin[j] = pb[j];                          // (wave 0, lane 0: no carry, r0 != prow)
+  }
+  // pass 2: runs in entry order, the first one continuing the carry; sums at segment ends
+  float na2 = 0.0f, nc2 = 0.0f;
+  {
+    const bool cont = r0 != NONE && prow == r0;
+    float run[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) run[j] = cont ? cin[j] : 0.0f;
+    uint32_t rr = r0;
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+      const uint32_t r = rowof(kc[e]);
+      if (r != NONE) {
+        if (r != rr) {
+          rr = r;
+#pragma unroll
+          for (int j = 0; j < NV; ++j) run[j] = 0.0f;
+        }
+        float* ve = vec + (size_t)(kc[e] & SMASK) * NV;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) run[j] += ve[j];
+        if ((endm >> e) & 1u) {
+          if ((int)r == D - 1) {
+#pragma unroll
+            for (int j = 0; j < NV; ++j) run[j] += tot[j];
+          }
+#pragma unroll
+          for (int j = 0; j < NV; ++j) ve[j] = run[j];
+#pragma unroll
+          for (int j = 0; j < 5; ++j) na2 += run[j] * run[j];
+          nc2 += run[5] * run[5];
+        }
+      }
     }
-    emit(pend_row, pend_first, run);
   }
   if (tid == 0 && !has_last) {
 #pragma unroll
@@ -498,31 +589,53 @@ TOUED_DEV void a2c_update_body(const A2CStage& S, uint32_t* key, float* vec, A2C
     nc2 += tot[5] * tot[5];
   }
   A2C_STAMP(4);
-  // 4) clip_by_global_norm + SGD (models/optim.py:5-11), discarded past the lifetime (a2c.py:71-75)
-  const float gna = sqrtf(block_sum(na2, red));
-  const float gnc = sqrtf(block_sum(nc2, red));
+  // 4) clip_by_global_norm + SGD (models/optim.py:5-11), discarded past the lifetime (a2c.py:71-75).  The rows of
+  //    this thread's segments are gathered before the norm reduction, so its barriers cover their latency.
   const int st = step[a];
   const bool applied = CRITIC_ONLY || (st + 1) <= levels[(size_t)a * LEVEL_WORDS + L_LIFETIME];
+  float rth[CH][5], rv[CH];
+#pragma unroll
+  for (int e = 0; e < CH; ++e) {
+    const bool on = applied && ((endm >> e) & 1u);
+    const size_t r = on ? (size_t)(kc[e] >> 11) : 0;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) rth[e][j] = (!CRITIC_ONLY && on) ? th[r * 5 + j] : 0.0f;
+    rv[e] = on ? v[r] : 0.0f;
+  }
+  float nn[2] = {na2, nc2};
+  block_sum_n<2>(nn, red);
+  const float gna = sqrtf(nn[0]), gnc = sqrtf(nn[1]);
   const bool clip_a = !(gna < max_norm), clip_c = !(gnc < max_norm);
   A2C_STAMP(5);
-  auto apply_row = [&](int r, const float* g) {
-    if (!CRITIC_ONLY) {
+  if (applied) {
 #pragma unroll
-      for (int j = 0; j < 5; ++j) {
-        const float gg = clip_a ? (g[j] / gna) * max_norm : g[j];
-        th[(size_t)r * 5 + j] = th[(size_t)r * 5 + j] + (-(lr_a * gg));
+    for (int e = 0; e < CH; ++e) {
+      if ((endm >> e) & 1u) {
+        const size_t r = kc[e] >> 11;
+        const float* g = vec + (size_t)(kc[e] & SMASK) * NV;
+        if (!CRITIC_ONLY) {
+#pragma unroll
+          for (int j = 0; j < 5; ++j) {
+            const float gg = clip_a ? (g[j] / gna) * max_norm : g[j];
+            th[r * 5 + j] = rth[e][j] + (-(lr_a * gg));
+          }
+        }
+        const float gg = clip_c ? (g[5] / gnc) * max_norm : g[5];
+        v[r] = rv[e] + (-(lr_c * gg));
       }
     }
-    const float gg = clip_c ? (g[5] / gnc) * max_norm : g[5];
-    v[r] = v[r] + (-(lr_c * gg));
-  };
-  if (applied) {
-    for (int e = i0; e < i1; ++e) {
-      const uint32_t ke = key[e];
-      if (ke == NONE) break;
-      if (e == 0 || (key[e - 1] >> 11) != (ke >> 11)) apply_row((int)(ke >> 11), vec + (size_t)(ke & SMASK) * NV);
+    if (tid == 0 && !has_last) {
+      const size_t r = (size_t)(D - 1);
+      if (!CRITIC_ONLY) {
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          const float gg = clip_a ? (tot[j] / gna) * max_norm : tot[j];
+          th[r * 5 + j] = th[r * 5 + j] + (-(lr_a * gg));
+        }
+      }
+      const float gg = clip_c ? (tot[5] / gnc) * max_norm : tot[5];
+      v[r] = v[r] + (-(lr_c * gg));
     }
-    if (tid == 0 && !has_last) apply_row(D - 1, tot);
   }
   if (tid == 0) {
     step[a] = applied ? st + 1 : st;
@@ -565,7 +678,7 @@ __global__ void __launch_bounds__(256) k_a2c_update(int W, int T, int D, float* 
 // obs_dim = 3201 table pair is 77 KB; two workgroups share a CU's LDS), read back by the next rollout after the
 // workgroup barrier.  Bit-identical to toued_rollout_env + toued_a2c_update per update
 // (tests/test_gpu_plr.py::test_a2c_chain_matches_launch_per_update).
-template <int NMAX>
+template <int NMAX, bool CAND>
 __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __restrict__ levels, int W, int T, int D,
                                                    int U, float* __restrict__ theta, float* __restrict__ vcrit,
                                                    int* __restrict__ state, const uint4* __restrict__ draws,
@@ -583,7 +696,7 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
   const float* v = vcrit + (size_t)a * D;
   const bool env = tid < W;
   const int i = a * W + tid;
-  TrainWorker<NMAX> wk;
+  TrainWorker<NMAX, CAND> wk;
   if (env) wk.init(sp, levels, a, theta, D, state, n, i);
   for (int u = 0; u < U; ++u) {
     if (tid == 0) sh.has_last = 0;
@@ -708,19 +821,26 @@ int toued_a2c_chain(EnvSpec sp, const int* levels, int N, int W, int T, int D, i
   TOUED_REQUIRE(dstride >= (long)U * N * W, "toued_a2c_chain: draw stride %ld < %ld", dstride, (long)U * N * W);
   if (N == 0 || U == 0) return 0;
   const size_t lds = a2c_update_lds(W, T);
-  static bool attr_set[6] = {false, false, false, false, false, false};
-#define TOUED_A2C_CHAIN_CASE(NM)                                                                                     \
-  case NM: {                                                                                                          \
-    if (!attr_set[NM]) {                                                                                              \
-      TOUED_REQUIRE(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_a2c_chain<NM>),                              \
+  // the env chain's row gathers: the chosen row after the choice (default: 68k vs 94k cycles per 20-step chain,
+  // profiles/r03/a2c_stamps_rows.log) or the five candidate rows ahead of it (TOUED_TRAIN_ROWS=cand; bit-identical)
+  static const bool cand = getenv("TOUED_TRAIN_ROWS") && strcmp(getenv("TOUED_TRAIN_ROWS"), "cand") == 0;
+  static bool attr_set[2][6] = {};
+#define TOUED_A2C_CHAIN_LAUNCH(NM, CD)                                                                               \
+  {                                                                                                                   \
+    if (!attr_set[CD][NM]) {                                                                                          \
+      TOUED_REQUIRE(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_a2c_chain<NM, CD>),                          \
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) == hipSuccess,        \
                     "toued_a2c_chain: cannot raise the dynamic LDS limit");                                           \
-      attr_set[NM] = true;                                                                                            \
+      attr_set[CD][NM] = true;                                                                                        \
     }                                                                                                                 \
-    hipLaunchKernelGGL(k_a2c_chain<NM>, dim3(N), dim3(256), lds, stream, sp, levels, W, T, D, U, theta, vcrit, state, \
-                       reinterpret_cast<const uint4*>(draws), dstride, gamma, lam, ent_coef, lr_a, lr_c, max_norm,    \
-                       step, loss_out);                                                                               \
-  } break;
+    hipLaunchKernelGGL((k_a2c_chain<NM, CD>), dim3(N), dim3(256), lds, stream, sp, levels, W, T, D, U, theta, vcrit, \
+                       state, reinterpret_cast<const uint4*>(draws), dstride, gamma, lam, ent_coef, lr_a, lr_c,       \
+                       max_norm, step, loss_out);                                                                     \
+  }
+#define TOUED_A2C_CHAIN_CASE(NM)                                                                                     \
+  case NM:                                                                                                            \
+    if (cand) TOUED_A2C_CHAIN_LAUNCH(NM, true) else TOUED_A2C_CHAIN_LAUNCH(NM, false)                                \
+    break;
   switch (sp.n_max) {
     TOUED_A2C_CHAIN_CASE(1)
     TOUED_A2C_CHAIN_CASE(2)
@@ -729,6 +849,7 @@ int toued_a2c_chain(EnvSpec sp, const int* levels, int N, int W, int T, int D, i
     TOUED_A2C_CHAIN_CASE(5)
     default: break;
   }
+#undef TOUED_A2C_CHAIN_LAUNCH
 #undef TOUED_A2C_CHAIN_CASE
   TOUED_CHECK_LAUNCH();
   return 0;

@@ -12,6 +12,9 @@
 // lane-contiguously ([agent][t][worker]) so every store is coalesced.
 #include "env_dev.h"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace {
 
 // ---------------------------------------------------------------- kernels
@@ -353,7 +356,7 @@ __global__ void __launch_bounds__(256) k_eval_returns(EnvSpec sp, const int* __r
 // of one batch on those draws.  On the tabular levels the auto-reset draws nothing (reset_env<TAB> is deterministic),
 // so every random decision of a step is in its four draw words.  Bit-identical to k_rollout
 // (tests/test_gpu_env.py::test_train_rollout_three_launches).
-template <int NMAX>
+template <int NMAX, bool CAND>
 __global__ void __launch_bounds__(256) k_train_env(EnvSpec sp, const int* __restrict__ levels,
                                                    const float* __restrict__ theta, int D, int* __restrict__ state,
                                                    int T, int W, int n, const uint4* __restrict__ draws, long dstride,
@@ -364,7 +367,7 @@ __global__ void __launch_bounds__(256) k_train_env(EnvSpec sp, const int* __rest
   if (i >= n) return;
   const int a = i / W, w = i - a * W;
   const float* tab = theta + (size_t)a * D * 5;
-  TrainWorker<NMAX> wk;
+  TrainWorker<NMAX, CAND> wk;
   wk.init(sp, levels, a, theta, D, state, n, i);
   wk.load_rows(tab, D);
   float cum = 0.0f, valid = 1.0f;
@@ -557,10 +560,20 @@ int toued_rollout_env(EnvSpec sp, const int* levels, const float* theta, int D, 
   TOUED_REQUIRE(dstride >= n, "toued_rollout_env: draw stride %ld < %d workers", dstride, n);
   TOUED_REQUIRE(traj_idx && traj_time && traj_action && traj_reward && traj_done, "toued_rollout_env: trajectory buffers");
   if (n == 0) return 0;
-  TOUED_DISPATCH_NMAX(sp.n_max, true, hipLaunchKernelGGL(k_train_env<NMAX>, dim3(nblk(n)), dim3(256), 0, stream, sp,
-                                                        levels, theta, D, state, T, W, n,
-                                                        reinterpret_cast<const uint4*>(draws), dstride, traj_idx,
-                                                        traj_time, traj_action, traj_reward, traj_done, cum_return));
+  // the row gathers: the chosen row after the choice (default; 73 vs 79 us per C2 train rollout) or the five
+  // candidate rows ahead of it (TOUED_TRAIN_ROWS=cand; bit-identical)
+  static const bool cand = getenv("TOUED_TRAIN_ROWS") && strcmp(getenv("TOUED_TRAIN_ROWS"), "cand") == 0;
+  if (cand) {
+    TOUED_DISPATCH_NMAX(sp.n_max, true, hipLaunchKernelGGL((k_train_env<NMAX, true>), dim3(nblk(n)), dim3(256), 0,
+                                                          stream, sp, levels, theta, D, state, T, W, n,
+                                                          reinterpret_cast<const uint4*>(draws), dstride, traj_idx,
+                                                          traj_time, traj_action, traj_reward, traj_done, cum_return));
+  } else {
+    TOUED_DISPATCH_NMAX(sp.n_max, true, hipLaunchKernelGGL((k_train_env<NMAX, false>), dim3(nblk(n)), dim3(256), 0,
+                                                          stream, sp, levels, theta, D, state, T, W, n,
+                                                          reinterpret_cast<const uint4*>(draws), dstride, traj_idx,
+                                                          traj_time, traj_action, traj_reward, traj_done, cum_return));
+  }
   TOUED_CHECK_LAUNCH();
   return 0;
 }

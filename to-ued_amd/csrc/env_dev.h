@@ -400,16 +400,18 @@ TOUED_DEV int choice5(uint2 key, const float* p) {
   return (c0 < r) + (c1 < r) + (c2 < r) + (c3 < r) + (c4 < r);
 }
 
-// One train-rollout worker on the state-independent draws of its steps (the env chain of the three-launch rollouts,
-// toued_rollout_env, and of the A2C chain, toued_a2c_chain): the level record in registers, the five candidate next
-// actor rows gathered before the choice (the next state of a step that does not end the episode is a function of
-// the action and the step's draws), the gymnax auto-reset (reset_env<TAB> draws nothing on the tabular levels).  One
-// code path for both kernels, so their trajectories are bit-identical.
 // a step's four draw words (choice bits, termination bits, respawn mask, 0) as a native vector: HIP's uint4 struct
 // copies in the two-ahead prefetch rotation went through scratch
 typedef unsigned draw4 __attribute__((ext_vector_type(4)));
 
-template <int NMAX>
+// One train-rollout worker on the state-independent draws of its steps (the env chain of the three-launch rollouts,
+// toued_rollout_env, and of the A2C chain, toued_a2c_chain): the level record in registers, the five candidate next
+// actor rows gathered before the choice (the next state of a step that does not end the episode is a function of
+// the action and the step's draws), the gymnax auto-reset (reset_env<TAB> draws nothing on the tabular levels).  One
+// code path for both kernels, so their trajectories are bit-identical.  CAND = false (the default of both launchers):
+// no candidate gathers, the chosen next row is gathered after the step -- one dependent round trip per step beats
+// five 64-lane row gathers ahead of the choice here (W = 64 workers of one agent per wave; measured).
+template <int NMAX, bool CAND = true>
 struct TrainWorker {
   LevR lev;
   EnvState s;
@@ -458,17 +460,19 @@ struct TrainWorker {
                       float& rew, bool& done) {
     int cpos[5], cex[5];
     float crow[5][5];
+    if (CAND) {
 #pragma unroll
-    for (int act = 0; act < 5; ++act) {
-      const int p = next_pos_r(grid, wl, s.pos, act);
-      int col = 0;
+      for (int act = 0; act < 5; ++act) {
+        const int p = next_pos_r(grid, wl, s.pos, act);
+        int col = 0;
 #pragma unroll
-      for (int o = 0; o < NMAX; ++o)
-        if (((s.exists >> o) & 1) && objpos[o] == p) col |= 1 << o;
-      cpos[act] = p;
-      cex[act] = col;
-      const int ci = p + G2 * ((s.exists | (int)dr.z) & ~col & used);
-      load_row5(rs_t, tab_off + (unsigned)ci * 20u, crow[act]);
+        for (int o = 0; o < NMAX; ++o)
+          if (((s.exists >> o) & 1) && objpos[o] == p) col |= 1 << o;
+        cpos[act] = p;
+        cex[act] = col;
+        const int ci = p + G2 * ((s.exists | (int)dr.z) & ~col & used);
+        load_row5(rs_t, tab_off + (unsigned)ci * 20u, crow[act]);
+      }
     }
     o_idx = idx;
     o_time = s.time;
@@ -476,14 +480,21 @@ struct TrainWorker {
     actor_probs5_row(row, last, s.time, p);
     action = choice5_bits(dr.x, p);
     int pos = 0, collected = 0;
+    if (CAND) {
 #pragma unroll
-    for (int act = 0; act < 5; ++act)
-      if (act == action) {
-        pos = cpos[act];
-        collected = cex[act];
+      for (int act = 0; act < 5; ++act)
+        if (act == action) {
+          pos = cpos[act];
+          collected = cex[act];
 #pragma unroll
-        for (int j = 0; j < 5; ++j) row[j] = crow[act][j];
-      }
+          for (int j = 0; j < 5; ++j) row[j] = crow[act][j];
+        }
+    } else {
+      pos = next_pos_r(grid, wl, s.pos, action);
+#pragma unroll
+      for (int o = 0; o < NMAX; ++o)
+        if (((s.exists >> o) & 1) && objpos[o] == pos) collected |= 1 << o;
+    }
     // step_env (gridworld.py:72-136), tabular: env_step's operation order
     float p_t = 0.0f;
     rew = 0.0f;
@@ -511,6 +522,7 @@ struct TrainWorker {
       s.exists = (s.exists | (int)dr.z) & ~collected & used;
       s.early_term = term;
       idx = tab_index(sp, s);   // == the candidate row's index: row already holds it
+      if (!CAND) load_row5(rs_t, tab_off + (unsigned)idx * 20u, row);
     }
   }
 };
