@@ -49,6 +49,7 @@ class A2CTrainer:
         self._bufs = None
         self._graph = None
         self._graph_key = None
+        self._side = None           # side stream of the chain path's draws
         # test hook: a list here makes train() run eagerly and append, after every update, the actor/critic
         # tables it started from, the rollout it ran and the tables it produced (tests/test_gpu_plr.py)
         self.record = None
@@ -67,9 +68,9 @@ class A2CTrainer:
                              z(n, T, W, dt=torch.uint8), z(n, T, W), z(n, T, W, dt=torch.uint8)),
             "Ga": z(n, D, 5), "Gv": z(n, D), "loss": z(n, 2),
             "chain": z(U, n, 2, dt=torch.int32),
-            # rollout draws of DRAW_CHUNK updates (split_rollouts): key-chain scratch and draws [T][chunk * n * W][4]
-            "dbuf": (z(T, min(U, DRAW_CHUNK) * n * W, 4, dt=torch.int32), z(T, min(U, DRAW_CHUNK) * n * W, 4,
-                                                                               dt=torch.int32)),
+            # rollout draws of DRAW_CHUNK updates (split_rollouts): two (key-chain scratch, draws [T][chunk * n * W][4])
+            # buffers, the chain kernel reading one while the side stream fills the other
+            "dbuf": [tuple(z(T, min(U, DRAW_CHUNK) * n * W, 4, dt=torch.int32) for _ in range(2)) for _ in range(2)],
             # graph-static inputs
             "rng": z(n, 2, dt=torch.int32), "theta": z(n, D, 5), "vcrit": z(n, D),
             "step": z(n, dt=torch.int32), "levels": z(n, LEVEL_WORDS, dt=torch.int32),
@@ -86,26 +87,67 @@ class A2CTrainer:
         return bool(_lib.lib().toued_a2c_chain_fits(W, T, D))
 
     def _chain_updates(self, b, n, D, W, T, U, tm):
-        """All U updates as toued_a2c_chain launches of DRAW_CHUNK updates each, every chunk on its precomputed draws."""
+        """All U updates as toued_a2c_chain launches of DRAW_CHUNK updates each, every chunk on its precomputed draws.
+        Untimed, the next chunk's draws (threefry VALU work, no LDS, ~24 VGPRs) run on a side stream beside the
+        current chunk's chain kernel (latency-bound, two workgroups per CU), into the other of two draw buffers."""
         L = _lib
         st = L.stream_ptr()
         lr_a, lr_c, mn = self.ah.actor_learning_rate, self.ah.critic_learning_rate, self.ah.max_grad_norm
         ch = min(U, DRAW_CHUNK)
-        for u in range(0, U, ch):
-            m = min(ch, U - u)
-            tok = tm.start("a2c_draws") if tm is not None else None
+        starts = list(range(0, U, ch))
+        overlap = tm is None and len(starts) > 1
+        main = torch.cuda.current_stream()
+        if overlap:
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=b["theta"].device)
+            side = self._side
+            fork = torch.cuda.Event()
+            fork.record(main)
+            side.wait_event(fork)
+
+        def draws_for(c, stream_ptr):
+            u, m = starts[c], min(ch, U - starts[c])
             keys = b["chain"][u:u + m]
             if m < ch:      # the last chunk: its unused key rows are never rolled
                 keys = torch.cat([keys, b["chain"][:ch - m]])
-            draws = self.ro.train_draws(keys, b["levels"], W, b["dbuf"])
-            if tm is not None:
-                tm.stop(tok)
-                tok = tm.start("a2c_chain")
+            return self.ro.train_draws(keys, b["levels"], W, b["dbuf"][c % 2] if overlap else b["dbuf"][0],
+                                       stream=stream_ptr)
+
+        d_ev, c_ev, pending = [], [], None
+        if overlap:
+            with torch.cuda.stream(side):
+                pending = draws_for(0, side.cuda_stream)
+            e = torch.cuda.Event()
+            e.record(side)
+            d_ev.append(e)
+        for c, u in enumerate(starts):
+            m = min(ch, U - u)
+            if overlap:
+                draws = pending
+                if c + 1 < len(starts):
+                    if c >= 1:
+                        side.wait_event(c_ev[c - 1])      # buffer (c + 1) % 2 was chunk c - 1's
+                    with torch.cuda.stream(side):
+                        pending = draws_for(c + 1, side.cuda_stream)
+                    e = torch.cuda.Event()
+                    e.record(side)
+                    d_ev.append(e)
+                main.wait_event(d_ev[c])
+            else:
+                tok = tm.start("a2c_draws") if tm is not None else None
+                draws = draws_for(c, None)
+                if tm is not None:
+                    tm.stop(tok)
+            tok = tm.start("a2c_chain") if tm is not None else None
             L.call("toued_a2c_chain", self.ro._c, L.ptr(b["levels"]), n, W, T, D, m, L.ptr(b["theta"]),
                    L.ptr(b["vcrit"]), L.ptr(b["state"]), L.ptr(draws), draws.shape[1], self.hyp.gamma,
                    self.hyp.gae_lambda, self.hyp.entropy_coeff, lr_a, lr_c, mn, L.ptr(b["step"]), L.ptr(b["loss"]), st)
             if tm is not None:
                 tm.stop(tok)
+            if overlap:
+                e = torch.cuda.Event()
+                e.record(main)
+                c_ev.append(e)
 
     def _updates(self, b, n, D, W, T, U, record=None):
         L = _lib
@@ -136,7 +178,7 @@ class A2CTrainer:
                 keys = b["chain"][u:u + ch]
                 if keys.shape[0] < ch:      # the last chunk: its unused key rows are never rolled
                     keys = torch.cat([keys, b["chain"][:ch - keys.shape[0]]])
-                draws = self.ro.train_draws(keys, b["levels"], W, b["dbuf"])
+                draws = self.ro.train_draws(keys, b["levels"], W, b["dbuf"][0])
                 if tm is not None:
                     tm.stop(tok)
             tok = tm.start("a2c_rollout") if tm is not None else None

@@ -66,8 +66,10 @@ def algorithmic_regret(sampler, keys: torch.Tensor, levels: torch.Tensor, lpg_th
     step = torch.zeros(n, dtype=torch.int32, device=keys.device)
     sampler.a2c_trainer().train(tr, theta, vcrit, step, levels, state, sampler.max_lifetime)
     lpg_rng, a2c_rng = _split2(rng)
-    r_lpg = eval_agent(ro, lpg_rng, levels, lpg_theta, W)
-    r_a2c = eval_agent(ro, a2c_rng, levels, theta, W)
+    # both eval_agent calls as one batch of 2n agents (each agent's rollout depends only on its own key, level and
+    # table: bit-identical to two calls, at about the latency of one -- the returns-only rollout is latency-bound)
+    r = eval_agent(ro, torch.cat([lpg_rng, a2c_rng]), torch.cat([levels, levels]), torch.cat([lpg_theta, theta]), W)
+    r_lpg, r_a2c = r[:n], r[n:]
     return r_a2c - r_lpg
 
 

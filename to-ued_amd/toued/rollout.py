@@ -127,11 +127,11 @@ class RolloutWrapper:
         return out, state, cum
 
     def train_draws(self, keys: torch.Tensor, levels: torch.Tensor, n_workers: int,
-                    bufs: tuple[torch.Tensor, torch.Tensor] | None = None) -> torch.Tensor:
+                    bufs: tuple[torch.Tensor, torch.Tensor] | None = None, stream: int | None = None) -> torch.Tensor:
         """The state-independent draws of U batches of train rollouts (toued_rollout_draws): keys [U, N, 2] (batch u's
         rollout keys), levels [N, words].  Returns u32 [T, U * N * W, 4]: in ``bufs`` = (chain scratch, draws), each
         at least [T, U * N * W, 4] (the step stride is theirs), or in a buffer of this wrapper reused by the next
-        call of the same shape."""
+        call of the same shape.  ``stream``: a raw HIP stream to launch on (default: torch's current stream)."""
         U, N = keys.shape[0], keys.shape[1]
         T, W = self.train_rollout_len, n_workers
         n = U * N * W
@@ -149,7 +149,7 @@ class RolloutWrapper:
         if n != U * N * W:
             raise ValueError("train_draws: the buffers' worker stride must equal U * N * W")
         _lib.call("toued_rollout_draws", self._c, _lib.ptr(levels), _lib.ptr(keys.contiguous()), N, U, W, T,
-                  _lib.ptr(chain), _lib.ptr(draws), _lib.stream_ptr())
+                  _lib.ptr(chain), _lib.ptr(draws), stream if stream is not None else _lib.stream_ptr())
         return draws
 
     def rollout_from_draws(self, draws: torch.Tensor, u: int, theta: torch.Tensor, levels: torch.Tensor,
