@@ -22,10 +22,23 @@
 
 namespace {
 
+// Wave sum, every lane gets it: the xor butterfly 1, 2, 4, 8, 16, 32 with the first four steps as DPP moves (quad
+// permutes, half-row and row mirrors: after the quad sums, lane i's mirror partner holds the same partial as its xor
+// partner), xor 16 as a swizzle and the last step on the two half sums -- the same additions in the same order as
+// the __shfl_xor butterfly (bit-identical), without its six LDS-crossbar permutes.
+template <int CTRL>
+TOUED_DEV float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
 TOUED_DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_f<0xB1>(v);    // quad_perm [1, 0, 3, 2]: xor 1
+  v += dpp_f<0x4E>(v);    // quad_perm [2, 3, 0, 1]: xor 2
+  v += dpp_f<0x141>(v);   // row_half_mirror: the other quad of the 8
+  v += dpp_f<0x140>(v);   // row_mirror: the other 8 of the row
+  v += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x401F));   // xor 16
+  const float lo = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+  const float hi = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+  return lo + hi;
 }
 
 // Block-wide sum for 256-thread blocks; every thread gets the result.
@@ -124,6 +137,7 @@ TOUED_DEV float a2c_gae(const A2CStage& S, int W, int T, float gamma, float lam,
   for (int w = tid; w < W; w += blockDim.x) {
     float vn = S.vt[T * W + w];
     float g = 0.0f, cl = 0.0f;
+#pragma unroll 4
     for (int t = T - 1; t >= 0; --t) {
       const float vv = S.vt[t * W + w];
       const float ndt = S.nd[t * W + w];
@@ -151,6 +165,7 @@ TOUED_DEV float a2c_gae(const A2CStage& S, int W, int T, float gamma, float lam,
   const float inv_sd = 1.0f / (sqrtf(block_sum(s_var, red) / n) + EPSF);
   for (int w = tid; w < W; w += blockDim.x) {
     float ab = 0.0f;
+#pragma unroll 4
     for (int t = 0; t < T; ++t) ab += (S.adv[w * T + t] - mean) * inv_sd;
     S.abar[w] = ab / (float)T;
   }
@@ -694,8 +709,15 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
   float* vec = reinterpret_cast<float*>(key + A2C_SORT_MAX);                    // [W*T][6]
   const float* tab = theta + (size_t)a * D * 5;
   const float* v = vcrit + (size_t)a * D;
-  const bool env = tid < W;
-  const int i = a * W + tid;
+  // env workers spread over the four waves (W % 4 == 0: W/4 lanes of each wave), so each wave's row gather touches
+  // W/4 cache lines instead of W (A2C_ENV_SPREAD=0: all W workers in wave 0)
+#ifndef A2C_ENV_SPREAD
+#define A2C_ENV_SPREAD 1
+#endif
+  const bool spread = A2C_ENV_SPREAD && W % 4 == 0;
+  const int w = spread ? (tid >> 6) * (W / 4) + (tid & 63) : tid;
+  const bool env = spread ? (tid & 63) < W / 4 : tid < W;
+  const int i = a * W + w;
   TrainWorker<NMAX, CAND> wk;
   if (env) wk.init(sp, levels, a, theta, D, state, n, i);
   for (int u = 0; u < U; ++u) {
@@ -716,14 +738,14 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
         float rew;
         bool done;
         wk.step(sp, tab, d, oi, ot, action, rew, done);
-        S.ix[t * W + tid] = oi;
-        S.cc[t * W + tid] = (float)ot * 0.001f;
-        S.act[t * W + tid] = (uint8_t)action;
-        S.rw[t * W + tid] = rew;
-        S.nd[t * W + tid] = done ? 0.0f : 1.0f;
+        S.ix[t * W + w] = oi;
+        S.cc[t * W + w] = (float)ot * 0.001f;
+        S.act[t * W + w] = (uint8_t)action;
+        S.rw[t * W + w] = rew;
+        S.nd[t * W + w] = done ? 0.0f : 1.0f;
       }
-      S.ix[T * W + tid] = wk.idx;
-      S.cc[T * W + tid] = (float)wk.s.time * 0.001f;
+      S.ix[T * W + w] = wk.idx;
+      S.cc[T * W + w] = (float)wk.s.time * 0.001f;
     }
     if (u == U - 1) A2C_STAMP(7);
     __syncthreads();

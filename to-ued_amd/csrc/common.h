@@ -113,10 +113,7 @@ TOUED_DEV float uniform_from_bits(uint32_t bits, float lo, float hi) {
 // Portable math (oracle/pmath.py)
 TOUED_DEV float pow2i(int k) { return __uint_as_float((uint32_t)(k + 127) << 23); }
 
-TOUED_DEV float pexp(float x) {
-  if (x != x) return x;
-  if (x > 88.72283905206835f) return __builtin_inff();
-  if (x < -103.972084f) return 0.0f;
+TOUED_DEV float pexp_core(float x) {
   const float k = rintf(__fmul_rn(x, 1.44269504088896341f));
   float r = __fsub_rn(x, __fmul_rn(k, 0.693145751953125f));
   r = __fsub_rn(r, __fmul_rn(k, 1.428606765330187045e-06f));
@@ -132,6 +129,14 @@ TOUED_DEV float pexp(float x) {
   const int c1 = k1 < -126 ? -126 : (k1 > 127 ? 127 : k1);
   const int c2 = k2 < -126 ? -126 : (k2 > 127 ? 127 : k2);
   return __fmul_rn(__fmul_rn(p, pow2i(c1)), pow2i(c2));
+}
+
+// branch-free: the special cases are selected after the main path (computed on 0 for them), so a wave runs one
+// straight-line sequence instead of three divergent branches per call
+TOUED_DEV float pexp(float x) {
+  const bool nan = x != x, hi = x > 88.72283905206835f, lo = x < -103.972084f;
+  const float r = pexp_core((nan || hi || lo) ? 0.0f : x);
+  return nan ? x : (hi ? __builtin_inff() : (lo ? 0.0f : r));
 }
 
 TOUED_DEV float plog(float x) {
