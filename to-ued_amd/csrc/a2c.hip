@@ -320,11 +320,35 @@ __global__ void __launch_bounds__(256) k_a2c_apply(int D, float* __restrict__ th
 #define A2C_SORT_MAX 2048
 #define A2C_NV 6
 
+// x of lane ^ M: DPP quad permutes (M = 1, 2), row shifts by M in both directions (M = 4, 8), a swizzle (16), a
+// permute through the LDS crossbar only for M = 32
+template <int CTRL>
+TOUED_DEV uint32_t dpp_u(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int M>
+TOUED_DEV uint32_t lane_xor(uint32_t x, int lane) {
+  if constexpr (M == 1) {
+    return dpp_u<0xB1>(x);
+  } else if constexpr (M == 2) {
+    return dpp_u<0x4E>(x);
+  } else if constexpr (M == 4 || M == 8) {
+    const uint32_t from_above = dpp_u<0x100 + M>(x);   // row_shl:M, lane i <- lane i + M
+    const uint32_t from_below = dpp_u<0x110 + M>(x);   // row_shr:M, lane i <- lane i - M
+    return (lane & M) ? from_below : from_above;
+  } else if constexpr (M == 16) {
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);   // bit mode: and 0x1F, xor 0x10
+  } else {
+    return (uint32_t)__shfl_xor((int)x, M, 64);
+  }
+}
+
 // bitonic sort of the 2048 keys in LDS with 256 threads, in registers: wave w holds keys [512 w, 512 w + 512), lane l
 // the eight keys 512 w + 8 l + r (two 16-byte LDS reads).  Stages with partner distance j < 8 are compare-selects
 // between a lane's own registers, 8 <= j <= 256 exchange registers between lanes (lane distance j / 8, one shuffle per
 // key), and the three stages with j >= 512 exchange whole halves through LDS between waves.  Every element keeps
 // min or max of itself and its partner i ^ j: min when (i & j == 0) == ascending, ascending = (i & k == 0).
+// The lane exchanges go through DPP where a pattern exists (lane_xor).
 // Begins and ends with a workgroup barrier; the sorted keys are back in `key`.
 template <int K, int J>
 TOUED_DEV void a2c_bitonic_stage(uint32_t (&x)[8], uint32_t* key, int lane, int wv) {
@@ -346,7 +370,7 @@ TOUED_DEV void a2c_bitonic_stage(uint32_t (&x)[8], uint32_t* key, int lane, int 
     for (int r = 0; r < 8; ++r) {
       const int i = 512 * wv + 8 * lane + r;
       const bool asc = (i & K) == 0;
-      const uint32_t p = (uint32_t)__shfl_xor((int)x[r], J / 8, 64);
+      const uint32_t p = lane_xor<J / 8>(x[r], lane);
       const uint32_t lo = x[r] < p ? x[r] : p, hi = x[r] < p ? p : x[r];
       x[r] = lowpos == asc ? lo : hi;
     }
@@ -444,6 +468,10 @@ TOUED_DEV void a2c_update_body(const A2CStage& S, uint32_t* key, float* vec, A2C
     for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
   }
   const float inv_n = 1.0f / (float)TW;
+  // actor rows through a buffer descriptor over the whole table array (host-checked < 4 GiB): a 16-byte and a
+  // 4-byte load per 20-byte row instead of five dword gathers
+  const __amdgpu_buffer_rsrc_t rs_th = theta_rsrc(CRITIC_ONLY ? vcrit : theta);
+  const unsigned th_off = (unsigned)((size_t)a * D * 20);
   int sidx[CH];
   float trow[CH][5];
 #pragma unroll
@@ -451,7 +479,8 @@ TOUED_DEV void a2c_update_body(const A2CStage& S, uint32_t* key, float* vec, A2C
     const int sl = tid + 256 * h;
     sidx[h] = sl < TW ? S.ix[sl] : 0;
 #pragma unroll
-    for (int j = 0; j < 5; ++j) trow[h][j] = (!CRITIC_ONLY && sl < TW) ? th[(size_t)sidx[h] * 5 + j] : 0.0f;
+    for (int j = 0; j < 5; ++j) trow[h][j] = 0.0f;
+    if (!CRITIC_ONLY && sl < TW) load_row5(rs_th, th_off + (unsigned)sidx[h] * 20u, trow[h]);
   }
   float acc[NV + 1] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};   // time-row partials [NV], actor loss
 #pragma unroll
@@ -614,7 +643,8 @@ TOUED_DEV void a2c_update_body(const A2CStage& S, uint32_t* key, float* vec, A2C
     const bool on = applied && ((endm >> e) & 1u);
     const size_t r = on ? (size_t)(kc[e] >> 11) : 0;
 #pragma unroll
-    for (int j = 0; j < 5; ++j) rth[e][j] = (!CRITIC_ONLY && on) ? th[r * 5 + j] : 0.0f;
+    for (int j = 0; j < 5; ++j) rth[e][j] = 0.0f;
+    if (!CRITIC_ONLY && on) load_row5(rs_th, th_off + (unsigned)r * 20u, rth[e]);
     rv[e] = on ? v[r] : 0.0f;
   }
   float nn[2] = {na2, nc2};
@@ -810,6 +840,7 @@ int toued_a2c_update(int N, int W, int T, int D, float* theta, float* vcrit, con
                      float* loss_out, hipStream_t stream) {
   TOUED_REQUIRE(toued_a2c_update_fits(W, T, D), "toued_a2c_update: D=%d W=%d T=%d unsupported (W*T <= %d; use "
                 "grad + apply)", D, W, T, A2C_SORT_MAX);
+  TOUED_REQUIRE((double)N * D * 20.0 < 4294967295.0, "toued_a2c_update: actor tables (%d x %d rows) exceed 4 GiB", N, D);
   const size_t lds = a2c_update_lds(W, T);
   if (N == 0) return 0;
   static bool attr_set = false;
