@@ -14,6 +14,7 @@
 //
 // Trajectory layout as the rollout kernel writes it: idx/time [N][T+1][W], act/done/rew [N][T][W].
 #include "env_dev.h"
+#include "wave_dev.h"
 
 #include <cstdlib>
 #include <cstring>
@@ -22,24 +23,7 @@
 
 namespace {
 
-// Wave sum, every lane gets it: the xor butterfly 1, 2, 4, 8, 16, 32 with the first four steps as DPP moves (quad
-// permutes, half-row and row mirrors: after the quad sums, lane i's mirror partner holds the same partial as its xor
-// partner), xor 16 as a swizzle and the last step on the two half sums -- the same additions in the same order as
-// the __shfl_xor butterfly (bit-identical), without its six LDS-crossbar permutes.
-template <int CTRL>
-TOUED_DEV float dpp_f(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
-}
-TOUED_DEV float wave_sum(float v) {
-  v += dpp_f<0xB1>(v);    // quad_perm [1, 0, 3, 2]: xor 1
-  v += dpp_f<0x4E>(v);    // quad_perm [2, 3, 0, 1]: xor 2
-  v += dpp_f<0x141>(v);   // row_half_mirror: the other quad of the 8
-  v += dpp_f<0x140>(v);   // row_mirror: the other 8 of the row
-  v += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x401F));   // xor 16
-  const float lo = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
-  const float hi = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
-  return lo + hi;
-}
+TOUED_DEV float wave_sum(float v) { return wsum_dpp(v); }
 
 // Block-wide sum for 256-thread blocks; every thread gets the result.
 TOUED_DEV float block_sum(float v, float* red) {
@@ -311,113 +295,15 @@ __global__ void __launch_bounds__(256) k_a2c_apply(int D, float* __restrict__ th
 // ---------------------------------------------------------------------------- deterministic fused update
 // One block (256 threads) per agent, W*T <= 2048 samples.  The reference's gradient is obs^T . dlogits over the
 // agent's [W, T] batch (XLA, deterministic); here every sample's 6-float row cotangent (5 actor + 1 critic) is
-// written to LDS, the keys (row << 11 | sample) are bitonic-sorted, and each row's segment is summed in sample
-// order, chunk partials combined in chunk order -- no atomics, so a replay gives bit-identical tables.  The row
-// sums stay in LDS (in the vector slot of the segment's first sample) until the two global norms are known;
-// then clip + SGD rewrite only the rows that have samples (an untouched row's update th + -(lr * 0) is the
-// identity).  The time row D-1 (every sample contributes c * v) is a block reduction.  LDS does not depend on
-// D: staged trajectory + 2048 keys + W*T*6 floats (~76 KB at W=64, T=20), so two agents share a CU.
+// written to LDS, the keys (row << 11 | sample) are bitonic-sorted in registers (wave_dev.h), and each row's
+// segment is summed by a segmented scan over the chunks (a fixed combination tree) -- no atomics, so a replay gives
+// bit-identical tables.  The row sums stay in LDS (in the vector slot of the segment's last sample) until the two
+// global norms are known; then clip + SGD rewrite only the rows that have samples (an untouched row's update
+// th + -(lr * 0) is the identity).  The time row D-1 (every sample contributes c * v) is a block reduction.  LDS
+// does not depend on D: staged trajectory + 2048 keys + W*T*6 floats (~77 KB at W=64, T=20), so two agents share
+// a CU.
 #define A2C_SORT_MAX 2048
 #define A2C_NV 6
-
-// x of lane ^ M: DPP quad permutes (M = 1, 2), row shifts by M in both directions (M = 4, 8), a swizzle (16), a
-// permute through the LDS crossbar only for M = 32
-template <int CTRL>
-TOUED_DEV uint32_t dpp_u(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
-}
-template <int M>
-TOUED_DEV uint32_t lane_xor(uint32_t x, int lane) {
-  if constexpr (M == 1) {
-    return dpp_u<0xB1>(x);
-  } else if constexpr (M == 2) {
-    return dpp_u<0x4E>(x);
-  } else if constexpr (M == 4 || M == 8) {
-    const uint32_t from_above = dpp_u<0x100 + M>(x);   // row_shl:M, lane i <- lane i + M
-    const uint32_t from_below = dpp_u<0x110 + M>(x);   // row_shr:M, lane i <- lane i - M
-    return (lane & M) ? from_below : from_above;
-  } else if constexpr (M == 16) {
-    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);   // bit mode: and 0x1F, xor 0x10
-  } else {
-    return (uint32_t)__shfl_xor((int)x, M, 64);
-  }
-}
-
-// bitonic sort of the 2048 keys in LDS with 256 threads, in registers: wave w holds keys [512 w, 512 w + 512), lane l
-// the eight keys 512 w + 8 l + r (two 16-byte LDS reads).  Stages with partner distance j < 8 are compare-selects
-// between a lane's own registers, 8 <= j <= 256 exchange registers between lanes (lane distance j / 8, one shuffle per
-// key), and the three stages with j >= 512 exchange whole halves through LDS between waves.  Every element keeps
-// min or max of itself and its partner i ^ j: min when (i & j == 0) == ascending, ascending = (i & k == 0).
-// The lane exchanges go through DPP where a pattern exists (lane_xor).
-// Begins and ends with a workgroup barrier; the sorted keys are back in `key`.
-template <int K, int J>
-TOUED_DEV void a2c_bitonic_stage(uint32_t (&x)[8], uint32_t* key, int lane, int wv) {
-  if constexpr (J < 8) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      if ((r & J) == 0) {
-        const int i = 512 * wv + 8 * lane + r;
-        const bool asc = (i & K) == 0;
-        const uint32_t a = x[r], b = x[r | J];
-        const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
-        x[r] = asc ? lo : hi;
-        x[r | J] = asc ? hi : lo;
-      }
-    }
-  } else if constexpr (J <= 256) {
-    const bool lowpos = (lane & (J / 8)) == 0;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int i = 512 * wv + 8 * lane + r;
-      const bool asc = (i & K) == 0;
-      const uint32_t p = lane_xor<J / 8>(x[r], lane);
-      const uint32_t lo = x[r] < p ? x[r] : p, hi = x[r] < p ? p : x[r];
-      x[r] = lowpos == asc ? lo : hi;
-    }
-  } else {
-    uint4* kv = reinterpret_cast<uint4*>(key);
-    const int me = (512 * wv + 8 * lane) / 4, pa = (512 * (wv ^ (J / 512)) + 8 * lane) / 4;
-    kv[me] = make_uint4(x[0], x[1], x[2], x[3]);
-    kv[me + 1] = make_uint4(x[4], x[5], x[6], x[7]);
-    __syncthreads();
-    const uint4 p0 = kv[pa], p1 = kv[pa + 1];
-    const uint32_t p[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
-    const bool lowpos = (wv & (J / 512)) == 0;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int i = 512 * wv + 8 * lane + r;
-      const bool asc = (i & K) == 0;
-      const uint32_t lo = x[r] < p[r] ? x[r] : p[r], hi = x[r] < p[r] ? p[r] : x[r];
-      x[r] = lowpos == asc ? lo : hi;
-    }
-    __syncthreads();   // every partner read before the next stage's writes
-  }
-}
-
-template <int K, int J>
-TOUED_DEV void a2c_bitonic_merge(uint32_t (&x)[8], uint32_t* key, int lane, int wv) {
-  a2c_bitonic_stage<K, J>(x, key, lane, wv);
-  if constexpr (J > 1) a2c_bitonic_merge<K, J / 2>(x, key, lane, wv);
-}
-
-template <int K>
-TOUED_DEV void a2c_bitonic_levels(uint32_t (&x)[8], uint32_t* key, int lane, int wv) {
-  a2c_bitonic_merge<K, K / 2>(x, key, lane, wv);
-  if constexpr (K < 2048) a2c_bitonic_levels<2 * K>(x, key, lane, wv);
-}
-
-TOUED_DEV void a2c_sort2048(uint32_t* key, int tid) {
-  const int lane = tid & 63, wv = tid >> 6;
-  __syncthreads();
-  uint4* kv = reinterpret_cast<uint4*>(key);
-  const int me = (512 * wv + 8 * lane) / 4;
-  const uint4 a = kv[me], b = kv[me + 1];
-  uint32_t x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  a2c_bitonic_levels<2>(x, key, lane, wv);
-  kv[me] = make_uint4(x[0], x[1], x[2], x[3]);
-  kv[me + 1] = make_uint4(x[4], x[5], x[6], x[7]);
-  __syncthreads();
-}
 
 #ifdef A2C_STAMPS
 // timing instrumentation (tools/a2c_stamps.py, built by tools/build_variant.py a2c.hip A2C_STAMPS=1): thread 0 of
@@ -515,7 +401,7 @@ TOUED_DEV void a2c_update_body(const A2CStage& S, uint32_t* key, float* vec, A2C
   const float al = acc[NV] * inv_n;
   A2C_STAMP(2);
   // 2) sort by (row, sample)
-  a2c_sort2048(key, tid);
+  sort2048_reg<256>(key, tid);
   A2C_STAMP(3);
   // 3) segmented row sums, deterministic (a fixed combination tree).  Thread t owns the sorted entries
   //    [CH t, CH t + CH) as runs of equal rows.  The part of a segment lying in earlier chunks (the carry) reaches the

@@ -20,6 +20,7 @@
 #include <string.h>
 #include <algorithm>
 #include "common.h"
+#include "wave_dev.h"
 
 #define EPSF 1e-8f
 
@@ -1111,56 +1112,24 @@ struct HvpOp {   // k_hvp
   TOUED_DEV void finish(int, float, float) const {}
 };
 
-// Stable sort of the 2048 keys (row << 12 | sample) in LDS: bitonic network in which every wave owns 256
-// contiguous keys, so the 60 of its 66 stages with partner distance j < 256 need only a wave barrier and
-// only the six with j >= 256 a workgroup barrier.
-TOUED_DEV void cmp_swap(uint32_t* key, int i, int j, int k) {
-  const int ij = i | j;
-  const uint32_t x = key[i], y = key[ij];
-  if ((x > y) == ((i & k) == 0)) { key[i] = y; key[ij] = x; }
-}
-
-TOUED_DEV void sort2048(uint32_t* key, int tid) {
-  const int lane = tid & 63, wv = tid >> 6;
-  for (int k = 2; k <= 2048; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const int lj = 31 - __builtin_clz(j);
-      if (j >= 256) {
-        __syncthreads();
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {       // 1024 pairs over 512 threads
-          const int pr = tid + 512 * h;
-          cmp_swap(key, ((pr >> lj) << (lj + 1)) | (pr & (j - 1)), j, k);
-        }
-        __syncthreads();
-      } else {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {       // this wave's 128 pairs
-          const int pr = lane + 64 * h;
-          cmp_swap(key, 256 * wv + (((pr >> lj) << (lj + 1)) | (pr & (j - 1))), j, k);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
-    }
-  }
-  __syncthreads();
-}
-
 template <class Op>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k_rows_sorted(Op op) {
   constexpr int NA = Op::NA, NC = Op::NC, NV = NA + NC, NM = Op::NM;
+  constexpr uint32_t NONE = 0xFFFFFFFFu, SMASK = 4095u;
   // unpadded vector stride (odd strides are bank-conflict free): 13-float rows keep a block's LDS at 75 KB,
   // so two agents' blocks share a CU and all N = 512 blocks are resident in one round
   constexpr int NVP = NV;
+  constexpr int CH = 4;                                 // sorted entries per thread
   extern __shared__ float lds[];
   __shared__ float red[8][NV + NM];
   __shared__ float tot[NV + NM];
   __shared__ int has_last;
+  __shared__ int scan_a[8];
+  __shared__ float scan_b[8][NV];
   uint32_t* key = reinterpret_cast<uint32_t*>(lds);   // [2048]
   float* vec = lds + 2048;                            // [T*W][NVP]
   const int a = blockIdx.x, tid = threadIdx.x, W = op.W, T = op.T, D = op.D, TW = T * W;
+  const int lane = tid & 63, wv = tid >> 6;
   if (tid == 0) has_last = 0;
   float part[NV + NM];
 #pragma unroll
@@ -1168,7 +1137,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   __syncthreads();
   // 1) per-sample row vectors -> LDS, sort keys, time-row and metric partial sums
   for (int sl = tid; sl < 2048; sl += 512) {
-    uint32_t kk = 0xFFFFFFFFu;
+    uint32_t kk = NONE;
     if (sl < TW) {
       const int t = sl / W, w = sl - t * W;
       int idx;
@@ -1186,8 +1155,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   }
 #pragma unroll
   for (int j = 0; j < NV + NM; ++j) {
-    const float r = wave_sum(part[j]);
-    if ((tid & 63) == 0) red[tid >> 6][j] = r;
+    const float r = wsum_dpp(part[j]);
+    if (lane == 0) red[wv][j] = r;
   }
   __syncthreads();
   if (tid < NV + NM) {
@@ -1196,79 +1165,124 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
     tot[tid] = r;
   }
   // 2) sort by (row, sample)
-  sort2048(key, tid);
-  // 3) segmented sums over the sorted keys, chunked so that no thread walks a long segment alone: thread t
-  //    sums the runs of its CH entries [CH t, CH t + CH); a run that continues a segment begun in an earlier
-  //    chunk leaves its partial in the vector row of the chunk's first sample (read only by this thread);
-  //    after a barrier each segment's owner (the thread holding its first entry) adds the partials of the
-  //    chunks its segment runs into, in chunk order (deterministic), and updates the table row.
-  constexpr int CH = 4;
-  float na2 = 0.0f, nc2 = 0.0f;
-  auto emit = [&](uint32_t row, float (&sum)[NV]) {
-    if ((int)row == D - 1) {
+  sort2048_reg<512>(key, tid);
+  // 3) segmented row sums, deterministic (a fixed combination tree): thread t owns the sorted entries
+  //    [CH t, CH t + CH) as runs of equal rows; the part of a segment in earlier chunks (the carry) reaches the chunk
+  //    where the segment ends through a segmented scan over the 512 chunks (carry_t = a_t carry_{t-1} + b_t, b_t the
+  //    sum of chunk t's last run, a_t = 1 iff chunk t is one run continuing chunk t-1's segment); the thread holding a
+  //    segment's last entry adds the segment to the table row (each row has exactly one writer in the grid)
+  auto rowof = [](uint32_t k) { return k == NONE ? NONE : (k >> 12); };
+  uint32_t kc[CH];
+  {
+    const uint4 x = reinterpret_cast<const uint4*>(key)[tid];
+    kc[0] = x.x; kc[1] = x.y; kc[2] = x.z; kc[3] = x.w;
+  }
+  const uint32_t prow = tid == 0 ? NONE : rowof(key[CH * tid - 1]);
+  const uint32_t nrow = tid == 511 ? NONE : rowof(key[CH * tid + CH]);
+  uint32_t endm = 0u;
 #pragma unroll
-      for (int j = 0; j < NV; ++j) sum[j] += tot[j];
-    }
-    float* ra = op.rowA(a, (int)row);
+  for (int e = 0; e < CH; ++e) {
+    const uint32_t r = rowof(kc[e]);
+    const uint32_t rn = e < CH - 1 ? rowof(kc[e + 1]) : nrow;
+    if (r != NONE && rn != r) endm |= 1u << e;
+  }
+  const uint32_t r0 = rowof(kc[0]);
+  const bool cont0 = r0 != NONE && prow == r0;
+  float sb[NV];
 #pragma unroll
-    for (int j = 0; j < NA; ++j) {
-      const float g = ra[j] + sum[j];
-      ra[j] = g;
-      if (Op::NORMS) na2 += g * g;
-    }
-    if (NC > 0) {
-      float* rc = op.rowC(a, (int)row);
+  for (int j = 0; j < NV; ++j) sb[j] = 0.0f;
+  int sa = cont0 ? 1 : 0;
+  {
+    uint32_t lr = r0;
 #pragma unroll
-      for (int j = 0; j < NC; ++j) {
-        const float g = rc[j] + sum[NA + j];
-        rc[j] = g;
-        if (Op::NORMS) nc2 += g * g;
+    for (int e = 0; e < CH; ++e) {
+      const uint32_t r = rowof(kc[e]);
+      if (r != lr) {
+        sa = 0;
+        lr = r;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) sb[j] = 0.0f;
+      }
+      if (r != NONE) {
+        const float* ve = vec + (size_t)(kc[e] & SMASK) * NVP;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) sb[j] += ve[j];
       }
     }
-  };
-  const int i0 = CH * tid, i1 = min(i0 + CH, TW);
-  const uint32_t NONE = 0xFFFFFFFFu;
-  float run[NV];
-  uint32_t run_row = NONE;
-  bool run_owned = false;
-  uint32_t pend_row = NONE;          // owned run reaching the chunk end whose segment continues
-  for (int e = i0; e <= i1; ++e) {
-    const uint32_t ke = e < i1 ? key[e] : NONE;
-    const uint32_t row = ke == NONE ? NONE : ke >> 12;
-    if (row != run_row && run_row != NONE) {
-      // the run [.., e) ends here (new row, invalid key or chunk end)
-      const bool cont_next = e == i1 && e < TW && key[e] != NONE && (key[e] >> 12) == run_row;
-      if (!run_owned) {
-        float* slot = vec + (key[i0] & 4095u) * NVP;
+  }
 #pragma unroll
-        for (int j = 0; j < NV; ++j) slot[j] = run[j];
-      } else if (cont_next) {
-        pend_row = run_row;
-      } else {
-        emit(run_row, run);
-      }
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const int oa = __shfl_up(sa, dd, 64);
+    float ob[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) ob[j] = __shfl_up(sb[j], dd, 64);
+    if (lane >= dd && sa) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) sb[j] = ob[j] + sb[j];
+      sa = oa;
     }
-    if (ke == NONE) break;
-    if (row != run_row) {
-      run_row = row;
-      run_owned = e == 0 || (key[e - 1] >> 12) != row;
+  }
+  if (lane == 63) {
+    scan_a[wv] = sa;
 #pragma unroll
-      for (int j = 0; j < NV; ++j) run[j] = 0.0f;
-    }
-    const float* ve = vec + (ke & 4095u) * NVP;
-#pragma unroll
-    for (int j = 0; j < NV; ++j) run[j] += ve[j];
+    for (int j = 0; j < NV; ++j) scan_b[wv][j] = sb[j];
   }
   __syncthreads();
-  if (pend_row != NONE) {
-    for (int c = tid + 1; CH * c < TW; ++c) {
-      const uint32_t kc = key[CH * c];
-      if (kc == NONE || (kc >> 12) != pend_row) break;
-      const float* slot = vec + (kc & 4095u) * NVP;
+  float pb[NV];
 #pragma unroll
-      for (int j = 0; j < NV; ++j) run[j] += slot[j];
+  for (int j = 0; j < NV; ++j) pb[j] = 0.0f;
+  for (int w2 = 0; w2 < wv; ++w2) {
+    const bool cont = w2 > 0 && scan_a[w2];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) pb[j] = cont ? pb[j] + scan_b[w2][j] : scan_b[w2][j];
+  }
+  float run[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const float x = (wv > 0 && sa) ? pb[j] + sb[j] : sb[j];   // carry at the end of this chunk
+    float cj = __shfl_up(x, 1, 64);
+    if (lane == 0) cj = pb[j];
+    run[j] = cont0 ? cj : 0.0f;
+  }
+  float na2 = 0.0f, nc2 = 0.0f;
+  {
+    uint32_t rr = r0;
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+      const uint32_t r = rowof(kc[e]);
+      if (r != NONE) {
+        if (r != rr) {
+          rr = r;
+#pragma unroll
+          for (int j = 0; j < NV; ++j) run[j] = 0.0f;
+        }
+        const float* ve = vec + (size_t)(kc[e] & SMASK) * NVP;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) run[j] += ve[j];
+        if ((endm >> e) & 1u) {
+          if ((int)r == D - 1) {
+#pragma unroll
+            for (int j = 0; j < NV; ++j) run[j] += tot[j];
+          }
+          float* ra = op.rowA(a, (int)r);
+#pragma unroll
+          for (int j = 0; j < NA; ++j) {
+            const float g = ra[j] + run[j];
+            ra[j] = g;
+            if (Op::NORMS) na2 += g * g;
+          }
+          if (NC > 0) {
+            float* rc = op.rowC(a, (int)r);
+#pragma unroll
+            for (int j = 0; j < NC; ++j) {
+              const float g = rc[j] + run[NA + j];
+              rc[j] = g;
+              if (Op::NORMS) nc2 += g * g;
+            }
+          }
+        }
+      }
     }
-    emit(pend_row, run);
   }
   if (tid == 0) {
     if (!has_last) {
@@ -1292,10 +1306,10 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
     op.metrics(a, tot + NV);
   }
   if (Op::NORMS) {   // global norms of the (complete) gradient tables: every nonzero row was written above
-    na2 = wave_sum(na2);
-    nc2 = wave_sum(nc2);
+    na2 = wsum_dpp(na2);
+    nc2 = wsum_dpp(nc2);
     __syncthreads();
-    if ((tid & 63) == 0) { red[tid >> 6][0] = na2; red[tid >> 6][1] = nc2; }
+    if (lane == 0) { red[wv][0] = na2; red[wv][1] = nc2; }
     __syncthreads();
     if (tid == 0) {
       float x = 0.0f, y = 0.0f;
