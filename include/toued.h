@@ -16,9 +16,9 @@
  *     error (-1 bad arguments, -2 launch failure); toued_last_error() returns
  *     a thread-local message.  Calls are re-entrant across streams.
  *   - Keys are jax.random threefry keys: uint32[n][2].
- *   - Levels are packed int32[n][64] records (layout in DESIGN.md §Data
- *     layout): scalars, raw obj_ids, static object cells, per-object resolved
- *     reward/p_terminate/p_respawn, 256-bit walls mask.
+ *   - Levels are packed int32[n][80] records (LEVEL_WORDS, layout in DESIGN.md
+ *     §Data layout): scalars, raw obj_ids, static object cells, per-object
+ *     resolved reward/p_terminate/p_respawn, 256-bit walls mask, type tables.
  *   - Env state is SoA int32[12][n]: time, pos, exists bitmask, early_term,
  *     obj_poss[8].
  *   - Compact observations: tab_idx = pos + max_grid^2 * exists_mask and the
@@ -96,9 +96,6 @@ int toued_batch_reset_masked(EnvSpec spec, const int* levels, const uint32_t* ag
 int toued_rollout(EnvSpec spec, const int* levels, const float* theta, int D, const uint32_t* agent_keys,
                   int* state, int n_agents, int W, int T, int* traj_idx, int* traj_time, uint8_t* traj_action,
                   float* traj_reward, uint8_t* traj_done, float* cum_return, hipStream_t stream);
-/* The same returns-only rollout (eval_agent, agents/agents.py:98-106 over rollout.py:45-102) in three launches,
- * bit-identical: the per-worker key chain (chain: uint32[T][n][4], n = n_agents*W), every state-independent draw of
- * every step in parallel (draws: uint32[T][n][4]), then the env chain on those draws (`state` read only). */
 /* RolloutWrapper.batch_rollout (environments/rollout.py:45-102) in three launches, bit-identical to toued_rollout:
  * the state-independent draws of U batches of train rollouts at once (keys [U][n_agents][2]; chain scratch and draws
  * out u32x4 [T][U * n_agents * W]), then each batch's env chain on its draws (draws = the batch's first worker at
@@ -109,6 +106,9 @@ int toued_rollout_draws(EnvSpec spec, const int* levels, const uint32_t* keys, i
 int toued_rollout_env(EnvSpec spec, const int* levels, const float* theta, int D, int* state, int n_agents, int W, int T,
                       const uint32_t* draws, long dstride, int* traj_idx, int* traj_time, uint8_t* traj_action,
                       float* traj_reward, uint8_t* traj_done, float* cum_return, hipStream_t stream);
+/* The same returns-only rollout (eval_agent, agents/agents.py:98-106 over rollout.py:45-102) in three launches,
+ * bit-identical: the per-worker key chain (chain: uint32[T][n][4], n = n_agents*W), every state-independent draw of
+ * every step in parallel (draws: uint32[T][n][4]), then the env chain on those draws (`state` read only). */
 int toued_eval_keys(const uint32_t* agent_keys, int n_agents, int W, int T, uint32_t* chain, hipStream_t stream);
 int toued_eval_draws(EnvSpec spec, const int* levels, int n_agents, int W, int T, const uint32_t* chain,
                      uint32_t* draws, hipStream_t stream);
@@ -278,6 +278,16 @@ int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit
  * eval_agent rollout) then occupies its own CUs instead of pushing one workgroup of every chunk into a second
  * round.  Workspace sizes queried before the change stay sufficient (fewer chunks).  Returns the previous value. */
 int toued_set_reserved_cus(int n);
+
+/* toued_agent_grad + toued_agent_apply fused, in place, for an agent chain that never reads the gradient tables
+ * (the ES candidates): clip + SGD on theta [N][D][5] / phi [N][D][8] of the touched rows only (bit-identical to
+ * the pair on zeroed tables), step advanced when applied, met accumulated, gstat [N][4] written.  Sizes where
+ * toued_agent_update_fits(W, T, D) is 1 (T*W <= 2048). */
+int toued_agent_update_fits(int W, int T, int D);
+int toued_agent_update(int N, int W, int T, int D, float* theta, float* phi, const int* tidx, const int* ttime,
+                       const uint8_t* tact, const float* trew, const uint8_t* tdone, const float* pi_hat,
+                       const float* y_hat, float alpha_y, float lr_a, float lr_c, float max_norm, float* met, int* step,
+                       const int* levels, float* gstat, hipStream_t stream);
 
 /* ES inference path: pack n candidates' forward fragments (candidate c at eta + c*eta_stride) */
 int toued_gru_pack_fwd_multi(const float* eta, long eta_stride, int n, const int* off, int F, float* fwdA,

@@ -111,6 +111,56 @@ def test_gru_fwd_multi_per_candidate():
                                    atol=5e-6, rtol=0)
 
 
+def test_es_fused_agent_update_bitexact():
+    """toued_agent_update (gradient + clip + SGD in place, the ES default) against toued_agent_grad + toued_agent_apply
+    into ping-pong tables: three agent updates per candidate, lifetime 2 on one agent (a discarded update), the ES
+    step's outputs bit-identical -- winners' tables, steps, env state, metrics, fitness and the new search mean."""
+    from toued import prng
+    from toued.env import L_LIFETIME
+    from toued.es import ESTrainStep
+    from toued.level_sampler import LevelSampler
+    from toued.lpg import LPGLayout
+    from toued.parse_args import parse_args
+    mode, N = "all_vrandlife", 3
+    args = parse_args(["--env_mode", mode, "--num_agents", str(N), "--num_mini_batches", "1", "--use_es",
+                       "--lifetime_conditioning", "--lpg_learning_rate", "0.01"])
+    outs = []
+    for fused in (False, True):
+        smp = LevelSampler(args)
+        buf = smp.initialize_buffer(prng.PRNGKey(0, "cuda"))
+        _, agents = smp.initial_sample(prng.PRNGKey(1, "cuda"), buf, N, False)
+        agents.theta.mul_(20.0)
+        agents.phi.mul_(20.0)
+        agents.levels[1, L_LIFETIME] = 2
+        step = ESTrainStep(args, smp, N, torch.zeros(LPGLayout(7).size, device="cuda"), "cuda", None,
+                           num_agent_updates=3)
+        assert step.fused_update                      # the default where the sizes fit
+        step.fused_update = fused
+        step.es.mean.copy_(torch.from_numpy(np.random.RandomState(5).randn(step.es.nd).astype(np.float32) * 0.05))
+        m = step(dk(jr.PRNGKey(7)), agents)
+        torch.cuda.synchronize()
+        outs.append((agents.theta.clone(), agents.phi.clone(), agents.step.clone(), agents.state.clone(),
+                     step.fitness.clone(), step.es.mean.clone(),
+                     {k: torch.as_tensor(v).detach().clone() for k, v in _flat(m).items()}))
+    nrow = 4 + olv.env_spec(mode).max_n_objs      # state rows the env uses (the rest are never written)
+    for i, name in enumerate(("theta", "phi", "step", "state", "fitness", "es mean")):
+        a, b = (outs[0][i][:nrow], outs[1][i][:nrow]) if name == "state" else (outs[0][i], outs[1][i])
+        assert torch.equal(a, b), name
+    assert outs[0][6].keys() == outs[1][6].keys()
+    for k in outs[0][6]:
+        assert torch.equal(outs[0][6][k], outs[1][6][k]), k
+
+
+def _flat(m, pre=""):
+    out = {}
+    for k, v in m.items():
+        if isinstance(v, dict):
+            out.update(_flat(v, pre + k + "."))
+        else:
+            out[pre + k] = v
+    return out
+
+
 def test_es_step_k1_matches_oracle():
     """K = 1: the device's one trajectory per candidate is fed to the oracle update (the K = 3 test below also
     regenerates the rollouts)."""
@@ -144,7 +194,7 @@ def test_es_step_k1_matches_oracle():
     idx, tm, act = tr.obs_idx.cpu().numpy(), tr.obs_time.cpu().numpy(), tr.action.cpu().numpy()
     rew, dn = tr.reward.cpu().numpy(), tr.done.cpu().numpy()
     hyp = ometa.Hypers(lifetime_conditioning=True)
-    theta_dev = step.theta[1].cpu().numpy()     # K=1: one ping-pong swap
+    theta_dev = step.theta[step.cur].cpu().numpy()     # the candidates' tables after the update
     from oracle.levels import L_LIFETIME
     for c in range(C):
         a = c // 2
@@ -215,7 +265,7 @@ def certify_es_step(args, smp, step, rng, pre, metrics, p_lv, chained=False):
         trajs.append({"idx": otr["idx"], "time": otr["time"], "action": otr["action"].astype(np.int64),
                       "reward": otr["reward"], "done": otr["done"].astype(bool)})
     hyp = ometa.Hypers(lifetime_conditioning=step.F == 7)
-    th_dev, ph_dev = step.theta[K % 2].cpu().numpy(), step.phi[K % 2].cpu().numpy()
+    th_dev, ph_dev = step.theta[step.cur].cpu().numpy(), step.phi[step.cur].cpu().numpy()
     # every update from the device's tables before it (trace): the parameter change within 2e-5 relative L2 of the
     # float64 update under the candidate's LPG (per update, as _a2c_follow: chained over K updates at the actor
     # lr 40 the float32 rounding of one update is amplified into the next one's inputs)

@@ -886,7 +886,7 @@ __global__ void __launch_bounds__(256) k_init_tables(const uint32_t* __restrict_
 
 struct GradOp {   // k_agent_grad (+ the global norms and the lifetime test of the update it feeds)
   static constexpr int NA = 5, NC = 8, NM = 3;
-  static constexpr bool NORMS = true;
+  static constexpr bool NORMS = true, APPLY = false;
   const float* theta; const float* phi; const int* tidx; const int* ttime; const uint8_t* tact; const float* trew;
   const uint8_t* tdone; const float* pi_hat; const float* y_hat; float alpha_y; float* Gth; float* Gph; float* met;
   const int* step; const int* levels; float* gstat;
@@ -937,9 +937,18 @@ struct GradOp {   // k_agent_grad (+ the global norms and the lifetime test of t
   TOUED_DEV void finish(int a, float na2, float nc2) const { grad_stats(a, na2, nc2, step, levels, gstat); }
 };
 
+// GradOp fused with apply_gradients for an agent chain that never reads the gradient tables (the ES candidates'
+// train_lpg_agent): the segment sums stay in LDS, the global norms are reduced in the block, then clip + SGD rewrite
+// the touched rows of theta/phi IN PLACE (an untouched row's update p + -(lr * 0) is the identity, so this is
+// bit-identical to k_agent_grad into zeroed tables + k_agent_apply), the step counter advances and gstat is filled.
+struct GradApplyOp : GradOp {
+  static constexpr bool APPLY = true;
+  float* theta_w; float* phi_w; float lr_a, lr_c, max_norm; int* step_w;
+};
+
 struct EntropyBwdOp {   // k_entropy, gradient mode
   static constexpr int NA = 5, NC = 8, NM = 1;
-  static constexpr bool NORMS = false;
+  static constexpr bool NORMS = false, APPLY = false;
   const float* theta; const float* phi; const int* tidx; const int* ttime; float coef_a, coef_c;
   float* adj_th; float* adj_ph;
   int N, W, T, D;
@@ -983,7 +992,7 @@ struct EntropyBwdOp {   // k_entropy, gradient mode
 
 struct LpgLossOp {   // k_lpgloss_grad
   static constexpr int NA = 5, NC = 0, NM = 1;
-  static constexpr bool NORMS = false;
+  static constexpr bool NORMS = false, APPLY = false;
   const float* theta; const int* tidx; const int* ttime; const uint8_t* tact; const float* abar; float* adj_th;
   int N, W, T, D;
   TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* v, float* m) const {
@@ -1016,7 +1025,7 @@ struct LpgLossOp {   // k_lpgloss_grad
 
 struct HvpOp {   // k_hvp
   static constexpr int NA = 5, NC = 8, NM = 1;
-  static constexpr bool NORMS = false;
+  static constexpr bool NORMS = false, APPLY = false;
   const float* theta; const float* phi; const int* tidx; const int* ttime; const uint8_t* tact;
   const float* pi_hat; const float* y_hat; const float* Gth; const float* Gph; const float* adj_th_in;
   const float* adj_ph_in; const float* coef; float lr_a, lr_c, alpha_y, b2, b3;
@@ -1264,6 +1273,16 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
 #pragma unroll
             for (int j = 0; j < NV; ++j) run[j] += tot[j];
           }
+          if constexpr (Op::APPLY) {   // the row's gradient (0 + sum, as a zeroed table would hold it) to LDS
+            float* slot = vec + (size_t)(kc[e] & SMASK) * NVP;
+#pragma unroll
+            for (int j = 0; j < NV; ++j) {
+              const float g = 0.0f + run[j];
+              slot[j] = g;
+              if (j < NA) na2 += g * g; else nc2 += g * g;
+            }
+            continue;
+          }
           float* ra = op.rowA(a, (int)r);
 #pragma unroll
           for (int j = 0; j < NA; ++j) {
@@ -1284,7 +1303,17 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
       }
     }
   }
-  if (tid == 0) {
+  // APPLY: the step counter and lifetime test before any thread writes them
+  bool applied = false;
+  if constexpr (Op::APPLY) applied = (op.step[a] + 1) <= op.levels[(size_t)a * LEVEL_WORDS + L_LIFETIME];
+  if (Op::APPLY && tid == 0 && !has_last) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const float g = 0.0f + tot[j];
+      if (j < NA) na2 += g * g; else nc2 += g * g;
+    }
+  }
+  if (!Op::APPLY && tid == 0) {
     if (!has_last) {
       float* ra = op.rowA(a, D - 1);
 #pragma unroll
@@ -1311,7 +1340,42 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
     __syncthreads();
     if (lane == 0) { red[wv][0] = na2; red[wv][1] = nc2; }
     __syncthreads();
-    if (tid == 0) {
+    if (Op::APPLY) {
+      if constexpr (Op::APPLY) {
+        float x = 0.0f, y = 0.0f;
+        for (int w = 0; w < 8; ++w) { x += red[w][0]; y += red[w][1]; }
+        const float gna = sqrtf(x), gnc = sqrtf(y);
+        const bool clip_a = !(gna < op.max_norm), clip_c = !(gnc < op.max_norm);
+        auto upd = [&](float p0, float g, bool clip, float gn, float lr) {
+          const float gg = clip ? (g / gn) * op.max_norm : g;
+          return p0 + (-(lr * gg));
+        };
+        auto apply_row = [&](size_t r, const float* g) {
+          float* ta = op.theta_w + ((size_t)a * D + r) * NA;
+          float* tc = op.phi_w + ((size_t)a * D + r) * NC;
+#pragma unroll
+          for (int j = 0; j < NA; ++j) ta[j] = upd(ta[j], g[j], clip_a, gna, op.lr_a);
+#pragma unroll
+          for (int j = 0; j < NC; ++j) tc[j] = upd(tc[j], g[NA + j], clip_c, gnc, op.lr_c);
+        };
+        if (applied) {
+#pragma unroll
+          for (int e = 0; e < CH; ++e)
+            if ((endm >> e) & 1u) apply_row(kc[e] >> 12, vec + (size_t)(kc[e] & SMASK) * NVP);
+          if (tid == 0 && !has_last) {
+            float g[NV];
+#pragma unroll
+            for (int j = 0; j < NV; ++j) g[j] = 0.0f + tot[j];
+            apply_row((size_t)(D - 1), g);
+          }
+        }
+        if (tid == 0) {
+          if (applied) op.step_w[a] += 1;
+          op.finish(a, x, y);
+          op.metrics(a, tot + NV);
+        }
+      }
+    } else if (tid == 0) {
       float x = 0.0f, y = 0.0f;
       for (int w = 0; w < 8; ++w) { x += red[w][0]; y += red[w][1]; }
       op.finish(a, x, y);
@@ -1386,6 +1450,34 @@ int toued_agent_grad(int N, int W, int T, int D, const float* theta, const float
                          ttime, tact, trew, tdone, pi_hat, y_hat, alpha_y, Gth, Gph, met);
   }
   hipLaunchKernelGGL(k_agent_norms, dim3(N), dim3(256), 0, stream, N, D, Gth, Gph, step, levels, gstat);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+// 1 when toued_agent_update supports these sizes (one agent's samples fit the sorted kernel)
+int toued_agent_update_fits(int W, int T, int D) { return W > 0 && T > 0 && T * W <= SORT_MAX_TW && D < (1 << 20) ? 1 : 0; }
+
+// toued_agent_grad + toued_agent_apply for an agent chain that never reads the gradient tables: clip + SGD in place
+// on theta [N][D][5] / phi [N][D][8] (bit-identical to grad into zeroed tables + apply into fresh tables), step
+// advanced when applied, met accumulated, gstat written
+int toued_agent_update(int N, int W, int T, int D, float* theta, float* phi, const int* tidx, const int* ttime,
+                       const uint8_t* tact, const float* trew, const uint8_t* tdone, const float* pi_hat,
+                       const float* y_hat, float alpha_y, float lr_a, float lr_c, float max_norm, float* met, int* step,
+                       const int* levels, float* gstat, hipStream_t stream) {
+  TOUED_REQUIRE(step && levels && gstat && met, "toued_agent_update: met, step, levels and gstat are required");
+  TOUED_REQUIRE(toued_agent_update_fits(W, T, D), "toued_agent_update: W=%d T=%d D=%d unsupported (T*W <= %d)", W, T, D,
+                SORT_MAX_TW);
+  if (N == 0) return 0;
+  GradApplyOp op;
+  static_cast<GradOp&>(op) = GradOp{theta, phi, tidx, ttime, tact, trew, tdone, pi_hat, y_hat, alpha_y, nullptr, nullptr,
+                                    met, step, levels, gstat, N, W, T, D};
+  op.theta_w = theta;
+  op.phi_w = phi;
+  op.lr_a = lr_a;
+  op.lr_c = lr_c;
+  op.max_norm = max_norm;
+  op.step_w = step;
+  TOUED_REQUIRE(launch_sorted(op, N, stream), "toued_agent_update: cannot launch the sorted kernel");
   TOUED_CHECK_LAUNCH();
   return 0;
 }

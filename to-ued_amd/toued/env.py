@@ -134,7 +134,7 @@ class LevelGenerator:
         self.program = torch.from_numpy(prog).to(_dev(device))
 
     def __call__(self, keys: torch.Tensor, buffer_ids: torch.Tensor | None = None, with_sub_mode=False):
-        """keys int32[n,2] (threefry) -> levels int32[n,64] (lifetime and buffer_id packed in)."""
+        """keys int32[n,2] (threefry) -> levels int32[n, LEVEL_WORDS = 80] (lifetime and buffer_id packed in)."""
         n = keys.shape[0]
         levels = torch.empty((n, LEVEL_WORDS), dtype=torch.int32, device=keys.device)
         sub = torch.empty((n,), dtype=torch.int32, device=keys.device) if with_sub_mode else None

@@ -19,6 +19,8 @@ the tell gradient is one all-reduce of a [num_params] vector per ES step.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -150,6 +152,10 @@ class ESTrainStep:
         # test hook: a list receives, per agent update k, the candidates' (theta_k, phi_k, env state before the
         # rollout, trajectory k) as device clones (tests/test_gpu_es.py regenerates every rollout from them)
         self.trace = None
+        # the fused in-place agent update (toued_agent_update) when one candidate's samples fit the sorted kernel;
+        # TOUED_ES_FUSED_UPDATE=0 keeps toued_agent_grad + toued_agent_apply (bit-identical)
+        self.fused_update = (os.environ.get("TOUED_ES_FUSED_UPDATE") != "0"
+                             and bool(_lib.lib().toued_agent_update_fits(self.W, self.T, self.D)))
         # HIP-event timing of the per-update launches (bench.py's C4 roofline); disabled by default
         from .meta import KernelTimers
         self.timers = KernelTimers()
@@ -208,16 +214,25 @@ class ESTrainStep:
             L.call("toued_gru_fwd_multi", R, T, W, self.F, W, ptr(self.X), T * R, 1, ptr(tr.done), ptr(self.fwdA),
                    ptr(self.x), nd, self.lay.c_offsets, ptr(self.pi_hat), ptr(self.y_hat), st)
             self.timers.stop(tok)
-            self.G_th.zero_()
-            self.G_ph.zero_()
-            L.call("toued_agent_grad", C, W, T, D, ptr(th), ptr(ph), ptr(tr.obs_idx), ptr(tr.obs_time),
-                   ptr(tr.action), ptr(tr.reward), ptr(tr.done), ptr(self.pi_hat), ptr(self.y_hat), self.alpha_y,
-                   ptr(self.G_th), ptr(self.G_ph), ptr(self.met), ptr(step), ptr(levels), ptr(self.gstat), st)
-            L.call("toued_agent_apply", C, D, ptr(th), ptr(ph), ptr(self.G_th), ptr(self.G_ph), self.lr_a, self.lr_c,
-                   self.mn, ptr(step), ptr(self.theta[1 - cur]), ptr(self.phi[1 - cur]), ptr(self.gstat), st)
-            cur = 1 - cur
+            if self.fused_update:
+                # gradient + clip + SGD in one kernel, in place on the candidates' tables (bit-identical to the pair
+                # below: the gradient tables are never read again on this path)
+                L.call("toued_agent_update", C, W, T, D, ptr(th), ptr(ph), ptr(tr.obs_idx), ptr(tr.obs_time),
+                       ptr(tr.action), ptr(tr.reward), ptr(tr.done), ptr(self.pi_hat), ptr(self.y_hat), self.alpha_y,
+                       self.lr_a, self.lr_c, self.mn, ptr(self.met), ptr(step), ptr(levels), ptr(self.gstat), st)
+            else:
+                self.G_th.zero_()
+                self.G_ph.zero_()
+                L.call("toued_agent_grad", C, W, T, D, ptr(th), ptr(ph), ptr(tr.obs_idx), ptr(tr.obs_time),
+                       ptr(tr.action), ptr(tr.reward), ptr(tr.done), ptr(self.pi_hat), ptr(self.y_hat), self.alpha_y,
+                       ptr(self.G_th), ptr(self.G_ph), ptr(self.met), ptr(step), ptr(levels), ptr(self.gstat), st)
+                L.call("toued_agent_apply", C, D, ptr(th), ptr(ph), ptr(self.G_th), ptr(self.G_ph), self.lr_a,
+                       self.lr_c, self.mn, ptr(step), ptr(self.theta[1 - cur]), ptr(self.phi[1 - cur]),
+                       ptr(self.gstat), st)
+                cur = 1 - cur
             L.call("toued_entropy", C, W, T, D, ptr(self.theta[cur]), ptr(self.phi[cur]), ptr(tr.obs_idx),
                    ptr(tr.obs_time), ptr(self.met), 0.0, 0.0, None, None, st)
+        self.cur = cur                  # index of the candidates' final tables in self.theta / self.phi
         # ---- fitness = eval_agent(rng_c) (:178-186)
         fitness = eval_agent(self.ro, fit_keys, levels, self.theta[cur], W)
         self.fitness = fitness
