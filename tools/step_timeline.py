@@ -23,3 +23,10 @@ for r in seg:
         print(f"q{r['Queue_Id']:>2} +{(r['s'] - s0) / 1e6:7.3f} {(r['e'] - r['s']) / 1e6:7.3f} ms  {r['n']}")
 for q, v in busy.items():
     print(f"queue {q}: busy {v / 1e6:.3f} ms")
+tot = collections.defaultdict(lambda: [0, 0.0])
+for r in seg:
+    tot[r["n"]][0] += 1
+    tot[r["n"]][1] += r["e"] - r["s"]
+print("per kernel over the step (launches, total ms):")
+for n, (c, t) in sorted(tot.items(), key=lambda x: -x[1][1]):
+    print(f"  {t / 1e6:7.3f} ms  x{c:<3d} {n}")

@@ -9,7 +9,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT" -o run -- python3 "$R/bench.py" --steps 3 \
-    --warmup 2 --no_cpu_baseline > "$OUT/bench.log" 2>&1
+    --warmup 2 --no_cpu_baseline --workloads none > "$OUT/bench.log" 2>&1
 python3 "$R/tools/step_timeline.py" "$OUT" > "$OUT/timeline.txt"
 rm -f "$OUT"/*.db
 find "$OUT" -name "*kernel_trace.csv" -exec gzip -f {} \;
