@@ -111,6 +111,35 @@ def test_gru_fwd_multi_per_candidate():
                                    atol=5e-6, rtol=0)
 
 
+def test_track_best_on_device_matches_evosax_rule():
+    """OpenES.track_best (device-side, no host sync) against evosax 0.1.4's get_best_fitness_member restated on the
+    host: first index of the largest fitness, replaced only when it beats the stored best in the minimisation frame
+    (gen 0 compares against the raw initial value), over generations with ties, a worse generation and a slice of
+    the population held locally (lo > 0)."""
+    from toued.es import OpenES
+    nd, pop = 37, 8
+    es = OpenES(pop, nd, device="cuda")
+    rs = np.random.RandomState(3)
+    x = torch.from_numpy(rs.randn(pop, nd).astype(np.float32)).cuda()
+    host_best, host_member = np.float32(np.finfo(np.float32).max), None
+    fits = [np.array([0.2, 0.9, 0.9, 0.1, 0.0, 0.5, 0.3, 0.9], np.float32),      # ties: the first maximum
+            np.array([0.1, 0.2, 0.3, 0.4, 0.5, 0.6, 0.7, 0.8], np.float32),      # worse: no replacement
+            np.array([0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.95, 0.0], np.float32)]     # better, in the slice below
+    lo = 2
+    for g, fit in enumerate(fits):
+        fmin = -fit
+        i = int(np.argmin(fmin))
+        best_min = -host_best if g > 0 else host_best
+        if fmin[i] < best_min:
+            host_member = x[i].cpu().numpy().copy()
+            best_min = fmin[i]
+        host_best = np.float32(-best_min)
+        es.track_best(x[lo:], torch.from_numpy(fit).cuda(), lo) if g == 2 else es.track_best(x, torch.from_numpy(fit).cuda(), 0)
+        es.gen_counter += 1
+        assert es.best_fitness == host_best, g
+        np.testing.assert_array_equal(es.best_member.cpu().numpy(), host_member, err_msg=str(g))
+
+
 def test_es_fused_agent_update_bitexact():
     """toued_agent_update (gradient + clip + SGD in place, the ES default) against toued_agent_grad + toued_agent_apply
     into ping-pong tables: three agent updates per candidate, lifetime 2 on one agent (a discarded update), the ES

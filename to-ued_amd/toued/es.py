@@ -45,9 +45,12 @@ class OpenES:
         self.popsize = popsize
         self.nd = num_dims
         self.lrate_init, self.sigma_init = np.float32(lrate_init), np.float32(sigma_init)
-        # evosax Strategy.tell's best-member tracker (get_best_fitness_member on the fitness given to tell)
-        self.best_member = None
-        self.best_fitness = np.float32(np.finfo(np.float32).max)
+        # evosax Strategy.tell's best-member tracker (get_best_fitness_member on the fitness given to tell), kept on
+        # the device (best_member / best_fitness read it back)
+        dev0 = torch.device(device) if device is not None else torch.device("cuda")
+        self._best_member_t = None
+        self._best_improved = None
+        self._best_fit_t = torch.tensor(np.finfo(np.float32).max, dtype=torch.float32, device=dev0)
         self.opt = 1 if opt_name == "adam" else 0
         self.lrate_decay, self.lrate_limit = np.float32(lrate_decay), np.float32(lrate_limit)
         self.sigma_decay, self.sigma_limit = np.float32(sigma_decay), np.float32(sigma_limit)
@@ -70,20 +73,36 @@ class OpenES:
     def track_best(self, x_local: torch.Tensor, rank_fitness: torch.Tensor, lo: int, world=None):
         """evosax 0.1.4 get_best_fitness_member (maximize=True) on the full rank-fitness vector, before the
         generation counter advances: the first candidate with the largest fitness replaces the best member when
-        it beats the stored best (compared in the minimisation frame; restated, unpinned)."""
-        fit = rank_fitness.float().cpu().numpy()
-        fmin = -fit
-        idx = int(np.argmin(fmin))
-        best_min = (-self.best_fitness) if self.gen_counter > 0 else self.best_fitness
-        if fmin[idx] < best_min:
-            row = torch.zeros(self.nd, dtype=torch.float32, device=self.mean.device)
-            if lo <= idx < lo + x_local.shape[0]:
-                row.copy_(x_local[idx - lo])
-            if world is not None:
-                world.all_reduce_sum(row)
-            self.best_member = row
-            best_min = fmin[idx]
-        self.best_fitness = np.float32(-best_min)
+        it beats the stored best (compared in the minimisation frame; restated, unpinned).  On the device, without
+        a host synchronisation: argmax's first maximum, the candidate's row masked in on the rank that holds it
+        (summed over ranks), and the replacement as selects."""
+        fmin = -rank_fitness.float()
+        idx = torch.argmin(fmin)                       # first minimum = first maximum of the fitness
+        val = fmin[idx]
+        best = self._best_fit_t
+        best_min = -best if self.gen_counter > 0 else best
+        better = val < best_min
+        n = x_local.shape[0]
+        rel = (idx - lo).clamp(0, n - 1)
+        mine = (idx >= lo) & (idx < lo + n)
+        row = torch.where(mine, x_local[rel].float(), torch.zeros((), device=x_local.device))
+        if world is not None:
+            world.all_reduce_sum(row)
+        prev = self._best_member_t if self._best_member_t is not None else torch.zeros_like(row)
+        self._best_member_t = torch.where(better, row, prev)
+        self._best_improved = better if self._best_improved is None else (self._best_improved | better)
+        self._best_fit_t = -torch.where(better, val, best_min)
+
+    @property
+    def best_member(self):
+        """the tracked best member (None until a generation has been scored), as evosax's EvoState.best_member"""
+        if self._best_member_t is None or not bool(self._best_improved):
+            return None
+        return self._best_member_t
+
+    @property
+    def best_fitness(self):
+        return np.float32(self._best_fit_t.item())
 
     def tell(self, x_local: torch.Tensor, rank_fitness_local: torch.Tensor, world=None):
         fit = (-rank_fitness_local).float().contiguous()          # FitnessShaper(maximize=True)
