@@ -321,6 +321,28 @@ def test_regret_trained_antagonist_matches_oracle(mode, max_lifetime, fused):
     np.testing.assert_allclose(got, r_a2c - r_lpg, atol=1e-5, rtol=0)
 
 
+def test_a2c_chain_full_size_matches_launch_per_update():
+    """C3's antagonist training at full size (512 all_shortlife antagonists x max_lifetime = 250 updates: eight chain
+    launches, the last one partial, draws double-buffered on the side stream) bit-identical to one toued_rollout_env +
+    one toued_a2c_update launch per update: tables, step counters, env state and the mean losses."""
+    from toued.a2c import A2CHyperparams, A2CTrainer
+    mode, N, W, T, U = "all_shortlife", 512, 64, 20, 250
+    ro, levels, p, lt, theta, vcrit, state, D = _a2c_setup(mode, N, W, T, seed=51, scale=1.0)
+    rng = dk(jr.split(jr.PRNGKey(53), N))
+    outs = []
+    for chain in (False, True):
+        th, vc, st = theta.clone(), vcrit.clone(), state.clone()
+        step = torch.zeros(N, dtype=torch.int32, device="cuda")
+        tr = A2CTrainer(ro, A2CHyperparams(), _ahyp(mode), chain=chain)
+        assert tr.use_chain(W, T, D) == chain
+        loss = tr.train(rng, th, vc, step, levels, st, U)
+        torch.cuda.synchronize()
+        outs.append((th, vc, st, step, loss))
+    for x, y, name in zip(outs[0], outs[1], ("theta", "vcrit", "state", "step", "loss")):
+        assert torch.equal(x, y), name
+    assert int(outs[1][3].max()) <= U and int(outs[1][3].min()) >= 1
+
+
 def test_regret_full_size_batch_invariant():
     """C3 at full size: N=512 all_shortlife antagonists trained for the mode's max_lifetime (250) updates in
     one batch (graph-replayed fused kernels).  Size-independent properties: every score finite; the regret of
