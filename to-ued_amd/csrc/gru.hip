@@ -243,6 +243,7 @@ struct FwdArgs {
   long M;
   int rpc;                             // rows per parameter candidate (inference mode, ES)
   long a_stride4, eta_stride;          // per-candidate strides of A (float4 units) and eta (floats)
+  int stagger;                         // inference mode: s_sleep(127) quanta half of the first round waits at start
 };
 
 #define NWAVE 8         // 512-thread workgroups: wave w owns units [32w, 32w+32)
@@ -673,6 +674,11 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   };
   const __amdgpu_buffer_rsrc_t rs_hin = rsrc_of(p.s_hin), rs_r = rsrc_of(p.s_r), rs_z = rsrc_of(p.s_z),
                                rs_hn = rsrc_of(p.s_hn);
+  // ES candidates: the per-candidate fragment stream from the Infinity Cache is what a step's contraction waits on,
+  // and the gate maths leave it idle; half of the first round's workgroups (alternate CUs of every XCD) start about
+  // half a step late so the two halves contract at different times (later rounds inherit the offset)
+  if (!SAVE && p.stagger > 0 && blockIdx.x < 256 && ((blockIdx.x >> 3) & 1))
+    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   for (int s = 0; s < T; ++s) {
     const int t = T - 1 - s;
     FWD_STAMP(0);
@@ -1544,6 +1550,9 @@ static int gru_fwd_launch(int R, int T, int W, int F, const float* X, long xs_f,
   memcpy(&p.o, off, sizeof(EtaOff));
   p.pi_hat = pi_hat; p.y_hat = y_hat; p.s_hin = s_hin; p.s_r = s_r; p.s_z = s_z; p.s_n = s_n; p.s_hn = s_hn; p.M = M;
   p.rpc = rpc; p.a_stride4 = (long)toued_gru_packed_floats(2) / 4; p.eta_stride = eta_stride;
+  // 3 quanta (~24 k cycles, about half a step): gru_fwd_multi 2.399 -> 2.363 ms at C4 (2 and 5: 2.372 / 2.363)
+  static const int stagger = getenv("TOUED_FWD_STAGGER") ? atoi(getenv("TOUED_FWD_STAGGER")) : 3;
+  p.stagger = stagger;
   // two row tiles per workgroup when the rows (and, for per-candidate parameters, each candidate's rows)
   // split into 64-row blocks
   const bool nt2 = R % (2 * RB) == 0 && (rpc == 0 || rpc % (2 * RB) == 0);
