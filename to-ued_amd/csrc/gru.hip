@@ -677,7 +677,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   // ES candidates: the per-candidate fragment stream from the Infinity Cache is what a step's contraction waits on,
   // and the gate maths leave it idle; half of the first round's workgroups (alternate CUs of every XCD) start about
   // half a step late so the two halves contract at different times (later rounds inherit the offset)
-  if (!SAVE && p.stagger > 0 && blockIdx.x < 256 && ((blockIdx.x >> 3) & 1))
+  if (p.stagger > 0 && blockIdx.x < 256 && ((blockIdx.x >> 3) & 1))
     for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   for (int s = 0; s < T; ++s) {
     const int t = T - 1 - s;
@@ -1552,7 +1552,9 @@ static int gru_fwd_launch(int R, int T, int W, int F, const float* X, long xs_f,
   p.rpc = rpc; p.a_stride4 = (long)toued_gru_packed_floats(2) / 4; p.eta_stride = eta_stride;
   // 3 quanta (~24 k cycles, about half a step): gru_fwd_multi 2.399 -> 2.363 ms at C4 (2 and 5: 2.372 / 2.363)
   static const int stagger = getenv("TOUED_FWD_STAGGER") ? atoi(getenv("TOUED_FWD_STAGGER")) : 3;
-  p.stagger = stagger;
+  // the SAVE instance (shared, L2-resident fragments) gains nothing from it: 1.064 ms vs 1.071 / 1.076 at 3 / 5
+  static const int stagger_save = getenv("TOUED_FWD_STAGGER_SAVE") ? atoi(getenv("TOUED_FWD_STAGGER_SAVE")) : 0;
+  p.stagger = save ? stagger_save : stagger;
   // two row tiles per workgroup when the rows (and, for per-candidate parameters, each candidate's rows)
   // split into 64-row blocks
   const bool nt2 = R % (2 * RB) == 0 && (rpc == 0 || rpc % (2 * RB) == 0);
