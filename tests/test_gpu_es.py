@@ -169,15 +169,16 @@ def test_es_fused_agent_update_bitexact():
         m = step(dk(jr.PRNGKey(7)), agents)
         torch.cuda.synchronize()
         outs.append((agents.theta.clone(), agents.phi.clone(), agents.step.clone(), agents.state.clone(),
-                     step.fitness.clone(), step.es.mean.clone(),
+                     step.fitness.clone(), step.es.mean.clone(), step.gstat.clone(),
                      {k: torch.as_tensor(v).detach().clone() for k, v in _flat(m).items()}))
     nrow = 4 + olv.env_spec(mode).max_n_objs      # state rows the env uses (the rest are never written)
-    for i, name in enumerate(("theta", "phi", "step", "state", "fitness", "es mean")):
+    # gstat of the last update: norms and the applied flag (step + 1 <= lifetime, read before the step advances)
+    for i, name in enumerate(("theta", "phi", "step", "state", "fitness", "es mean", "gstat")):
         a, b = (outs[0][i][:nrow], outs[1][i][:nrow]) if name == "state" else (outs[0][i], outs[1][i])
         assert torch.equal(a, b), name
-    assert outs[0][6].keys() == outs[1][6].keys()
-    for k in outs[0][6]:
-        assert torch.equal(outs[0][6][k], outs[1][6][k]), k
+    assert outs[0][7].keys() == outs[1][7].keys()
+    for k in outs[0][7]:
+        assert torch.equal(outs[0][7][k], outs[1][7][k]), k
 
 
 def _flat(m, pre=""):

@@ -487,6 +487,47 @@ def test_mini_batches_match_full_batch(nmb):
     assert float((e1 - e2).abs().max()) < 1e-7
 
 
+@pytest.mark.parametrize("mode,N,lc", [("tabular", 512, False), ("all_vrandlife", 16, True)])
+def test_fused_agent_step_matches_dense_path(monkeypatch, mode, N, lc):
+    """The inner updates as toued_agent_step (theta_{k+1} copied on the side stream, touched rows rewritten,
+    gradient rows and row lists kept, clip_dot over those rows) against the dense toued_agent_grad + apply +
+    clip_dot path, over two consecutive meta-steps (the second one's gradient tables hold the first one's rows
+    where it does not write): every theta_k / phi_k, the agents, metrics and gstat bit-identical; the
+    meta-gradient up to the clip-VJP dot's summation order (1e-6)."""
+    from toued.lpg import init_lpg_params
+    from toued.meta import AdamState, LpgHyperparams, MetaGradStep
+    W, T, K = 64, 20, 5
+    ro, ag0 = _agents_for(mode, N, W, T, 90)
+    eta0 = init_lpg_params(91, 7 if lc else 5)
+    out = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("TOUED_META_FUSED_STEP", fused)
+        ag = _clone_agents(ag0)
+        step = MetaGradStep(ro, N, LpgHyperparams(num_agent_updates=K), lc)
+        assert step.fused_step == (fused == "1")
+        hist = []
+        for i in range(2):   # the same eta both times (Adam's step would carry the gradients' last-bit difference)
+            eta = eta0.clone()
+            met = step(torch.tensor([5, 60 + i], dtype=torch.int32, device="cuda"), eta,
+                       AdamState(eta.numel(), "cuda"), ag)
+            torch.cuda.synchronize()
+            hist.append((step.theta_h.clone(), step.phi_h.clone(), step.gstat.clone(), step.grad.clone(), met))
+        out.append((ag, hist))
+    (a0, h0), (a1, h1) = out
+    for name in ("theta", "phi", "step", "state", "vstep"):
+        assert torch.equal(getattr(a0, name), getattr(a1, name)), name
+    for (th0, ph0, gs0, g0, m0), (th1, ph1, gs1, g1, m1) in zip(h0, h1):
+        assert torch.equal(th0, th1) and torch.equal(ph0, ph1)
+        assert torch.equal(gs0, gs1)
+        for k in m0["lpg_agent"]:
+            assert torch.equal(m0["lpg_agent"][k], m1["lpg_agent"][k]), k
+        for k in ("lpg_loss", "lpg_agent_return"):
+            assert torch.equal(m0[k], m1[k]), k
+        rel = float((g0 - g1).norm() / g0.norm())
+        print(f"meta-gradient fused vs dense rel L2 {rel:.2e}")
+        assert rel < 1e-6
+
+
 def test_1024_agents_two_mini_batches_on_one_gpu():
     """A reference-legal --num_agents 1024 --num_mini_batches 2 on one GPU (one 512-agent batch alone is the
     bench's size; 1024 at once exceeds the GRU kernels' 4 GiB operand range): each chunk equals an unchunked

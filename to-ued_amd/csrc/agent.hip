@@ -23,6 +23,8 @@
 #include "wave_dev.h"
 
 #define EPSF 1e-8f
+#define SORT_MAX_TW 2048                  // samples per agent the sorted row kernel holds
+#define ROWS_STRIDE (SORT_MAX_TW + 4)     // per-agent row list of toued_agent_step (uint32)
 
 namespace {
 
@@ -550,6 +552,25 @@ __global__ void __launch_bounds__(256) k_lpgloss_grad(int N, int W, int T, int D
 // thread and table so four vector loads are in flight per thread.
 TOUED_DEV float dot4(float4 x, float4 y) { return x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w; }
 
+// the clip VJP coefficients of agent a from sa = <G_theta, adj_theta>, sc = <G_phi, adj_phi> (optax
+// clip_by_global_norm: g * max_norm / |g| when |g| >= max_norm)
+TOUED_DEV void clip_coef(int a, float sa, float sc, const float* gstat, float lr_a, float lr_c, float max_norm,
+                         float* coef) {
+  const float gna = gstat[a * 4 + 0], gnc = gstat[a * 4 + 1];
+  const bool applied = gstat[a * 4 + 2] > 0.5f;
+  float aa = 0.0f, ba = 0.0f, ac = 0.0f, bc = 0.0f;
+  if (applied) {
+    if (gna < max_norm) { aa = 1.0f; }
+    else { aa = max_norm / gna; ba = -max_norm * (-lr_a * sa) / (gna * gna * gna); }
+    if (gnc < max_norm) { ac = 1.0f; }
+    else { ac = max_norm / gnc; bc = -max_norm * (-lr_c * sc) / (gnc * gnc * gnc); }
+  }
+  coef[a * 4 + 0] = aa;
+  coef[a * 4 + 1] = ba;
+  coef[a * 4 + 2] = ac;
+  coef[a * 4 + 3] = bc;
+}
+
 __global__ void __launch_bounds__(1024) k_clip_dot(int N, int D, const float* __restrict__ Gth,
                                                    const float* __restrict__ Gph, const float* __restrict__ adj_th,
                                                    const float* __restrict__ adj_ph, const float* __restrict__ gstat,
@@ -602,19 +623,42 @@ __global__ void __launch_bounds__(1024) k_clip_dot(int N, int D, const float* __
   if (threadIdx.x == 0) {
     float sa = 0.0f, sc = 0.0f;
     for (int i = 0; i < 16; ++i) { sa += red[0][i]; sc += red[1][i]; }
-    const float gna = gstat[a * 4 + 0], gnc = gstat[a * 4 + 1];
-    const bool applied = gstat[a * 4 + 2] > 0.5f;
-    float aa = 0.0f, ba = 0.0f, ac = 0.0f, bc = 0.0f;
-    if (applied) {
-      if (gna < max_norm) { aa = 1.0f; }
-      else { aa = max_norm / gna; ba = -max_norm * (-lr_a * sa) / (gna * gna * gna); }
-      if (gnc < max_norm) { ac = 1.0f; }
-      else { ac = max_norm / gnc; bc = -max_norm * (-lr_c * sc) / (gnc * gnc * gnc); }
-    }
-    coef[a * 4 + 0] = aa;
-    coef[a * 4 + 1] = ba;
-    coef[a * 4 + 2] = ac;
-    coef[a * 4 + 3] = bc;
+    clip_coef(a, sa, sc, gstat, lr_a, lr_c, max_norm, coef);
+  }
+}
+
+// <G, adjoint> over the rows update k touched only (toued_agent_step's row lists; the gradient tables hold stale
+// values elsewhere): one 512-thread block per agent, four list entries per thread plus the time-row entry
+__global__ void __launch_bounds__(512) k_clip_dot_rows(int D, const uint32_t* __restrict__ rows,
+                                                       const float* __restrict__ Gth, const float* __restrict__ Gph,
+                                                       const float* __restrict__ adj_th,
+                                                       const float* __restrict__ adj_ph,
+                                                       const float* __restrict__ gstat, float lr_a, float lr_c,
+                                                       float max_norm, float* __restrict__ coef) {
+  const int a = blockIdx.x, tid = threadIdx.x;
+  __shared__ float red[2][8];
+  const uint32_t* lr = rows + (size_t)a * ROWS_STRIDE;
+  const uint4 x = reinterpret_cast<const uint4*>(lr)[tid];
+  const uint32_t rr[5] = {x.x, x.y, x.z, x.w, tid == 0 ? lr[SORT_MAX_TW] : 0xFFFFFFFFu};
+  const size_t baseA = (size_t)a * D * 5, baseC = (size_t)a * D * 8;
+  float da = 0.0f, dc = 0.0f;
+#pragma unroll
+  for (int e = 0; e < 5; ++e) {
+    if (rr[e] == 0xFFFFFFFFu) continue;
+    const size_t oa = baseA + (size_t)rr[e] * 5, oc = baseC + (size_t)rr[e] * 8;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) da += Gth[oa + j] * adj_th[oa + j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dc += Gph[oc + j] * adj_ph[oc + j];
+  }
+  da = wsum_dpp(da);
+  dc = wsum_dpp(dc);
+  if ((tid & 63) == 0) { red[0][tid >> 6] = da; red[1][tid >> 6] = dc; }
+  __syncthreads();
+  if (tid == 0) {
+    float sa = 0.0f, sc = 0.0f;
+    for (int i = 0; i < 8; ++i) { sa += red[0][i]; sc += red[1][i]; }
+    clip_coef(a, sa, sc, gstat, lr_a, lr_c, max_norm, coef);
   }
 }
 
@@ -882,11 +926,10 @@ __global__ void __launch_bounds__(256) k_init_tables(const uint32_t* __restrict_
 // read-modify-write (each row has exactly one writer in the grid).  Same sums, no atomics, and the result is
 // deterministic.  The time row (D-1, every sample contributes c * v) is a block reduction added by its
 // segment's owner (or thread 0).
-#define SORT_MAX_TW 2048
 
 struct GradOp {   // k_agent_grad (+ the global norms and the lifetime test of the update it feeds)
   static constexpr int NA = 5, NC = 8, NM = 3;
-  static constexpr bool NORMS = true, APPLY = false;
+  static constexpr bool NORMS = true, APPLY = false, WRITE_G = false;
   const float* theta; const float* phi; const int* tidx; const int* ttime; const uint8_t* tact; const float* trew;
   const uint8_t* tdone; const float* pi_hat; const float* y_hat; float alpha_y; float* Gth; float* Gph; float* met;
   const int* step; const int* levels; float* gstat;
@@ -944,11 +987,21 @@ struct GradOp {   // k_agent_grad (+ the global norms and the lifetime test of t
 struct GradApplyOp : GradOp {
   static constexpr bool APPLY = true;
   float* theta_w; float* phi_w; float lr_a, lr_c, max_norm; int* step_w;
+  uint32_t* rows;
+};
+
+// The meta-gradient's inner update k (toued_agent_step): GradApplyOp reading theta_k / phi_k (GradOp::theta, phi)
+// and rewriting the touched rows of theta_{k+1} / phi_{k+1} (theta_w, phi_w: copies of theta_k / phi_k made
+// beforehand), and keeping what the reverse pass reads of the update: the gradient rows it touched (Gth / Gph, rows
+// never read elsewhere are left as they were) and where they are (rows: [ROWS_STRIDE] per agent, the row at each
+// sorted segment's last entry and NONE elsewhere, entry SORT_MAX_TW the time row D-1 when no sample visited it).
+struct GradStepOp : GradApplyOp {
+  static constexpr bool WRITE_G = true;
 };
 
 struct EntropyBwdOp {   // k_entropy, gradient mode
   static constexpr int NA = 5, NC = 8, NM = 1;
-  static constexpr bool NORMS = false, APPLY = false;
+  static constexpr bool NORMS = false, APPLY = false, WRITE_G = false;
   const float* theta; const float* phi; const int* tidx; const int* ttime; float coef_a, coef_c;
   float* adj_th; float* adj_ph;
   int N, W, T, D;
@@ -992,7 +1045,7 @@ struct EntropyBwdOp {   // k_entropy, gradient mode
 
 struct LpgLossOp {   // k_lpgloss_grad
   static constexpr int NA = 5, NC = 0, NM = 1;
-  static constexpr bool NORMS = false, APPLY = false;
+  static constexpr bool NORMS = false, APPLY = false, WRITE_G = false;
   const float* theta; const int* tidx; const int* ttime; const uint8_t* tact; const float* abar; float* adj_th;
   int N, W, T, D;
   TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* v, float* m) const {
@@ -1025,7 +1078,7 @@ struct LpgLossOp {   // k_lpgloss_grad
 
 struct HvpOp {   // k_hvp
   static constexpr int NA = 5, NC = 8, NM = 1;
-  static constexpr bool NORMS = false, APPLY = false;
+  static constexpr bool NORMS = false, APPLY = false, WRITE_G = false;
   const float* theta; const float* phi; const int* tidx; const int* ttime; const uint8_t* tact;
   const float* pi_hat; const float* y_hat; const float* Gth; const float* Gph; const float* adj_th_in;
   const float* adj_ph_in; const float* coef; float lr_a, lr_c, alpha_y, b2, b3;
@@ -1275,10 +1328,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
           }
           if constexpr (Op::APPLY) {   // the row's gradient (0 + sum, as a zeroed table would hold it) to LDS
             float* slot = vec + (size_t)(kc[e] & SMASK) * NVP;
+            float* ga = nullptr;
+            float* gc = nullptr;
+            if constexpr (Op::WRITE_G) { ga = op.rowA(a, (int)r); gc = op.rowC(a, (int)r); }
 #pragma unroll
             for (int j = 0; j < NV; ++j) {
               const float g = 0.0f + run[j];
               slot[j] = g;
+              if constexpr (Op::WRITE_G) { if (j < NA) ga[j] = g; else gc[j - NA] = g; }
               if (j < NA) na2 += g * g; else nc2 += g * g;
             }
             continue;
@@ -1307,11 +1364,23 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   bool applied = false;
   if constexpr (Op::APPLY) applied = (op.step[a] + 1) <= op.levels[(size_t)a * LEVEL_WORDS + L_LIFETIME];
   if (Op::APPLY && tid == 0 && !has_last) {
+    float* ga = nullptr;
+    float* gc = nullptr;
+    if constexpr (Op::WRITE_G) { ga = op.rowA(a, D - 1); gc = op.rowC(a, D - 1); }
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
       const float g = 0.0f + tot[j];
+      if constexpr (Op::WRITE_G) { if (j < NA) ga[j] = g; else gc[j - NA] = g; }
       if (j < NA) na2 += g * g; else nc2 += g * g;
     }
+  }
+  if constexpr (Op::WRITE_G) {   // where the gradient rows are, for the reverse pass's <G, adjoint>
+    uint32_t* lr = op.rows + (size_t)a * ROWS_STRIDE;
+    uint32_t o[CH];
+#pragma unroll
+    for (int e = 0; e < CH; ++e) o[e] = ((endm >> e) & 1u) ? (kc[e] >> 12) : NONE;
+    reinterpret_cast<uint4*>(lr)[tid] = make_uint4(o[0], o[1], o[2], o[3]);
+    if (tid == 0) lr[SORT_MAX_TW] = has_last ? NONE : (uint32_t)(D - 1);
   }
   if (!Op::APPLY && tid == 0) {
     if (!has_last) {
@@ -1350,13 +1419,16 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
           const float gg = clip ? (g / gn) * op.max_norm : g;
           return p0 + (-(lr * gg));
         };
+        // read theta / phi (theta_k), write theta_w / phi_w (the same tables in place, or theta_{k+1})
         auto apply_row = [&](size_t r, const float* g) {
+          const float* src_a = op.theta + ((size_t)a * D + r) * NA;
+          const float* src_c = op.phi + ((size_t)a * D + r) * NC;
           float* ta = op.theta_w + ((size_t)a * D + r) * NA;
           float* tc = op.phi_w + ((size_t)a * D + r) * NC;
 #pragma unroll
-          for (int j = 0; j < NA; ++j) ta[j] = upd(ta[j], g[j], clip_a, gna, op.lr_a);
+          for (int j = 0; j < NA; ++j) ta[j] = upd(src_a[j], g[j], clip_a, gna, op.lr_a);
 #pragma unroll
-          for (int j = 0; j < NC; ++j) tc[j] = upd(tc[j], g[NA + j], clip_c, gnc, op.lr_c);
+          for (int j = 0; j < NC; ++j) tc[j] = upd(src_c[j], g[NA + j], clip_c, gnc, op.lr_c);
         };
         if (applied) {
 #pragma unroll
@@ -1370,9 +1442,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
           }
         }
         if (tid == 0) {
-          if (applied) op.step_w[a] += 1;
-          op.finish(a, x, y);
+          op.finish(a, x, y);   // reads step[a]: before the increment
           op.metrics(a, tot + NV);
+          if (applied) op.step_w[a] += 1;
         }
       }
     } else if (tid == 0) {
@@ -1477,10 +1549,56 @@ int toued_agent_update(int N, int W, int T, int D, float* theta, float* phi, con
   op.lr_c = lr_c;
   op.max_norm = max_norm;
   op.step_w = step;
+  op.rows = nullptr;
   TOUED_REQUIRE(launch_sorted(op, N, stream), "toued_agent_update: cannot launch the sorted kernel");
   TOUED_CHECK_LAUNCH();
   return 0;
 }
+
+// The meta-gradient's inner update k: toued_agent_grad + toued_agent_apply without the dense passes.  theta1 / phi1
+// must already hold copies of theta / phi (theta_k); the touched rows of theta1 / phi1 are rewritten by clip + SGD
+// (bit-identical to toued_agent_apply), the touched gradient rows go to Gth / Gph (bit-identical to toued_agent_grad
+// there; the other rows are not written and must not be read: toued_clip_dot_rows and toued_hvp read touched rows
+// only) and their row lists to rows [N][ROWS_STRIDE].  step advanced when applied, met accumulated, gstat written.
+int toued_agent_step(int N, int W, int T, int D, const float* theta, const float* phi, float* theta1, float* phi1,
+                     const int* tidx, const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
+                     const float* pi_hat, const float* y_hat, float alpha_y, float lr_a, float lr_c, float max_norm,
+                     float* Gth, float* Gph, uint32_t* rows, float* met, int* step, const int* levels, float* gstat,
+                     hipStream_t stream) {
+  TOUED_REQUIRE(step && levels && gstat && met && Gth && Gph && rows && theta1 && phi1,
+                "toued_agent_step: every output is required");
+  TOUED_REQUIRE(toued_agent_update_fits(W, T, D), "toued_agent_step: W=%d T=%d D=%d unsupported (T*W <= %d)", W, T, D,
+                SORT_MAX_TW);
+  TOUED_REQUIRE(theta1 != theta && phi1 != phi, "toued_agent_step: theta1 / phi1 must be separate tables");
+  if (N == 0) return 0;
+  GradStepOp op;
+  static_cast<GradOp&>(op) = GradOp{theta, phi, tidx, ttime, tact, trew, tdone, pi_hat, y_hat, alpha_y, Gth, Gph,
+                                    met, step, levels, gstat, N, W, T, D};
+  op.theta_w = theta1;
+  op.phi_w = phi1;
+  op.lr_a = lr_a;
+  op.lr_c = lr_c;
+  op.max_norm = max_norm;
+  op.step_w = step;
+  op.rows = rows;
+  TOUED_REQUIRE(launch_sorted(op, N, stream), "toued_agent_step: cannot launch the sorted kernel");
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_clip_dot_rows(int N, int D, const uint32_t* rows, const float* Gth, const float* Gph, const float* adj_th,
+                        const float* adj_ph, const float* gstat, float lr_a, float lr_c, float max_norm, float* coef,
+                        hipStream_t stream) {
+  if (N == 0) return 0;
+  TOUED_REQUIRE(rows && aligned16(rows), "toued_clip_dot_rows: rows must be a 16-byte aligned [N][%d] list",
+                ROWS_STRIDE);
+  hipLaunchKernelGGL(k_clip_dot_rows, dim3(N), dim3(512), 0, stream, D, rows, Gth, Gph, adj_th, adj_ph, gstat, lr_a,
+                     lr_c, max_norm, coef);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_agent_rows_stride(void) { return ROWS_STRIDE; }
 
 int toued_agent_apply(int N, int D, const float* th0, const float* ph0, const float* Gth, const float* Gph,
                       float lr_a, float lr_c, float max_norm, int* step, float* th1, float* ph1, const float* gstat,

@@ -16,6 +16,7 @@ train_lpg_agent, then the eval-rollout and eval_agent keys).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -138,6 +139,14 @@ class MetaGradStep:
         self.phi_h = z(K + 1, N, D, Y)
         self.G_th = z(K, N, D, 5)
         self.G_ph = z(K, N, D, Y)
+        # inner updates as toued_agent_step (sparse: theta_{k+1} copied on a side stream beside rollout k and the
+        # LPG forward, then only the touched rows rewritten; gradient rows and their lists kept for the reverse
+        # pass's clip_dot_rows) where one agent's samples fit the sorted row kernel; TOUED_META_FUSED_STEP=0 keeps
+        # the dense grad + apply + clip_dot path
+        self.fused_step = (os.environ.get("TOUED_META_FUSED_STEP", "1") != "0"
+                           and bool(_lib.lib().toued_agent_update_fits(W, T, D)))
+        self.rows = (torch.empty(K, N, _lib.lib().toued_agent_rows_stride(), dtype=torch.int32, device=dev)
+                     if self.fused_step else None)
         self.gstat = z(K, N, 4)
         self.met = z(K, N, 8)
         self.traj = Transition(z(K + 1, N, T + 1, W, dt=i32), z(K + 1, N, T + 1, W, dt=i32),
@@ -225,15 +234,23 @@ class MetaGradStep:
                ptr(self.keys_ea_reset), ptr(self.keys_ea_roll), st)
         self.theta_h[0].copy_(agents.theta)
         self.phi_h[0].copy_(agents.phi)
-        self.G_th.zero_()
-        self.G_ph.zero_()
+        if not self.fused_step:   # the fused step writes the touched gradient rows, and nothing reads the others
+            self.G_th.zero_()
+            self.G_ph.zero_()
         self.met.zero_()
+        main = torch.cuda.current_stream()
         e1w, e1b = self._eta(eta, "e1_w"), self._eta(eta, "e1_b")
         e2w, e2b = self._eta(eta, "e2_w"), self._eta(eta, "e2_b")
         state = agents.state
         # ---------------- forward: K inner updates (agents/lpg_agent.py:88-140)
         for k in range(K):
             tk = self._t(k)
+            if self.fused_step:
+                # theta_{k+1} <- theta_k beside this update's rollout and LPG forward (theta_k is final here)
+                self.side.wait_stream(main)
+                with torch.cuda.stream(self.side):
+                    self.theta_h[k + 1].copy_(self.theta_h[k])
+                    self.phi_h[k + 1].copy_(self.phi_h[k])
             tok = self.timers.start("rollout")
             self.ro.batch_rollout(self.keys_roll[k], self.theta_h[k], agents.levels, state, out=tk,
                                   inplace_state=True)
@@ -245,16 +262,24 @@ class MetaGradStep:
             tok = self.timers.start("gru_fwd")
             self.gru.forward(k, self.X, tk.done, eta, self.pi_hat, self.y_hat)
             self.timers.stop(tok)
-            L.call("toued_agent_grad", N, W, T, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(tk.obs_idx),
-                   ptr(tk.obs_time), ptr(tk.action), ptr(tk.reward), ptr(tk.done), ptr(self.pi_hat[k]),
-                   ptr(self.y_hat[k]), hyp.agent_target_coeff, ptr(self.G_th[k]), ptr(self.G_ph[k]),
-                   ptr(self.met[k]), ptr(agents.step), ptr(agents.levels), ptr(self.gstat[k]), st)
-            L.call("toued_agent_apply", N, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(self.G_th[k]),
-                   ptr(self.G_ph[k]), hyp.actor_lr, hyp.critic_lr, hyp.max_grad_norm, ptr(agents.step),
-                   ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(self.gstat[k]), st)
+            if self.fused_step:
+                main.wait_stream(self.side)
+                L.call("toued_agent_step", N, W, T, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]),
+                       ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(tk.obs_idx), ptr(tk.obs_time),
+                       ptr(tk.action), ptr(tk.reward), ptr(tk.done), ptr(self.pi_hat[k]), ptr(self.y_hat[k]),
+                       hyp.agent_target_coeff, hyp.actor_lr, hyp.critic_lr, hyp.max_grad_norm, ptr(self.G_th[k]),
+                       ptr(self.G_ph[k]), ptr(self.rows[k]), ptr(self.met[k]), ptr(agents.step), ptr(agents.levels),
+                       ptr(self.gstat[k]), st)
+            else:
+                L.call("toued_agent_grad", N, W, T, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(tk.obs_idx),
+                       ptr(tk.obs_time), ptr(tk.action), ptr(tk.reward), ptr(tk.done), ptr(self.pi_hat[k]),
+                       ptr(self.y_hat[k]), hyp.agent_target_coeff, ptr(self.G_th[k]), ptr(self.G_ph[k]),
+                       ptr(self.met[k]), ptr(agents.step), ptr(agents.levels), ptr(self.gstat[k]), st)
+                L.call("toued_agent_apply", N, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(self.G_th[k]),
+                       ptr(self.G_ph[k]), hyp.actor_lr, hyp.critic_lr, hyp.max_grad_norm, ptr(agents.step),
+                       ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(self.gstat[k]), st)
             L.call("toued_entropy", N, W, T, D, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(tk.obs_idx),
                    ptr(tk.obs_time), ptr(self.met[k]), 0.0, 0.0, None, None, st)
-        main = torch.cuda.current_stream()
         # ---------------- value critic on the train rollouts (--fix_value_critic), eval rollout, lpg loss
         if hyp.fix_value_critic:
             self.vc_loss.zero_()
@@ -304,9 +329,14 @@ class MetaGradStep:
             L.call("toued_entropy", N, W, T, D, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(tk.obs_idx),
                    ptr(tk.obs_time), None, -hyp.policy_entropy_coeff / K, -hyp.target_entropy_coeff / K,
                    ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]), st)
-            L.call("toued_clip_dot", N, D, ptr(self.G_th[k]), ptr(self.G_ph[k]), ptr(self.adj_th[a_in]),
-                   ptr(self.adj_ph[a_in]), ptr(self.gstat[k]), hyp.actor_lr, hyp.critic_lr, hyp.max_grad_norm,
-                   ptr(self.coef), st)
+            if self.fused_step:
+                L.call("toued_clip_dot_rows", N, D, ptr(self.rows[k]), ptr(self.G_th[k]), ptr(self.G_ph[k]),
+                       ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]), ptr(self.gstat[k]), hyp.actor_lr,
+                       hyp.critic_lr, hyp.max_grad_norm, ptr(self.coef), st)
+            else:
+                L.call("toued_clip_dot", N, D, ptr(self.G_th[k]), ptr(self.G_ph[k]), ptr(self.adj_th[a_in]),
+                       ptr(self.adj_ph[a_in]), ptr(self.gstat[k]), hyp.actor_lr, hyp.critic_lr, hyp.max_grad_norm,
+                       ptr(self.coef), st)
             # theta_bar_k = theta_bar_{k+1} + (sparse second-order rows): accumulated in place.  k_rows_sorted reads
             # every sample's adjoint rows before its first row write (the sort's barriers separate the phases), and
             # each agent's tables belong to one workgroup, so no copy of the 144 MB adjoint is needed.
