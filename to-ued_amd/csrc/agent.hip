@@ -803,7 +803,15 @@ __global__ void __launch_bounds__(256) k_embed_bwd(int N, int W, int T, int D, i
   const int total = K * NTW;
   const int R = N * W;
   const int nthr = gridDim.x * (blockDim.x >> 2);
-  for (int g = blockIdx.x * (blockDim.x >> 2) + (threadIdx.x >> 2); g < total; g += nthr) {
+  // a sample's loads that do not depend on its observation rows: issued one sample ahead (the clamped index keeps
+  // the prefetch unconditional, so the wait counts stay per load)
+  struct In {
+    const float* ph;
+    int ix[2];
+    float cx[2], cg[2], lastC[8];
+  };
+  auto load_in = [&](int g) {
+    In v;
     const int k = (unsigned)g / (unsigned)NTW;
     const int s = g - k * NTW;
     const int at = (unsigned)s / (unsigned)W;
@@ -814,18 +822,38 @@ __global__ void __launch_bounds__(256) k_embed_bwd(int N, int W, int T, int D, i
     const int* tidx = tidx_hist + k * tidx_stride;
     const int* ttime = ttime_hist + k * tidx_stride;
     const uint8_t* tdone = tdone_hist + k * tstep_stride;
-    const float* ph = phi_hist + k * phi_stride + (size_t)a * D * 8;
+    v.ph = phi_hist + k * phi_stride + (size_t)a * D * 8;
     const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
-    float lastC[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
+    for (int j = 0; j < 8; ++j) v.lastC[j] = v.ph[(size_t)(D - 1) * 8 + j];
     const size_t o = (size_t)k * dx_stride_k + (size_t)t * R + r;
+    v.ix[0] = tidx[o0];
+    v.ix[1] = tidx[o0 + W];
+    v.cx[0] = (float)ttime[o0] * 0.001f;
+    v.cx[1] = (float)ttime[o0 + W] * 0.001f;
+    v.cg[0] = dX3[o];
+    v.cg[1] = tdone[s] ? 0.0f : dX4[o];
+    return v;
+  };
+  const int g0 = blockIdx.x * (blockDim.x >> 2) + (threadIdx.x >> 2);
+  In nx = load_in(min(g0, total - 1));
+  for (int g = g0; g < total; g += nthr) {
+    const In cur = nx;
+    nx = load_in(min(g + nthr, total - 1));
+    const float* ph = cur.ph;
+    const int (&ix)[2] = cur.ix;
+    const float (&cx)[2] = cur.cx;
+    const float (&cgs)[2] = cur.cg;
+    const float (&lastC)[8] = cur.lastC;
+    // both observations' row gathers issued before either is used (two independent chains per sample)
+    float ys[2][8];
+#pragma unroll
+    for (int which = 0; which < 2; ++which) probs_of<8>(ph, lastC, ix[which], cx[which], ys[which]);
+#pragma unroll
     for (int which = 0; which < 2; ++which) {
-      const float cg = which == 0 ? dX3[o] : (tdone[s] ? 0.0f : dX4[o]);
+      const float cg = cgs[which];
       if (cg == 0.0f) continue;
-      float y[8];
-      probs_of<8>(ph, lastC, which == 0 ? tidx[o0] : tidx[o0 + W],
-                  (float)ttime[which == 0 ? o0 : o0 + W] * 0.001f, y);
+      const float (&y)[8] = ys[which];
       if (q == 0) ac += cg;  // e2_b
 #pragma unroll
       for (int u = 0; u < 4; ++u) {

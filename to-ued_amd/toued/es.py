@@ -27,9 +27,10 @@ import torch
 from . import _lib, prng
 from .agents import eval_agent
 from .lpg import LPGLayout
-from .rollout import Transition
+from .rollout import Transition, split_rollouts
 
 _Y = 8
+DRAW_CHUNK = 32        # candidate-update rollouts whose draws are made in one launch
 
 
 class OpenES:
@@ -215,12 +216,21 @@ class ESTrainStep:
         e1w, e1b, e2w, e2b = (self._eta(n) for n in ("e1_w", "e1_b", "e2_w", "e2_b"))
         tr = self.tr
         # ---- train_lpg_agent for K = max_lifetime updates (agents/lpg_agent.py:88-140)
+        split = split_rollouts()
+        draws = None
         for k in range(K):
             th, ph = self.theta[cur], self.phi[cur]
             if self.trace is not None:
                 rec = {"theta": th.clone(), "phi": ph.clone(), "state": state.clone(), "step": step.clone()}
             tok = self.timers.start("rollout")
-            self.ro.batch_rollout(chain[k], th, levels, state, out=tr, inplace_state=True)
+            if split:
+                # the state-independent draws of DRAW_CHUNK updates' rollouts in one launch, then each update's
+                # env chain on its batch (bit-identical to the per-update rollout)
+                if k % DRAW_CHUNK == 0:
+                    draws = self.ro.train_draws(chain[k:k + DRAW_CHUNK], levels, W)
+                self.ro.rollout_from_draws(draws, k % DRAW_CHUNK, th, levels, state, tr)
+            else:
+                self.ro.batch_rollout(chain[k], th, levels, state, out=tr, inplace_state=True)
             self.timers.stop(tok)
             if self.trace is not None:
                 rec["traj"] = Transition(tr.obs_idx.clone(), tr.obs_time.clone(), tr.action.clone(), tr.reward.clone(),

@@ -23,7 +23,7 @@ import torch
 
 from . import _lib, prng
 from .lpg import LPGGRU, LPGLayout, Y
-from .rollout import RolloutWrapper, Transition
+from .rollout import RolloutWrapper, Transition, split_rollouts
 
 
 @dataclass
@@ -242,6 +242,11 @@ class MetaGradStep:
         e1w, e1b = self._eta(eta, "e1_w"), self._eta(eta, "e1_b")
         e2w, e2b = self._eta(eta, "e2_w"), self._eta(eta, "e2_b")
         state = agents.state
+        # the state-independent draws of all K + 1 train-length rollouts of the step (K inner updates + the eval
+        # rollout; keys and levels are known now) in one launch instead of one per rollout
+        draws = None
+        if split_rollouts():
+            draws = self.ro.train_draws(torch.cat([self.keys_roll, self.keys_eval.unsqueeze(0)]), agents.levels, W)
         # ---------------- forward: K inner updates (agents/lpg_agent.py:88-140)
         for k in range(K):
             tk = self._t(k)
@@ -252,8 +257,11 @@ class MetaGradStep:
                     self.theta_h[k + 1].copy_(self.theta_h[k])
                     self.phi_h[k + 1].copy_(self.phi_h[k])
             tok = self.timers.start("rollout")
-            self.ro.batch_rollout(self.keys_roll[k], self.theta_h[k], agents.levels, state, out=tk,
-                                  inplace_state=True)
+            if draws is not None:
+                self.ro.rollout_from_draws(draws, k, self.theta_h[k], agents.levels, state, tk)
+            else:
+                self.ro.batch_rollout(self.keys_roll[k], self.theta_h[k], agents.levels, state, out=tk,
+                                      inplace_state=True)
             self.timers.stop(tok)
             L.call("toued_lpg_inputs", N, W, T, D, self.F, ptr(self.theta_h[k]), ptr(self.phi_h[k]),
                    ptr(tk.obs_idx), ptr(tk.obs_time), ptr(tk.action), ptr(tk.reward), ptr(tk.done),
@@ -286,7 +294,10 @@ class MetaGradStep:
             for k in range(K):
                 self._value_critic_update(self._t(k), agents)
         te = self._t(K)
-        self.ro.batch_rollout(self.keys_eval, self.theta_h[K], agents.levels, state, out=te, inplace_state=True)
+        if draws is not None:
+            self.ro.rollout_from_draws(draws, K, self.theta_h[K], agents.levels, state, te)
+        else:
+            self.ro.batch_rollout(self.keys_eval, self.theta_h[K], agents.levels, state, out=te, inplace_state=True)
         L.call("toued_eval_loss", N, W, T, D, ptr(self.theta_h[K]), ptr(agents.vcrit), ptr(te.obs_idx),
                ptr(te.obs_time), ptr(te.action), ptr(te.reward), ptr(te.done), hyp.gamma, hyp.gae_lambda,
                ptr(self.adv), ptr(self.abar), ptr(self.loss_out), st)
