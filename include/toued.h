@@ -267,6 +267,13 @@ int toued_gru_bwd_small(long M, const float* s_hin, const float* DG, const float
 size_t toued_wgrad_workspace_floats(int ra, int rb, long K);
 int toued_wgrad(int ra, int rb, long K, const float* A, long lda, const float* B, long ldb, float* C, float* work,
                 size_t work_floats, hipStream_t stream);
+/* toued_wgrad into C with row stride ldc */
+int toued_wgrad_ldc(int ra, int rb, long K, const float* A, long lda, const float* B, long ldb, float* C, int ldc,
+                    float* work, size_t work_floats, hipStream_t stream);
+/* C[i * ldc] = sum_k A[i][k] (row stride lda; K and lda multiples of 4), deterministic (chunk partials in work) */
+size_t toued_rowsum_workspace_floats(int ra, long K);
+int toued_rowsum_into(int ra, long K, const float* A, long lda, float* C, int ldc, float* work, size_t work_floats,
+                      hipStream_t stream);
 /* The LPG's main weight-gradient reduction on block-floating-point fp16 pairs (3 products instead of the bf16
  * split's 6): rows [0, a_unit_rows) of A must satisfy |a| <= 1 (scale 2^14), the others are scaled from their
  * measured maximum; col_exp[m] (from toued_gru_bwd) scales B's columns per K chunk.  Deterministic. */

@@ -84,6 +84,33 @@ def test_wgrad_empty_k_and_errors():
         L.call("toued_wgrad", 3, 5, 64, L.ptr(A), 64, L.ptr(A), 64, L.ptr(C), L.ptr(A), 1, L.stream_ptr())
 
 
+def test_wgrad_ldc_and_rowsum_build_the_head_block():
+    """The backward's head block [9][257] = DH . [relu(h_out); 1]^T as toued_gru_bwd_small builds it: the 256 unit
+    columns by toued_wgrad_ldc (row stride 257), the bias column by toued_rowsum_into (DH's row sums), against
+    float64; the ldc result bit-identical to toued_wgrad's columns and the other entries of the block untouched."""
+    from toued import _lib as L
+    ra, rb, K = 9, 256, 32 * 2000 + 32 * 7
+    g = torch.Generator(device="cuda").manual_seed(11)
+    A = torch.randn(ra, K, generator=g, device="cuda")
+    B = torch.randn(rb, K, generator=g, device="cuda")
+    blk = torch.full((ra + 1, rb + 1), float("nan"), device="cuda")
+    need = max(int(L.lib().toued_wgrad_workspace_floats(ra, rb, K)), int(L.lib().toued_rowsum_workspace_floats(ra, K)))
+    work = torch.empty(need, device="cuda")
+    L.call("toued_wgrad_ldc", ra, rb, K, L.ptr(A), K, L.ptr(B), K, L.ptr(blk), rb + 1, L.ptr(work), need,
+           L.stream_ptr())
+    L.call("toued_rowsum_into", ra, K, L.ptr(A), K, L.ptr(blk) + 4 * rb, rb + 1, L.ptr(work), need, L.stream_ptr())
+    C = torch.empty(ra, rb, device="cuda")
+    L.call("toued_wgrad", ra, rb, K, L.ptr(A), K, L.ptr(B), K, L.ptr(C), L.ptr(work), need, L.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(blk[:ra, :rb], C)
+    assert torch.isnan(blk[ra]).all()                      # the row past the block is not written
+    Ad, Bd = A.double(), B.double()
+    ref, mag = Ad @ Bd.t(), Ad.abs() @ Bd.abs().t()
+    assert ((C.double() - ref).abs() <= 2e-6 * math.sqrt(K) * mag).all()
+    rs, rmag = Ad.sum(1), Ad.abs().sum(1)
+    assert ((blk[:ra, rb].double() - rs).abs() <= 2e-6 * math.sqrt(K) * rmag).all()
+
+
 def _col_exp(B):
     """the backward's per-column exponent: 2^e * max_j |B[j][m]| < 2^14 (127 for an all-zero column)"""
     mx = B.abs().amax(dim=0)

@@ -33,6 +33,11 @@
 extern "C" size_t toued_wgrad_workspace_floats(int ra, int rb, long K);
 extern "C" int toued_wgrad(int ra, int rb, long K, const float* A, long lda, const float* B, long ldb, float* C,
                            float* work, size_t work_floats, hipStream_t stream);
+extern "C" int toued_wgrad_ldc(int ra, int rb, long K, const float* A, long lda, const float* B, long ldb, float* C,
+                               int ldc, float* work, size_t work_floats, hipStream_t stream);
+extern "C" size_t toued_rowsum_workspace_floats(int ra, long K);
+extern "C" int toued_rowsum_into(int ra, long K, const float* A, long lda, float* C, int ldc, float* work,
+                                 size_t work_floats, hipStream_t stream);
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
@@ -1656,19 +1661,32 @@ int toued_dbg_bwd_stamps(unsigned long long* host) {
 #endif
 
 size_t toued_gru_bwd_small_work_floats(long M) {
-  return std::max(toued_wgrad_workspace_floats(8, HU, M), toued_wgrad_workspace_floats(9, HU + 1, M));
+  return std::max(toued_wgrad_workspace_floats(8, HU, M),
+                  std::max(toued_wgrad_workspace_floats(9, HU, M), toued_rowsum_workspace_floats(9, M)));
 }
 
 // the backward's small weight-gradient reductions (HBM streams over dn, relu(h_out) and the head cotangents):
 // GI = [8][256] ([X; 1; 0] . dn^T) | [9][257] (DH . [relu(h_out); 1]^T).  (Folding them into the lockstep
 // kernel was measured: its register file is full and the spills cost more than the 7 GB of streams saved.)
+// The head block's bias column (DH's row sums) is a separate row-sum reduction: as a 257th B row it made the
+// column tiles of 128 rows three instead of two, each K chunk 1.5x longer (1.04 vs 0.65 ms per launch).
 int toued_gru_bwd_small(long M, const float* s_hin, const float* DG, const float* RH, const float* DH, float* GI,
                         float* work, size_t work_floats, hipStream_t stream) {
   TOUED_REQUIRE(work_floats >= toued_gru_bwd_small_work_floats(M), "toued_gru_bwd_small: workspace %zu < %zu floats",
                 work_floats, toued_gru_bwd_small_work_floats(M));
   int rc = toued_wgrad(8, HU, M, s_hin + (size_t)HU * M, M, DG + (size_t)3 * HU * M, M, GI, work, work_floats, stream);
   if (rc) return rc;
-  return toued_wgrad(9, HU + 1, M, DH, M, RH, M, GI + 8 * HU, work, work_floats, stream);
+  // TOUED_HEADS_SPLIT=0: the bias as a 257th B row (comparison runs).  The row sums go first: issued between the
+  // head product and the main reduction they left k_wgrad_h3 at 5.9-7.1 ms instead of 4.0-4.1 (measured, same box;
+  // padding the final row-sum grid to a multiple of 8 workgroups changed nothing)
+  static const bool split = [] {
+    const char* e = getenv("TOUED_HEADS_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  if (!split) return toued_wgrad(9, HU + 1, M, DH, M, RH, M, GI + 8 * HU, work, work_floats, stream);
+  rc = toued_rowsum_into(9, M, DH, M, GI + 8 * HU + HU, HU + 1, work, work_floats, stream);
+  if (rc) return rc;
+  return toued_wgrad_ldc(9, HU, M, DH, M, RH, M, GI + 8 * HU, HU + 1, work, work_floats, stream);
 }
 
 }  // extern "C"

@@ -573,20 +573,20 @@ __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict
 
 // C[i][j] = sum over chunks (in chunk order) of part[s][i][j], i < ra, j < rb
 __global__ void k_wgrad_reduce(const float* __restrict__ part, int S, int RA, int rbp, int ra, int rb,
-                               float* __restrict__ C) {
+                               float* __restrict__ C, int ldc) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long)ra * rb) return;
   const int i = (int)(idx / rb), j = (int)(idx - (long)i * rb);
   float s = 0.0f;
   for (int c = 0; c < S; ++c) s += part[((long)c * RA + i) * rbp + j];
-  C[idx] = s;
+  C[(long)i * ldc + j] = s;
 }
 
 // Many chunks (the small HBM-stream reductions split K ~500 ways): one wave per output element, lane l sums
 // chunks l, l + 64, ... in order, then a fixed xor-butterfly across the wave -- still deterministic, and
 // ~S/64 dependent loads per lane instead of S.
 __global__ void k_wgrad_reduce_wave(const float* __restrict__ part, int S, int RA, int rbp, int ra, int rb,
-                                    float* __restrict__ C) {
+                                    float* __restrict__ C, int ldc) {
   const long idx = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (idx >= (long)ra * rb) return;
@@ -595,7 +595,37 @@ __global__ void k_wgrad_reduce_wave(const float* __restrict__ part, int S, int R
   for (int c = lane; c < S; c += 64) s += part[((long)c * RA + i) * rbp + j];
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
-  if (lane == 0) C[idx] = s;
+  if (lane == 0) C[(long)i * ldc + j] = s;
+}
+
+// Row sums of A [ra][K] (row stride lda) into C[i * ldc]: per (K chunk, row) partials in a fixed order (float4 loads,
+// 256 threads, a block tree), then one wave per row over the chunks.  Deterministic.
+__global__ void __launch_bounds__(256) k_rowsum_part(const float* __restrict__ A, long lda, long K, long kchunk,
+                                                     float* __restrict__ part) {
+  const int c = blockIdx.x, i = blockIdx.y, ra = gridDim.y;
+  const long kb = (long)c * kchunk, ke = kb + kchunk < K ? kb + kchunk : K;
+  const float4* a4 = reinterpret_cast<const float4*>(A + (long)i * lda + kb);
+  const long n4 = (ke - kb) / 4;
+  float s = 0.0f;
+  for (long m = threadIdx.x; m < n4; m += 256) {
+    const float4 v = a4[m];
+    s += (v.x + v.y) + (v.z + v.w);
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[(long)c * ra + i] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void k_rowsum_final(const float* __restrict__ part, int S, int ra, float* __restrict__ C, int ldc) {
+  const int i = blockIdx.x, lane = threadIdx.x;
+  float s = 0.0f;
+  for (int c = lane; c < S; c += 64) s += part[(long)c * ra + i];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+  if (lane == 0) C[(long)i * ldc] = s;
 }
 
 struct Plan {
@@ -661,15 +691,57 @@ size_t toued_wgrad_workspace_floats(int ra, int rb, long K) {
   return (size_t)p.S * p.nrt * 16 * p.ncol * p.ct;
 }
 
+static int wgrad_ldc(int ra, int rb, long K, const float* A, long lda, const float* B, long ldb, float* C, int ldc,
+                     float* work, size_t work_floats, hipStream_t stream);
+
 int toued_wgrad(int ra, int rb, long K, const float* A, long lda, const float* B, long ldb, float* C, float* work,
                 size_t work_floats, hipStream_t stream) {
+  return wgrad_ldc(ra, rb, K, A, lda, B, ldb, C, rb, work, work_floats, stream);
+}
+
+// C [ra][rb] with row stride ldc (the backward's head block [9][257] takes its 256 unit columns from here and the
+// bias column from toued_rowsum_into)
+int toued_wgrad_ldc(int ra, int rb, long K, const float* A, long lda, const float* B, long ldb, float* C, int ldc,
+                    float* work, size_t work_floats, hipStream_t stream) {
+  return wgrad_ldc(ra, rb, K, A, lda, B, ldb, C, ldc, work, work_floats, stream);
+}
+
+// rows sums: the chunks and the partials' floats the workspace needs
+static long rowsum_chunk(long K) {
+  long kc = ((K + 255) / 256 + 31) / 32 * 32;
+  return kc < 32 ? 32 : kc;
+}
+size_t toued_rowsum_workspace_floats(int ra, long K) {
+  return K > 0 ? (size_t)((K + rowsum_chunk(K) - 1) / rowsum_chunk(K)) * ra : 0;
+}
+int toued_rowsum_into(int ra, long K, const float* A, long lda, float* C, int ldc, float* work, size_t work_floats,
+                      hipStream_t stream) {
+  TOUED_REQUIRE(ra >= 1 && K >= 0 && K % 4 == 0 && lda % 4 == 0, "toued_rowsum_into: ra=%d K=%ld lda=%ld", ra, K, lda);
+  TOUED_REQUIRE(work_floats >= toued_rowsum_workspace_floats(ra, K), "toued_rowsum_into: workspace too small");
+  if (K == 0) {
+    for (int i = 0; i < ra; ++i)
+      TOUED_REQUIRE(hipMemsetAsync(C + (long)i * ldc, 0, sizeof(float), stream) == hipSuccess, "memset failed");
+    return 0;
+  }
+  const long kc = rowsum_chunk(K);
+  const int S = (int)((K + kc - 1) / kc);
+  hipLaunchKernelGGL(k_rowsum_part, dim3(S, ra), dim3(256), 0, stream, A, lda, K, kc, work);
+  hipLaunchKernelGGL(k_rowsum_final, dim3(ra), dim3(64), 0, stream, work, S, ra, C, ldc);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+static int wgrad_ldc(int ra, int rb, long K, const float* A, long lda, const float* B, long ldb, float* C, int ldc,
+                     float* work, size_t work_floats, hipStream_t stream) {
   TOUED_REQUIRE(ra >= 1 && ra <= 272 && rb >= 1 && K >= 0, "toued_wgrad: ra=%d (1..272) rb=%d K=%ld", ra, rb, K);
   TOUED_REQUIRE(K % 32 == 0, "toued_wgrad: K=%ld must be a multiple of 32", K);
   TOUED_REQUIRE(lda % 4 == 0 && ldb % 4 == 0, "toued_wgrad: lda=%ld ldb=%ld must be multiples of 4 (16-byte rows)",
                 lda, ldb);
   TOUED_REQUIRE(A && B && C, "toued_wgrad: null operand");
   if (K == 0) {
-    TOUED_REQUIRE(hipMemsetAsync(C, 0, sizeof(float) * ra * rb, stream) == hipSuccess, "toued_wgrad: memset failed");
+    for (int i = 0; i < ra; ++i)
+      TOUED_REQUIRE(hipMemsetAsync(C + (long)i * ldc, 0, sizeof(float) * rb, stream) == hipSuccess,
+                    "toued_wgrad: memset failed");
     return 0;
   }
   const Plan p = plan(ra, rb, K);
@@ -685,10 +757,10 @@ int toued_wgrad(int ra, int rb, long K, const float* A, long lda, const float* B
   const long n = (long)ra * rb;
   if (p.S > 128)
     hipLaunchKernelGGL(k_wgrad_reduce_wave, dim3((unsigned)((n * 64 + 255) / 256)), dim3(256), 0, stream, work, p.S,
-                       p.nrt * 16, p.ncol * p.ct, ra, rb, C);
+                       p.nrt * 16, p.ncol * p.ct, ra, rb, C, ldc);
   else
     hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, work, p.S,
-                       p.nrt * 16, p.ncol * p.ct, ra, rb, C);
+                       p.nrt * 16, p.ncol * p.ct, ra, rb, C, ldc);
   TOUED_CHECK_LAUNCH();
   return 0;
 }
@@ -763,7 +835,7 @@ int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit
                        a_unit_rows, bits, B, ldb, rb, col_exp, K, p.kchunk, work);
   const long n = (long)ra * rb;
   hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, work, p.S, 17 * 16,
-                     p.ncol * p.ct, ra, rb, C);
+                     p.ncol * p.ct, ra, rb, C, rb);
   TOUED_CHECK_LAUNCH();
   return 0;
 }

@@ -98,12 +98,16 @@ _SIGS = {
     "toued_plr_sample": [_I, _I, _P, _P, _P, _P, _I, _F, _F, _P, _P, _P, _P, _P],
     "toued_wgrad_workspace_floats": [_I, _I, _L],
     "toued_wgrad": [_I, _I, _L, _P, _L, _P, _L, _P, _P, ctypes.c_size_t, _P],
+    "toued_wgrad_ldc": [_I, _I, _L, _P, _L, _P, _L, _P, _I, _P, ctypes.c_size_t, _P],
+    "toued_rowsum_workspace_floats": [_I, _L],
+    "toued_rowsum_into": [_I, _L, _P, _L, _P, _I, _P, ctypes.c_size_t, _P],
     "toued_last_error": [],
     "toued_abi_version": [],
 }
 _RESTYPES = {"toued_last_error": ctypes.c_char_p, "toued_mode_program_bytes": ctypes.c_size_t,
              "toued_gru_packed_floats": ctypes.c_size_t, "toued_wgrad_workspace_floats": ctypes.c_size_t,
-             "toued_gru_bwd_small_work_floats": ctypes.c_size_t, "toued_wgrad_bfp_workspace_floats": ctypes.c_size_t}
+             "toued_gru_bwd_small_work_floats": ctypes.c_size_t, "toued_wgrad_bfp_workspace_floats": ctypes.c_size_t,
+             "toued_rowsum_workspace_floats": ctypes.c_size_t}
 
 _lib = None
 

@@ -221,10 +221,12 @@ class LPGGRU:
         del Xk
 
     def backward(self, done_all: torch.Tensor, eta: torch.Tensor, y_hat: torch.Tensor, d_pi_hat: torch.Tensor,
-                 d_y_hat: torch.Tensor, X: torch.Tensor, grad: torch.Tensor, timers=None, after_bwd=None):
+                 d_y_hat: torch.Tensor, X: torch.Tensor, grad: torch.Tensor, timers=None, after_bwd=None,
+                 before_main_wgrad=None):
         """done_all: u8 [K(+1), N, T, W] (first K slots used).  Accumulates d(loss)/d(eta) into ``grad``
         (all parameters except the embedding MLP, which needs dX3/dX4 -> agent-side kernel).  ``after_bwd()`` is
-        called right after the recurrent backward kernel is enqueued, before the weight-gradient reductions."""
+        called right after the recurrent backward kernel is enqueued, before the weight-gradient reductions;
+        ``before_main_wgrad()`` right before the main one (after the small products)."""
         R, T, K, M = self.R, self.T, self.K, self.M
         S = self.S
         stride_k = done_all[0].numel()
@@ -251,6 +253,8 @@ class LPGGRU:
         st = _lib.stream_ptr()
         _lib.call("toued_gru_bwd_small", M, _lib.ptr(self.A), _lib.ptr(DG), _lib.ptr(self.RH), _lib.ptr(self.DH),
                   _lib.ptr(self.GI), ws, wn, st)
+        if before_main_wgrad is not None:
+            before_main_wgrad()
         tok_main = timers.start("wgrad_main") if timers is not None else None
         if self.bfp:
             _lib.call("toued_wgrad_bfp", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, H, _lib.ptr(DG), M,

@@ -325,6 +325,10 @@ class MetaGradStep:
                 (_, _), ea["state"] = self.ro.batch_reset(self.keys_ea_reset, agents.levels, hyp.eval_workers)
                 self._ea_draws = self.ro.eval_draws(self.keys_ea_roll, agents.levels, hyp.eval_workers,
                                                     self._ea_draws)
+                # the draws kernel spreads over the whole chip for ~0.1 ms: the main weight-gradient reduction (one
+                # workgroup per CU) starts after it (ea_draws_done), or its workgroups wait behind the draws' blocks
+                ea["draws_done"] = torch.cuda.Event()
+                ea["draws_done"].record(self.side)
                 ea["cum"] = self.ro.eval_returns_from_draws(self._ea_draws, self.theta_h[K], agents.levels,
                                                             ea["state"])
             ea["prev_reserve"] = L.lib().toued_set_reserved_cus(eval_cus)
@@ -358,7 +362,8 @@ class MetaGradStep:
                    ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]), ptr(self.d_pi_hat[k]), ptr(self.d_y_hat[k]), st)
         try:
             self.gru.backward(self.traj.done, eta, self.y_hat, self.d_pi_hat, self.d_y_hat, self.X, self.grad,
-                              self.timers, after_bwd=launch_eval)
+                              self.timers, after_bwd=launch_eval,
+                              before_main_wgrad=lambda: main.wait_event(ea["draws_done"]))
         finally:
             # the CU reservation is process-global split-K planning state: restore it whatever happened
             if "prev_reserve" in ea:
