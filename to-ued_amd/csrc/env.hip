@@ -239,6 +239,34 @@ __global__ void __launch_bounds__(256) k_eval_keys(const uint32_t* __restrict__ 
   }
 }
 
+// The same key chain with the two threefry blocks of each split on a lane pair (lanes 2i, 2i+1: blocks (0,2) and
+// (1,3)), exchanged by a DPP quad permute: half the instructions per wave and step for 32 chains per wave.  The
+// chain is issue-bound at one wave per SIMD, so eval_agent's few chains (4 per agent) finish in half the time on twice
+// the SIMDs; bit-identical to k_eval_keys (the train rollouts' wide chains keep k_eval_keys).
+__global__ void __launch_bounds__(256) k_eval_keys_pairs(const uint32_t* __restrict__ agent_keys, int W, int T, int n,
+                                                         uint2* __restrict__ chain) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = g >> 1;
+  const uint32_t j = (uint32_t)(g & 1);
+  if (i >= n) return;   // both lanes of a pair leave together: the DPP partners below are always active
+  const int a = i / W, w = i - a * W;
+  uint2 r = split_at(make_uint2(agent_keys[2 * a], agent_keys[2 * a + 1]), (uint32_t)W, (uint32_t)w);
+  auto xor1 = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false); };
+  // split(r) -> (r', sub): r' = (y0.x, y1.x), sub = (y0.y, y1.y); lane j holds y_j
+  auto split_pair = [&](uint2& key, uint2& sub) {
+    const uint2 y = threefry(key.x, key.y, j, j + 2u);
+    const uint32_t px = xor1(y.x), py = xor1(y.y);
+    key = j ? make_uint2(px, y.x) : make_uint2(y.x, px);
+    sub = j ? make_uint2(py, y.y) : make_uint2(y.y, py);
+  };
+  for (int t = 0; t < T; ++t) {
+    uint2 sub, sub_env;
+    split_pair(r, sub);
+    split_pair(r, sub_env);
+    chain[((size_t)t * n + i) * 2 + j] = j ? sub_env : sub;   // (sub, sub_env) as one 16-byte record per chain
+  }
+}
+
 // (n workers per step; worker i plays level (i / W) % na: the train rollouts' U update batches share the levels)
 template <int NMAX>
 __global__ void __launch_bounds__(256) k_eval_draws(const int* __restrict__ levels, int W, int na, int n, long total,
@@ -484,8 +512,8 @@ int toued_eval_keys(const uint32_t* agent_keys, int n_agents, int W, int T, uint
   TOUED_REQUIRE(n_agents >= 0 && W >= 1 && T >= 0, "toued_eval_keys: bad sizes N=%d W=%d T=%d", n_agents, W, T);
   const int n = n_agents * W;
   if (n == 0 || T == 0) return 0;
-  hipLaunchKernelGGL(k_eval_keys, dim3(nblk(n)), dim3(256), 0, stream, agent_keys, W, T, n,
-                     reinterpret_cast<uint4*>(chain));
+  hipLaunchKernelGGL(k_eval_keys_pairs, dim3((unsigned)((2L * n + 255) / 256)), dim3(256), 0, stream, agent_keys, W, T,
+                     n, reinterpret_cast<uint2*>(chain));
   TOUED_CHECK_LAUNCH();
   return 0;
 }

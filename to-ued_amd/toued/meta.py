@@ -317,6 +317,7 @@ class MetaGradStep:
         # K*R/64/256 rounds of the chip, any CU held pushes that kernel into one more round; beside the
         # latency-bound agent kernels the key chain slowed them by more than it took.)
         eval_cus = -(-N * hyp.eval_workers // 256)
+        key_cus = 2 * eval_cus      # the key chain runs two lanes per eval worker (k_eval_keys_pairs)
         ea = {}
 
         def launch_eval():
@@ -331,7 +332,12 @@ class MetaGradStep:
                 ea["draws_done"].record(self.side)
                 ea["cum"] = self.ro.eval_returns_from_draws(self._ea_draws, self.theta_h[K], agents.levels,
                                                             ea["state"])
-            ea["prev_reserve"] = L.lib().toued_set_reserved_cus(eval_cus)
+            # the small products run beside the key chain, the main reduction beside the env chain
+            ea["prev_reserve"] = L.lib().toued_set_reserved_cus(key_cus)
+
+        def before_main_wgrad():
+            main.wait_event(ea["draws_done"])
+            L.lib().toued_set_reserved_cus(eval_cus)
         # ---------------- reverse: explicit adjoint w.r.t. eta
         a_in = 0
         self.adj_th[a_in].zero_()
@@ -363,7 +369,7 @@ class MetaGradStep:
         try:
             self.gru.backward(self.traj.done, eta, self.y_hat, self.d_pi_hat, self.d_y_hat, self.X, self.grad,
                               self.timers, after_bwd=launch_eval,
-                              before_main_wgrad=lambda: main.wait_event(ea["draws_done"]))
+                              before_main_wgrad=before_main_wgrad)
         finally:
             # the CU reservation is process-global split-K planning state: restore it whatever happened
             if "prev_reserve" in ea:
