@@ -243,7 +243,7 @@ __global__ void __launch_bounds__(256) k_eval_keys(const uint32_t* __restrict__ 
 // (1,3)), exchanged by a DPP quad permute: half the instructions per wave and step for 32 chains per wave.  The
 // chain is issue-bound at one wave per SIMD, so eval_agent's few chains (4 per agent) finish in half the time on twice
 // the SIMDs; bit-identical to k_eval_keys (the train rollouts' wide chains keep k_eval_keys).
-__global__ void __launch_bounds__(256) k_eval_keys_pairs(const uint32_t* __restrict__ agent_keys, int W, int T, int n,
+__global__ void __launch_bounds__(1024) k_eval_keys_pairs(const uint32_t* __restrict__ agent_keys, int W, int T, int n,
                                                          uint2* __restrict__ chain) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   const int i = g >> 1;
@@ -512,7 +512,12 @@ int toued_eval_keys(const uint32_t* agent_keys, int n_agents, int W, int T, uint
   TOUED_REQUIRE(n_agents >= 0 && W >= 1 && T >= 0, "toued_eval_keys: bad sizes N=%d W=%d T=%d", n_agents, W, T);
   const int n = n_agents * W;
   if (n == 0 || T == 0) return 0;
-  hipLaunchKernelGGL(k_eval_keys_pairs, dim3((unsigned)((2L * n + 255) / 256)), dim3(256), 0, stream, agent_keys, W, T,
+  // one-wave workgroups: the dispatcher spreads them one per SIMD slot instead of packing four waves per CU
+  static const int kb = [] {
+    const char* e = getenv("TOUED_EVAL_KEYS_BLOCK");
+    return e ? atoi(e) : 64;
+  }();
+  hipLaunchKernelGGL(k_eval_keys_pairs, dim3((unsigned)((2L * n + kb - 1) / kb)), dim3(kb), 0, stream, agent_keys, W, T,
                      n, reinterpret_cast<uint2*>(chain));
   TOUED_CHECK_LAUNCH();
   return 0;
