@@ -297,21 +297,20 @@ int toued_agent_update(int N, int W, int T, int D, float* theta, float* phi, con
                        const int* levels, float* gstat, hipStream_t stream);
 
 /* The meta-gradient's inner update k (agents/lpg_agent.py:88-140 inside meta/train.py:41-58) without dense table
- * passes: replaces toued_agent_grad + toued_agent_apply + toued_clip_dot where toued_agent_update_fits(W, T, D).
- * theta1 / phi1 must already hold copies of theta / phi (theta_k); the touched rows of theta1 / phi1 are rewritten
- * (bit-identical to toued_agent_apply), the touched gradient rows go to Gth / Gph (bit-identical to
- * toued_agent_grad on zeroed tables there; the other rows are NOT written) and their row lists to
- * rows [N][toued_agent_rows_stride()] (uint32, 16-byte aligned).  toued_clip_dot_rows is toued_clip_dot over those
- * rows (the reverse pass, meta/train.py:174); toued_hvp reads touched rows only. */
-int toued_agent_rows_stride(void);
+ * passes: replaces toued_agent_grad + toued_agent_apply where toued_agent_update_fits(W, T, D).  theta1 / phi1 must
+ * already hold copies of theta / phi (theta_k); the touched rows of theta1 / phi1 are rewritten (bit-identical to
+ * toued_agent_apply), the touched gradient rows go to Gth / Gph (bit-identical to toued_agent_grad on zeroed tables
+ * there; the other rows are NOT written).  The reverse pass (meta/train.py:174) reads touched rows only:
+ * toued_entropy_clip is toued_entropy's gradient mode + toued_clip_dot over those rows in one kernel, toued_hvp
+ * reads the rows of its own samples. */
 int toued_agent_step(int N, int W, int T, int D, const float* theta, const float* phi, float* theta1, float* phi1,
                      const int* tidx, const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
                      const float* pi_hat, const float* y_hat, float alpha_y, float lr_a, float lr_c, float max_norm,
-                     float* Gth, float* Gph, uint32_t* rows, float* met, int* step, const int* levels, float* gstat,
-                     hipStream_t stream);
-int toued_clip_dot_rows(int N, int D, const uint32_t* rows, const float* Gth, const float* Gph, const float* adj_th,
-                        const float* adj_ph, const float* gstat, float lr_a, float lr_c, float max_norm, float* coef,
-                        hipStream_t stream);
+                     float* Gth, float* Gph, float* met, int* step, const int* levels, float* gstat, hipStream_t stream);
+int toued_entropy_clip(int N, int W, int T, int D, const float* theta, const float* phi, const int* tidx,
+                       const int* ttime, float coef_a, float coef_c, float* adj_th, float* adj_ph, const float* Gth,
+                       const float* Gph, const float* gstat, float lr_a, float lr_c, float max_norm, float* coef,
+                       hipStream_t stream);
 
 /* ES inference path: pack n candidates' forward fragments (candidate c at eta + c*eta_stride) */
 int toued_gru_pack_fwd_multi(const float* eta, long eta_stride, int n, const int* off, int F, float* fwdA,

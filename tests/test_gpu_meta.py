@@ -490,8 +490,8 @@ def test_mini_batches_match_full_batch(nmb):
 @pytest.mark.parametrize("mode,N,lc", [("tabular", 512, False), ("all_vrandlife", 16, True)])
 def test_fused_agent_step_matches_dense_path(monkeypatch, mode, N, lc):
     """The inner updates as toued_agent_step (theta_{k+1} copied on the side stream, touched rows rewritten,
-    gradient rows and row lists kept, clip_dot over those rows) against the dense toued_agent_grad + apply +
-    clip_dot path, over two consecutive meta-steps (the second one's gradient tables hold the first one's rows
+    gradient rows kept; the reverse pass's entropy gradient and clip-VJP dot fused over those rows) against the
+    dense toued_agent_grad + apply + entropy + clip_dot path, over two consecutive meta-steps (the second one's gradient tables hold the first one's rows
     where it does not write): every theta_k / phi_k, the agents, metrics and gstat bit-identical; the
     meta-gradient up to the clip-VJP dot's summation order (1e-6)."""
     from toued.lpg import init_lpg_params

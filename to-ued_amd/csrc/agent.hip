@@ -24,7 +24,6 @@
 
 #define EPSF 1e-8f
 #define SORT_MAX_TW 2048                  // samples per agent the sorted row kernel holds
-#define ROWS_STRIDE (SORT_MAX_TW + 4)     // per-agent row list of toued_agent_step (uint32)
 
 namespace {
 
@@ -627,41 +626,6 @@ __global__ void __launch_bounds__(1024) k_clip_dot(int N, int D, const float* __
   }
 }
 
-// <G, adjoint> over the rows update k touched only (toued_agent_step's row lists; the gradient tables hold stale
-// values elsewhere): one 512-thread block per agent, four list entries per thread plus the time-row entry
-__global__ void __launch_bounds__(512) k_clip_dot_rows(int D, const uint32_t* __restrict__ rows,
-                                                       const float* __restrict__ Gth, const float* __restrict__ Gph,
-                                                       const float* __restrict__ adj_th,
-                                                       const float* __restrict__ adj_ph,
-                                                       const float* __restrict__ gstat, float lr_a, float lr_c,
-                                                       float max_norm, float* __restrict__ coef) {
-  const int a = blockIdx.x, tid = threadIdx.x;
-  __shared__ float red[2][8];
-  const uint32_t* lr = rows + (size_t)a * ROWS_STRIDE;
-  const uint4 x = reinterpret_cast<const uint4*>(lr)[tid];
-  const uint32_t rr[5] = {x.x, x.y, x.z, x.w, tid == 0 ? lr[SORT_MAX_TW] : 0xFFFFFFFFu};
-  const size_t baseA = (size_t)a * D * 5, baseC = (size_t)a * D * 8;
-  float da = 0.0f, dc = 0.0f;
-#pragma unroll
-  for (int e = 0; e < 5; ++e) {
-    if (rr[e] == 0xFFFFFFFFu) continue;
-    const size_t oa = baseA + (size_t)rr[e] * 5, oc = baseC + (size_t)rr[e] * 8;
-#pragma unroll
-    for (int j = 0; j < 5; ++j) da += Gth[oa + j] * adj_th[oa + j];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dc += Gph[oc + j] * adj_ph[oc + j];
-  }
-  da = wsum_dpp(da);
-  dc = wsum_dpp(dc);
-  if ((tid & 63) == 0) { red[0][tid >> 6] = da; red[1][tid >> 6] = dc; }
-  __syncthreads();
-  if (tid == 0) {
-    float sa = 0.0f, sc = 0.0f;
-    for (int i = 0; i < 8; ++i) { sa += red[0][i]; sc += red[1][i]; }
-    clip_coef(a, sa, sc, gstat, lr_a, lr_c, max_norm, coef);
-  }
-}
-
 // ---------------------------------------------------------------------------- HVP + LPG-output cotangents
 template <bool UNIF>
 __global__ void __launch_bounds__(256) k_hvp(int N, int W, int T, int D, int K, const float* __restrict__ theta,
@@ -957,7 +921,7 @@ __global__ void __launch_bounds__(256) k_init_tables(const uint32_t* __restrict_
 
 struct GradOp {   // k_agent_grad (+ the global norms and the lifetime test of the update it feeds)
   static constexpr int NA = 5, NC = 8, NM = 3;
-  static constexpr bool NORMS = true, APPLY = false, WRITE_G = false;
+  static constexpr bool NORMS = true, APPLY = false, WRITE_G = false, CLIPDOT = false;
   const float* theta; const float* phi; const int* tidx; const int* ttime; const uint8_t* tact; const float* trew;
   const uint8_t* tdone; const float* pi_hat; const float* y_hat; float alpha_y; float* Gth; float* Gph; float* met;
   const int* step; const int* levels; float* gstat;
@@ -1015,21 +979,19 @@ struct GradOp {   // k_agent_grad (+ the global norms and the lifetime test of t
 struct GradApplyOp : GradOp {
   static constexpr bool APPLY = true;
   float* theta_w; float* phi_w; float lr_a, lr_c, max_norm; int* step_w;
-  uint32_t* rows;
 };
 
 // The meta-gradient's inner update k (toued_agent_step): GradApplyOp reading theta_k / phi_k (GradOp::theta, phi)
 // and rewriting the touched rows of theta_{k+1} / phi_{k+1} (theta_w, phi_w: copies of theta_k / phi_k made
-// beforehand), and keeping what the reverse pass reads of the update: the gradient rows it touched (Gth / Gph, rows
-// never read elsewhere are left as they were) and where they are (rows: [ROWS_STRIDE] per agent, the row at each
-// sorted segment's last entry and NONE elsewhere, entry SORT_MAX_TW the time row D-1 when no sample visited it).
+// beforehand), and keeping the gradient rows it touched (Gth / Gph) for the reverse pass; rows never touched are left
+// as they were (the reverse pass reads touched rows only: toued_entropy_clip, toued_hvp).
 struct GradStepOp : GradApplyOp {
   static constexpr bool WRITE_G = true;
 };
 
 struct EntropyBwdOp {   // k_entropy, gradient mode
   static constexpr int NA = 5, NC = 8, NM = 1;
-  static constexpr bool NORMS = false, APPLY = false, WRITE_G = false;
+  static constexpr bool NORMS = false, APPLY = false, WRITE_G = false, CLIPDOT = false;
   const float* theta; const float* phi; const int* tidx; const int* ttime; float coef_a, coef_c;
   float* adj_th; float* adj_ph;
   int N, W, T, D;
@@ -1071,9 +1033,20 @@ struct EntropyBwdOp {   // k_entropy, gradient mode
   TOUED_DEV void finish(int, float, float) const {}
 };
 
+// EntropyBwdOp of the reverse pass's step k fused with the clip-VJP dot that follows it: the rows it rewrites are
+// exactly the rows update k touched (the same trajectory, plus the time row), so the thread owning a row adds
+// <G_k[row], adjoint[row]> as it writes the row, and thread 0 turns the block's sums into coef (k_clip_dot's
+// coefficients up to the summation order: the untouched rows, zero in the dense tables, are not visited)
+struct EntropyClipOp : EntropyBwdOp {
+  static constexpr bool CLIPDOT = true;
+  const float* Gth; const float* Gph; const float* gstat; float lr_a, lr_c, max_norm; float* coef;
+  TOUED_DEV float gA(int a, int r, int j) const { return Gth[((size_t)a * D + r) * 5 + j]; }
+  TOUED_DEV float gC(int a, int r, int j) const { return Gph[((size_t)a * D + r) * 8 + j]; }
+};
+
 struct LpgLossOp {   // k_lpgloss_grad
   static constexpr int NA = 5, NC = 0, NM = 1;
-  static constexpr bool NORMS = false, APPLY = false, WRITE_G = false;
+  static constexpr bool NORMS = false, APPLY = false, WRITE_G = false, CLIPDOT = false;
   const float* theta; const int* tidx; const int* ttime; const uint8_t* tact; const float* abar; float* adj_th;
   int N, W, T, D;
   TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* v, float* m) const {
@@ -1106,7 +1079,7 @@ struct LpgLossOp {   // k_lpgloss_grad
 
 struct HvpOp {   // k_hvp
   static constexpr int NA = 5, NC = 8, NM = 1;
-  static constexpr bool NORMS = false, APPLY = false, WRITE_G = false;
+  static constexpr bool NORMS = false, APPLY = false, WRITE_G = false, CLIPDOT = false;
   const float* theta; const float* phi; const int* tidx; const int* ttime; const uint8_t* tact;
   const float* pi_hat; const float* y_hat; const float* Gth; const float* Gph; const float* adj_th_in;
   const float* adj_ph_in; const float* coef; float lr_a, lr_c, alpha_y, b2, b3;
@@ -1374,6 +1347,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
             const float g = ra[j] + run[j];
             ra[j] = g;
             if (Op::NORMS) na2 += g * g;
+            if constexpr (Op::CLIPDOT) na2 += op.gA(a, (int)r, j) * g;
           }
           if (NC > 0) {
             float* rc = op.rowC(a, (int)r);
@@ -1382,6 +1356,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
               const float g = rc[j] + run[NA + j];
               rc[j] = g;
               if (Op::NORMS) nc2 += g * g;
+              if constexpr (Op::CLIPDOT) nc2 += op.gC(a, (int)r, j) * g;
             }
           }
         }
@@ -1402,14 +1377,6 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
       if (j < NA) na2 += g * g; else nc2 += g * g;
     }
   }
-  if constexpr (Op::WRITE_G) {   // where the gradient rows are, for the reverse pass's <G, adjoint>
-    uint32_t* lr = op.rows + (size_t)a * ROWS_STRIDE;
-    uint32_t o[CH];
-#pragma unroll
-    for (int e = 0; e < CH; ++e) o[e] = ((endm >> e) & 1u) ? (kc[e] >> 12) : NONE;
-    reinterpret_cast<uint4*>(lr)[tid] = make_uint4(o[0], o[1], o[2], o[3]);
-    if (tid == 0) lr[SORT_MAX_TW] = has_last ? NONE : (uint32_t)(D - 1);
-  }
   if (!Op::APPLY && tid == 0) {
     if (!has_last) {
       float* ra = op.rowA(a, D - 1);
@@ -1418,6 +1385,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
         const float g = ra[j] + tot[j];
         ra[j] = g;
         if (Op::NORMS) na2 += g * g;
+        if constexpr (Op::CLIPDOT) na2 += op.gA(a, D - 1, j) * g;
       }
       if (NC > 0) {
         float* rc = op.rowC(a, D - 1);
@@ -1426,10 +1394,23 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
           const float g = rc[j] + tot[NA + j];
           rc[j] = g;
           if (Op::NORMS) nc2 += g * g;
+          if constexpr (Op::CLIPDOT) nc2 += op.gC(a, D - 1, j) * g;
         }
       }
     }
     op.metrics(a, tot + NV);
+  }
+  if constexpr (Op::CLIPDOT) {   // <G_k, adjoint> of the block -> the clip-VJP coefficients
+    na2 = wsum_dpp(na2);
+    nc2 = wsum_dpp(nc2);
+    __syncthreads();
+    if (lane == 0) { red[wv][0] = na2; red[wv][1] = nc2; }
+    __syncthreads();
+    if (tid == 0) {
+      float x = 0.0f, y = 0.0f;
+      for (int w = 0; w < 8; ++w) { x += red[w][0]; y += red[w][1]; }
+      clip_coef(a, x, y, op.gstat, op.lr_a, op.lr_c, op.max_norm, op.coef);
+    }
   }
   if (Op::NORMS) {   // global norms of the (complete) gradient tables: every nonzero row was written above
     na2 = wsum_dpp(na2);
@@ -1577,7 +1558,6 @@ int toued_agent_update(int N, int W, int T, int D, float* theta, float* phi, con
   op.lr_c = lr_c;
   op.max_norm = max_norm;
   op.step_w = step;
-  op.rows = nullptr;
   TOUED_REQUIRE(launch_sorted(op, N, stream), "toued_agent_update: cannot launch the sorted kernel");
   TOUED_CHECK_LAUNCH();
   return 0;
@@ -1586,14 +1566,13 @@ int toued_agent_update(int N, int W, int T, int D, float* theta, float* phi, con
 // The meta-gradient's inner update k: toued_agent_grad + toued_agent_apply without the dense passes.  theta1 / phi1
 // must already hold copies of theta / phi (theta_k); the touched rows of theta1 / phi1 are rewritten by clip + SGD
 // (bit-identical to toued_agent_apply), the touched gradient rows go to Gth / Gph (bit-identical to toued_agent_grad
-// there; the other rows are not written and must not be read: toued_clip_dot_rows and toued_hvp read touched rows
-// only) and their row lists to rows [N][ROWS_STRIDE].  step advanced when applied, met accumulated, gstat written.
+// there; the other rows are not written and must not be read: toued_entropy_clip and toued_hvp read touched rows
+// only).  step advanced when applied, met accumulated, gstat written.
 int toued_agent_step(int N, int W, int T, int D, const float* theta, const float* phi, float* theta1, float* phi1,
                      const int* tidx, const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
                      const float* pi_hat, const float* y_hat, float alpha_y, float lr_a, float lr_c, float max_norm,
-                     float* Gth, float* Gph, uint32_t* rows, float* met, int* step, const int* levels, float* gstat,
-                     hipStream_t stream) {
-  TOUED_REQUIRE(step && levels && gstat && met && Gth && Gph && rows && theta1 && phi1,
+                     float* Gth, float* Gph, float* met, int* step, const int* levels, float* gstat, hipStream_t stream) {
+  TOUED_REQUIRE(step && levels && gstat && met && Gth && Gph && theta1 && phi1,
                 "toued_agent_step: every output is required");
   TOUED_REQUIRE(toued_agent_update_fits(W, T, D), "toued_agent_step: W=%d T=%d D=%d unsupported (T*W <= %d)", W, T, D,
                 SORT_MAX_TW);
@@ -1608,25 +1587,33 @@ int toued_agent_step(int N, int W, int T, int D, const float* theta, const float
   op.lr_c = lr_c;
   op.max_norm = max_norm;
   op.step_w = step;
-  op.rows = rows;
   TOUED_REQUIRE(launch_sorted(op, N, stream), "toued_agent_step: cannot launch the sorted kernel");
   TOUED_CHECK_LAUNCH();
   return 0;
 }
 
-int toued_clip_dot_rows(int N, int D, const uint32_t* rows, const float* Gth, const float* Gph, const float* adj_th,
-                        const float* adj_ph, const float* gstat, float lr_a, float lr_c, float max_norm, float* coef,
-                        hipStream_t stream) {
+// toued_entropy's gradient mode followed by toued_clip_dot over the touched rows, in one kernel (the reverse pass of toued_agent_step's
+// update k: Gth / Gph hold that update's touched rows, which are the rows this trajectory's entropy gradient writes)
+int toued_entropy_clip(int N, int W, int T, int D, const float* theta, const float* phi, const int* tidx,
+                       const int* ttime, float coef_a, float coef_c, float* adj_th, float* adj_ph, const float* Gth,
+                       const float* Gph, const float* gstat, float lr_a, float lr_c, float max_norm, float* coef,
+                       hipStream_t stream) {
+  TOUED_REQUIRE(toued_agent_update_fits(W, T, D), "toued_entropy_clip: W=%d T=%d D=%d unsupported", W, T, D);
   if (N == 0) return 0;
-  TOUED_REQUIRE(rows && aligned16(rows), "toued_clip_dot_rows: rows must be a 16-byte aligned [N][%d] list",
-                ROWS_STRIDE);
-  hipLaunchKernelGGL(k_clip_dot_rows, dim3(N), dim3(512), 0, stream, D, rows, Gth, Gph, adj_th, adj_ph, gstat, lr_a,
-                     lr_c, max_norm, coef);
+  EntropyClipOp op;
+  static_cast<EntropyBwdOp&>(op) = EntropyBwdOp{theta, phi, tidx, ttime, coef_a, coef_c, adj_th, adj_ph, N, W, T, D};
+  op.Gth = Gth;
+  op.Gph = Gph;
+  op.gstat = gstat;
+  op.lr_a = lr_a;
+  op.lr_c = lr_c;
+  op.max_norm = max_norm;
+  op.coef = coef;
+  TOUED_REQUIRE(launch_sorted(op, N, stream), "toued_entropy_clip: cannot launch the sorted kernel");
   TOUED_CHECK_LAUNCH();
   return 0;
 }
 
-int toued_agent_rows_stride(void) { return ROWS_STRIDE; }
 
 int toued_agent_apply(int N, int D, const float* th0, const float* ph0, const float* Gth, const float* Gph,
                       float lr_a, float lr_c, float max_norm, int* step, float* th1, float* ph1, const float* gstat,

@@ -84,9 +84,8 @@ _SIGS = {
     "toued_a2c_update": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _F, _P, _P, _P, _P],
     "toued_agent_update_fits": [_I, _I, _I],
     "toued_agent_update": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _F, _P, _P, _P, _P, _P],
-    "toued_agent_rows_stride": [],
-    "toued_agent_step": [_I, _I, _I, _I] + [_P] * 11 + [_F] * 4 + [_P] * 8,
-    "toued_clip_dot_rows": [_I, _I, _P, _P, _P, _P, _P, _P, _F, _F, _F, _P, _P],
+    "toued_agent_step": [_I, _I, _I, _I] + [_P] * 11 + [_F] * 4 + [_P] * 7,
+    "toued_entropy_clip": [_I, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _F, _F, _F, _P, _P],
     "toued_a2c_chain_fits": [_I, _I, _I],
     "toued_a2c_chain": [EnvSpecC, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _P, _P, _P],
     "toued_gru_pack_fwd_multi": [_P, _L, _I, _P, _I, _P, _P],

@@ -140,13 +140,11 @@ class MetaGradStep:
         self.G_th = z(K, N, D, 5)
         self.G_ph = z(K, N, D, Y)
         # inner updates as toued_agent_step (sparse: theta_{k+1} copied on a side stream beside rollout k and the
-        # LPG forward, then only the touched rows rewritten; gradient rows and their lists kept for the reverse
-        # pass's clip_dot_rows) where one agent's samples fit the sorted row kernel; TOUED_META_FUSED_STEP=0 keeps
-        # the dense grad + apply + clip_dot path
+        # LPG forward, then only the touched rows rewritten; the touched gradient rows kept for the reverse pass's
+        # toued_entropy_clip / toued_hvp) where one agent's samples fit the sorted row kernel;
+        # TOUED_META_FUSED_STEP=0 keeps the dense grad + apply + entropy + clip_dot path
         self.fused_step = (os.environ.get("TOUED_META_FUSED_STEP", "1") != "0"
                            and bool(_lib.lib().toued_agent_update_fits(W, T, D)))
-        self.rows = (torch.empty(K, N, _lib.lib().toued_agent_rows_stride(), dtype=torch.int32, device=dev)
-                     if self.fused_step else None)
         self.gstat = z(K, N, 4)
         self.met = z(K, N, 8)
         self.traj = Transition(z(K + 1, N, T + 1, W, dt=i32), z(K + 1, N, T + 1, W, dt=i32),
@@ -276,8 +274,8 @@ class MetaGradStep:
                        ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(tk.obs_idx), ptr(tk.obs_time),
                        ptr(tk.action), ptr(tk.reward), ptr(tk.done), ptr(self.pi_hat[k]), ptr(self.y_hat[k]),
                        hyp.agent_target_coeff, hyp.actor_lr, hyp.critic_lr, hyp.max_grad_norm, ptr(self.G_th[k]),
-                       ptr(self.G_ph[k]), ptr(self.rows[k]), ptr(self.met[k]), ptr(agents.step), ptr(agents.levels),
-                       ptr(self.gstat[k]), st)
+                       ptr(self.G_ph[k]), ptr(self.met[k]), ptr(agents.step), ptr(agents.levels), ptr(self.gstat[k]),
+                       st)
             else:
                 L.call("toued_agent_grad", N, W, T, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(tk.obs_idx),
                        ptr(tk.obs_time), ptr(tk.action), ptr(tk.reward), ptr(tk.done), ptr(self.pi_hat[k]),
@@ -346,15 +344,19 @@ class MetaGradStep:
                ptr(te.action), ptr(self.abar), ptr(self.adj_th[a_in]), st)
         for k in range(K - 1, -1, -1):
             tk = self._t(k)
-            # d(-b0*H_pi - b1*H_y)/K at (theta_{k+1}, phi_{k+1}) on rollout k
-            L.call("toued_entropy", N, W, T, D, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(tk.obs_idx),
-                   ptr(tk.obs_time), None, -hyp.policy_entropy_coeff / K, -hyp.target_entropy_coeff / K,
-                   ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]), st)
+            # d(-b0*H_pi - b1*H_y)/K at (theta_{k+1}, phi_{k+1}) on rollout k, then the clip-VJP coefficients
             if self.fused_step:
-                L.call("toued_clip_dot_rows", N, D, ptr(self.rows[k]), ptr(self.G_th[k]), ptr(self.G_ph[k]),
-                       ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]), ptr(self.gstat[k]), hyp.actor_lr,
-                       hyp.critic_lr, hyp.max_grad_norm, ptr(self.coef), st)
+                # one kernel: the entropy gradient's rows are the rows update k touched, so their owners add
+                # <G_k, adjoint> as they write them (toued_clip_dot's dot up to the summation order)
+                L.call("toued_entropy_clip", N, W, T, D, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]),
+                       ptr(tk.obs_idx), ptr(tk.obs_time), -hyp.policy_entropy_coeff / K,
+                       -hyp.target_entropy_coeff / K, ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]),
+                       ptr(self.G_th[k]), ptr(self.G_ph[k]), ptr(self.gstat[k]), hyp.actor_lr, hyp.critic_lr,
+                       hyp.max_grad_norm, ptr(self.coef), st)
             else:
+                L.call("toued_entropy", N, W, T, D, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]),
+                       ptr(tk.obs_idx), ptr(tk.obs_time), None, -hyp.policy_entropy_coeff / K,
+                       -hyp.target_entropy_coeff / K, ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]), st)
                 L.call("toued_clip_dot", N, D, ptr(self.G_th[k]), ptr(self.G_ph[k]), ptr(self.adj_th[a_in]),
                        ptr(self.adj_ph[a_in]), ptr(self.gstat[k]), hyp.actor_lr, hyp.critic_lr, hyp.max_grad_norm,
                        ptr(self.coef), st)
