@@ -50,6 +50,8 @@ int toued_abi_version(void);
 /* ---- PRNG (jax 0.4.13 threefry, environments/* and meta/* call sites) ---- */
 /* out[i][j] = jax.random.split(keys[i], num)[j] */
 int toued_split(const uint32_t* keys, int n, int num, uint32_t* out, hipStream_t stream);
+/* the same keys in planar order: out[j][i] = jax.random.split(keys[i], num)[j] (each j a contiguous key batch) */
+int toued_split_planar(const uint32_t* keys, int n, int num, uint32_t* out, hipStream_t stream);
 /* out[i] = jax.random.fold_in(keys[i], data) */
 int toued_fold_in(const uint32_t* keys, int n, uint32_t data, uint32_t* out, hipStream_t stream);
 /* out[i][j] = jax.random.bits(keys[i], (m,))[j] */
@@ -307,6 +309,10 @@ int toued_agent_step(int N, int W, int T, int D, const float* theta, const float
                      const int* tidx, const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
                      const float* pi_hat, const float* y_hat, float alpha_y, float lr_a, float lr_c, float max_norm,
                      float* Gth, float* Gph, float* met, int* step, const int* levels, float* gstat, hipStream_t stream);
+/* The per-agent metrics of a meta-step (meta/train.py:101-117) from met [K][N][8] (k_agent_grad / k_entropy slots) and
+ * loss_out [N][2]: out [6][N] = reg_lpg_loss, policy_l2, policy_entropy, critic_loss, critic_l2, critic_entropy */
+int toued_meta_metrics(int N, int K, const float* met, float inv_wt, const float* loss_out, float pec, float pl2,
+                       float tec, float tl2, float* out, hipStream_t stream);
 int toued_entropy_clip(int N, int W, int T, int D, const float* theta, const float* phi, const int* tidx,
                        const int* ttime, float coef_a, float coef_c, float* adj_th, float* adj_ph, const float* Gth,
                        const float* Gph, const float* gstat, float lr_a, float lr_c, float max_norm, float* coef,

@@ -285,6 +285,12 @@ __global__ void __launch_bounds__(256) k_eval_draws(const int* __restrict__ leve
   draws[j] = make_uint4(cbits, tbits, (uint32_t)resp, 0u);
 }
 
+#ifdef H3_PLACE
+__device__ unsigned g_evr_place[64 * 64 * 2];   // (XCC_ID, HW_ID) of eval_returns' workgroups per launch (ring of 64)
+__device__ unsigned g_evr_launch;
+__global__ void k_evr_next() { if (threadIdx.x == 0) atomicAdd(&g_evr_launch, 1u); }
+#endif
+
 template <int NMAX>
 __global__ void __launch_bounds__(256) k_eval_returns(EnvSpec sp, const int* __restrict__ levels,
                                                       const float* __restrict__ theta, int D,
@@ -375,6 +381,13 @@ __global__ void __launch_bounds__(256) k_eval_returns(EnvSpec sp, const int* __r
     s.early_term = term;
   }
   cum_return[i] = cum;
+#ifdef H3_PLACE
+  if (threadIdx.x == 0 && blockIdx.x < 64) {
+    const unsigned slot = g_evr_launch & 63u;
+    g_evr_place[(slot * 64 + blockIdx.x) * 2] = (unsigned)__builtin_amdgcn_s_getreg((3 << 11) | 20);
+    g_evr_place[(slot * 64 + blockIdx.x) * 2 + 1] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+  }
+#endif
 }
 
 // ---------------------------------------------------------------- train rollouts in three launches
@@ -552,9 +565,19 @@ int toued_eval_returns(EnvSpec sp, const int* levels, const float* theta, int D,
   TOUED_DISPATCH_NMAX(sp.n_max, true, hipLaunchKernelGGL(k_eval_returns<NMAX>, dim3(nblk(n)), dim3(256), 0, stream, sp,
                                                         levels, theta, D, state, T, W, n,
                                                         reinterpret_cast<const uint4*>(draws), cum_return));
+#ifdef H3_PLACE
+  hipLaunchKernelGGL(k_evr_next, dim3(1), dim3(64), 0, stream);
+#endif
   TOUED_CHECK_LAUNCH();
   return 0;
 }
+
+#ifdef H3_PLACE
+int toued_dbg_evr_place(unsigned* host, unsigned* launches) {
+  if (hipMemcpyFromSymbol(launches, HIP_SYMBOL(g_evr_launch), sizeof(unsigned)) != hipSuccess) return 1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_evr_place), sizeof(g_evr_place)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 // the state-independent draws of U batches of train rollouts (T steps, n_agents x W workers each): keys [U][n_agents][2]
 // (the rollout keys of each batch), chain scratch and draws out [T][U * n_agents * W] of uint32x4

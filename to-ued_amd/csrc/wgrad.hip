@@ -364,6 +364,13 @@ __device__ unsigned long long g_wg_stamps[64 * 8 * 64 * 4];
 #define WG_STAMP(s, ph) do {} while (0)
 #endif
 
+#ifdef H3_PLACE
+// placement instrumentation (tools/h3_place.py): per launch (ring of 64) and workgroup, the XCC the workgroup ran on,
+// its HW_ID word, and its start and end times (s_memrealtime, 100 MHz)
+__device__ unsigned long long g_h3_place[64 * 256 * 4];
+__device__ unsigned int g_h3_launch;
+#endif
+
 // NW waves per workgroup, BT B tiles of 16 rows per wave: <4, 3> one wave per SIMD (acc 17 x 3, 512-register
 // budget), <8, 2> two waves per SIMD (acc 17 x 2 in 256 registers) so that one wave's waits are the other's issue.
 template <int NW, int BT>
@@ -371,14 +378,38 @@ __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict
                                                         int a_unit_rows, const int* __restrict__ rowmax_bits,
                                                         const float* __restrict__ B, long ldb, int rb,
                                                         const int8_t* __restrict__ colexp, long K, long kchunk,
-                                                        float* __restrict__ part) {
+                                                        float* __restrict__ part, int ntiles, int* __restrict__ qctr) {
   constexpr int NT = 64 * NW;
   constexpr int CT = 16 * BT * NW;                          // B rows per workgroup
   constexpr int NS = (X6_AQ + NT - 1) / NT;                 // A staging rounds per thread
   static_assert(NS <= 17 && 2 * BT < 17 - NS, "side-work schedule: B splits, B issue, then the staging rounds");
-  const int G = gridDim.x, ncol = (rb + CT - 1) / CT;
-  const int xcd = blockIdx.x & 7;
-  const int L = xcd * (G >> 3) + (xcd < (G & 7) ? xcd : (G & 7)) + (blockIdx.x >> 3);
+  const int ncol = (rb + CT - 1) / CT;
+#ifdef H3_PLACE
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
+  // Tile queues, one per XCD: XCD x owns the linear slots [base(x), base(x) + cnt(x)) (consecutive slots are the
+  // ncol column tiles of one K chunk, which read each A slab through that XCD's L2).  A workgroup takes the next slot
+  // of the XCD it runs on (XCC_ID), or of the next XCD with slots left.  The grid has more workgroups than tiles: a
+  // workgroup the dispatcher could not place at launch (a CU of its shader engine held by the eval chain beside this
+  // kernel) starts after the first ones finish, finds the queues empty and leaves -- instead of a tile of its own
+  // in a second round (6.9 vs 4.0 ms with a fixed blockIdx -> tile map; tools/h3_place.py).
+  __shared__ int s_slot;
+  if (threadIdx.x == 0) {
+    const int x = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;   // HW_REG_XCC_ID
+    const int per = ntiles >> 3, rem = ntiles & 7;
+    int got = -1;
+    for (int y = 0; y < 8 && got < 0; ++y) {
+      const int q = (x + y) & 7;
+      const int cnt = per + (q < rem ? 1 : 0);
+      if (cnt == 0) continue;
+      const int t = atomicAdd(&qctr[q], 1);
+      if (t < cnt) got = q * per + (q < rem ? q : rem) + t;
+    }
+    s_slot = got;
+  }
+  __syncthreads();
+  const int L = s_slot;
+  if (L < 0) return;
   __shared__ f16x8 As[2][2][X6_RA * 4];    // [buffer][piece][slot]: 69,632 B
   __shared__ float asc[X6_RA];             // 2^s_i of A row i
   __shared__ int cred[NW];
@@ -569,6 +600,17 @@ __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict
 #pragma unroll
       for (int t = 0; t < BT; ++t) out[(long)(16 * i + 4 * oct + r) * rbp + brow[t]] = (acc[i][t][r] * ia) * ib;
     }
+#ifdef H3_PLACE
+  __syncthreads();
+  if (threadIdx.x == 0 && blockIdx.x < 256) {
+    const unsigned slot = g_h3_launch & 63u;
+    unsigned long long* e = g_h3_place + ((size_t)slot * 256 + blockIdx.x) * 4;
+    e[0] = (unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20);   // XCC_ID[3:0]
+    e[1] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+    e[2] = t_start;
+    e[3] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 
 // C[i][j] = sum over chunks (in chunk order) of part[s][i][j], i < ra, j < rb
@@ -673,6 +715,13 @@ static Plan plan(int ra, int rb, long K) {
 
 extern "C" {
 
+#ifdef H3_PLACE
+int toued_dbg_h3_place(unsigned long long* host, unsigned* launches) {
+  if (hipMemcpyFromSymbol(launches, HIP_SYMBOL(g_h3_launch), sizeof(unsigned)) != hipSuccess) return 1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_h3_place), sizeof(g_h3_place)) == hipSuccess ? 0 : 1;
+}
+__global__ void k_h3_next() { if (threadIdx.x == 0) atomicAdd(&g_h3_launch, 1u); }
+#endif
 #ifdef WG_STAMPS
 int toued_dbg_wgrad_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wg_stamps), sizeof(g_wg_stamps)) == hipSuccess ? 0 : 1;
@@ -777,6 +826,29 @@ static bool wgrad_h8() {
   return f;
 }
 
+// CUs the plan's tiles leave unused (TOUED_H3_SLACK, default 16) and workgroups launched beyond the tiles
+// (TOUED_H3_EXTRA, default 16).  Measured (tools/h3_place.py, tools/h3_timing.py, 25 launches each beside the eval
+// chain): the dispatcher deals workgroups to XCDs and shader engines in turn and dispatches them in order, so one
+// workgroup it cannot place (its engine's free CUs taken) holds back every later one until a CU frees -- a tile in
+// a second round (6.9 instead of 4.0 ms).  With 16 tiles fewer than the free CUs and the grid at the free CUs, the
+// held-back workgroups are spares: 0 of 25 launches slow (8 / 16: 14 of 25; 8 / 8: 6 of 17; a fixed
+// blockIdx -> tile map: 7 of 22, all 17 without HIP timing events in the stream)
+static int h3_slack() {
+  static const int v = [] {
+    const char* e = getenv("TOUED_H3_SLACK");
+    return e ? atoi(e) : 16;
+  }();
+  return v;
+}
+
+static int h3_extra() {
+  static const int v = [] {
+    const char* e = getenv("TOUED_H3_EXTRA");
+    return e ? atoi(e) : 16;
+  }();
+  return v;
+}
+
 // the k_wgrad_h3 variant's plan: B rows per workgroup, column tiles and K chunks (one workgroup per CU)
 static Plan plan_bfp(int ra, int rb, long K) {
   Plan p = plan(ra > 16 ? ra : 17, rb, K);
@@ -788,6 +860,7 @@ static Plan plan_bfp(int ra, int rb, long K) {
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
     cus = 256;
   cus = cus - g_reserved_cus > cus / 2 ? cus - g_reserved_cus : cus / 2;
+  cus = cus - h3_slack() > cus / 2 ? cus - h3_slack() : cus / 2;
   int S = cus / p.ncol;
   if (S < 1) S = 1;
   const long slabs = K / 32;
@@ -801,7 +874,7 @@ static Plan plan_bfp(int ra, int rb, long K) {
 size_t toued_wgrad_bfp_workspace_floats(int ra, int rb, long K) {
   if (ra <= 0 || rb <= 0 || K <= 0) return 0;
   const Plan p = plan_bfp(ra, rb, K);
-  return (size_t)p.S * 17 * 16 * p.ncol * p.ct + X6_RA;
+  return (size_t)p.S * 17 * 16 * p.ncol * p.ct + X6_RA + 8;
 }
 
 int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit_rows, const float* B, long ldb,
@@ -817,22 +890,27 @@ int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit
   const Plan p = plan_bfp(ra, rb, K);
   TOUED_REQUIRE(p.kchunk % 16 == 0, "toued_wgrad_bfp: chunk %ld", p.kchunk);
   const size_t need = (size_t)p.S * 17 * 16 * p.ncol * p.ct;
-  TOUED_REQUIRE(work && work_floats >= need + X6_RA, "toued_wgrad_bfp: workspace of %zu floats needed (got %zu)",
-                need + X6_RA, work_floats);
+  TOUED_REQUIRE(work && work_floats >= need + X6_RA + 8, "toued_wgrad_bfp: workspace of %zu floats needed (got %zu)",
+                need + X6_RA + 8, work_floats);
   int* bits = reinterpret_cast<int*>(work + need);
+  int* qctr = bits + X6_RA;                                // the eight per-XCD tile queue counters
   const int nmeas = ra - a_unit_rows;
-  TOUED_REQUIRE(hipMemsetAsync(bits, 0, sizeof(int) * X6_RA, stream) == hipSuccess, "toued_wgrad_bfp: memset");
+  TOUED_REQUIRE(hipMemsetAsync(bits, 0, sizeof(int) * (X6_RA + 8), stream) == hipSuccess, "toued_wgrad_bfp: memset");
+  const int ntiles = p.ncol * p.S, grid = ntiles + h3_extra();
   if (nmeas > 0) {
     const long kper = 65536;
     hipLaunchKernelGGL(k_wgrad_rowmax, dim3((unsigned)((K + kper - 1) / kper), nmeas), dim3(256), 0, stream, A, lda,
                        a_unit_rows, K, kper, bits);
   }
   if (wgrad_h8())
-    hipLaunchKernelGGL((k_wgrad_h3<8, 2>), dim3(p.ncol * p.S), dim3(512), 0, stream, A, lda, ra, a_unit_rows, bits, B,
-                       ldb, rb, col_exp, K, p.kchunk, work);
+    hipLaunchKernelGGL((k_wgrad_h3<8, 2>), dim3(grid), dim3(512), 0, stream, A, lda, ra, a_unit_rows, bits, B,
+                       ldb, rb, col_exp, K, p.kchunk, work, ntiles, qctr);
   else
-    hipLaunchKernelGGL((k_wgrad_h3<X6_NW, X6_BT>), dim3(p.ncol * p.S), dim3(64 * X6_NW), 0, stream, A, lda, ra,
-                       a_unit_rows, bits, B, ldb, rb, col_exp, K, p.kchunk, work);
+    hipLaunchKernelGGL((k_wgrad_h3<X6_NW, X6_BT>), dim3(grid), dim3(64 * X6_NW), 0, stream, A, lda, ra,
+                       a_unit_rows, bits, B, ldb, rb, col_exp, K, p.kchunk, work, ntiles, qctr);
+#ifdef H3_PLACE
+  hipLaunchKernelGGL(k_h3_next, dim3(1), dim3(64), 0, stream);
+#endif
   const long n = (long)ra * rb;
   hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, work, p.S, 17 * 16,
                      p.ncol * p.ct, ra, rb, C, rb);

@@ -33,6 +33,7 @@ _L = ctypes.c_long
 # name -> argtypes (restype int unless listed in _RESTYPES)
 _SIGS = {
     "toued_split": [_P, _I, _I, _P, _P],
+    "toued_split_planar": [_P, _I, _I, _P, _P],
     "toued_fold_in": [_P, _I, _U, _P, _P],
     "toued_random_bits": [_P, _I, _I, _P, _P],
     "toued_uniform": [_P, _I, _I, _F, _F, _P, _P],
@@ -85,6 +86,7 @@ _SIGS = {
     "toued_agent_update_fits": [_I, _I, _I],
     "toued_agent_update": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _F, _P, _P, _P, _P, _P],
     "toued_agent_step": [_I, _I, _I, _I] + [_P] * 11 + [_F] * 4 + [_P] * 7,
+    "toued_meta_metrics": [_I, _I, _P, _F, _P, _F, _F, _F, _F, _P, _P],
     "toued_entropy_clip": [_I, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _F, _F, _F, _P, _P],
     "toued_a2c_chain_fits": [_I, _I, _I],
     "toued_a2c_chain": [EnvSpecC, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _P, _P, _P],

@@ -328,12 +328,19 @@ class MetaGradStep:
                 # workgroup per CU) starts after it (ea_draws_done), or its workgroups wait behind the draws' blocks
                 ea["draws_done"] = torch.cuda.Event()
                 ea["draws_done"].record(self.side)
-                ea["cum"] = self.ro.eval_returns_from_draws(self._ea_draws, self.theta_h[K], agents.levels,
-                                                            ea["state"])
             # the small products run beside the key chain, the main reduction beside the env chain
             ea["prev_reserve"] = L.lib().toued_set_reserved_cus(key_cus)
 
         def before_main_wgrad():
+            # (enqueued after the small products) the env chain's 8 workgroups start once the small products are
+            # done, beside the main reduction (which plans its tiles around the CUs they hold: k_wgrad_h3's tile
+            # queues in wgrad.hip)
+            small_done = torch.cuda.Event()
+            small_done.record(main)
+            self.side.wait_event(small_done)
+            with torch.cuda.stream(self.side):
+                ea["cum"] = self.ro.eval_returns_from_draws(self._ea_draws, self.theta_h[K], agents.levels,
+                                                            ea["state"])
             main.wait_event(ea["draws_done"])
             L.lib().toued_set_reserved_cus(eval_cus)
         # ---------------- reverse: explicit adjoint w.r.t. eta
@@ -394,16 +401,14 @@ class MetaGradStep:
         ea["state"].record_stream(main)
         agents.theta.copy_(self.theta_h[K])
         agents.phi.copy_(self.phi_h[K])
-        inv_wt = 1.0 / (W * T)
-        m = self.met * inv_wt                                     # [K, N, 8]
-        agent_m = m.mean(dim=0)
-        lpg_loss = self.loss_out[:, 0]
-        reg = (lpg_loss - hyp.policy_entropy_coeff * agent_m[:, 3] + hyp.policy_l2_coeff * agent_m[:, 1]
-               - hyp.target_entropy_coeff * agent_m[:, 4] + hyp.target_l2_coeff * agent_m[:, 2])
+        # (met * inv_wt).mean over the K updates and the regularised loss, one launch (toued_meta_metrics)
+        mo = torch.empty((6, N), dtype=torch.float32, device=self.dev)
+        L.call("toued_meta_metrics", N, K, ptr(self.met), 1.0 / (W * T), ptr(self.loss_out),
+               hyp.policy_entropy_coeff, hyp.policy_l2_coeff, hyp.target_entropy_coeff, hyp.target_l2_coeff, ptr(mo), st)
         return {
-            "lpg_loss": lpg_loss, "reg_lpg_loss": reg, "value_loss": self.loss_out[:, 1],
-            "lpg_agent": {"policy_l2": agent_m[:, 1], "policy_entropy": agent_m[:, 3], "critic_loss": agent_m[:, 0],
-                          "critic_l2": agent_m[:, 2], "critic_entropy": agent_m[:, 4]},
+            "lpg_loss": self.loss_out[:, 0], "reg_lpg_loss": mo[0], "value_loss": self.loss_out[:, 1],
+            "lpg_agent": {"policy_l2": mo[1], "policy_entropy": mo[2], "critic_loss": mo[3],
+                          "critic_l2": mo[4], "critic_entropy": mo[5]},
             "lpg_agent_return": ea_cum.mean(dim=1),
         }
 

@@ -10,16 +10,19 @@ ROOT = Path(__file__).resolve().parents[1] / "to-ued_amd"
 sys.path.insert(0, str(ROOT))
 import build as B  # noqa: E402
 
-src = ROOT / "csrc" / sys.argv[1]
+srcs = [ROOT / "csrc" / x for x in sys.argv[1].split(",")]   # one source, or several comma-separated
 defs = sys.argv[2:]
 tag = "_".join(d.replace("=", "_") for d in defs)
 out_dir = ROOT / "exp"
 out_dir.mkdir(exist_ok=True)
 B.build(verbose=False)
-obj = out_dir / f"{src.stem}_{tag}.o"
 cc = B.hipcc()
-subprocess.run([cc, *B._flags(src), *[f"-D{d}" for d in defs], "-c", str(src), "-o", str(obj)], check=True)
-objs = [obj if o.stem == src.stem else o for o in (B.OBJ / (s.stem + ".o") for s in sorted(B.CSRC.glob("*.hip")))]
+built = {}
+for src in srcs:
+    obj = out_dir / f"{src.stem}_{tag}.o"
+    subprocess.run([cc, *B._flags(src), *[f"-D{d}" for d in defs], "-c", str(src), "-o", str(obj)], check=True)
+    built[src.stem] = obj
+objs = [built.get(o.stem, o) for o in (B.OBJ / (s.stem + ".o") for s in sorted(B.CSRC.glob("*.hip")))]
 so = out_dir / f"libtoued_{tag}.so"
 subprocess.run([cc, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(so)], check=True)
 print(so)
