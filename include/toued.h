@@ -194,6 +194,13 @@ int toued_lpg_inputs(int N, int W, int T, int D, int F, const float* theta, cons
                      const float* eta_e1w, const float* eta_e1b, const float* eta_e2w, const float* eta_e2b,
                      const int* step, const int* levels, float* X, long xs_f, long xs_col, long eta_stride,
                      hipStream_t stream);
+/* toued_lpg_inputs with one thread per GRU row walking its T steps (W a multiple of 64): each step gathers one critic
+ * row and evaluates the embedding MLP once (y_{t+1}'s embedding is the next step's y_t one); bit-identical */
+int toued_lpg_inputs_rows(int N, int W, int T, int D, int F, const float* theta, const float* phi, const int* tidx,
+                          const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
+                          const float* eta_e1w, const float* eta_e1b, const float* eta_e2w, const float* eta_e2b,
+                          const int* step, const int* levels, float* X, long xs_f, long xs_col, long eta_stride,
+                          hipStream_t stream);
 /* lpg_agent_train_step gradients (lpg_agent.py:36-70) given pi_hat [T][R], y_hat [T][8][R], added to the
  * zeroed tables Gth/Gph; also gstat[a] = {|G_theta|, |G_phi|, step + 1 <= lifetime} for toued_agent_apply */
 int toued_agent_grad(int N, int W, int T, int D, const float* theta, const float* phi, const int* tidx,

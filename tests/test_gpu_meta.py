@@ -596,3 +596,43 @@ def test_fix_value_critic_matches_oracle():
                                atol=1e-7)
     g = step.grad.cpu().numpy() / N
     assert np.linalg.norm(g - g_ref) / np.linalg.norm(g_ref) < 1e-5
+
+
+@pytest.mark.parametrize("F,per_agent", [(5, False), (7, True)])
+def test_lpg_inputs_rows_bitexact(F, per_agent):
+    """toued_lpg_inputs_rows (one thread per GRU row over its T steps, the next step's critic embedding reused) against
+    the per-sample toued_lpg_inputs (models/lpg.py:48-77): the LPG input matrix bit-identical, with shared and
+    per-agent (ES candidate) embedding parameters, episode ends (done) in the trajectories and a strided X."""
+    from toued import _lib as L
+    from toued.env import L_LIFETIME
+    N, W, T, D = 6, 128, 20, 1937
+    g = torch.Generator(device="cuda").manual_seed(F)
+    theta = torch.randn(N, D, 5, generator=g, device="cuda") * 3
+    phi = torch.randn(N, D, 8, generator=g, device="cuda") * 3
+    tidx = torch.randint(0, D - 1, (N, T + 1, W), generator=g, device="cuda", dtype=torch.int32)
+    ttime = torch.randint(0, 250, (N, T + 1, W), generator=g, device="cuda", dtype=torch.int32)
+    tact = torch.randint(0, 5, (N, T, W), generator=g, device="cuda", dtype=torch.uint8)
+    trew = torch.randn(N, T, W, generator=g, device="cuda")
+    tdone = (torch.rand(N, T, W, generator=g, device="cuda") < 0.1).to(torch.uint8)
+    ns = N if per_agent else 1
+    stride = 161 if per_agent else 0
+    eta = torch.randn(ns, 161, generator=g, device="cuda") * 0.5
+    e1w, e1b, e2w, e2b = eta[:, 0:128], eta[:, 128:144], eta[:, 144:160], eta[:, 160:161]
+    step = torch.randint(0, 100, (N,), generator=g, device="cuda", dtype=torch.int32)
+    levels = torch.zeros(N, 80, dtype=torch.int32, device="cuda")
+    levels[:, L_LIFETIME] = torch.randint(100, 3000, (N,), generator=g, device="cuda", dtype=torch.int32)
+    R = N * W
+    xs_col, xs_f = 2, 2 * T * R + 64
+    outs = []
+    for fn in ("toued_lpg_inputs", "toued_lpg_inputs_rows"):
+        X = torch.full((F * xs_f,), float("nan"), device="cuda")
+        L.call(fn, N, W, T, D, F, L.ptr(theta), L.ptr(phi), L.ptr(tidx), L.ptr(ttime), L.ptr(tact), L.ptr(trew),
+               L.ptr(tdone), L.ptr(eta) + 0, L.ptr(eta) + 4 * 128, L.ptr(eta) + 4 * 144, L.ptr(eta) + 4 * 160,
+               L.ptr(step), L.ptr(levels), L.ptr(X), xs_f, xs_col, stride, L.stream_ptr())
+        torch.cuda.synchronize()
+        outs.append(X)
+    a, b = outs
+    assert torch.isnan(a).sum() == torch.isnan(b).sum()      # the same elements written (strided X)
+    m = ~torch.isnan(a)
+    assert int(m.sum()) == F * T * R
+    assert torch.equal(a[m], b[m])

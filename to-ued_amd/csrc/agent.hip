@@ -210,6 +210,100 @@ __global__ void __launch_bounds__(256) k_lpg_inputs(int N, int W, int T, int D, 
   }
 }
 
+// The same inputs with one thread per GRU row (agent a, worker w) walking its T steps: the embedding of y_{t+1}
+// (critic probabilities at the next observation) is the next step's embedding of y_t -- the same inputs, so the same
+// bits -- so each step gathers one critic row instead of two and evaluates the embedding MLP once instead of twice;
+// the next step's index loads and row gathers are issued before this step's arithmetic.  Bit-identical to
+// k_lpg_inputs (tests/test_gpu_meta.py::test_lpg_inputs_rows_bitexact).
+template <int F>
+__global__ void __launch_bounds__(64) k_lpg_inputs_rows(int N, int W, int T, int D, const float* __restrict__ theta,
+                                                        const float* __restrict__ phi, const int* __restrict__ tidx,
+                                                        const int* __restrict__ ttime, const uint8_t* __restrict__ tact,
+                                                        const float* __restrict__ trew,
+                                                        const uint8_t* __restrict__ tdone,
+                                                        const float* __restrict__ e1w, const float* __restrict__ e1b,
+                                                        const float* __restrict__ e2w, const float* __restrict__ e2b,
+                                                        const int* __restrict__ step, const int* __restrict__ levels,
+                                                        float* __restrict__ X, long xs_f, long xs_col,
+                                                        long eta_stride) {
+  const int r = blockIdx.x * 64 + threadIdx.x;   // W % 64 == 0: the block's 64 rows belong to one agent
+  if (r >= N * W) return;
+  const int a = __builtin_amdgcn_readfirstlane(r / W);
+  const int w = r - a * W;
+  const int R = N * W;
+  e1w += a * eta_stride;
+  e1b += a * eta_stride;
+  e2w += a * eta_stride;
+  e2b += a * eta_stride;
+  const float* th = theta + (size_t)a * D * 5;
+  const float* ph = phi + (size_t)a * D * 8;
+  float lastA[5], lastC[8];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
+  auto emb = [&](const float (&y)[8]) {   // embedding MLP [16, 1] (models/common.py:6-18), k_lpg_inputs' order
+    float e = e2b[0];
+#pragma unroll
+    for (int h = 0; h < 16; ++h) {
+      float hh = e1b[h];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) hh += y[i] * e1w[i * 16 + h];
+      e += fmaxf(hh, 0.0f) * e2w[h];
+    }
+    return e;
+  };
+  float fstep = 0.0f, flife = 0.0f;
+  if (F == 7) {
+    fstep = (float)step[a];
+    flife = (float)levels[(size_t)a * LEVEL_WORDS + L_LIFETIME];
+  }
+  const size_t ob = (size_t)a * (T + 1) * W + w;   // obs slot t at ob + t * W
+  const size_t sb = (size_t)a * T * W + w;         // step slot t at sb + t * W
+  int idx0 = tidx[ob];
+  float c0 = (float)ttime[ob] * 0.001f;
+  float e0;
+  {
+    float y0[8];
+    probs_of<8>(ph, lastC, idx0, c0, y0);
+    e0 = emb(y0);
+  }
+  int idx1 = tidx[ob + W];
+  float c1 = (float)ttime[ob + W] * 0.001f;
+  for (int t = 0; t < T; ++t) {
+    const size_t s = sb + (size_t)t * W;
+    const int act = tact[s];
+    const float rew = trew[s];
+    const int done = tdone[s];
+    // next step's observation (slot t + 2, clamped) loaded ahead
+    const int tn = t + 2 <= T ? t + 2 : T;
+    const int idx2 = tidx[ob + (size_t)tn * W];
+    const float c2 = (float)ttime[ob + (size_t)tn * W] * 0.001f;
+    float p[5], y1[8];
+    probs_of<5>(th, lastA, idx0, c0, p);
+    probs_of<8>(ph, lastC, idx1, c1, y1);
+    float pa = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) pa = (j == act) ? p[j] + EPSF : pa;
+    const float e1 = emb(y1);
+    const size_t o = ((size_t)t * R + r) * xs_col;
+    X[0 * xs_f + o] = rew;
+    X[1 * xs_f + o] = done ? 1.0f : 0.0f;
+    X[2 * xs_f + o] = pa;
+    X[3 * xs_f + o] = e0;
+    X[4 * xs_f + o] = done ? 0.0f : e1;
+    if (F == 7) {
+      X[5 * xs_f + o] = fstep;
+      X[6 * xs_f + o] = flife;
+    }
+    e0 = e1;
+    idx0 = idx1;
+    c0 = c1;
+    idx1 = idx2;
+    c1 = c2;
+  }
+}
+
 // ---------------------------------------------------------------------------- agent gradient
 // met slots: 0 kl_sum, 1 pihat^2 sum, 2 sum_j yhat^2 sum, 3 actor entropy sum, 4 critic entropy sum
 template <bool UNIF>
@@ -624,6 +718,35 @@ __global__ void __launch_bounds__(1024) k_clip_dot(int N, int D, const float* __
     for (int i = 0; i < 16; ++i) { sa += red[0][i]; sc += red[1][i]; }
     clip_coef(a, sa, sc, gstat, lr_a, lr_c, max_norm, coef);
   }
+}
+
+// ---------------------------------------------------------------------------- meta-step metrics
+// The per-agent metrics of a meta-step (meta/train.py:101-117) in one launch: m = met * inv_wt averaged over the K
+// updates (sum in update order, times 1/K, as torch's mean), and reg = lpg_loss - b0 H_pi + b2 |pi|^2 - b1 H_y +
+// b3 |y|^2 evaluated left to right.  out rows: reg, policy_l2, policy_entropy, critic_loss, critic_l2, critic_entropy.
+__global__ void k_meta_metrics(int N, int K, const float* __restrict__ met, float inv_wt,
+                               const float* __restrict__ loss_out, float pec, float pl2, float tec, float tl2,
+                               float* __restrict__ out) {
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= N) return;
+  float m[5];
+  const float invk = 1.0f / (float)K;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    float acc = 0.0f;
+    for (int k = 0; k < K; ++k) acc = __fadd_rn(acc, __fmul_rn(met[((size_t)k * N + a) * 8 + j], inv_wt));
+    m[j] = __fmul_rn(acc, invk);
+  }
+  float reg = __fsub_rn(loss_out[a * 2], __fmul_rn(pec, m[3]));
+  reg = __fadd_rn(reg, __fmul_rn(pl2, m[1]));
+  reg = __fsub_rn(reg, __fmul_rn(tec, m[4]));
+  reg = __fadd_rn(reg, __fmul_rn(tl2, m[2]));
+  out[a] = reg;
+  out[1 * N + a] = m[1];
+  out[2 * N + a] = m[3];
+  out[3 * N + a] = m[0];
+  out[4 * N + a] = m[2];
+  out[5 * N + a] = m[4];
 }
 
 // ---------------------------------------------------------------------------- HVP + LPG-output cotangents
@@ -1512,6 +1635,25 @@ int toued_lpg_inputs(int N, int W, int T, int D, int F, const float* theta, cons
   return 0;
 }
 
+int toued_lpg_inputs_rows(int N, int W, int T, int D, int F, const float* theta, const float* phi, const int* tidx,
+                          const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
+                          const float* eta_e1w, const float* eta_e1b, const float* eta_e2w, const float* eta_e2b,
+                          const int* step, const int* levels, float* X, long xs_f, long xs_col, long eta_stride,
+                          hipStream_t stream) {
+  TOUED_REQUIRE(F == 5 || F == 7, "toued_lpg_inputs_rows: F=%d", F);
+  TOUED_REQUIRE(W % 64 == 0, "toued_lpg_inputs_rows: W=%d must be a multiple of 64", W);
+  if ((long)N * W * T == 0) return 0;
+  const unsigned nb = (unsigned)((N * W) / 64);
+  if (F == 5)
+    hipLaunchKernelGGL(k_lpg_inputs_rows<5>, dim3(nb), dim3(64), 0, stream, N, W, T, D, theta, phi, tidx, ttime, tact,
+                       trew, tdone, eta_e1w, eta_e1b, eta_e2w, eta_e2b, step, levels, X, xs_f, xs_col, eta_stride);
+  else
+    hipLaunchKernelGGL(k_lpg_inputs_rows<7>, dim3(nb), dim3(64), 0, stream, N, W, T, D, theta, phi, tidx, ttime, tact,
+                       trew, tdone, eta_e1w, eta_e1b, eta_e2w, eta_e2b, step, levels, X, xs_f, xs_col, eta_stride);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
 int toued_agent_grad(int N, int W, int T, int D, const float* theta, const float* phi, const int* tidx,
                      const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
                      const float* pi_hat, const float* y_hat, float alpha_y, float* Gth, float* Gph, float* met,
@@ -1594,6 +1736,16 @@ int toued_agent_step(int N, int W, int T, int D, const float* theta, const float
 
 // toued_entropy's gradient mode followed by toued_clip_dot over the touched rows, in one kernel (the reverse pass of toued_agent_step's
 // update k: Gth / Gph hold that update's touched rows, which are the rows this trajectory's entropy gradient writes)
+int toued_meta_metrics(int N, int K, const float* met, float inv_wt, const float* loss_out, float pec, float pl2,
+                       float tec, float tl2, float* out, hipStream_t stream) {
+  if (N == 0) return 0;
+  TOUED_REQUIRE(K >= 1, "toued_meta_metrics: K=%d", K);
+  hipLaunchKernelGGL(k_meta_metrics, dim3((N + 255) / 256), dim3(256), 0, stream, N, K, met, inv_wt, loss_out, pec, pl2,
+                     tec, tl2, out);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
 int toued_entropy_clip(int N, int W, int T, int D, const float* theta, const float* phi, const int* tidx,
                        const int* ttime, float coef_a, float coef_c, float* adj_th, float* adj_ph, const float* Gth,
                        const float* Gph, const float* gstat, float lr_a, float lr_c, float max_norm, float* coef,

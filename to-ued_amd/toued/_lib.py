@@ -53,6 +53,8 @@ _SIGS = {
     "toued_eval_returns": [EnvSpecC, _P, _P, _I, _P, _I, _I, _I, _P, _P, _P],
     "toued_meta_keys": [_P, _I, _I, _P, _P, _P, _P, _P],
     "toued_lpg_inputs": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _L, _L, _P],
+    "toued_lpg_inputs_rows": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _L, _L,
+                              _P],
     "toued_agent_grad": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P],
     "toued_agent_apply": [_I, _I, _P, _P, _P, _P, _F, _F, _F, _P, _P, _P, _P, _P],
     "toued_entropy": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P],

@@ -27,6 +27,7 @@ import torch
 from . import _lib, prng
 from .agents import eval_agent
 from .lpg import LPGLayout
+from .meta import lpg_inputs_fn
 from .rollout import Transition, split_rollouts
 
 _Y = 8
@@ -236,7 +237,7 @@ class ESTrainStep:
                 rec["traj"] = Transition(tr.obs_idx.clone(), tr.obs_time.clone(), tr.action.clone(), tr.reward.clone(),
                                          tr.done.clone())
                 self.trace.append(rec)
-            L.call("toued_lpg_inputs", C, W, T, D, self.F, ptr(th), ptr(ph), ptr(tr.obs_idx), ptr(tr.obs_time),
+            L.call(lpg_inputs_fn(C * W, W), C, W, T, D, self.F, ptr(th), ptr(ph), ptr(tr.obs_idx), ptr(tr.obs_time),
                    ptr(tr.action), ptr(tr.reward), ptr(tr.done), ptr(e1w), ptr(e1b), ptr(e2w), ptr(e2b), ptr(step),
                    ptr(levels), ptr(self.X), T * R, 1, nd, st)
             tok = self.timers.start("gru_fwd_multi")

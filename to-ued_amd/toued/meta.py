@@ -54,6 +54,17 @@ class AdamState:
         self.count = 0
 
 
+def lpg_inputs_fn(rows: int, W: int) -> str:
+    """toued_lpg_inputs_rows (one thread per GRU row over its T steps: half the critic gathers and embedding MLPs) for
+    64k rows and more with W a multiple of 64 (the ES candidates: 58.8 vs 66.7 us per launch), else the per-sample
+    toued_lpg_inputs (the C2 batch's 32 k rows are too few threads for T-step chains: 42 vs 21 us);
+    TOUED_LPG_INPUTS_ROWS=0 / 1 forces either (bit-identical)."""
+    force = os.environ.get("TOUED_LPG_INPUTS_ROWS")
+    if W % 64 == 0 and (force == "1" or (force is None and rows >= 65536)):
+        return "toued_lpg_inputs_rows"
+    return "toued_lpg_inputs"
+
+
 class KernelTimers:
     """HIP-event timing of selected launches on the stream they are enqueued on (torch's current stream)."""
 
@@ -261,7 +272,7 @@ class MetaGradStep:
                 self.ro.batch_rollout(self.keys_roll[k], self.theta_h[k], agents.levels, state, out=tk,
                                       inplace_state=True)
             self.timers.stop(tok)
-            L.call("toued_lpg_inputs", N, W, T, D, self.F, ptr(self.theta_h[k]), ptr(self.phi_h[k]),
+            L.call(lpg_inputs_fn(R, W), N, W, T, D, self.F, ptr(self.theta_h[k]), ptr(self.phi_h[k]),
                    ptr(tk.obs_idx), ptr(tk.obs_time), ptr(tk.action), ptr(tk.reward), ptr(tk.done),
                    ptr(e1w), ptr(e1b), ptr(e2w), ptr(e2b), ptr(agents.step), ptr(agents.levels),
                    ptr(self.X) + 4 * k * T * R, self.gru.M, 1, 0, st)
