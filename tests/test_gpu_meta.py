@@ -80,6 +80,7 @@ def test_meta_step_matches_oracle(mode, lc):
     rew = tr.reward.cpu().numpy()
     dn = tr.done.cpu().numpy()
     th_h = step.theta_h.cpu().numpy()
+    th_h[0] = theta0          # slot 0 is the agents' own table storage: after the step it holds theta_K
     # ---- trajectories: every rollout k = 0..K bit-exact vs the numpy rollout driven by the GPU's theta_k
     spec = olv.env_spec(mode)
     keys = jr.split(jr.PRNGKey(0), N)

@@ -146,6 +146,8 @@ class MetaGradStep:
         self.R = R
         f32, i32, u8 = torch.float32, torch.int32, torch.uint8
         z = lambda *s, dt=f32: torch.zeros(s, dtype=dt, device=dev)
+        # parameter history theta_0 .. theta_K; slot 0 doubles as the agents' own table storage (AgentBatch.theta is
+        # bound to it at the first step), so after a step it holds theta_K
         self.theta_h = z(K + 1, N, D, 5)
         self.phi_h = z(K + 1, N, D, Y)
         self.G_th = z(K, N, D, 5)
@@ -241,8 +243,17 @@ class MetaGradStep:
         ptr = L.ptr
         L.call("toued_meta_keys", ptr(agent_keys), N, K, ptr(self.keys_roll), ptr(self.keys_eval),
                ptr(self.keys_ea_reset), ptr(self.keys_ea_roll), st)
-        self.theta_h[0].copy_(agents.theta)
-        self.phi_h[0].copy_(agents.phi)
+        if self.n_chunks == 1 and type(agents).__name__ == "AgentBatch":
+            # the agents' tables live in history slot 0 (bound there at the first step): theta_0 needs no copy, and the
+            # step ends by writing theta_K back into it
+            if agents.theta.data_ptr() != self.theta_h[0].data_ptr():
+                self.theta_h[0].copy_(agents.theta)
+                self.phi_h[0].copy_(agents.phi)
+                agents.theta = self.theta_h[0]
+                agents.phi = self.phi_h[0]
+        else:
+            self.theta_h[0].copy_(agents.theta)
+            self.phi_h[0].copy_(agents.phi)
         if not self.fused_step:   # the fused step writes the touched gradient rows, and nothing reads the others
             self.G_th.zero_()
             self.G_ph.zero_()
