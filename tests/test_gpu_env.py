@@ -47,6 +47,8 @@ def test_device_split_and_uniform():
     keys = jr.split(jr.PRNGKey(5), 33)
     dk = dev_keys(keys)
     np.testing.assert_array_equal(prng.to_uint32_numpy(prng.split(dk, 7)), jr.split(keys, 7))
+    np.testing.assert_array_equal(prng.to_uint32_numpy(prng.split_planar(dk, 7)),
+                                  np.ascontiguousarray(jr.split(keys, 7).transpose(1, 0, 2)))
     np.testing.assert_array_equal(prng.to_uint32_numpy(prng.fold_in(dk, 123)), jr.fold_in(keys, 123))
     np.testing.assert_array_equal(prng.to_uint32_numpy(prng.random_bits(dk, 9)), jr.random_bits(keys, (9,)))
     np.testing.assert_array_equal(prng.uniform(dk, 5, -1.0, 1.0).cpu().numpy(), jr.uniform(keys, (5,), -1.0, 1.0))

@@ -5,15 +5,17 @@
 
 namespace {
 
-// out[i, j] = split(keys[i], num)[j]
+// out[i, j] = split(keys[i], num)[j]; PLANAR: the same key at out[j, i] (each j one contiguous key batch)
+template <bool PLANAR>
 __global__ void __launch_bounds__(256) k_split(const uint32_t* __restrict__ keys, int num, uint32_t* __restrict__ out,
                                                int n) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long)n * num) return;
   const int i = (int)(t / num), j = (int)(t - (long)i * num);
   const uint2 k = split_at(make_uint2(keys[2 * i], keys[2 * i + 1]), (uint32_t)num, (uint32_t)j);
-  out[2 * t] = k.x;
-  out[2 * t + 1] = k.y;
+  const long o = PLANAR ? (long)j * n + i : t;
+  out[2 * o] = k.x;
+  out[2 * o + 1] = k.y;
 }
 
 __global__ void __launch_bounds__(256) k_fold_in(const uint32_t* __restrict__ keys, uint32_t data,
@@ -62,7 +64,16 @@ int toued_split(const uint32_t* keys, int n, int num, uint32_t* out, hipStream_t
   TOUED_REQUIRE(n >= 0 && num >= 1, "toued_split: n=%d num=%d", n, num);
   const long tot = (long)n * num;
   if (tot == 0) return 0;
-  hipLaunchKernelGGL(k_split, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, keys, num, out, n);
+  hipLaunchKernelGGL(k_split<false>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, keys, num, out, n);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_split_planar(const uint32_t* keys, int n, int num, uint32_t* out, hipStream_t stream) {
+  TOUED_REQUIRE(n >= 0 && num >= 1, "toued_split_planar: n=%d num=%d", n, num);
+  const long tot = (long)n * num;
+  if (tot == 0) return 0;
+  hipLaunchKernelGGL(k_split<true>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, keys, num, out, n);
   TOUED_CHECK_LAUNCH();
   return 0;
 }

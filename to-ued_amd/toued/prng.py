@@ -27,6 +27,14 @@ def split(keys: torch.Tensor, num: int = 2) -> torch.Tensor:
     return out.reshape(lead + (num, 2))
 
 
+def split_planar(keys: torch.Tensor, num: int = 2) -> torch.Tensor:
+    """split with the num axis first: keys [n, 2] -> [num, n, 2] (out[j] = split(keys, num)[:, j], contiguous)."""
+    flat = keys.reshape(-1, 2).contiguous()
+    out = torch.empty((num, flat.shape[0], 2), dtype=torch.int32, device=keys.device)
+    _lib.call("toued_split_planar", _lib.ptr(flat), flat.shape[0], num, _lib.ptr(out), _lib.stream_ptr())
+    return out
+
+
 def fold_in(keys: torch.Tensor, data: int) -> torch.Tensor:
     lead = keys.shape[:-1]
     flat = keys.reshape(-1, 2).contiguous()
