@@ -320,14 +320,14 @@ def workload_c3(a, cpu: bool):
     if "a2c_chain" in ks:
         # toued_a2c_chain: DRAW_CHUNK updates per launch.  Algorithmic bytes per agent-env-step: its draws (16 B),
         # the chosen actor row (20 B) and the V(obs) gather (4 B); the trajectory never leaves LDS
-        from toued.a2c import DRAW_CHUNK
-        upl = min(U, DRAW_CHUNK)
+        # launches of 4..32 updates (toued.a2c.chunk_sizes): the per-launch figures are over the mean chunk
+        upl = U / ks["a2c_chain"][0]
         chain_ms = ks["a2c_chain"][1]
-        dom = _hbm_roofline("k_a2c_chain (A2C antagonist: env chain + fused update, %d updates per launch)" % upl,
-                            steps_launch * upl * 40, chain_ms,
+        dom = _hbm_roofline("k_a2c_chain (A2C antagonist: env chain + fused update, %.2f updates per launch on "
+                            "average)" % upl, int(steps_launch * upl * 40), chain_ms,
                             "latency-bound: per update a T-step dependent env chain, then the LDS sort/segment update")
-        draws_rf = _hbm_roofline("k_eval_keys + k_eval_draws (state-independent draws of %d updates)" % upl,
-                                 steps_launch * upl * 32, ks["a2c_draws"][1], "threefry VALU-bound")
+        draws_rf = _hbm_roofline("k_eval_keys + k_eval_draws (state-independent draws of %.2f updates on average)"
+                                 % upl, int(steps_launch * upl * 32), ks["a2c_draws"][1], "threefry VALU-bound")
         secondary = {"a2c_chain": dom, "a2c_draws": draws_rf,
                      "per_update_ms": round((chain_ms + ks["a2c_draws"][1]) / upl, 4)}
     else:

@@ -1,0 +1,41 @@
+"""Host logic of the A2C chain path: the chunking of a U-update chain into toued_a2c_chain launches
+(toued.a2c.chunk_sizes) and the regret round's sink scatter into the level buffer (toued.plr._scatter_into)."""
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "to-ued_amd"))
+
+
+@pytest.mark.parametrize("U", [0, 1, 3, 4, 5, 10, 53, 54, 55, 86, 100, 250, 2500])
+def test_chunk_sizes_cover_u(U):
+    from toued.a2c import DRAW_CHUNK, DRAW_RAMP, chunk_sizes
+    c = chunk_sizes(U)
+    assert sum(c) == U
+    assert all(1 <= m <= DRAW_CHUNK for m in c)
+    assert c == sorted(c)                       # short chunks first, full ones last
+    if U >= sum(DRAW_RAMP) + DRAW_CHUNK:
+        assert c[0] == DRAW_RAMP[0] or c[0] < DRAW_RAMP[0]
+        assert c[-1] == DRAW_CHUNK
+
+
+def test_chunk_sizes_ramp_off(monkeypatch):
+    from toued.a2c import DRAW_CHUNK, chunk_sizes
+    monkeypatch.setenv("TOUED_A2C_RAMP", "0")
+    c = chunk_sizes(250)
+    assert c == sorted(c) and sum(c) == 250 and c.count(DRAW_CHUNK) == 7 and len(c) == 8
+
+
+def test_scatter_into_sink_drops_writes():
+    from toued.plr import _scatter_into
+    score = torch.arange(6, dtype=torch.float32)
+    term = torch.tensor([True, False, True, False])
+    old = torch.tensor([1, 1, 4, 5])
+    ids = torch.where(term, old, 6)
+    _scatter_into(score, ids, torch.tensor([10.0, 20.0, 30.0, 40.0]))
+    assert score.tolist() == [0.0, 10.0, 2.0, 3.0, 30.0, 5.0]
+    active = torch.ones(6, dtype=torch.bool)
+    _scatter_into(active, ids, False)
+    assert active.tolist() == [True, False, True, True, False, True]

@@ -618,6 +618,12 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
                                                    float* __restrict__ loss_out) {
   extern __shared__ float lds[];
   __shared__ A2CShared sh;
+#ifndef A2C_PRIO
+#define A2C_PRIO 3
+#endif
+  // the chain is latency-bound and the next chunk's draws (VALU-bound threefry) run beside it on the same SIMDs:
+  // its waves take the issue slots first
+  __builtin_amdgcn_s_setprio(A2C_PRIO);
   const int a = blockIdx.x, tid = threadIdx.x, n = (int)gridDim.x * W;
   A2CStage S;
   S.carve(lds, W, T);

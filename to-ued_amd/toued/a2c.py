@@ -24,6 +24,25 @@ from .rollout import RolloutWrapper, Transition, split_rollouts
 
 # updates whose rollout draws are produced by one toued_rollout_draws call (32 x N x W x T x 16 B of scratch)
 DRAW_CHUNK = 32
+# chunk sizes of the chain path: the first chunk's draws are the only ones not made beside a chain launch, so the chunks
+# start short and grow ~1.5x (a chain launch of m updates covers the side stream's draws of ~1.6 m updates), then
+# DRAW_CHUNK (TOUED_A2C_RAMP=0: DRAW_CHUNK throughout)
+DRAW_RAMP = (4, 6, 9, 14, 21)
+
+
+def chunk_sizes(U: int) -> list[int]:
+    """Update counts of the successive toued_a2c_chain launches of a U-update chain."""
+    out, done = [], 0
+    ramp = DRAW_RAMP if os.environ.get("TOUED_A2C_RAMP", "1") != "0" else ()
+    for m in ramp:
+        if done >= U:
+            break
+        out.append(min(m, U - done))
+        done += out[-1]
+    full, r = divmod(U - done, DRAW_CHUNK)
+    if r:   # a partial chunk goes with the short ones: the last launches stay full (they cover the eval draws)
+        out.append(r)
+    return sorted(out) + [DRAW_CHUNK] * full
 
 
 @dataclass
@@ -42,6 +61,8 @@ class A2CTrainer:
         self.hyp = hyp
         self.ah = agent_hypers
         self.use_graph = use_graph
+        self._graphs = {}
+        self.eval_draws_out = None
         self.fused = fused          # None: the LDS-fused update whenever it fits (toued_a2c_update_fits)
         # None: the whole update chain in one kernel per DRAW_CHUNK updates (toued_a2c_chain) whenever it fits and
         # the rollouts are split (unless TOUED_A2C_CHAIN=0); False: one rollout + one update launch per update
@@ -77,7 +98,22 @@ class A2CTrainer:
             "state": z(12, n * W, dt=torch.int32),
         }
         self._graph = None
+        self._graphs = {}
         return self._bufs
+
+    def _eval_bufs(self, b, keys, levels, W):
+        """Graph-static buffers of the eval draws enqueued behind the update chain (train(..., eval_keys=...))."""
+        n2, T = keys.shape[0], self.ro.eval_rollout_len
+        dev = keys.device
+        if b.get("ev_shape") != (n2, W, T):
+            b["ev_shape"] = (n2, W, T)
+            b["ev_keys"] = torch.zeros((n2, 2), dtype=torch.int32, device=dev)
+            b["ev_levels"] = torch.zeros((n2, LEVEL_WORDS), dtype=torch.int32, device=dev)
+            b["ev_draws"] = torch.zeros((T, n2 * W, 4), dtype=torch.int32, device=dev)
+            self._graphs.pop(True, None)
+        b["ev_keys"].copy_(keys)
+        b["ev_levels"].copy_(levels)
+        return lambda: self.ro.eval_draws(b["ev_keys"], b["ev_levels"], W, buf=b["ev_draws"])
 
     def use_chain(self, W, T, D) -> bool:
         if self.chain is False or os.environ.get("TOUED_A2C_CHAIN") == "0" or not split_rollouts():
@@ -86,15 +122,17 @@ class A2CTrainer:
             return False
         return bool(_lib.lib().toued_a2c_chain_fits(W, T, D))
 
-    def _chain_updates(self, b, n, D, W, T, U, tm):
+    def _chain_updates(self, b, n, D, W, T, U, tm, ev=None):
         """All U updates as toued_a2c_chain launches of DRAW_CHUNK updates each, every chunk on its precomputed draws.
         Untimed, the next chunk's draws (threefry VALU work, no LDS, ~24 VGPRs) run on a side stream beside the
-        current chunk's chain kernel (latency-bound, two workgroups per CU), into the other of two draw buffers."""
+        current chunk's chain kernel (latency-bound, two workgroups per CU), into the other of two draw buffers.
+        `ev` (the eval rollout's draws, state-independent) is enqueued on the side stream behind the last chunk's
+        draws, beside the last two chain launches; without the overlap it runs after the chain."""
         L = _lib
         st = L.stream_ptr()
         lr_a, lr_c, mn = self.ah.actor_learning_rate, self.ah.critic_learning_rate, self.ah.max_grad_norm
-        ch = min(U, DRAW_CHUNK)
-        starts = list(range(0, U, ch))
+        sizes = chunk_sizes(U)
+        starts = [sum(sizes[:c]) for c in range(len(sizes))]
         overlap = tm is None and len(starts) > 1
         main = torch.cuda.current_stream()
         if overlap:
@@ -106,11 +144,11 @@ class A2CTrainer:
             side.wait_event(fork)
 
         def draws_for(c, stream_ptr):
-            u, m = starts[c], min(ch, U - starts[c])
-            keys = b["chain"][u:u + m]
-            if m < ch:      # the last chunk: its unused key rows are never rolled
-                keys = torch.cat([keys, b["chain"][:ch - m]])
-            return self.ro.train_draws(keys, b["levels"], W, b["dbuf"][c % 2] if overlap else b["dbuf"][0],
+            u, m = starts[c], sizes[c]
+            full = b["dbuf"][c % 2] if overlap else b["dbuf"][0]
+            # the chunk's (key-chain scratch, draws) as contiguous [T][m * n * W][4] views of the DRAW_CHUNK buffers
+            bufs = tuple(x.view(-1)[:T * m * n * W * 4].view(T, m * n * W, 4) for x in full)
+            return self.ro.train_draws(b["chain"][u:u + m], b["levels"], W, bufs,
                                        stream=stream_ptr)
 
         d_ev, c_ev, pending = [], [], None
@@ -121,7 +159,7 @@ class A2CTrainer:
             e.record(side)
             d_ev.append(e)
         for c, u in enumerate(starts):
-            m = min(ch, U - u)
+            m = sizes[c]
             if overlap:
                 draws = pending
                 if c + 1 < len(starts):
@@ -132,6 +170,11 @@ class A2CTrainer:
                     e = torch.cuda.Event()
                     e.record(side)
                     d_ev.append(e)
+                    if ev is not None and c + 2 == len(starts):
+                        with torch.cuda.stream(side):
+                            ev()
+                        ev_done = torch.cuda.Event()
+                        ev_done.record(side)
                 main.wait_event(d_ev[c])
             else:
                 tok = tm.start("a2c_draws") if tm is not None else None
@@ -148,18 +191,27 @@ class A2CTrainer:
                 e = torch.cuda.Event()
                 e.record(main)
                 c_ev.append(e)
+        if ev is not None:
+            if overlap:
+                main.wait_event(ev_done)
+            else:
+                ev()
 
-    def _updates(self, b, n, D, W, T, U, record=None):
+    def _updates(self, b, n, D, W, T, U, record=None, ev=None):
         L = _lib
         st = L.stream_ptr()
         b["loss"].zero_()
         if U == 0:
+            if ev is not None:
+                ev()
             return
         L.call("toued_key_chain", L.ptr(b["rng"]), n, U, L.ptr(b["chain"]), st)
         tm = self.timers if self.timers is not None and self.timers.enabled else None
         if record is None and self.use_chain(W, T, D):
-            self._chain_updates(b, n, D, W, T, U, tm)
+            self._chain_updates(b, n, D, W, T, U, tm, ev)
             return
+        if ev is not None:   # the eval draws first: the per-update path below returns from inside its loop
+            ev()
         tr = b["tr"]
         lr_a, lr_c, mn = self.ah.actor_learning_rate, self.ah.critic_learning_rate, self.ah.max_grad_norm
         fits = bool(L.lib().toued_a2c_update_fits(W, T, D))
@@ -212,9 +264,13 @@ class A2CTrainer:
                                "vcrit_out": b["vcrit"].clone(), "step_out": b["step"].clone()})
 
     def train(self, rng: torch.Tensor, theta: torch.Tensor, vcrit: torch.Tensor, step: torch.Tensor,
-              levels: torch.Tensor, state: torch.Tensor, num_train_steps: int):
+              levels: torch.Tensor, state: torch.Tensor, num_train_steps: int, eval_keys: torch.Tensor | None = None,
+              eval_levels: torch.Tensor | None = None):
         """train_a2c_agent (a2c.py:79-125) for n agents; updates theta [n,D,5], vcrit [n,D], step [n],
-        state [12, n*W] in place.  Returns mean (actor_loss, critic_loss) over the updates, [n, 2]."""
+        state [12, n*W] in place.  Returns mean (actor_loss, critic_loss) over the updates, [n, 2].
+        With eval_keys [m,2] / eval_levels [m,80] (the rollout keys and levels of a later eval_returns over W
+        workers), that rollout's state-independent draws (RolloutWrapper.eval_draws) are produced beside the update
+        chain; they are in `self.eval_draws_out` afterwards, for RolloutWrapper.eval_returns_from_draws."""
         n, D = theta.shape[0], theta.shape[1]
         if n == 0:
             return torch.zeros((0, 2), device=theta.device)
@@ -225,8 +281,11 @@ class A2CTrainer:
         for name, src in (("rng", rng), ("theta", theta), ("vcrit", vcrit.reshape(n, D)), ("step", step),
                           ("levels", levels), ("state", state)):
             b[name].copy_(src)
+        ev = self._eval_bufs(b, eval_keys, eval_levels, W) if eval_keys is not None else None
+        self.eval_draws_out = b["ev_draws"] if ev is not None else None
+        self._graph = self._graphs.get(ev is not None)
         if self.record is not None or (self.timers is not None and self.timers.enabled):
-            self._updates(b, n, D, W, T, U, self.record)
+            self._updates(b, n, D, W, T, U, self.record, ev)
         elif self.use_graph and U > 0:
             if self._graph is None:
                 # warm the path once outside capture (library load, kernel code objects)
@@ -235,16 +294,17 @@ class A2CTrainer:
                 with torch.cuda.stream(s):
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, stream=s):
-                        self._updates(b, n, D, W, T, U)
+                        self._updates(b, n, D, W, T, U, ev=ev)
                 torch.cuda.current_stream().wait_stream(s)
                 self._graph = g
+                self._graphs[ev is not None] = g
                 # the capture did not execute: restore inputs and run it
                 for name, src in (("rng", rng), ("theta", theta), ("vcrit", vcrit.reshape(n, D)), ("step", step),
                                   ("levels", levels), ("state", state)):
                     b[name].copy_(src)
             self._graph.replay()
         else:
-            self._updates(b, n, D, W, T, U)
+            self._updates(b, n, D, W, T, U, ev=ev)
         theta.copy_(b["theta"])
         vcrit.copy_(b["vcrit"].reshape(vcrit.shape))
         step.copy_(b["step"])

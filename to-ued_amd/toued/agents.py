@@ -124,7 +124,15 @@ class AgentBatch:
 def eval_agent(ro, rng: torch.Tensor, levels: torch.Tensor, theta: torch.Tensor, num_workers: int) -> torch.Tensor:
     """agents/agents.py:98-106 for n agents: (rng, _rng) = split(rng) -> batch_reset(_rng, W);
     (rng, _rng) = split(rng) -> eval rollout; mean first-episode return per agent, f32 [n]."""
+    state, keys = eval_agent_reset(ro, rng, levels, num_workers)
+    return ro.eval_returns(keys, theta, levels, state).mean(dim=1)
+
+
+def eval_agent_reset(ro, rng: torch.Tensor, levels: torch.Tensor, num_workers: int):
+    """eval_agent's table-independent part: the worker reset and the rollout keys (agents/agents.py:100-103).
+    Returns (state [12, n*W], rollout keys [n, 2]) for RolloutWrapper.eval_returns(keys, theta, levels, state) or,
+    through RolloutWrapper.eval_draws(keys, levels, W), eval_returns_from_draws."""
     ks = prng.split(rng, 2)
     (_, _), state = ro.batch_reset(ks[:, 1].contiguous(), levels, num_workers)
     ks2 = prng.split(ks[:, 0].contiguous(), 2)
-    return ro.eval_returns(ks2[:, 1].contiguous(), theta, levels, state).mean(dim=1)
+    return state, ks2[:, 1].contiguous()

@@ -19,11 +19,13 @@ only on its own key, level and actor, so skipping the masked-out ones changes no
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib, prng
 from .a2c import A2CHyperparams, A2CTrainer
-from .agents import AgentBatch, create_agents, eval_agent
+from .agents import AgentBatch, create_agents, eval_agent, eval_agent_reset
 from .env import L_BUFID
 
 
@@ -44,8 +46,8 @@ def reset_lowest_scoring(sampler, rng: torch.Tensor, buffer, n_new: int) -> torc
     buffer.levels.index_copy_(0, il, levels)
     buffer.score.index_fill_(0, il, 0.0)
     new = buffer.active.clone()
-    new[il] = True
-    buffer.active[il] = False
+    new.index_fill_(0, il, True)
+    buffer.active.index_fill_(0, il, False)
     buffer.new = new
     return ids
 
@@ -64,13 +66,45 @@ def algorithmic_regret(sampler, keys: torch.Tensor, levels: torch.Tensor, lpg_th
     vcrit = vcrit.reshape(n, ro.obs_dim).contiguous()
     rng, tr = _split2(rng)
     step = torch.zeros(n, dtype=torch.int32, device=keys.device)
-    sampler.a2c_trainer().train(tr, theta, vcrit, step, levels, state, sampler.max_lifetime)
     lpg_rng, a2c_rng = _split2(rng)
     # both eval_agent calls as one batch of 2n agents (each agent's rollout depends only on its own key, level and
-    # table: bit-identical to two calls, at about the latency of one -- the returns-only rollout is latency-bound)
-    r = eval_agent(ro, torch.cat([lpg_rng, a2c_rng]), torch.cat([levels, levels]), torch.cat([lpg_theta, theta]), W)
+    # table: bit-identical to two calls, at about the latency of one -- the returns-only rollout is latency-bound).
+    # eval_agent's keys, reset and draws do not depend on the tables: the draws are made beside the antagonist's
+    # update chain, and after it only the env chain runs (eval_agent_reset / eval_returns_from_draws, bit-identical)
+    ev_levels = torch.cat([levels, levels])
+    ev_state, ev_keys = eval_agent_reset(ro, torch.cat([lpg_rng, a2c_rng]), ev_levels, W)
+    split_eval = (os.environ.get("TOUED_REGRET_SPLIT_EVAL", "1") != "0"
+                  and _eval_draw_bytes(ro, 2 * n, W) <= EVAL_DRAWS_MAX_BYTES)
+    trainer = sampler.a2c_trainer()
+    trainer.train(tr, theta, vcrit, step, levels, state, sampler.max_lifetime,
+                  eval_keys=ev_keys if split_eval else None, eval_levels=ev_levels if split_eval else None)
+    both = torch.cat([lpg_theta, theta])
+    if split_eval:
+        cum = ro.eval_returns_from_draws(trainer.eval_draws_out, both, ev_levels, ev_state)
+    else:
+        cum = ro.eval_returns(ev_keys, both, ev_levels, ev_state)
+    r = cum.mean(dim=1)
     r_lpg, r_a2c = r[:n], r[n:]
     return r_a2c - r_lpg
+
+
+# the regret round's eval draws ([eval_len][2n * W][4] u32, plus as much key-chain scratch) are made ahead when they fit
+EVAL_DRAWS_MAX_BYTES = 4 << 30
+
+
+def _eval_draw_bytes(ro, n_agents: int, W: int) -> int:
+    return 2 * 16 * ro.eval_rollout_len * n_agents * W
+
+
+def _scatter_into(dst: torch.Tensor, ids: torch.Tensor, val) -> None:
+    """dst[ids] = val for ids in [0, B], where id B (= len(dst)) is a sink whose writes are dropped."""
+    ext = torch.empty(dst.shape[0] + 1, dtype=dst.dtype, device=dst.device)
+    ext[:-1].copy_(dst)
+    if isinstance(val, torch.Tensor):
+        ext.index_put_((ids,), val.to(dst.dtype))
+    else:   # a Python scalar goes in as a kernel argument (a host tensor would be copied in behind a stream sync)
+        ext.index_fill_(0, ids, val)
+    dst.copy_(ext[:-1])
 
 
 def plr_sample(sampler, rng: torch.Tensor, buffer, agents: AgentBatch, term: torch.Tensor, sl=None):
@@ -81,7 +115,15 @@ def plr_sample(sampler, rng: torch.Tensor, buffer, agents: AgentBatch, term: tor
     B = len(buffer)
     dev = agents.levels.device
     rng, sub = _split2(rng)
-    reset_lowest_scoring(sampler, sub, buffer, N)
+    # _reset_lowest_scoring touches only the buffer, which the regret round below does not read: it runs on a side
+    # stream beside the antagonists' training, joined before the buffer update
+    main = torch.cuda.current_stream()
+    side = getattr(sampler, "_plr_side", None)
+    if side is None:
+        side = sampler._plr_side = torch.cuda.Stream(device=dev)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        reset_lowest_scoring(sampler, sub, buffer, N)
     rng, sub = _split2(rng)
     keys = prng.split(sub, N)
     if sl is not None:
@@ -101,11 +143,15 @@ def plr_sample(sampler, rng: torch.Tensor, buffer, agents: AgentBatch, term: tor
         old_g = world.all_gather_cat(old_ids)
     else:
         term_g, score_g, old_g = term, score, old_ids
-    # buffer update for terminated levels (:188-200)
-    t_ids = old_g[term_g].long()
-    buffer.score[t_ids] = score_g[term_g]
-    buffer.active[t_ids] = False
-    buffer.new[t_ids] = False
+    main.wait_stream(side)
+    buffer.new.record_stream(main)     # allocated on the side stream
+    # buffer update for terminated levels (:188-200), without a boolean-mask gather (a host sync that would hold the
+    # host's launches of the rest of sample() until the regret round has finished): every agent scatters, the
+    # non-terminated ones into a sink slot B past the buffer's end
+    t_ids = torch.where(term_g, old_g.long(), B)
+    _scatter_into(buffer.score, t_ids, score_g)
+    _scatter_into(buffer.active, t_ids, False)
+    _scatter_into(buffer.new, t_ids, False)
     # replay vs random (:203-227)
     ks = prng.split(rng, 3)                           # rng, replay_rng, random_rng
     kbuf = torch.stack([ks[1], ks[2], ks[0]]).contiguous()
@@ -119,7 +165,7 @@ def plr_sample(sampler, rng: torch.Tensor, buffer, agents: AgentBatch, term: tor
     r1, _ = _split2(ks[0].contiguous())               # bernoulli: rng, _rng = split(rng)
     rng, _ = _split2(r1)                              # permutation: rng, _rng = split(rng)
     new_ids = torch.where(term_g, chosen, old_g)
-    buffer.active[new_ids.long()] = True              # (:232-234)
+    buffer.active.index_fill_(0, new_ids.long(), True)   # (:232-234)
     lo, hi = (0, N) if sl is None else (sl[0], sl[1])
     new_levels = buffer.levels[new_ids[lo:hi].long()]
     return rng, buffer, new_levels
