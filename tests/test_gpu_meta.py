@@ -531,7 +531,8 @@ def test_fused_agent_step_matches_dense_path(monkeypatch, mode, N, lc):
 
 def test_1024_agents_two_mini_batches_on_one_gpu():
     """A reference-legal --num_agents 1024 --num_mini_batches 2 on one GPU (one 512-agent batch alone is the
-    bench's size; 1024 at once exceeds the GRU kernels' 4 GiB operand range): each chunk equals an unchunked
+    bench's size; 1024 at once exceeds the GRU kernels' 4 GiB operand range, so --num_mini_batches 1 runs the same
+    two chunks): each chunk equals an unchunked
     512-agent step over the same agents and keys (rank_slice = the chunk of split(rng, 1024))."""
     from toued.lpg import init_lpg_params
     from toued.meta import AdamState, LpgHyperparams, MetaGradStep
@@ -548,6 +549,15 @@ def test_1024_agents_two_mini_batches_on_one_gpu():
     g_big = big.grad.clone()
     assert torch.isfinite(g_big).all() and torch.isfinite(met["lpg_agent_return"]).all()
     del big
+    # --num_mini_batches 1 with the same 1024 agents: past the kernels' range (meta.gru_max_agents = 635) the batch
+    # runs as the same two chunks by itself, bit-identical
+    one = MetaGradStep(ro, N, hyp, False, num_mini_batches=1)
+    assert one.n_chunks == 2
+    ag1 = _clone_agents(ag0)
+    one(rng, eta0.clone(), AdamState(eta0.numel(), "cuda"), ag1)
+    torch.cuda.synchronize()
+    assert torch.equal(one.grad, g_big) and torch.equal(ag1.theta, ag.theta)
+    del one, ag1
     half = MetaGradStep(ro, 512, hyp, False)
     g_sum = torch.zeros_like(g_big)
     for lo in (0, 512):

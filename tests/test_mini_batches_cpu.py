@@ -32,3 +32,15 @@ def test_global_split_checked():
 def test_uneven_rank_share_rounds_to_a_divisor():
     # 5 agents on this rank, mini-batch of 2: ceil(5/2) = 3 chunks does not divide 5 -> 5 chunks of 1
     assert local_mini_batches(5, 10, 5) == 5
+
+
+def test_kernel_range_bounds_a_chunk():
+    # one GPU, --num_agents 1024 --num_mini_batches 1: the C2 shape's 1024-agent batch exceeds the GRU kernels'
+    # 32-bit operand range (635 agents at K=5, T=20, W=64), so it runs as two equal chunks (numerically a no-op)
+    from toued.meta import GRU_MAX_COLUMNS, gru_max_agents
+    cap = gru_max_agents(5, 20, 64)
+    assert cap == 635 and cap * 5 * 20 * 64 * 264 * 4 < 2 ** 32 and (cap + 1) * 5 * 20 * 64 <= GRU_MAX_COLUMNS + 6400
+    assert local_mini_batches(1024, 1024, 1, cap) == 2
+    assert local_mini_batches(512, 512, 1, cap) == 1
+    assert local_mini_batches(4096, 4096, 1, cap) == 8
+    assert local_mini_batches(1024, 1024, 4, cap) == 4      # the requested split is already finer

@@ -99,13 +99,25 @@ class KernelTimers:
         self.events = {}
 
 
-def local_mini_batches(n_local: int, num_agents: int, num_mini_batches: int) -> int:
+# the GRU kernels address one batch's K * T * N * W columns (up to 264 floats each) through 32-bit buffer offsets
+GRU_MAX_COLUMNS = 4294967295 // (264 * 4) - 1
+
+
+def gru_max_agents(K: int, T: int, W: int) -> int:
+    """The most agents one meta-gradient batch can hold (K updates of T steps, W workers) in the GRU kernels'
+    32-bit operand range (635 at K=5, T=20, W=64)."""
+    return max(1, GRU_MAX_COLUMNS // (K * T * W))
+
+
+def local_mini_batches(n_local: int, num_agents: int, num_mini_batches: int, max_chunk: int | None = None) -> int:
     """This rank's sequential chunk count for ``--num_mini_batches``.
 
     The reference checks the split globally: mini_batch_vmap reshapes all num_agents into num_mini_batches
     equal batches (util/jax.py:25-41), each of num_agents / num_mini_batches agents.  Chunking is a memory bound
     (the summed meta-gradient is the same), so each rank runs its n_local agents as the fewest equal chunks no
-    larger than that batch: the smallest divisor of n_local that is >= ceil(n_local / batch)."""
+    larger than that batch: the smallest divisor of n_local that is >= ceil(n_local / batch).  ``max_chunk`` (the
+    kernels' range, gru_max_agents) bounds a chunk the same way, so that a batch too large for one launch runs as
+    equal chunks instead of failing."""
     if num_mini_batches < 1 or num_agents % num_mini_batches:
         raise ValueError(f"num_agents={num_agents} does not split into num_mini_batches={num_mini_batches} equal "
                          "mini-batches (util/jax.py:25-41 reshapes them)")
@@ -113,6 +125,8 @@ def local_mini_batches(n_local: int, num_agents: int, num_mini_batches: int) -> 
         raise ValueError(f"this rank holds {n_local} agents")
     batch = num_agents // num_mini_batches
     need = -(-n_local // batch)
+    if max_chunk:
+        need = max(need, -(-n_local // max_chunk))
     return next(d for d in range(need, n_local + 1) if n_local % d == 0)
 
 
@@ -125,7 +139,9 @@ class MetaGradStep:
     def __init__(self, rollout: RolloutWrapper, n_agents: int, hyp: LpgHyperparams, lifetime_conditioning: bool,
                  device=None, world=None, num_mini_batches: int = 1, num_agents_global: int | None = None):
         self.n_total_local = n_agents
-        self.n_chunks = local_mini_batches(n_agents, num_agents_global or n_agents, num_mini_batches)
+        self.n_chunks = local_mini_batches(n_agents, num_agents_global or n_agents, num_mini_batches,
+                                           gru_max_agents(hyp.num_agent_updates, rollout.train_rollout_len,
+                                                          rollout.env_workers))
         n_agents //= self.n_chunks
         self.ro = rollout
         self.N = n_agents
