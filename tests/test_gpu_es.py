@@ -400,3 +400,35 @@ def test_es_step_k3_matches_oracle():
     _, _, winners, steps_w, th_w, ph_w, _ = certify_es_step(args, smp, step, rng, pre, m, p_lv, chained=True)
     assert np.array_equal(agents.theta.cpu().numpy(), th_w) and np.array_equal(agents.phi.cpu().numpy(), ph_w)
     assert np.array_equal(agents.step.cpu().numpy(), steps_w)
+
+
+def test_es_draws_ahead_bit_identical(monkeypatch):
+    """The ES step with its rollout draws made one chunk ahead on a side stream (double-buffered, three chunks at
+    K = 70) and the fitness eval's draws behind the last chunk's (TOUED_ES_AHEAD=1, an option: measured no faster)
+    is bit-identical to the in-order default (TOUED_ES_AHEAD=0): fitness, kept agents, env states and the ES
+    state."""
+    from toued import prng
+    from toued.es import ESTrainStep
+    from toued.level_sampler import LevelSampler
+    from toued.lpg import LPGLayout
+    from toued.parse_args import parse_args
+    mode, N, K = "all_vrandlife", 4, 70
+    args = parse_args(["--env_mode", mode, "--num_agents", str(N), "--num_mini_batches", "1", "--use_es",
+                       "--lifetime_conditioning", "--lpg_learning_rate", "0.01"])
+    smp = LevelSampler(args)
+    out = []
+    for ahead in ("1", "0"):
+        monkeypatch.setenv("TOUED_ES_AHEAD", ahead)
+        buf = smp.initialize_buffer(prng.PRNGKey(0, "cuda"))
+        _, agents = smp.initial_sample(prng.PRNGKey(1, "cuda"), buf, N, False)
+        agents.theta.mul_(20.0)
+        agents.phi.mul_(20.0)
+        step = ESTrainStep(args, smp, N, torch.zeros(LPGLayout(7).size, device="cuda"), "cuda", None,
+                           num_agent_updates=K)
+        step.es.mean.copy_(torch.from_numpy(np.random.RandomState(5).randn(step.es.nd).astype(np.float32) * 0.05))
+        step(dk(jr.PRNGKey(11)), agents)
+        torch.cuda.synchronize()
+        out.append([step.fitness.clone(), agents.theta.clone(), agents.phi.clone(), agents.step.clone(),
+                    agents.state.clone(), step.es.mean.clone(), step.es.m.clone()])
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
