@@ -132,7 +132,6 @@ def eval_agent_reset(ro, rng: torch.Tensor, levels: torch.Tensor, num_workers: i
     """eval_agent's table-independent part: the worker reset and the rollout keys (agents/agents.py:100-103).
     Returns (state [12, n*W], rollout keys [n, 2]) for RolloutWrapper.eval_returns(keys, theta, levels, state) or,
     through RolloutWrapper.eval_draws(keys, levels, W), eval_returns_from_draws."""
-    ks = prng.split(rng, 2)
-    (_, _), state = ro.batch_reset(ks[:, 1].contiguous(), levels, num_workers)
-    ks2 = prng.split(ks[:, 0].contiguous(), 2)
-    return state, ks2[:, 1].contiguous()
+    ks = prng.split_planar(rng, 2)     # ks[j] = split(rng, 2)[:, j], contiguous
+    (_, _), state = ro.batch_reset(ks[1], levels, num_workers)
+    return state, prng.split_planar(ks[0], 2)[1]

@@ -170,7 +170,7 @@ class GridWorld:
     def reset(self, keys, levels, W: int = 1):
         n = keys.shape[0]
         dev = keys.device
-        state = torch.empty((STATE_FIELDS, n), dtype=torch.int32, device=dev)
+        state = torch.zeros((STATE_FIELDS, n), dtype=torch.int32, device=dev)
         idx = torch.empty(n, dtype=torch.int32, device=dev)
         tm = torch.empty(n, dtype=torch.int32, device=dev)
         _lib.call("toued_gw_reset", self._c, _lib.ptr(levels), W, _lib.ptr(keys), _lib.ptr(state), _lib.ptr(idx),

@@ -30,6 +30,9 @@ from .env import L_BUFID
 
 
 def _split2(rng):
+    if rng.dim() == 2:                 # a batch of keys: both halves contiguous from one planar split
+        ks = prng.split_planar(rng, 2)
+        return ks[0], ks[1]
     ks = prng.split(rng, 2)
     return ks[..., 0, :].contiguous(), ks[..., 1, :].contiguous()
 

@@ -65,7 +65,8 @@ class RolloutWrapper:
         N = agent_keys.shape[0]
         dev = agent_keys.device
         n = N * W
-        state = torch.empty((STATE_FIELDS, n), dtype=torch.int32, device=dev)
+        # zeroed: the kernel writes the mode's fields only (object slots past max_n_objs stay 0, not stale memory)
+        state = torch.zeros((STATE_FIELDS, n), dtype=torch.int32, device=dev)
         idx = torch.empty(n, dtype=torch.int32, device=dev)
         tm = torch.empty(n, dtype=torch.int32, device=dev)
         _lib.call("toued_batch_reset", self._c, _lib.ptr(levels), _lib.ptr(agent_keys.contiguous()), N, W,
