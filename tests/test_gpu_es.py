@@ -74,7 +74,8 @@ def test_gru_fwd_multi_per_candidate():
     C, W, T, F = 3, 64, 20, 7
     R = C * W
     lay = LPGLayout(F)
-    etas = torch.stack([init_lpg_params(10 + c, F) + torch.randn(lay.size, device="cuda") * 0.05
+    gen = torch.Generator(device="cuda").manual_seed(1234)   # seeded: the same inputs on every run
+    etas = torch.stack([init_lpg_params(10 + c, F) + torch.randn(lay.size, device="cuda", generator=gen) * 0.05
                         for c in range(C)]).contiguous()
     fwdA = torch.zeros(C, _lib.lib().toued_gru_packed_floats(2), device="cuda")
     _lib.call("toued_gru_pack_fwd_multi", _lib.ptr(etas), lay.size, C, lay.c_offsets, F, _lib.ptr(fwdA),
@@ -237,7 +238,7 @@ def test_es_step_k1_matches_oracle():
                                                   int(lev[a, L_LIFETIME]), eta_c, traj, hyp)
         d_ref = th1.detach().numpy() - th0[a]
         d_dev = theta_dev[c].astype(np.float64) - th0[a]
-        assert np.linalg.norm(d_dev - d_ref) <= 2e-4 * np.linalg.norm(d_ref) + 1e-6, c
+        assert np.linalg.norm(d_dev - d_ref) <= 2e-5 * np.linalg.norm(d_ref) + 1e-7, c
     # fitness = eval_agent(rng_c) on the device-trained actor
     ck = jr.split(jr.split(ks[0], 2)[1], 2 * N)
     fit_keys = jr.split(ck, 2)[:, 0]

@@ -722,7 +722,7 @@ __global__ void __launch_bounds__(1024) k_clip_dot(int N, int D, const float* __
 
 // ---------------------------------------------------------------------------- meta-step metrics
 // The per-agent metrics of a meta-step (meta/train.py:101-117) in one launch: m = met * inv_wt averaged over the K
-// updates (sum in update order, times 1/K, as torch's mean), and reg = lpg_loss - b0 H_pi + b2 |pi|^2 - b1 H_y +
+// updates (sum in update order, then divided by K, as jnp.mean's sum / n), and reg = lpg_loss - b0 H_pi + b2 |pi|^2 - b1 H_y +
 // b3 |y|^2 evaluated left to right.  out rows: reg, policy_l2, policy_entropy, critic_loss, critic_l2, critic_entropy.
 __global__ void k_meta_metrics(int N, int K, const float* __restrict__ met, float inv_wt,
                                const float* __restrict__ loss_out, float pec, float pl2, float tec, float tl2,
@@ -730,12 +730,11 @@ __global__ void k_meta_metrics(int N, int K, const float* __restrict__ met, floa
   const int a = blockIdx.x * blockDim.x + threadIdx.x;
   if (a >= N) return;
   float m[5];
-  const float invk = 1.0f / (float)K;
 #pragma unroll
   for (int j = 0; j < 5; ++j) {
     float acc = 0.0f;
     for (int k = 0; k < K; ++k) acc = __fadd_rn(acc, __fmul_rn(met[((size_t)k * N + a) * 8 + j], inv_wt));
-    m[j] = __fmul_rn(acc, invk);
+    m[j] = __fdiv_rn(acc, (float)K);
   }
   float reg = __fsub_rn(loss_out[a * 2], __fmul_rn(pec, m[3]));
   reg = __fadd_rn(reg, __fmul_rn(pl2, m[1]));

@@ -291,7 +291,11 @@ class ESTrainStep:
                     used[c].record(main)
             elif split:
                 if k % DRAW_CHUNK == 0:
-                    draws = self.ro.train_draws(chain[k:k + DRAW_CHUNK], levels, W)
+                    # this step's own buffers (a short last chunk views a prefix of them): the rollout wrapper's shared
+                    # buffer would be reallocated at every change of shape and is also used by other callers
+                    m = min(DRAW_CHUNK, K - k)
+                    bufs = tuple(x.view(-1)[:T * m * C * W * 4].view(T, m * C * W, 4) for x in self._chunk_bufs(C, W)[0])
+                    draws = self.ro.train_draws(chain[k:k + m], levels, W, bufs)
                 self.ro.rollout_from_draws(draws, k % DRAW_CHUNK, th, levels, state, tr)
             else:
                 self.ro.batch_rollout(chain[k], th, levels, state, out=tr, inplace_state=True)

@@ -22,6 +22,7 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib, prng
+from .agents import AgentBatch
 from .lpg import LPGGRU, LPGLayout, Y
 from .rollout import RolloutWrapper, Transition, split_rollouts
 
@@ -202,6 +203,7 @@ class MetaGradStep:
         self.timers = KernelTimers()
         self.side = torch.cuda.Stream(device=dev)
         self._ea_draws = None   # eval_agent draws buffer (rollout.eval_draws), reused every step
+        self._draws = None      # the K + 1 train rollouts' draws (rollout.train_draws), reused every step
 
     # ------------------------------------------------------------------ helpers
     def _t(self, k: int) -> Transition:
@@ -259,7 +261,7 @@ class MetaGradStep:
         ptr = L.ptr
         L.call("toued_meta_keys", ptr(agent_keys), N, K, ptr(self.keys_roll), ptr(self.keys_eval),
                ptr(self.keys_ea_reset), ptr(self.keys_ea_roll), st)
-        if self.n_chunks == 1 and type(agents).__name__ == "AgentBatch":
+        if self.n_chunks == 1 and isinstance(agents, AgentBatch):
             # the agents' tables live in history slot 0 (bound there at the first step): theta_0 needs no copy, and the
             # step ends by writing theta_K back into it
             if agents.theta.data_ptr() != self.theta_h[0].data_ptr():
@@ -282,7 +284,11 @@ class MetaGradStep:
         # rollout; keys and levels are known now) in one launch instead of one per rollout
         draws = None
         if split_rollouts():
-            draws = self.ro.train_draws(torch.cat([self.keys_roll, self.keys_eval.unsqueeze(0)]), agents.levels, W)
+            if self._draws is None:    # the step's own (chain scratch, draws) pair: [T][(K + 1) * N * W][4]
+                self._draws = tuple(torch.empty((T, (K + 1) * N * W, 4), dtype=torch.int32, device=self.dev)
+                                    for _ in range(2))
+            draws = self.ro.train_draws(torch.cat([self.keys_roll, self.keys_eval.unsqueeze(0)]), agents.levels, W,
+                                        self._draws)
         # ---------------- forward: K inner updates (agents/lpg_agent.py:88-140)
         for k in range(K):
             tk = self._t(k)
@@ -555,7 +561,10 @@ def make_lpg_train_step(args, level_sampler, n_agents: int | None = None, world=
     ``(lpg_train_state, agent_states, value_critic_states, metrics)``.
 
     agent_states: agents.AgentBatch of this rank's agents (``rank_slice`` = (lo, hi, n_total) under data
-    parallelism; n_agents defaults to its size).  value_critic_states: ValueCriticStates or None (then the ones
+    parallelism; n_agents defaults to its size).  The meta-gradient step rebinds ``agent_states.theta`` / ``.phi`` at
+    its first call to its own history slot 0 (copying the tables once) and updates them there in place, so the
+    returned states alias the inputs from then on; a tensor reference taken to the tables BEFORE the first step is
+    not updated.  value_critic_states: ValueCriticStates or None (then the ones
     inside agent_states are used); ignored by the ES step, as in the reference.  ``impl``: an already built
     MetaGradStep / ESTrainStep to drive (train.Trainer keeps its instance for timers and buffers)."""
     n_local = n_agents if n_agents is not None else (args.num_agents if rank_slice is None

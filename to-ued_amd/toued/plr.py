@@ -125,6 +125,10 @@ def plr_sample(sampler, rng: torch.Tensor, buffer, agents: AgentBatch, term: tor
     if side is None:
         side = sampler._plr_side = torch.cuda.Stream(device=dev)
     side.wait_stream(main)
+    # the side kernels read `sub` and the old `buffer.new` (both from main's allocator pool) after this function has
+    # dropped them: keep their blocks from being reused by main until the side stream's work has passed them
+    sub.record_stream(side)
+    buffer.new.record_stream(side)
     with torch.cuda.stream(side):
         reset_lowest_scoring(sampler, sub, buffer, N)
     rng, sub = _split2(rng)
