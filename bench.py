@@ -52,6 +52,10 @@ GRU_BWD_FLOP_PER_ELEM = 2 * 256 * 768              # dh_prev = dG . W_h^T per (k
 # y_hat (1 + 8 + 8) and writing dX3/dX4 (2)
 GRU_FWD_BYTES_PER_ELEM = {F: 4 * (4 * 256 + F + 1 + 9) for F in (5, 7)}
 GRU_BWD_BYTES_PER_ELEM = {F: 4 * (4 * 256 + F + 5 * 256 + 9 + 17 + 2) for F in (5, 7)}
+# with the small weight-gradient products fused (toued_gru_bwd_fused, F <= 6): the four saves and x read, the three
+# contraction cotangents DG written (dn_pre, relu(h_out) and DH stay on chip), the head inputs (17 floats) read,
+# dX3/dX4 written, one column-exponent byte; the per-workgroup partials (4672 floats per 64 rows x T) are < 0.2 %
+GRU_BWD_FUSED_BYTES_PER_ELEM = {F: 4 * (4 * 256 + F + 3 * 256 + 17 + 2) + 1 for F in (5,)}
 # main weight-gradient reduction [h_in; x; 1] (256 + F + 1 rows) x [dr; dz; dhn] (768 rows) over M columns: f32-equiv
 # FLOP 2 * rows * 768 per column, issued as 3 fp16 products (block-floating-point pairs); algorithmic bytes = both
 # operands once (the A rows are re-read by 4 column tiles through L2)
@@ -148,9 +152,15 @@ def launcher_selftest(a):
     if world.active:
         import torch.distributed as dist
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    # the collectives the step uses, through World: the meta-gradient's all-reduce(SUM) and the sampler's gather
+    # of per-agent vectors over the contiguous agent slices (C5: 4096 agents over the ranks)
+    lo, hi, n = world.agent_slice(4096)
+    s = world.all_reduce_sum(torch.full((4,), float(world.rank + 1)))
+    g = world.all_gather_cat(torch.arange(lo, hi, dtype=torch.int32))
     if world.rank == 0:
         print(json.dumps({"metric": "launcher_selftest", "n_gpus": world.size, "ranks_seen": world.size,
-                          "max_dt": float(dt)}), flush=True)
+                          "max_dt": float(dt), "sum_ranks": float(s[0]), "slice0": [lo, hi, n],
+                          "gathered_ok": bool(torch.equal(g, torch.arange(n, dtype=torch.int32)))}), flush=True)
     if world.active:
         import torch.distributed as dist
         dist.barrier()
@@ -575,7 +585,8 @@ def main():
     # the roofline bound is whichever roof sets the longer minimum time (bytes / 8 TB/s vs the bf16 MFMA work
     # the f32-accurate split issues / 2.5 PF/s)
     work = {"gru_fwd": (R * T * GRU_FWD_FLOP_PER_ELEM[F], R * T * GRU_FWD_BYTES_PER_ELEM[F]),
-            "gru_bwd": (K * R * T * GRU_BWD_FLOP_PER_ELEM, K * R * T * GRU_BWD_BYTES_PER_ELEM[F])}
+            "gru_bwd": (K * R * T * GRU_BWD_FLOP_PER_ELEM,
+                        K * R * T * (GRU_BWD_FUSED_BYTES_PER_ELEM[F] if step.gru.fused else GRU_BWD_BYTES_PER_ELEM[F]))}
     cand = [(n, ksum[n][2], ksum[n][1]) for n in work if n in ksum]
     dom, _, mean_ms = max(cand, key=lambda c: c[1])
     flop, nbytes = work[dom]

@@ -262,6 +262,19 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
                   float* DG, float* RH, float* DH, float* dX3, float* dX4, int8_t* col_exp, hipStream_t stream);
 /* 1 when toued_gru_bwd runs its lockstep split-precision kernel for R rows (the one that writes col_exp) */
 int toued_gru_bwd_col_exp(int R);
+/* 1 when toued_gru_bwd_fused applies: the lockstep kernel for R rows and LPG input width F <= 6 */
+int toued_gru_bwd_fused_fits(int R, int F);
+/* floats of `work` toued_gru_bwd_fused needs: per-workgroup partials of the small products + their chunk sums */
+size_t toued_gru_bwd_fused_work_floats(int R, int K);
+/* the VJP with the small weight-gradient products fused (replaces toued_gru_bwd + toued_gru_bwd_small where it fits):
+ * DG3 [3][256][M] = dr, dz, d(W_hn h + b_hn) (the main reduction's B operand), dX3/dX4, col_exp (required), and GI as
+ * toued_gru_bwd_small writes it; dn, relu(h_out) and the head cotangents stay on chip (no s_n: n is recomputed).
+ * Deterministic: per-workgroup partials summed in a fixed order. */
+int toued_gru_bwd_fused(int R, int T, int W, int K, const uint8_t* done, long done_stride_k, const float* bwdA,
+                        const float* eta, const int* off, const float* y_hat, const float* d_pi_hat,
+                        const float* d_y_hat, const float* s_hin, const float* s_r, const float* s_z,
+                        const float* s_hn, long M, float* DG3, float* dX3, float* dX4, int8_t* col_exp, float* GI,
+                        float* work, size_t work_floats, hipStream_t stream);
 /* the backward's small weight-gradient products: GI = [8][256] ([X; 1; 0] . dn^T: dW_in rows, b_in) followed by
  * [9][257] (DH . [relu(h_out); 1]^T: head kernels and biases); X rows start at s_hin + 256*M.
  * `work`: toued_gru_bwd_small_work_floats(M) floats. */

@@ -9,6 +9,8 @@ import subprocess
 import sys
 from pathlib import Path
 
+import pytest
+
 ROOT = Path(__file__).resolve().parents[1]
 
 
@@ -21,16 +23,20 @@ def _env():
     return env
 
 
-def test_bench_self_launches_two_ranks():
-    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--launcher_selftest"],
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_self_launches_ranks(n):
+    """n = 8 is the driver's C5 node: eight gloo ranks through the same launcher, barrier and MAX timing."""
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(n), "--launcher_selftest"],
                        capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["ranks_seen"] == 2
-    # max over ranks: rank 1 sleeps 20 ms inside the timed region
-    assert out["max_dt"] >= 0.02
+    assert out["n_gpus"] == n and out["ranks_seen"] == n
+    # max over ranks: rank r sleeps 10 (r + 1) ms inside the timed region
+    assert out["max_dt"] >= 0.01 * n
+    assert out["sum_ranks"] == n * (n + 1) / 2
+    assert out["slice0"] == [0, 4096 // n, 4096] and out["gathered_ok"]
 
 
 def test_bench_too_many_gpus_fails_loudly():

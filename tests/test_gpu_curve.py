@@ -101,7 +101,7 @@ def test_meta_return_curve_certified(seed, life0):
         th_h = sf.theta_h.cpu().numpy()
         th_h[0] = pre["theta"]    # slot 0 is the agents' own table storage: after the step it holds theta_K
         R = N * W
-        hpos = (sf.gru.RH[:256] > 0).cpu().numpy().reshape(256, K, T, R)
+        hpos = (sf.gru.relu_out() > 0).cpu().numpy().reshape(256, K, T, R)
         g_sum = sf.grad.cpu().numpy()
         ret_gpu = metrics["lpg_agent_return"].cpu().numpy()
         loss_gpu = metrics["lpg_loss"].cpu().numpy()

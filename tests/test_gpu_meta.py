@@ -265,7 +265,7 @@ def _gru_bwd_case(N, W, T, K, F, eta, xs, done, d_pi, d_y):
     gru.backward(done_t, eta, y_hat, torch.from_numpy(d_pi).cuda(), torch.from_numpy(d_y).cuda(), X, grad)
     torch.cuda.synchronize()
     # float64 autograd oracle, relu branches from the device (RH = relu(h_out) rows [256][M], column (k, t, r))
-    relu_dev = (gru.RH[:256] > 0).cpu().numpy().reshape(256, K, T, R)
+    relu_dev = (gru.relu_out() > 0).cpu().numpy().reshape(256, K, T, R)
     flips = []
     flat = torch.tensor(eta.cpu().numpy(), dtype=torch.float64, requires_grad=True)
     P = olpg.unflatten(flat, F)
@@ -382,7 +382,10 @@ def test_gru_independent_of_scratch_contents(N, W, wscale):
     outs = {}
     for how in ("zero", "nan", "random", "zero"):
         gru = LPGGRU(lay, R, T, K, W, "cuda")
-        for t in (gru.S, gru.DG, gru.DH, gru.dX3, gru.dX4, gru._ggi, gru.CE, gru.wg_work, gru.A[:H], gru.RH[:H]):
+        bufs = [gru.S, gru.DG, gru.dX3, gru.dX4, gru._ggi, gru.CE, gru.wg_work, gru.A[:H]]
+        if not gru.fused:
+            bufs += [gru.DH, gru.RH[:H]]
+        for t in bufs:
             if t.numel():
                 fill(t, how)
         gru.pack(eta)
@@ -647,3 +650,49 @@ def test_lpg_inputs_rows_bitexact(F, per_agent):
     m = ~torch.isnan(a)
     assert int(m.sum()) == F * T * R
     assert torch.equal(a[m], b[m])
+
+
+@pytest.mark.parametrize("N,wscale", [(2, 4.0), (12, 1.0)])
+def test_gru_backward_fused_small_matches_unfused(N, wscale):
+    """k_gru_bwd6n<true> (the two small weight-gradient products accumulated in the kernel on 16x16x4 f32 MFMAs,
+    reduced from per-workgroup partials) against the unfused pair k_gru_bwd6n<false> + toued_gru_bwd_small: the
+    contraction cotangents, column exponents and input cotangents bit-identical (the same gate maths), the small
+    products GI within 2e-6 relative (exact f32 products, another summation order), the flat gradient within 1e-6
+    relative L2."""
+    from toued.lpg import LPGGRU, LPGLayout, init_lpg_params
+    W, T, K, F = 64, 6, 2, 5
+    R = N * W
+    lay = LPGLayout(F)
+    eta = init_lpg_params(7, F)
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    eta += torch.randn(eta.shape, device="cuda", generator=gen) * 0.05
+    for name in ("hr_w", "hz_w", "hn_w"):
+        lay.view(eta, name).mul_(wscale)
+    rs = np.random.RandomState(9)
+    xs = torch.from_numpy(rs.randn(F, K, T, R).astype(np.float32)).cuda()
+    done_t = torch.from_numpy((rs.rand(K, N, T, W) < 0.15).astype(np.uint8)).cuda()
+    d_pi = torch.from_numpy(rs.randn(K, T, R).astype(np.float32)).cuda()
+    d_y = torch.from_numpy(rs.randn(K, T, 8, R).astype(np.float32)).cuda()
+    outs = []
+    for fused in (False, True):
+        gru = LPGGRU(lay, R, T, K, W, "cuda", fused=fused)
+        assert gru.fused == fused
+        gru.pack(eta)
+        gru.X.copy_(xs)
+        pi_hat = torch.zeros(K, T, R, device="cuda")
+        y_hat = torch.zeros(K, T, 8, R, device="cuda")
+        for k in range(K):
+            gru.forward(k, gru.X, done_t[k], eta, pi_hat, y_hat)
+        grad = torch.zeros(lay.size, device="cuda")
+        gru.backward(done_t, eta, y_hat, d_pi, d_y, gru.X, grad)
+        torch.cuda.synchronize()
+        outs.append((gru.DG[:3].clone(), gru.CE.clone(), gru.dX3.clone(), gru.dX4.clone(), gru.GI.clone(), grad))
+    (dg0, ce0, x30, x40, gi0, g0), (dg1, ce1, x31, x41, gi1, g1) = outs
+    assert torch.equal(dg0, dg1) and torch.equal(ce0, ce1)
+    assert torch.equal(x30, x31) and torch.equal(x40, x41)
+    gi0, gi1 = gi0.double(), gi1.double()
+    # per block ([8][256] then [9][257]), elementwise against the block's scale
+    for a, b in ((gi0[:8 * 256], gi1[:8 * 256]), (gi0[8 * 256:], gi1[8 * 256:])):
+        assert float((a - b).abs().max()) <= 2e-6 * float(a.abs().max()), float((a - b).abs().max())
+    g0, g1 = g0.double(), g1.double()
+    assert float((g0 - g1).norm() / g0.norm()) < 1e-6

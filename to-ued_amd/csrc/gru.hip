@@ -40,6 +40,7 @@ extern "C" int toued_rowsum_into(int ra, long K, const float* A, long lda, float
                                  size_t work_floats, hipStream_t stream);
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 #define HU 256          // GRU width (lpg_gru_width)
 #define RB 32           // batch rows per workgroup
@@ -898,7 +899,12 @@ struct BwdArgs {
   int8_t* CE;       // [M] (optional, lockstep kernel): column m's cotangent scale exponent for the weight-gradient
                     // reduction (2^CE[m] max over dr, dz, dhn of column m < 2^14; 127 = all zero)
   int F;            // LPG input width (lockstep kernel: x rows at s_hin + 256 M, n recomputed by gate_n)
+  float* SP;        // fused small products (k_gru_bwd6n<true>): per-workgroup partials [n_wg][SP_FLOATS]
 };
+// fused small weight-gradient products: per workgroup C[16][256] (rows 0..F-1: X . dn^T, row F: the ones row,
+// rows F+1..F+9: DH . relu(h_out)^T) then the head cotangents' row sums [9][64 rows]
+#define SP_C (16 * HU)
+#define SP_FLOATS (SP_C + 9 * 64)
 
 // NT row tiles of 32 rows per workgroup.  NT = 2: one workgroup per CU (150 KB LDS, 256 VGPRs), every
 // packed W_h^T fragment feeds 8 MFMAs instead of 4 (half the L2 fragment stream per FLOP).
@@ -1120,6 +1126,10 @@ __device__ unsigned long long g_bwd_stamps[64 * 32 * 8];
 //     dr is split once into three bf16 pieces in the one LDS cotangent image, dz and dhn wait in registers;
 //   contraction: dh_prev = sum_g W_g . dg_g with the pieces as B fragments (no per-wave re-split), the image
 //     refilled with dz, then dhn, between the three gate passes.
+//   SMALL (F <= 6): the two small weight-gradient products GI = [X; 1] . dn^T and DH . relu(h_out)^T accumulate in
+//     the kernel (16x16x4 f32 MFMA, exact f32 products) instead of streaming dn and relu(h_out) to HBM for a later
+//     reduction: see small_mfma below.
+template <bool SMALL>
 __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   constexpr int RBT = 2 * RB;
   constexpr int PP = HU + 8;                       // piece image row pitch (bf16): 528 B
@@ -1132,6 +1142,12 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   __shared__ float wIs[8 * 4 * 64];                // gate_ain's W_in fragments [wave][kk][lane] (read at each tile)
   __shared__ float wAs[8 * 5 * 64];                // W_heads^T A fragments [wave][kk][lane] (read at each tile)
   __shared__ int dns[RBT];                         // done flags of the step's rows (loaded with the head cotangents)
+  // SMALL: the A operand of the small products per row pair s of the step: Atab[s][lane] = A[i = lane & 15][k = lane
+  // >> 4] with k = 0, 1: [x; 1] of rows 2s, 2s+1 (i < F, i == F) and k = 2, 3: the head cotangents of rows 2s, 2s+1
+  // (i = F+1 .. F+9); and the head cotangents' running row sums over the steps (the heads' bias column)
+  __shared__ __attribute__((aligned(16))) float Atab[SMALL ? 32 * 64 : 4];
+  __shared__ float hvs[SMALL ? 9 * RBT : 1];
+  __shared__ floatx4 accl[SMALL ? 8 * 2 * 64 : 1];
   // dr in f32 while the memory part streams ([row][unit], pitch DRP), over image slots 1 and 2
   constexpr int DRP = HU + 4;
   static_assert(RBT * DRP * 4 <= 2 * RBT * PP * 2, "dr staging exceeds image slots 1-2");
@@ -1166,13 +1182,24 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int q = 0; q < 16; ++q) dh[h][q] = 0.0f;
+  // SMALL: the running accumulators C[i][unit 32 wave + 16 uh + (l & 15)] of the wave's two 16-unit halves wait in
+  // LDS between the steps ([wave][uh][lane] float4): the register file has no room for them across the step
+  if (SMALL) {
+    for (int i = tid; i < 9 * RBT; i += 512) hvs[i] = 0.0f;
+    for (int i = tid; i < 8 * 2 * 64; i += 512) accl[i] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+  }
+  // SMALL: dn_pre, relu(h_out) and DH stay on chip (optional debug stores behind a runtime branch measured 336 B of
+  // scratch per lane: the kernel is at the 256-VGPR bound); the tests take the relu decisions from the unfused kernel
+  constexpr bool st_rh = !SMALL, st_dn = !SMALL;
   const __amdgpu_buffer_rsrc_t rs_hin = rsrc_of(p.s_hin), rs_r = rsrc_of(p.s_r), rs_z = rsrc_of(p.s_z),
-                               rs_hn = rsrc_of(p.s_hn), rs_rh = rsrc_of(p.RH);
+                               rs_hn = rsrc_of(p.s_hn), rs_rh = rsrc_of(SMALL ? p.s_hin : p.RH);
   const __amdgpu_buffer_rsrc_t rs_x = rsrc_of(p.s_hin + (size_t)HU * p.M);   // the rows' inputs x [F][M]
   const __amdgpu_buffer_rsrc_t rs_dg[4] = {rsrc_of(p.DG), rsrc_of(p.DG + 1L * HU * p.M),
-                                           rsrc_of(p.DG + 2L * HU * p.M), rsrc_of(p.DG + 3L * HU * p.M)};
+                                           rsrc_of(p.DG + 2L * HU * p.M),
+                                           rsrc_of(SMALL ? p.DG : p.DG + 3L * HU * p.M)};
+  constexpr bool st_DH = !SMALL;
   const __amdgpu_buffer_rsrc_t rs_yh = rsrc_of(p.y_hat), rs_dyh = rsrc_of(p.d_y_hat), rs_dpi = rsrc_of(p.d_pi_hat),
-                               rs_DH = rsrc_of(p.DH), rs_dx3 = rsrc_of(p.dX3), rs_dx4 = rsrc_of(p.dX4),
+                               rs_DH = rsrc_of(SMALL ? p.dX3 : p.DH), rs_dx3 = rsrc_of(p.dX3), rs_dx4 = rsrc_of(p.dX4),
                                rs_done = rsrc_of(reinterpret_cast<const float*>(p.done + (long)k * p.done_stride_k));
   // head cotangents of step t (softmax VJP of y_hat, d pi_hat) -> hv, DH
   auto head_cot = [&](int t) {
@@ -1196,14 +1223,43 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += yh[j] * dy[j];
       const float dpi = ld_u(rs_dpi, vrw, (unsigned)(o * 4));
+      float xr[6];   // SMALL: this row's inputs x_0 .. x_{F-1} (F <= 6)
+      if (SMALL) {
+#pragma unroll
+        for (int f = 0; f < 6; ++f)
+          xr[f] = ld_u(rs_x, vrw, (unsigned)(((long)(f < F ? f : 0) * p.M + o) * 4));
+      }
       dns[tl] = dnv;
       hv[tl] = dpi;
-      st_u(rs_DH, vrw, (unsigned)(o * 4), dpi);
+      if (st_DH) st_u(rs_DH, vrw, (unsigned)(o * 4), dpi);
+      float hvv[9];
+      hvv[0] = dpi;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float v = yh[j] * (dy[j] - s);
         hv[(j + 1) * RBT + tl] = v;
-        st_u(rs_DH, vrw, (unsigned)(((long)(j + 1) * p.M + o) * 4), v);
+        hvv[j + 1] = v;
+        if (st_DH) st_u(rs_DH, vrw, (unsigned)(((long)(j + 1) * p.M + o) * 4), v);
+      }
+      if (SMALL) {
+        // row tl = 2 s + par: lanes 16 par + i (k = par: [x; 1; 0]) and 32 + 16 par + i (k = 2 + par: head
+        // cotangents at i = F + 1 ..): zeros, then the entries at their (uniform, runtime) positions
+        float* at = Atab + (tl >> 1) * 64 + 16 * (tl & 1);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (c >= 2) *reinterpret_cast<float4*>(at + 4 * c) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          *reinterpret_cast<float4*>(at + 32 + 4 * c) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
+        at[6] = 0.0f;
+        at[7] = 0.0f;
+        *reinterpret_cast<float4*>(at) = make_float4(0 < F ? xr[0] : 0.0f, 1 < F ? xr[1] : 0.0f, 2 < F ? xr[2] : 0.0f,
+                                                     3 < F ? xr[3] : 0.0f);
+        *reinterpret_cast<float2*>(at + 4) = make_float2(4 < F ? xr[4] : 0.0f, 5 < F ? xr[5] : 0.0f);
+        at[F] = 1.0f;
+#pragma unroll
+        for (int o9 = 0; o9 < 9; ++o9) at[32 + F + 1 + o9] = hvv[o9];
+#pragma unroll
+        for (int o9 = 0; o9 < 9; ++o9) hvs[o9 * RBT + tl] += hvv[o9];
       }
     }
   };
@@ -1262,6 +1318,31 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     for (int e = 0; e < 4; ++e) split2h(v[e] * sc, x0, x1, e);
     *reinterpret_cast<f16x4*>(&dgB[0][row * PP + u0]) = x0;
     *reinterpret_cast<f16x4*>(&dgB[1][row * PP + u0]) = x1;
+  };
+  // SMALL: the wave's dn and relu(h_out) of one row tile and one 16-unit half go through a wave-private [row][unit]
+  // f32 block in image slot 0 (free during the memory part) as the B operand B[k][j = unit] of 16x16x4 f32 MFMAs over
+  // the tile's 16 row pairs, k = 0, 1: dn of rows 2s, 2s+1; k = 2, 3: relu(h_out) of rows 2s, 2s+1, against Atab's
+  // A[i][k] ([x; 1] rows for k < 2, head cotangent rows for k >= 2).  Unit quads are XOR-swizzled by (row >> 2) & 3
+  // (conflict-free 16-byte writes and dword reads); the second array sits 544 floats after the first (other banks).
+  float* priv = reinterpret_cast<float*>(&dgB[0][0]) + 1056 * wave;
+  auto small_mfma = [&](int h, int g4, const float (&dnq)[4], const float (&rhq)[4]) {
+    const int ln = lane_now(), row = ln & 31, c = 2 * (g4 & 1) + (ln >> 5);
+    const int wo = row * 16 + ((c ^ ((row >> 2) & 3)) << 2);
+    *reinterpret_cast<float4*>(priv + wo) = make_float4(dnq[0], dnq[1], dnq[2], dnq[3]);
+    *reinterpret_cast<float4*>(priv + 544 + wo) = make_float4(rhq[0], rhq[1], rhq[2], rhq[3]);
+    if (g4 & 1) {
+      const int l2 = lane_now(), kk = l2 >> 4, j = l2 & 15;
+      const int rb = (kk >> 1) * 544 + (kk & 1) * 16 + (j & 3);
+      floatx4& al = accl[(wave * 2 + (g4 >> 1)) * 64 + l2];
+      floatx4 acc = al;
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) {
+        const float b = priv[rb + 32 * s2 + ((((j >> 2) ^ ((s2 >> 1) & 3))) << 2)];
+        const float a = Atab[(16 * h + s2) * 64 + l2];
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+      }
+      al = acc;
+    }
   };
   for (int t = 0; t < T; ++t) {
     const long ctr = ((long)k * T + t) * R;
@@ -1363,8 +1444,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         rhq[jj] = fmaxf(hout, 0.0f);
         dnq[jj] = dnp;
       }
-      st_q(rs_rh, h, g4, rhq);
-      st_q(rs_dg[3], h, g4, dnq);   // dr, dz and dhn leave beside the contraction passes
+      if (st_rh) st_q(rs_rh, h, g4, rhq);
+      if (st_dn) st_q(rs_dg[3], h, g4, dnq);   // dr, dz and dhn leave beside the contraction passes
+      if (SMALL) small_mfma(h, g4, dnq, rhq);
       *reinterpret_cast<float4*>(&drs[rown(h) * DRP + ubn() + 8 * g4]) = make_float4(drq[0], drq[1], drq[2], drq[3]);
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) rmr[h] = fmaxf(rmr[h], fabsf(drq[jj]));
@@ -1504,6 +1586,54 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     BWD_STAMP(7);
     lds_barrier();   // hv, dxp and the image are rewritten next step
   }
+  if (SMALL) {
+    // this workgroup's partials: C[i = 4 (l >> 4) + r][unit 32 wave + 16 uh + (l & 15)], then the head rows' sums
+    float* out = p.SP + (size_t)blockIdx.x * SP_FLOATS;
+    const int ln = lane_now();
+#pragma unroll
+    for (int uh = 0; uh < 2; ++uh) {
+      const floatx4 a = accl[(wave * 2 + uh) * 64 + ln];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(4 * (ln >> 4) + r) * HU + 32 * wave + 16 * uh + (ln & 15)] = a[r];
+    }
+    for (int i = tid; i < 9 * RBT; i += 512) out[SP_C + i] = hvs[i];
+  }
+}
+
+// Sum of the fused small products' per-workgroup partials in a fixed order (deterministic): level 1, block (chunk c of
+// 64 workgroups, 256 outputs) -> part2[c][out]; level 2 (k_small_final) the chunks in order, and the head bias column
+// over the 64 rows, into GI = [8][256] ([x; 1; 0] . dn^T) | [9][257] (DH . [relu(h_out); 1]^T)
+#define SR_CHUNK 64
+__global__ void __launch_bounds__(256) k_small_part(const float* __restrict__ sp, int n_wg, float* __restrict__ part2) {
+  const int o = blockIdx.x * 256 + threadIdx.x;
+  if (o >= SP_FLOATS) return;
+  const int c = blockIdx.y, w0 = c * SR_CHUNK, w1 = min(n_wg, w0 + SR_CHUNK);
+  float a = 0.0f;
+  for (int w = w0; w < w1; ++w) a += sp[(size_t)w * SP_FLOATS + o];
+  part2[(size_t)c * SP_FLOATS + o] = a;
+}
+__global__ void __launch_bounds__(256) k_small_final(const float* __restrict__ part2, int n_chunk, int F,
+                                                     float* __restrict__ GI) {
+  const int o = blockIdx.x * 256 + threadIdx.x;   // output element of GI
+  if (o >= 8 * HU + 9 * (HU + 1)) return;
+  float a = 0.0f;
+  if (o < 8 * HU) {                               // [x; 1; 0] . dn^T
+    const int i = o / HU, u = o % HU;
+    if (i <= F)
+      for (int c = 0; c < n_chunk; ++c) a += part2[(size_t)c * SP_FLOATS + i * HU + u];
+  } else {
+    const int e = o - 8 * HU, oo = e / (HU + 1), u = e % (HU + 1);
+    if (u < HU) {
+      for (int c = 0; c < n_chunk; ++c) a += part2[(size_t)c * SP_FLOATS + (F + 1 + oo) * HU + u];
+    } else {                                       // bias column: sum of the head cotangents over every row
+      for (int c = 0; c < n_chunk; ++c) {
+        float rs = 0.0f;
+        for (int r = 0; r < 64; ++r) rs += part2[(size_t)c * SP_FLOATS + SP_C + oo * 64 + r];
+        a += rs;
+      }
+    }
+  }
+  GI[o] = a;
 }
 
 }  // namespace
@@ -1640,10 +1770,57 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
   p.DG = DG; p.RH = RH; p.DH = DH; p.dX3 = dX3; p.dX4 = dX4; p.CE = col_exp;
   p.F = (p.o.ir_b - p.o.in_w) / HU;   // in_w [F][256] is followed by ir_b in the flat layout (lpg.LPGLayout)
   TOUED_REQUIRE(p.F >= 1 && p.F <= 7 && p.o.ir_b - p.o.in_w == p.F * HU, "toued_gru_bwd: LPG layout F=%d", p.F);
+  p.SP = nullptr;
   if (toued_gru_bwd_col_exp(R))
-    hipLaunchKernelGGL(k_gru_bwd6n, dim3(K * (R / (2 * RB))), dim3(512), 0, stream, p);
+    hipLaunchKernelGGL(k_gru_bwd6n<false>, dim3(K * (R / (2 * RB))), dim3(512), 0, stream, p);
   else
     hipLaunchKernelGGL(k_gru_bwd<1>, dim3(K * (R / RB)), dim3(512), 0, stream, p);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+// 1 when toued_gru_bwd_fused applies: the lockstep kernel (R a multiple of 64) with F + 10 <= 16 A rows
+int toued_gru_bwd_fused_fits(int R, int F) { return toued_gru_bwd_col_exp(R) && F >= 1 && F <= 6 ? 1 : 0; }
+
+size_t toued_gru_bwd_fused_work_floats(int R, int K) {
+  const long n_wg = (long)K * (R / (2 * RB)), n_chunk = (n_wg + SR_CHUNK - 1) / SR_CHUNK;
+  return (size_t)(n_wg + n_chunk) * SP_FLOATS;
+}
+
+// The backward with the small weight-gradient products fused (k_gru_bwd6n<true>): writes the three contraction
+// cotangents DG = [dr_pre; dz_pre; d(hn)] (the main reduction's B operand), the column exponents, dX3/dX4, and GI =
+// [8][256] ([x; 1; 0] . dn^T) | [9][257] (DH . [relu(h_out); 1]^T) through per-workgroup partials reduced in a fixed
+// order.  dn_pre, relu(h_out) and DH are not streamed to HBM.
+int toued_gru_bwd_fused(int R, int T, int W, int K, const uint8_t* done, long done_stride_k, const float* bwdA,
+                        const float* eta, const int* off, const float* y_hat, const float* d_pi_hat,
+                        const float* d_y_hat, const float* s_hin, const float* s_r, const float* s_z,
+                        const float* s_hn, long M, float* DG3, float* dX3, float* dX4, int8_t* col_exp, float* GI,
+                        float* work, size_t work_floats, hipStream_t stream) {
+  TOUED_REQUIRE(R % (2 * RB) == 0 && W % RB == 0 && !gru_f32_forced(),
+                "toued_gru_bwd_fused: rows R=%d must be a multiple of 64 (W=%d), split-precision kernels", R, W);
+  TOUED_REQUIRE((double)M * 264.0 * 4.0 < 4294967295.0, "toued_gru_bwd_fused: M=%ld columns exceed the 4 GiB range",
+                M);
+  TOUED_REQUIRE(M == (long)K * T * R, "toued_gru_bwd_fused: M=%ld != K*T*R", M);
+  TOUED_REQUIRE(work_floats >= toued_gru_bwd_fused_work_floats(R, K), "toued_gru_bwd_fused: workspace %zu < %zu",
+                work_floats, toued_gru_bwd_fused_work_floats(R, K));
+  TOUED_REQUIRE(col_exp != nullptr, "toued_gru_bwd_fused: col_exp is required");
+  BwdArgs p;
+  p.R = R; p.T = T; p.W = W; p.K = K; p.done = done; p.done_stride_k = done_stride_k;
+  p.A = reinterpret_cast<const float4*>(bwdA); p.eta = eta;
+  p.A6 = bwdA + (size_t)8 * 3 * 32 * 64 * 4;
+  memcpy(&p.o, off, sizeof(EtaOff));
+  p.y_hat = y_hat; p.d_pi_hat = d_pi_hat; p.d_y_hat = d_y_hat;
+  p.s_hin = s_hin; p.s_r = s_r; p.s_z = s_z; p.s_n = nullptr; p.s_hn = s_hn; p.M = M;
+  p.DG = DG3; p.RH = nullptr; p.DH = nullptr; p.dX3 = dX3; p.dX4 = dX4; p.CE = col_exp;
+  p.F = (p.o.ir_b - p.o.in_w) / HU;
+  TOUED_REQUIRE(p.F >= 1 && p.F <= 6 && p.o.ir_b - p.o.in_w == p.F * HU, "toued_gru_bwd_fused: LPG layout F=%d", p.F);
+  const int n_wg = K * (R / (2 * RB)), n_chunk = (n_wg + SR_CHUNK - 1) / SR_CHUNK;
+  p.SP = work;
+  float* part2 = work + (size_t)n_wg * SP_FLOATS;
+  hipLaunchKernelGGL(k_gru_bwd6n<true>, dim3(n_wg), dim3(512), 0, stream, p);
+  hipLaunchKernelGGL(k_small_part, dim3((SP_FLOATS + 255) / 256, n_chunk), dim3(256), 0, stream, work, n_wg, part2);
+  hipLaunchKernelGGL(k_small_final, dim3((8 * HU + 9 * (HU + 1) + 255) / 256), dim3(256), 0, stream, part2, n_chunk,
+                     p.F, GI);
   TOUED_CHECK_LAUNCH();
   return 0;
 }

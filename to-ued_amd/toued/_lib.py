@@ -73,6 +73,10 @@ _SIGS = {
     "toued_gru_bwd": [_I, _I, _I, _I, _P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _P, _P, _P, _P, _P,
                       _P, _P],
     "toued_gru_bwd_col_exp": [_I],
+    "toued_gru_bwd_fused_fits": [_I, _I],
+    "toued_gru_bwd_fused_work_floats": [_I, _I],
+    "toued_gru_bwd_fused": [_I, _I, _I, _I, _P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _P, _P, _P, _P, _P,
+                            _P, ctypes.c_size_t, _P],
     "toued_set_reserved_cus": [_I],
     "toued_wgrad_bfp_workspace_floats": [_I, _I, _L],
     "toued_wgrad_bfp": [_I, _I, _L, _P, _L, _I, _P, _L, _P, _P, _P, ctypes.c_size_t, _P],
@@ -110,7 +114,8 @@ _SIGS = {
 _RESTYPES = {"toued_last_error": ctypes.c_char_p, "toued_mode_program_bytes": ctypes.c_size_t,
              "toued_gru_packed_floats": ctypes.c_size_t, "toued_wgrad_workspace_floats": ctypes.c_size_t,
              "toued_gru_bwd_small_work_floats": ctypes.c_size_t, "toued_wgrad_bfp_workspace_floats": ctypes.c_size_t,
-             "toued_rowsum_workspace_floats": ctypes.c_size_t}
+             "toued_rowsum_workspace_floats": ctypes.c_size_t,
+             "toued_gru_bwd_fused_work_floats": ctypes.c_size_t}
 
 _lib = None
 

@@ -141,7 +141,7 @@ class LPGGRU:
     operand layout of the weight-gradient GEMMs.
     """
 
-    def __init__(self, lay: LPGLayout, R: int, T: int, K: int, W: int, device):
+    def __init__(self, lay: LPGLayout, R: int, T: int, K: int, W: int, device, fused: bool | None = None):
         self.lay, self.R, self.T, self.K, self.W = lay, R, T, K, W
         self.M = K * T * R
         L = _lib.lib()
@@ -156,11 +156,21 @@ class LPGGRU:
         self.A = torch.zeros((H + 8, M), dtype=f32, device=dev)
         self.A[H + lay.F].fill_(1.0)
         self.X = self.A[H:H + lay.F].view(lay.F, K, T, R)
-        self.S = torch.empty((4, H, M), dtype=f32, device=dev)          # r, z, n, hn
-        self.DG = torch.empty((4, H, M), dtype=f32, device=dev)         # dr_pre, dz_pre, d(hn), dn_pre
-        self.RH = torch.zeros((H + 1, M), dtype=f32, device=dev)        # relu(h_out) + ones row
-        self.RH[H].fill_(1.0)
-        self.DH = torch.empty((9, M), dtype=f32, device=dev)            # head cotangents
+        self.S = torch.empty((4, H, M), dtype=f32, device=dev)          # r, z, n (f32 fallback only), hn
+        # the small weight-gradient products fused into the backward (toued_gru_bwd_fused) where the lockstep kernel
+        # runs and F <= 6: then dn_pre, relu(h_out) and the head cotangents never reach HBM (TOUED_BWD_FUSED=0: the
+        # unfused kernel + toued_gru_bwd_small)
+        fits = bool(L.toued_gru_bwd_fused_fits(R, lay.F))
+        self.fused = (fits and os.environ.get("TOUED_BWD_FUSED", "1") != "0") if fused is None else (fused and fits)
+        # dr_pre, dz_pre, d(hn) (+ dn_pre when unfused)
+        self.DG = torch.empty((3 if self.fused else 4, H, M), dtype=f32, device=dev)
+        if self.fused:
+            self.RH = self.DH = None
+        else:
+            self.RH = torch.zeros((H + 1, M), dtype=f32, device=dev)    # relu(h_out) + ones row
+            self.RH[H].fill_(1.0)
+            self.DH = torch.empty((9, M), dtype=f32, device=dev)        # head cotangents
+        self._last_bwd = None
         self.dX3 = torch.empty((K, T, R), dtype=f32, device=dev)
         self.dX4 = torch.empty((K, T, R), dtype=f32, device=dev)
         # weight-gradient reductions (csrc/wgrad.hip): outputs and the per-K-chunk partial-sum workspace
@@ -178,7 +188,7 @@ class LPGGRU:
         self.CE = torch.empty(M if self.bfp else 0, dtype=torch.int8, device=dev)
         need = max(int(L.toued_wgrad_workspace_floats(H + lay.F + 1, 3 * H, M)),
                    int(L.toued_wgrad_bfp_workspace_floats(H + lay.F + 1, 3 * H, M)),
-                   int(L.toued_gru_bwd_small_work_floats(M)))
+                   int(L.toued_gru_bwd_fused_work_floats(R, K)) if self.fused else int(L.toued_gru_bwd_small_work_floats(M)))
         self.wg_work = torch.empty(max(need, 1), dtype=f32, device=dev)
 
     def _scatter_indices(self, dev):
@@ -220,6 +230,27 @@ class LPGGRU:
                   _lib.ptr(S) + 4 * (3 * H * M + col), M, _lib.stream_ptr())
         del Xk
 
+    def relu_out(self) -> torch.Tensor:
+        """relu(h_out) [256][M] of the last backward (tests: the relu decisions the backward took).  On the fused path
+        the backward keeps it on chip, so the unfused kernel recomputes it from the same saves into scratch buffers
+        (the same gate maths, so the same decisions)."""
+        if not self.fused:
+            return self.RH[:H]
+        done_all, eta, y_hat, d_pi_hat, d_y_hat = self._last_bwd
+        M, dev, f32 = self.M, self.A.device, torch.float32
+        DG4 = torch.empty((4, H, M), dtype=f32, device=dev)
+        RH = torch.empty((H, M), dtype=f32, device=dev)
+        DH = torch.empty((9, M), dtype=f32, device=dev)
+        dX = torch.empty((2, M), dtype=f32, device=dev)
+        CE = torch.empty(M, dtype=torch.int8, device=dev)
+        S = self.S
+        _lib.call("toued_gru_bwd", self.R, self.T, self.W, self.K, _lib.ptr(done_all), done_all[0].numel(),
+                  _lib.ptr(self.bwdA), _lib.ptr(eta), self.lay.c_offsets, _lib.ptr(y_hat), _lib.ptr(d_pi_hat),
+                  _lib.ptr(d_y_hat), _lib.ptr(self.A), _lib.ptr(S[0]), _lib.ptr(S[1]), _lib.ptr(S[2]), _lib.ptr(S[3]),
+                  M, _lib.ptr(DG4), _lib.ptr(RH), _lib.ptr(DH), _lib.ptr(dX[0]), _lib.ptr(dX[1]), _lib.ptr(CE),
+                  _lib.stream_ptr())
+        return RH
+
     def backward(self, done_all: torch.Tensor, eta: torch.Tensor, y_hat: torch.Tensor, d_pi_hat: torch.Tensor,
                  d_y_hat: torch.Tensor, X: torch.Tensor, grad: torch.Tensor, timers=None, after_bwd=None,
                  before_main_wgrad=None):
@@ -230,12 +261,22 @@ class LPGGRU:
         R, T, K, M = self.R, self.T, self.K, self.M
         S = self.S
         stride_k = done_all[0].numel()
+        ws, wn = _lib.ptr(self.wg_work), self.wg_work.numel()
+        self._last_bwd = (done_all, eta, y_hat, d_pi_hat, d_y_hat)
         tok = timers.start("gru_bwd") if timers is not None else None
-        _lib.call("toued_gru_bwd", R, T, self.W, K, _lib.ptr(done_all), stride_k, _lib.ptr(self.bwdA), _lib.ptr(eta),
-                  self.lay.c_offsets, _lib.ptr(y_hat), _lib.ptr(d_pi_hat), _lib.ptr(d_y_hat),
-                  _lib.ptr(self.A), _lib.ptr(S[0]), _lib.ptr(S[1]), _lib.ptr(S[2]), _lib.ptr(S[3]), M,
-                  _lib.ptr(self.DG), _lib.ptr(self.RH), _lib.ptr(self.DH), _lib.ptr(self.dX3), _lib.ptr(self.dX4),
-                  _lib.ptr(self.CE) if self.bfp else None, _lib.stream_ptr())
+        if self.fused:
+            # the recurrent backward with GI (both small products) reduced from its per-workgroup partials
+            _lib.call("toued_gru_bwd_fused", R, T, self.W, K, _lib.ptr(done_all), stride_k, _lib.ptr(self.bwdA),
+                      _lib.ptr(eta), self.lay.c_offsets, _lib.ptr(y_hat), _lib.ptr(d_pi_hat), _lib.ptr(d_y_hat),
+                      _lib.ptr(self.A), _lib.ptr(S[0]), _lib.ptr(S[1]), _lib.ptr(S[3]), M, _lib.ptr(self.DG),
+                      _lib.ptr(self.dX3), _lib.ptr(self.dX4), _lib.ptr(self.CE), _lib.ptr(self.GI), ws, wn,
+                      _lib.stream_ptr())
+        else:
+            _lib.call("toued_gru_bwd", R, T, self.W, K, _lib.ptr(done_all), stride_k, _lib.ptr(self.bwdA),
+                      _lib.ptr(eta), self.lay.c_offsets, _lib.ptr(y_hat), _lib.ptr(d_pi_hat), _lib.ptr(d_y_hat),
+                      _lib.ptr(self.A), _lib.ptr(S[0]), _lib.ptr(S[1]), _lib.ptr(S[2]), _lib.ptr(S[3]), M,
+                      _lib.ptr(self.DG), _lib.ptr(self.RH), _lib.ptr(self.DH), _lib.ptr(self.dX3), _lib.ptr(self.dX4),
+                      _lib.ptr(self.CE) if self.bfp else None, _lib.stream_ptr())
         if timers is not None:
             timers.stop(tok)
         if after_bwd is not None:
@@ -249,10 +290,10 @@ class LPGGRU:
         #   [h_in; X; 1] (262 x M) . [dr; dz; dhn]^T  -> dW_h (rows 0..255), dW_ir/dW_iz (X rows), biases (ones row)
         #   GI: [X; 1] . dn^T -> dW_in, b_in;   DH . [relu(h_out); 1]^T -> head kernels and biases
         G = self.G
-        ws, wn = _lib.ptr(self.wg_work), self.wg_work.numel()
         st = _lib.stream_ptr()
-        _lib.call("toued_gru_bwd_small", M, _lib.ptr(self.A), _lib.ptr(DG), _lib.ptr(self.RH), _lib.ptr(self.DH),
-                  _lib.ptr(self.GI), ws, wn, st)
+        if not self.fused:
+            _lib.call("toued_gru_bwd_small", M, _lib.ptr(self.A), _lib.ptr(DG), _lib.ptr(self.RH), _lib.ptr(self.DH),
+                      _lib.ptr(self.GI), ws, wn, st)
         if before_main_wgrad is not None:
             before_main_wgrad()
         tok_main = timers.start("wgrad_main") if timers is not None else None

@@ -68,12 +68,19 @@ def main():
         o = gru
 
         def bwd():
+            if o.fused:   # the recurrent backward with both small weight-gradient products (and their reduction)
+                L.call("toued_gru_bwd_fused", R, T, W, K, L.ptr(done), done[0].numel(), L.ptr(o.bwdA), L.ptr(eta),
+                       lay.c_offsets, L.ptr(y_hat), L.ptr(d_pi), L.ptr(d_y), L.ptr(o.A), L.ptr(o.S[0]),
+                       L.ptr(o.S[1]), L.ptr(o.S[3]), o.M, L.ptr(o.DG), L.ptr(o.dX3), L.ptr(o.dX4), L.ptr(o.CE),
+                       L.ptr(o.GI), L.ptr(o.wg_work), o.wg_work.numel(), L.stream_ptr())
+                return
             L.call("toued_gru_bwd", R, T, W, K, L.ptr(done), done[0].numel(), L.ptr(o.bwdA), L.ptr(eta),
                    lay.c_offsets, L.ptr(y_hat), L.ptr(d_pi), L.ptr(d_y), L.ptr(o.A), L.ptr(o.S[0]), L.ptr(o.S[1]),
                    L.ptr(o.S[2]), L.ptr(o.S[3]), o.M, L.ptr(o.DG), L.ptr(o.RH), L.ptr(o.DH), L.ptr(o.dX3),
                    L.ptr(o.dX4), L.ptr(o.CE) if o.bfp else None, L.stream_ptr())
         ms = timed(bwd)
         res["gru_bwd_ms"] = round(ms, 3)
+        res["gru_bwd_fused_small"] = bool(o.fused)
         res["gru_bwd_tflops"] = round(K * R * T * 393216 / (ms * 1e-3) / 1e12, 1)
     print(json.dumps(res), flush=True)
 

@@ -33,7 +33,7 @@ N, W, T, K, F = a.N, 64, 6, 2, 5
 R = N * W
 M = K * T * R
 lay = LPGLayout(F)
-gru = LPGGRU(lay, R, T, K, W, "cuda")
+gru = LPGGRU(lay, R, T, K, W, "cuda", fused=False)   # DG[3] and RH are read below
 eta0 = init_lpg_params(5, F)
 
 
