@@ -242,6 +242,14 @@ int toued_embed_bwd(int N, int W, int T, int D, int K, const float* phi_hist, lo
 int toued_adam(int P, float* eta, const float* grad, float* m, float* v, float n_mean, float lr, double b1, double b2,
                float eps, int count, hipStream_t stream);
 
+/* util/metrics.py:17-38 gae(value, reward, done, discount, gae_lambda) for N x W workers at once: value
+ * [N][T+1][W], reward [N][T][W] f32, done [N][T][W] u8 -> advantages adv and value targets target [N][T][W];
+ * gamma_lambda = f32(discount * gae_lambda) as the reference's python-float product.  Bit-exact with the f32
+ * restatement (the reference's operation order, no contraction).  The meta-gradient and A2C kernels run the same
+ * scan fused on their staged trajectories (k_eval_loss, k_a2c_update). */
+int toued_gae(int N, int W, int T, const float* value, const float* reward, const uint8_t* done, float gamma,
+              float gamma_lambda, float* adv, float* target, hipStream_t stream);
+
 /* ---- LPG reverse-time GRU on MFMA (models/lpg.py:11-35, flax GRUCell) ---- */
 size_t toued_gru_packed_floats(int which);
 /* repack eta's GRU weights into MFMA A-fragment order (fwdA / bwdA) */

@@ -243,3 +243,23 @@ def adam_update(eta, grad, m, v, count, lr=1e-4, b1=0.9, b2=0.999, eps=1e-8):
     vh = v / (1 - b2 ** count)
     upd = mh / (np.sqrt(vh) + eps)
     return eta - lr * upd, m, v, count
+
+
+def gae_f32(value, reward, done, discount, gae_lambda):
+    """util/metrics.py:17-38 in numpy float32 with the reference's operation order, per element (bit-exact target of
+    toued_gae): value [..., T+1], reward/done [..., T].  discount * gae_lambda is a python-float product (weak-typed
+    constants: f32 of the double product); (1 - done) is exactly 0 or 1."""
+    f = np.float32
+    value = np.asarray(value, f)
+    reward = np.asarray(reward, f)
+    nd = (1 - np.asarray(done).astype(np.int32)).astype(f)
+    g_d, gl = f(discount), f(float(discount) * float(gae_lambda))
+    T = reward.shape[-1]
+    adv = np.zeros(reward.shape, f)
+    g = np.zeros(reward.shape[:-1], f)
+    for t in reversed(range(T)):
+        value_diff = (g_d * value[..., t + 1]).astype(f) * nd[..., t] - value[..., t]
+        delta = reward[..., t] + value_diff
+        g = (delta + (gl * nd[..., t]).astype(f) * g).astype(f)
+        adv[..., t] = g
+    return adv, (adv + value[..., :-1]).astype(f)

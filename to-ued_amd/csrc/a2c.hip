@@ -689,7 +689,46 @@ static size_t a2c_update_lds(int W, int T) {
   return (A2CStage::floats(W, T) + A2C_SORT_MAX + (size_t)W * T * A2C_NV) * sizeof(float);
 }
 
+// util/metrics.py:17-38 gae() over n = N * W independent workers: one lane per worker runs the reverse scan over T
+// (the recurrence carries one float; T = 20 dependent FMAs per lane), reading value [N][T+1][W], reward and done
+// [N][T][W] and writing adv / target [N][T][W] -- each (t, agent) row of W workers is one coalesced 4 W-byte access
+// per wave.  The reference's operation order, in f32 with no contraction: value_diff = (gamma v[t+1]) (1 - d) - v[t];
+// delta = r + value_diff; gae = delta + ((gamma lambda) (1 - d)) gae; target = gae + v[t].  17 B per (worker, t).
+__global__ void __launch_bounds__(256) k_gae(int n, int W, int T, const float* __restrict__ value,
+                                              const float* __restrict__ reward, const uint8_t* __restrict__ done,
+                                              float gamma, float gl, float* __restrict__ adv,
+                                              float* __restrict__ target) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int a = i / W, w = i - a * W;
+  const long vb = (long)a * (T + 1) * W + w, sb = (long)a * T * W + w;
+  float vn = __builtin_nontemporal_load(value + vb + (long)T * W);
+  float g = 0.0f;
+#pragma unroll 4
+  for (int t = T - 1; t >= 0; --t) {
+    const float v = __builtin_nontemporal_load(value + vb + (long)t * W);
+    const float nd = __builtin_nontemporal_load(done + sb + (long)t * W) ? 0.0f : 1.0f;
+    const float r = __builtin_nontemporal_load(reward + sb + (long)t * W);
+    const float delta = r + (gamma * vn * nd - v);
+    g = delta + gl * nd * g;
+    __builtin_nontemporal_store(g, adv + sb + (long)t * W);
+    __builtin_nontemporal_store(g + v, target + sb + (long)t * W);
+    vn = v;
+  }
+}
+
 extern "C" {
+
+int toued_gae(int N, int W, int T, const float* value, const float* reward, const uint8_t* done, float gamma,
+              float gamma_lambda, float* adv, float* target, hipStream_t stream) {
+  TOUED_REQUIRE(N >= 0 && W >= 1 && T >= 1 && (long)N * W < (1L << 31), "toued_gae: N=%d W=%d T=%d", N, W, T);
+  const int n = N * W;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_gae, dim3((n + 255) / 256), dim3(256), 0, stream, n, W, T, value, reward, done, gamma,
+                     gamma_lambda, adv, target);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
 
 #ifdef A2C_STAMPS
 int toued_dbg_a2c_stamps(unsigned long long* host) {
