@@ -65,14 +65,15 @@ ROLLOUT_BYTES_PER_STEP = 34
 
 
 def train_rollout_roof():
-    """(label, algorithmic bytes per agent-env-step) of the train rollout as it runs: the split path (key chain
-    u32x4 written + read, draws u32x4 written + read, 20-B chosen actor row, 14 B of trajectory) or the fused
-    single kernel (20-B row + 14 B)."""
+    """(label, algorithmic bytes per agent-env-step, implementation scratch bytes per agent-env-step) of the train
+    rollout as it runs.  The algorithmic figure is SURVEY §8(d)'s 34 B (14 written, the 20-B actor row read) for
+    either path; the split path (draws kernel + env chain) also moves its key chain and draws through HBM (u32x4
+    written and read back each: 64 B), which is implementation traffic, reported beside it, not counted as work."""
     from toued.rollout import split_rollouts
     if split_rollouts():
         return "toued_rollout_draws + toued_rollout_env (train rollout: threefry draws VALU-bound, env chain " \
-               "latency-bound)", 16 * 4 + 20 + 14
-    return "k_rollout (train, fused)", ROLLOUT_BYTES_PER_STEP
+               "latency-bound)", ROLLOUT_BYTES_PER_STEP, 16 * 4
+    return "k_rollout (train, fused)", ROLLOUT_BYTES_PER_STEP, 0
 
 
 # device kernel behind each timed region, as rocprofv3 names it (prof_summary.short)
@@ -470,9 +471,11 @@ def workload_c4(a, cpu: bool):
           "unit": "TFLOP/s (16-bit issued)", "frac": round(t_mfma / (g_ms * 1e-3), 4), "mean_ms": round(g_ms, 4),
           "flop_per_launch_f32": flop, "f32_equiv_tflops": round(flop / (g_ms * 1e-3) / 1e12, 1)}
     roll_ms = ks["rollout"][1]
-    rl, rb = train_rollout_roof()
+    rl, rb, rs_ = train_rollout_roof()
     rollout_rf = _hbm_roofline(rl + " of the candidates", R * T * rb, roll_ms,
                                "bound by its dependent chains (threefry draws, then the env steps), not by bytes")
+    rollout_rf["traffic_model"] = R * T * (rb + rs_)
+    rollout_rf["traffic_note"] = "algorithmic 34 B + the draws path's key-chain / draws scratch (64 B) per step"
     steps = C * U * W * T
     out = {"workload": f"C4 TA-LPG OpenES env_mode=all_vrandlife lifetime_conditioning num_agents={N} candidates={C} "
                        f"W={W} T={T} updates per candidate U={U}",
@@ -529,6 +532,67 @@ def c4_cpu_baseline(args, sampler, target_s: float = 12.0):
                       f"update) of ONE candidate's first {n} of {sampler.max_lifetime} updates (W={W}, T={T}), "
                       f"env_mode={mode}; {dt:.1f} s; a full ES step is 1024 such candidates x "
                       f"{sampler.max_lifetime} updates (extrapolated: {1024 * sampler.max_lifetime * W * T / (n * W * T / dt):.0f} s)"}
+
+
+def _event_ms(fn, n):
+    """Mean duration (ms) of fn's launches on the current stream, bracketed by HIP events on that stream."""
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / n
+
+
+def micro_gae(n_rows: int = 16384, W: int = 64, T: int = 20):
+    """GAE (util/metrics.py:17-38, toued_gae) at the regret round's scale: 32 updates' trajectories of 512 agents
+    (16384 x 64 workers x 20 steps = 21 M elements).  SURVEY §8(d): 17 B per element (reward 4 + done 1 + value 4
+    read, adv 4 + target 4 written) against 8 TB/s; the value row T (one per worker) is added to the bytes."""
+    from toued import _lib
+    g = torch.Generator(device="cuda").manual_seed(0)
+    v = torch.randn(n_rows, T + 1, W, device="cuda", generator=g)
+    r = torch.randn(n_rows, T, W, device="cuda", generator=g)
+    d = (torch.rand(n_rows, T, W, device="cuda", generator=g) < 0.05).to(torch.uint8)
+    adv, tgt = torch.empty_like(r), torch.empty_like(r)
+    gl = float(torch.tensor(0.99 * 0.95, dtype=torch.float32))
+
+    def run():
+        _lib.call("toued_gae", n_rows, W, T, _lib.ptr(v), _lib.ptr(r), _lib.ptr(d), 0.99, gl, _lib.ptr(adv),
+                  _lib.ptr(tgt), _lib.stream_ptr())
+    ms = _event_ms(run, 20)
+    elems = n_rows * W * T
+    out = _hbm_roofline("k_gae (toued_gae, one lane per worker, reverse scan over T)", elems * 17 + n_rows * W * 4, ms,
+                        traffic_kernel="k_gae")
+    out["elements"] = elems
+    out["elements_per_sec"] = round(elems / (ms * 1e-3), 1)
+    return out
+
+
+def micro_plr(B: int = 4000, N: int = 512, reps: int = 50):
+    """The PLR sampler's latency per call at the reference's buffer size (µs per call, not a
+    roofline fraction): toued_plr_reset_ids (_reset_lowest_scoring's stable argsort, level_sampler.py:331-353) and
+    toued_plr_sample (rank replay + random-new + selection, :203-227, :355-408) on a random buffer, HIP events."""
+    from toued import _lib
+    g = torch.Generator(device="cuda").manual_seed(1)
+    score = torch.rand(B, device="cuda", generator=g)
+    active = (torch.rand(B, device="cuda", generator=g) < 0.6).to(torch.uint8)
+    new = (torch.rand(B, device="cuda", generator=g) < 0.3).to(torch.uint8)
+    ids = torch.empty(N, dtype=torch.int32, device="cuda")
+    keys = torch.randint(0, 2 ** 31 - 1, (3, 2), dtype=torch.int32, device="cuda", generator=g)
+    chosen, rep, rnd, use = (torch.empty(N, dtype=torch.int32, device="cuda") for _ in range(4))
+    st = _lib.stream_ptr()
+    t_reset = _event_ms(lambda: _lib.call("toued_plr_reset_ids", B, N, _lib.ptr(score), _lib.ptr(active),
+                                          _lib.ptr(new), _lib.ptr(ids), st), reps)
+    out = {"buffer_size": B, "num_agents": N, "reset_ids_us": round(t_reset * 1e3, 2)}
+    for name, prop in (("sample_rank_us", 0), ("sample_proportional_us", 1)):
+        t = _event_ms(lambda: _lib.call("toued_plr_sample", B, N, _lib.ptr(score), _lib.ptr(active), _lib.ptr(new),
+                                        _lib.ptr(keys), prop, 1.0, 0.5, _lib.ptr(chosen), _lib.ptr(rep),
+                                        _lib.ptr(rnd), _lib.ptr(use), st), reps)
+        out[name] = round(t * 1e3, 2)
+    out["note"] = "latency-bound single-workgroup kernels (LDS bitonic sort of 8192 keys); µs per call"
+    return out
 
 
 def main():
@@ -621,11 +685,14 @@ def main():
     if "rollout" in ksum:
         rsec = ksum["rollout"][1] * 1e-3
         rsteps = R * T
-        rl, rb = train_rollout_roof()
+        rl, rb, rs_ = train_rollout_roof()
         secondary["rollout"] = {"bound": "dependent chains (threefry, env steps); hbm by bytes", "kernel": rl,
                                 "achieved": round(rsteps * rb / rsec / 1e9, 1),
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                 "frac": round(rsteps * rb / rsec / 1e9 / HBM_PEAK_GBS, 4),
+                                "bytes_per_launch": rsteps * rb, "traffic_model": rsteps * (rb + rs_),
+                                "traffic_note": "algorithmic 34 B + the draws path's key-chain / draws scratch (64 B) "
+                                                "per agent-env-step",
                                 "agent_env_steps_per_sec": round(rsteps / rsec, 1), "mean_ms": round(rsec * 1e3, 4)}
     out = {
         "metric": "agent-env-steps/sec (inner rollout) at num_agents=512; meta-updates/sec",
@@ -651,6 +718,8 @@ def main():
             out["cpu_baseline"] = cpu_baseline(a.env_mode, a.lifetime_conditioning, a.cpu_agents)
         else:
             out["cpu_baseline"] = None
+    if n_gpus == 1:
+        out["micro"] = {"gae": micro_gae(), "plr_sampler": micro_plr()}
     wl = [w for w in a.workloads.split(",") if w and w != "none"]
     if wl and n_gpus == 1:
         del tr, step
