@@ -60,6 +60,10 @@ GRU_BWD_FUSED_BYTES_PER_ELEM = {F: 4 * (4 * 256 + F + 3 * 256 + 17 + 2) + 1 for 
 # FLOP 2 * rows * 768 per column, issued as 3 fp16 products (block-floating-point pairs); algorithmic bytes = both
 # operands once (the A rows are re-read by 4 column tiles through L2)
 WGRAD_PRODUCTS = 3.0
+# the forward's packed fragments per (candidate, step): 16 carry k-steps x 8 unit tiles x 3 gates x 2 fp16 pieces +
+# 8 unit tiles x 4 gates x 3 bf16 pieces of the augmented k-step, 1 KiB each (csrc/gru.hip F6_NFH + F6_NFA)
+FWD6_FRAG_BYTES_PER_STEP = (16 * 8 * 3 * 2 + 8 * 4 * 3) * 1024
+IC_RANDOM_ROWS_GBS = 8600.0        # MI355X_MICROARCH.md: uniformly random rows served by the Infinity Cache
 # train rollout: 34 B per agent-env-step (14 written: idx, time, action, reward, done; 20 read: the actor row)
 ROLLOUT_BYTES_PER_STEP = 34
 
@@ -466,10 +470,20 @@ def workload_c4(a, cpu: bool):
     flop = R * T * GRU_FWD_FLOP_PER_ELEM[F]
     g_ms = ks["gru_fwd_multi"][1]
     t_mfma = SPLIT_PRODUCTS["gru_fwd"] * flop / (MFMA_BF16_PEAK_TFLOPS * 1e12)
-    rf = {"bound": "mfma", "kernel": "k_gru_fwd6<false> (per-candidate LPG GRU forward)",
-          "achieved": round(SPLIT_PRODUCTS["gru_fwd"] * flop / (g_ms * 1e-3) / 1e12, 1), "peak": MFMA_BF16_PEAK_TFLOPS,
-          "unit": "TFLOP/s (16-bit issued)", "frac": round(t_mfma / (g_ms * 1e-3), 4), "mean_ms": round(g_ms, 4),
-          "flop_per_launch_f32": flop, "f32_equiv_tflops": round(flop / (g_ms * 1e-3) / 1e12, 1)}
+    # what binds it: every (candidate, step) streams the candidate's whole packed W_h / W_i fragment set (no other
+    # workgroup shares it, and 256 resident candidates x 840 KB do not fit the L2s) from the Infinity Cache, against
+    # MI355X_MICROARCH.md's 8.6 TB/s (33.5 GB/s per CU) for uniformly random rows served by the Infinity Cache;
+    # MFMA (the f32-accurate split's 16-bit products) is the secondary roof
+    frag_bytes = C * T * FWD6_FRAG_BYTES_PER_STEP
+    sec = g_ms * 1e-3
+    rf = {"bound": "infinity-cache", "kernel": "k_gru_fwd6<false> (per-candidate LPG GRU forward)",
+          "achieved": round(frag_bytes / sec / 1e9, 1), "peak": IC_RANDOM_ROWS_GBS, "unit": "GB/s",
+          "frac": round(frag_bytes / sec / 1e9 / IC_RANDOM_ROWS_GBS, 4), "bytes_per_launch": frag_bytes,
+          "mean_ms": round(g_ms, 4),
+          "mfma_secondary": {"achieved": round(SPLIT_PRODUCTS["gru_fwd"] * flop / sec / 1e12, 1),
+                             "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s (16-bit issued)",
+                             "frac": round(t_mfma / sec, 4)},
+          "flop_per_launch_f32": flop, "f32_equiv_tflops": round(flop / sec / 1e12, 1)}
     roll_ms = ks["rollout"][1]
     rl, rb, rs_ = train_rollout_roof()
     rollout_rf = _hbm_roofline(rl + " of the candidates", R * T * rb, roll_ms,
