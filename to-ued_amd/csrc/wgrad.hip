@@ -393,17 +393,23 @@ __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict
   // workgroup the dispatcher could not place at launch (a CU of its shader engine held by the eval chain beside this
   // kernel) starts after the first ones finish, finds the queues empty and leaves -- instead of a tile of its own
   // in a second round (6.9 vs 4.0 ms with a fixed blockIdx -> tile map; tools/h3_place.py).
+  // The ranges hold whole K chunks (all ncol column tiles of a chunk on one XCD, so its A slabs come through one L2
+  // only; ranges cut inside a chunk had two XCDs fetch that chunk's A); a workgroup stealing from another XCD takes
+  // that XCD's slots from the back, so a chunk is split between two XCDs at most at the end of a range.
   __shared__ int s_slot;
   if (threadIdx.x == 0) {
     const int x = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;   // HW_REG_XCC_ID
-    const int per = ntiles >> 3, rem = ntiles & 7;
+    const int nch = ntiles / ncol, per = nch >> 3, rem = nch & 7;
     int got = -1;
     for (int y = 0; y < 8 && got < 0; ++y) {
       const int q = (x + y) & 7;
-      const int cnt = per + (q < rem ? 1 : 0);
+      const int cnt = ncol * (per + (q < rem ? 1 : 0));
       if (cnt == 0) continue;
-      const int t = atomicAdd(&qctr[q], 1);
-      if (t < cnt) got = q * per + (q < rem ? q : rem) + t;
+      // one word per queue: slots claimed from the front (low 16 bits) and from the back (high 16 bits); a claim
+      // succeeds while the two together are below cnt, so every slot goes out exactly once
+      const int old = atomicAdd(&qctr[q], y == 0 ? 1 : 1 << 16);
+      const int f = old & 0xFFFF, b = old >> 16;
+      if (f + b < cnt) got = ncol * (q * per + (q < rem ? q : rem)) + (y == 0 ? f : cnt - 1 - b);
     }
     s_slot = got;
   }
