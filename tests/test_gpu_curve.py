@@ -61,6 +61,7 @@ def test_meta_return_curve_certified(seed, life0):
     args = parse_args(["--env_mode", MODE, "--num_agents", str(N), "--num_mini_batches", "1", "--seed", str(seed),
                        "--score_function", "random"])
     tr = Trainer(args)
+    tr.step_fn.gru.keep_inputs = True     # the relu decisions of every step's backward (gru.relu_out)
     spec = olv.env_spec(MODE)
     W, T, K, Y = args.env_workers, args.train_rollout_len, args.num_agent_updates, 8
     L = tr.sampler.max_rollout_len

@@ -253,6 +253,7 @@ def _gru_bwd_case(N, W, T, K, F, eta, xs, done, d_pi, d_y):
     R = N * W
     lay = LPGLayout(F)
     gru = LPGGRU(lay, R, T, K, W, "cuda")
+    gru.keep_inputs = True      # relu_out() below
     gru.pack(eta)
     gru.X.copy_(torch.from_numpy(xs))
     X = gru.X

@@ -214,8 +214,7 @@ __global__ void k_pack_bwd(const float* __restrict__ eta, EtaOff o, float4* __re
 // A[i = input unit 32 ut + (l & 31)][k = gate unit 16 ks + 8 (l >> 5) + e] = W_g[i][k], split in three bf16
 #define B6_NF (16 * 8 * 3 * 3)
 #define B6_SCALES (B6_NF * 256)            // float offset of the per-input-unit scales 2^s of W_z, W_hn [256]
-#define B6_BOUNDS (B6_SCALES + HU)         // cotangent bound constants: c, Q_0 .. Q_8 (k_bwd6_bounds)
-#define B6_FLOATS (B6_BOUNDS + 16)
+#define B6_FLOATS (B6_SCALES + HU)
 // One k-major LDS buffer ([unit][row], pitch RB*NT + 1; h^T in the forward, a gate cotangent in the
 // backward) of NT row tiles out to its row-major [unit][M] array: per instruction lane l stores row
 // RB*h + (l & 31) of unit 32*wave + 2i + (l >> 5), so every wave instruction writes 2 units x 128
@@ -566,35 +565,6 @@ __global__ void __launch_bounds__(256) k_bwd6_scales(const float* __restrict__ e
       sc = min(20, max(-30, 14 - e));
     }
     out[i] = ldexpf(1.0f, sc);
-  }
-}
-
-// Constants of the backward's per-row cotangent bound (k_gru_bwd6n, BWD_EARLY): with d_u = dh_u + relu'(h_out) hacc_u
-// the step's gate cotangents obey |dhn_u| <= |d_u|, |dz_pre_u| <= |d_u| / 2 and |dr_pre_u| <= |d_u| |hn_u| / 4 with
-// |hn_u| = |W_hn h + b_hn| <= HN_u = sum_k |W_hn[k][u]| + |b_hn[u]| (|h| < 1), and |hacc_u| <= sum_o |Wh[u][o]| |hv_o|;
-// so max_u over all three <= c max_u |dh_u| + sum_o Q_o |hv_o| with c = max(1, max_u HN_u / 4) and
-// Q_o = c max_u |Wh[u][o]| (Wh: the heads pi_w | y_w).  out[0] = c, out[1 + o] = Q_o.  One 256-thread block.
-__global__ void __launch_bounds__(256) k_bwd6_bounds(const float* __restrict__ eta, EtaOff o, float* __restrict__ out) {
-  __shared__ float red[10][4];
-  const int u = threadIdx.x, lane = u & 63, w = u >> 6;
-  float hn = fabsf(eta[o.hn_b + u]);
-  for (int k = 0; k < HU; ++k) hn += fabsf(eta[o.hn_w + k * HU + u]);
-  float v[10];
-  v[0] = hn;
-  v[1] = fabsf(eta[o.pi_w + u]);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[2 + j] = fabsf(eta[o.y_w + u * 8 + j]);
-#pragma unroll
-  for (int j = 0; j < 10; ++j) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v[j] = fmaxf(v[j], __shfl_xor(v[j], d));
-    if (lane == 0) red[j][w] = v[j];
-  }
-  __syncthreads();
-  if (u < 10) {
-    const float m = fmaxf(fmaxf(red[u][0], red[u][1]), fmaxf(red[u][2], red[u][3]));
-    const float c = fmaxf(1.0f, fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3])) * 0.25f);
-    out[u] = u == 0 ? c : c * m;
   }
 }
 
@@ -1169,13 +1139,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   __shared__ __attribute__((aligned(8))) float dxp[8 * RBT * 2];   // [wave][row][dx3 | dx4]
   __shared__ __attribute__((aligned(16))) float wsc[HU];          // 2^s of W_g row i (fp16 A scale)
   __shared__ float rmx[8 * RBT];                   // per-wave row maxima of |dr|, |dz|, |dhn| (fp16 B scale)
-#ifndef BWD_EARLY
-#define BWD_EARLY 0
-#endif
-  // BWD_EARLY: each row's image scale 2^t from the cotangent bound (k_bwd6_bounds), known when the step starts, so dr
-  // goes into the image as fp16 pieces straight from the memory part (no f32 staging, no split phase); rmx then also
-  // carries the per-wave row maxima of |dh| from the previous step's end to head_cot
-  __shared__ float bsc[BWD_EARLY ? RBT : 1];
   __shared__ float wIs[8 * 4 * 64];                // gate_ain's W_in fragments [wave][kk][lane] (read at each tile)
   __shared__ float wAs[8 * 5 * 64];                // W_heads^T A fragments [wave][kk][lane] (read at each tile)
   __shared__ int dns[RBT];                         // done flags of the step's rows (loaded with the head cotangents)
@@ -1221,8 +1184,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     for (int q = 0; q < 16; ++q) dh[h][q] = 0.0f;
   // SMALL: the running accumulators C[i][unit 32 wave + 16 uh + (l & 15)] of the wave's two 16-unit halves wait in
   // LDS between the steps ([wave][uh][lane] float4): the register file has no room for them across the step
-  if (BWD_EARLY)
-    for (int i = tid; i < 8 * RBT; i += 512) rmx[i] = 0.0f;
   if (SMALL) {
     for (int i = tid; i < 9 * RBT; i += 512) hvs[i] = 0.0f;
     for (int i = tid; i < 8 * 2 * 64; i += 512) accl[i] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -1279,23 +1240,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         hv[(j + 1) * RBT + tl] = v;
         hvv[j + 1] = v;
         if (st_DH) st_u(rs_DH, vrw, (unsigned)(((long)(j + 1) * p.M + o) * 4), v);
-      }
-      if (BWD_EARLY) {
-        const float* bnd = reinterpret_cast<const float*>(p.A6) + B6_BOUNDS;
-        float dm = 0.0f;
-#pragma unroll
-        for (int w8 = 0; w8 < 8; ++w8) dm = fmaxf(dm, rmx[w8 * RBT + tl]);
-        float b = bnd[0] * dm;
-#pragma unroll
-        for (int o9 = 0; o9 < 9; ++o9) b += bnd[1 + o9] * fabsf(hvv[o9]);
-        b *= 1.0625f;   // margin for the rounding of the bound's own sums (the fp16 range leaves 4x besides)
-        int sc = 0;
-        if (b > 0.0f && b <= 3.0e38f) {
-          int e;
-          frexpf(b, &e);
-          sc = min(40, max(-40, 14 - e));
-        }
-        bsc[tl] = ldexpf(1.0f, sc);
       }
       if (SMALL) {
         // row tl = 2 s + par: lanes 16 par + i (k = par: [x; 1; 0]) and 32 + 16 par + i (k = 2 + par: head
@@ -1418,23 +1362,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #endif
     constexpr int NR = BWD_NR;
     float vr[NR][4][4];   // NR-slot ring: quads i+1 .. i+NR-1 in flight while quad i is processed (NR = 2: 10.11 ms)
-#ifndef BWD_DWORD_LD
-#define BWD_DWORD_LD 0
-#endif
     auto load_q = [&](int h, int g4, float (&v)[4][4]) {
-      if (BWD_DWORD_LD) {
-        // per-unit dword loads, lane = row (the stores' pattern): no lane-quad transposes, 4x the load instructions
-        const unsigned vb = (unsigned)(((long)ub * p.M + r0 + RB * h + col) * 4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const unsigned so = (unsigned)(((long)qunit(4 * g4 + e) * p.M + ctr) * 4);
-          v[0][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_hin, (int)vb, (int)so, GRU_LD_AUX));
-          v[1][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_r, (int)vb, (int)so, GRU_LD_AUX));
-          v[2][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_z, (int)vb, (int)so, GRU_LD_AUX));
-          v[3][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_hn, (int)vb, (int)so, GRU_LD_AUX));
-        }
-        return;
-      }
       const unsigned vq = (unsigned)((((long)(ub + (col & 3))) * p.M + r0 + RB * h + (col & 28)) * 4);
       const unsigned so = (unsigned)(((long)8 * g4 * p.M + ctr) * 4);
       ld4(rs_hin, vq, so, v[0]);
@@ -1493,8 +1421,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         dx4 = 0.0f;
       }
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
-        if (!BWD_DWORD_LD) quad_transpose(v[a], lane);
+      for (int a = 0; a < 4; ++a) quad_transpose(v[a], lane);
       const float* wil = wi34 + ubn();
       float drq[4], rhq[4], dnq[4];
 #pragma unroll
@@ -1522,19 +1449,18 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       }
       if (st_rh) st_q(rs_rh, h, g4, rhq);
       if (st_dn) st_q(rs_dg[3], h, g4, dnq);   // dr, dz and dhn leave beside the contraction passes
-      if (SMALL) small_mfma(h, g4, dnq, rhq);
-      if (BWD_EARLY) {
-        // dr's fp16 pieces in the row's (bound-derived) frame straight into image slots 1, 2; DG from registers
-        const float bsh = bsc[rown(h)];
-        f16x4 x0, x1;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) split2h(drq[e] * bsh, x0, x1, e);
-        *reinterpret_cast<f16x4*>(&dgB[1][rown(h) * PP + ubn() + 8 * g4]) = x0;
-        *reinterpret_cast<f16x4*>(&dgB[2][rown(h) * PP + ubn() + 8 * g4]) = x1;
-        st_q(rs_dg[0], h, g4, drq);
-      } else {
-        *reinterpret_cast<float4*>(&drs[rown(h) * DRP + ubn() + 8 * g4]) = make_float4(drq[0], drq[1], drq[2], drq[3]);
+#ifndef BWD_STMEM
+#define BWD_STMEM 0
+#endif
+      if (BWD_STMEM >= 1) {   // (variant) dz and dhn to DG from the memory part instead of the refill phases
+        const float zq[4] = {dz_r[h][4 * g4], dz_r[h][4 * g4 + 1], dz_r[h][4 * g4 + 2], dz_r[h][4 * g4 + 3]};
+        const float nq[4] = {dhn_r[h][4 * g4], dhn_r[h][4 * g4 + 1], dhn_r[h][4 * g4 + 2], dhn_r[h][4 * g4 + 3]};
+        st_q(rs_dg[1], h, g4, zq);
+        st_q(rs_dg[2], h, g4, nq);
       }
+      if (BWD_STMEM >= 2) st_q(rs_dg[0], h, g4, drq);
+      if (SMALL) small_mfma(h, g4, dnq, rhq);
+      *reinterpret_cast<float4*>(&drs[rown(h) * DRP + ubn() + 8 * g4]) = make_float4(drq[0], drq[1], drq[2], drq[3]);
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) rmr[h] = fmaxf(rmr[h], fabsf(drq[jj]));
       if (g4 == 3) {
@@ -1574,7 +1500,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         sc = min(40, max(-40, 14 - e));
         ce = min(126, max(-126, 14 - e));
       }
-      bs[h] = BWD_EARLY ? bsc[rown(h)] : ldexpf(1.0f, sc);
+      bs[h] = ldexpf(1.0f, sc);
       if (p.CE && wave == 0 && lane_now() < 32) p.CE[ctr + r0 + rown(h)] = (int8_t)ce;
     }
     // a lane's four units ub + 8 g4 .. +3 of batch row `row` of gate cotangent g to DG, issued beside the
@@ -1582,7 +1508,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     auto store_dg = [&](int g, int row, int g4, const float (&v)[4]) { st_q(rs_dg[g], row >= RB, g4, v); };
     // dr -> fp16 pieces: x0 straight into slot 0, x1 held until every lane has read its staged f32 values
     // (slot 1 overlaps the staging)
-    if (!BWD_EARLY) {
+    {
       f16x4 x1h[2][4];
 #pragma unroll
       for (int h = 0; h < 2; ++h)
@@ -1595,7 +1521,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) split2h(v4[e] * bs[h], x0, x1h[h][g4], e);
           *reinterpret_cast<f16x4*>(&dgB[0][row * PP + un + 8 * g4]) = x0;
-          store_dg(0, RB * h, g4, v4);
+          if (BWD_STMEM < 2) store_dg(0, RB * h, g4, v4);
         }
       lds_barrier();
 #pragma unroll
@@ -1619,7 +1545,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         for (int e = 0; e < 4; ++e) acc[h][4 * g4 + e] = dh[h][4 * g4 + e] * (wv[e] * bs[h]);
     }
     BWD_STAMP(4);
-    contract_h(0, BWD_EARLY ? 1 : 0);
+    contract_h(0, 0);
     lds_barrier();
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -1627,7 +1553,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       for (int g4 = 0; g4 < 4; ++g4) {
         const float v4[4] = {dz_r[h][4 * g4], dz_r[h][4 * g4 + 1], dz_r[h][4 * g4 + 2], dz_r[h][4 * g4 + 3]};
         put4h(rown(h), ubn() + 8 * g4, v4, bs[h]);
-        store_dg(1, RB * h, g4, v4);
+        if (BWD_STMEM < 1) store_dg(1, RB * h, g4, v4);
       }
     lds_barrier();
     BWD_STAMP(5);
@@ -1639,7 +1565,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       for (int g4 = 0; g4 < 4; ++g4) {
         const float v4[4] = {dhn_r[h][4 * g4], dhn_r[h][4 * g4 + 1], dhn_r[h][4 * g4 + 2], dhn_r[h][4 * g4 + 3]};
         put4h(rown(h), ubn() + 8 * g4, v4, bs[h]);
-        store_dg(2, RB * h, g4, v4);
+        if (BWD_STMEM < 1) store_dg(2, RB * h, g4, v4);
       }
     lds_barrier();
     BWD_STAMP(6);
@@ -1671,17 +1597,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       const bool dn = dns[RB * h + (lane_now() & 31)] != 0;
 #pragma unroll
       for (int q = 0; q < 16; ++q) dh[h][q] = dn ? 0.0f : acc[h][q];
-    }
-    if (BWD_EARLY) {   // the carry's per-wave row maxima for the next step's bound (head_cot)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        float m = 0.0f;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) m = fmaxf(m, fabsf(dh[h][q]));
-        m = fmaxf(m, __shfl_xor(m, 32));
-        const int ln = lane_now();
-        if (ln < 32) rmx[wave * RBT + RB * h + ln] = m;
-      }
     }
     BWD_STAMP(7);
     lds_barrier();   // hv, dxp and the image are rewritten next step
@@ -1753,7 +1668,6 @@ int toued_gru_pack(const float* eta, const int* off, int F, float* fwdA, float* 
   hipLaunchKernelGGL(k_pack_bwd, dim3((n2 + 255) / 256), dim3(256), 0, stream, eta, o,
                      reinterpret_cast<float4*>(bwdA));
   hipLaunchKernelGGL(k_bwd6_scales, dim3(HU / 4), dim3(256), 0, stream, eta, o, bwdA + (size_t)n2 * 4 + B6_SCALES);
-  hipLaunchKernelGGL(k_bwd6_bounds, dim3(1), dim3(256), 0, stream, eta, o, bwdA + (size_t)n2 * 4 + B6_BOUNDS);
   hipLaunchKernelGGL(k_pack_bwd6, dim3((16 * 8 * 3 * 64 + 255) / 256), dim3(256), 0, stream, eta, o,
                      reinterpret_cast<__bf16*>(bwdA + (size_t)n2 * 4));
   TOUED_CHECK_LAUNCH();

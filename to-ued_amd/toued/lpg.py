@@ -171,6 +171,7 @@ class LPGGRU:
             self.RH[H].fill_(1.0)
             self.DH = torch.empty((9, M), dtype=f32, device=dev)        # head cotangents
         self._last_bwd = None
+        self.keep_inputs = False   # tests: keep copies of the backward's inputs for relu_out()
         self.dX3 = torch.empty((K, T, R), dtype=f32, device=dev)
         self.dX4 = torch.empty((K, T, R), dtype=f32, device=dev)
         # weight-gradient reductions (csrc/wgrad.hip): outputs and the per-K-chunk partial-sum workspace
@@ -236,6 +237,8 @@ class LPGGRU:
         (the same gate maths, so the same decisions)."""
         if not self.fused:
             return self.RH[:H]
+        if self._last_bwd is None:
+            raise RuntimeError("relu_out: set keep_inputs = True before the backward (the fused path keeps no relu rows)")
         done_all, eta, y_hat, d_pi_hat, d_y_hat = self._last_bwd
         M, dev, f32 = self.M, self.A.device, torch.float32
         DG4 = torch.empty((4, H, M), dtype=f32, device=dev)
@@ -262,7 +265,8 @@ class LPGGRU:
         S = self.S
         stride_k = done_all[0].numel()
         ws, wn = _lib.ptr(self.wg_work), self.wg_work.numel()
-        self._last_bwd = (done_all, eta, y_hat, d_pi_hat, d_y_hat)
+        if self.keep_inputs:   # relu_out() recomputes from these after the caller has moved on (Adam updates eta)
+            self._last_bwd = (done_all.clone(), eta.clone(), y_hat.clone(), d_pi_hat.clone(), d_y_hat.clone())
         tok = timers.start("gru_bwd") if timers is not None else None
         if self.fused:
             # the recurrent backward with GI (both small products) reduced from its per-workgroup partials

@@ -11,6 +11,9 @@ bash tools/gpu_steps.sh r04c \
   "v4:120:TOUED_LIB=${E}BWD_EARLY_1.so $B && TOUED_LIB=${E}BWD_EARLY_1.so $B" \
   "v5:120:TOUED_LIB=${E}BWD_EARLY_1_BWD_DWORD_LD_1.so $B && TOUED_LIB=${E}BWD_EARLY_1_BWD_DWORD_LD_1.so $B" \
   "v6:120:TOUED_LIB=${E}BWD_EARLY_1_BWD_DWORD_LD_1_BWD_NR_4.so $B && TOUED_LIB=${E}BWD_EARLY_1_BWD_DWORD_LD_1_BWD_NR_4.so $B" \
+  "f0:120:python tools/bench_gru.py --which fwd && python tools/bench_gru.py --which fwd" \
+  "f1:120:TOUED_LIB=${E}FWD_LAZY_1.so python tools/bench_gru.py --which fwd && TOUED_LIB=${E}FWD_LAZY_1.so python tools/bench_gru.py --which fwd" \
+  "parF:300:TOUED_LIB=${E}FWD_LAZY_1.so python -u -m pytest tests/test_gpu_meta.py tests/test_gpu_es.py -x -q --timeout 120 --timeout-method thread" \
   "stamps:120:TOUED_LIB=${E}BWD_STAMPS_1.so python tools/bwd_stamps.py" \
   "stamps1:120:TOUED_LIB=${E}BWD_DWORD_LD_1_BWD_STAMPS_1.so python tools/bwd_stamps.py" \
   "stamps5:120:TOUED_LIB=${E}BWD_EARLY_1_BWD_DWORD_LD_1_BWD_STAMPS_1.so python tools/bwd_stamps.py" \
