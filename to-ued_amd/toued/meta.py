@@ -364,14 +364,15 @@ class MetaGradStep:
 
         def launch_eval():
             self.side.wait_stream(main)
-            with torch.cuda.stream(self.side):
-                (_, _), ea["state"] = self.ro.batch_reset(self.keys_ea_reset, agents.levels, hyp.eval_workers)
-                self._ea_draws = self.ro.eval_draws(self.keys_ea_roll, agents.levels, hyp.eval_workers,
-                                                    self._ea_draws)
-                # the draws kernel spreads over the whole chip for ~0.1 ms: the main weight-gradient reduction (one
-                # workgroup per CU) starts after it (ea_draws_done), or its workgroups wait behind the draws' blocks
-                ea["draws_done"] = torch.cuda.Event()
-                ea["draws_done"].record(self.side)
+            if "draws_done" not in ea:
+                with torch.cuda.stream(self.side):
+                    (_, _), ea["state"] = self.ro.batch_reset(self.keys_ea_reset, agents.levels, hyp.eval_workers)
+                    self._ea_draws = self.ro.eval_draws(self.keys_ea_roll, agents.levels, hyp.eval_workers,
+                                                        self._ea_draws)
+                    # the draws kernel spreads over the whole chip for ~0.1 ms: the main weight-gradient reduction
+                    # (one workgroup per CU) starts after it (ea_draws_done), or its workgroups wait behind its blocks
+                    ea["draws_done"] = torch.cuda.Event()
+                    ea["draws_done"].record(self.side)
             # the small products run beside the key chain, the main reduction beside the env chain
             ea["prev_reserve"] = L.lib().toued_set_reserved_cus(key_cus)
 
@@ -387,6 +388,18 @@ class MetaGradStep:
                                                             ea["state"])
             main.wait_event(ea["draws_done"])
             L.lib().toued_set_reserved_cus(eval_cus)
+        if eval_keys_early():
+            # eval_agent's worker reset, key chain and draws read only the step's keys and the levels: beside the
+            # reverse agent loop (latency-bound per-agent kernels) instead of in front of the weight-gradient
+            # reduction, which waits for the draws (with the small products fused into the backward nothing else
+            # covers them there); only the env chain on the draws waits for theta_K and the backward
+            self.side.wait_stream(main)
+            with torch.cuda.stream(self.side):
+                (_, _), ea["state"] = self.ro.batch_reset(self.keys_ea_reset, agents.levels, hyp.eval_workers)
+                self._ea_draws = self.ro.eval_draws(self.keys_ea_roll, agents.levels, hyp.eval_workers,
+                                                    self._ea_draws)
+                ea["draws_done"] = torch.cuda.Event()
+                ea["draws_done"].record(self.side)
         # ---------------- reverse: explicit adjoint w.r.t. eta
         a_in = 0
         self.adj_th[a_in].zero_()
@@ -554,6 +567,12 @@ def create_lpg_train_state(rng: torch.Tensor, args) -> LpgTrainState:
     from .lpg import flax_init_lpg_params
     eta = flax_init_lpg_params(rng, 7 if args.lifetime_conditioning else 5)
     return LpgTrainState(eta, None if args.use_es else AdamState(eta.numel(), eta.device))
+
+
+def eval_keys_early() -> bool:
+    """TOUED_EVAL_KEYS_EARLY=1: the meta-step's eval_agent key chain beside the reverse agent loop (else after the
+    backward, in front of the draws)."""
+    return os.environ.get("TOUED_EVAL_KEYS_EARLY", "0") == "1"
 
 
 def make_lpg_train_step(args, level_sampler, n_agents: int | None = None, world=None, rank_slice=None, impl=None):

@@ -13,4 +13,5 @@ bash tools/gpu_steps.sh r04d \
   "stamps1:120:TOUED_LIB=${E}BWD_STMEM_1_BWD_STAMPS_1.so python tools/bwd_stamps.py" \
   "gputest:900:python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread" \
   "smoke:200:python -c 'import __graft_entry__ as g; g.smoke()'" \
-  "bench:400:python bench.py"
+  "bench:400:python bench.py" \
+  "trace:300:bash tools/trace_step.sh r04d"
