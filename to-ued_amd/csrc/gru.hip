@@ -1449,16 +1449,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       }
       if (st_rh) st_q(rs_rh, h, g4, rhq);
       if (st_dn) st_q(rs_dg[3], h, g4, dnq);   // dr, dz and dhn leave beside the contraction passes
-#ifndef BWD_STMEM
-#define BWD_STMEM 0
-#endif
-      if (BWD_STMEM >= 1) {   // (variant) dz and dhn to DG from the memory part instead of the refill phases
-        const float zq[4] = {dz_r[h][4 * g4], dz_r[h][4 * g4 + 1], dz_r[h][4 * g4 + 2], dz_r[h][4 * g4 + 3]};
-        const float nq[4] = {dhn_r[h][4 * g4], dhn_r[h][4 * g4 + 1], dhn_r[h][4 * g4 + 2], dhn_r[h][4 * g4 + 3]};
-        st_q(rs_dg[1], h, g4, zq);
-        st_q(rs_dg[2], h, g4, nq);
-      }
-      if (BWD_STMEM >= 2) st_q(rs_dg[0], h, g4, drq);
       if (SMALL) small_mfma(h, g4, dnq, rhq);
       *reinterpret_cast<float4*>(&drs[rown(h) * DRP + ubn() + 8 * g4]) = make_float4(drq[0], drq[1], drq[2], drq[3]);
 #pragma unroll
@@ -1521,7 +1511,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) split2h(v4[e] * bs[h], x0, x1h[h][g4], e);
           *reinterpret_cast<f16x4*>(&dgB[0][row * PP + un + 8 * g4]) = x0;
-          if (BWD_STMEM < 2) store_dg(0, RB * h, g4, v4);
+          store_dg(0, RB * h, g4, v4);
         }
       lds_barrier();
 #pragma unroll
@@ -1553,7 +1543,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       for (int g4 = 0; g4 < 4; ++g4) {
         const float v4[4] = {dz_r[h][4 * g4], dz_r[h][4 * g4 + 1], dz_r[h][4 * g4 + 2], dz_r[h][4 * g4 + 3]};
         put4h(rown(h), ubn() + 8 * g4, v4, bs[h]);
-        if (BWD_STMEM < 1) store_dg(1, RB * h, g4, v4);
+        store_dg(1, RB * h, g4, v4);
       }
     lds_barrier();
     BWD_STAMP(5);
@@ -1565,7 +1555,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       for (int g4 = 0; g4 < 4; ++g4) {
         const float v4[4] = {dhn_r[h][4 * g4], dhn_r[h][4 * g4 + 1], dhn_r[h][4 * g4 + 2], dhn_r[h][4 * g4 + 3]};
         put4h(rown(h), ubn() + 8 * g4, v4, bs[h]);
-        if (BWD_STMEM < 1) store_dg(2, RB * h, g4, v4);
+        store_dg(2, RB * h, g4, v4);
       }
     lds_barrier();
     BWD_STAMP(6);
