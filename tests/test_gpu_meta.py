@@ -383,7 +383,8 @@ def test_gru_independent_of_scratch_contents(N, W, wscale):
     outs = {}
     for how in ("zero", "nan", "random", "zero"):
         gru = LPGGRU(lay, R, T, K, W, "cuda")
-        bufs = [gru.S, gru.DG, gru.dX3, gru.dX4, gru._ggi, gru.CE, gru.wg_work, gru.A[:H]]
+        # (fwdA / bwdA: the packed weights, whose unused piece slots the pack kernels leave unwritten)
+        bufs = [gru.S, gru.DG, gru.dX3, gru.dX4, gru._ggi, gru.CE, gru.wg_work, gru.A[:H], gru.fwdA, gru.bwdA]
         if not gru.fused:
             bufs += [gru.DH, gru.RH[:H]]
         for t in bufs:
