@@ -5,5 +5,8 @@ bash tools/gpu_steps.sh r04e \
   "e0:200:TOUED_EVAL_KEYS_EARLY=0 $B && TOUED_EVAL_KEYS_EARLY=0 $B" \
   "e1:200:TOUED_EVAL_KEYS_EARLY=1 $B && TOUED_EVAL_KEYS_EARLY=1 $B" \
   "e0b:200:TOUED_EVAL_KEYS_EARLY=0 $B" \
+  "n1:200:TOUED_EVAL_KEYS_EARLY=1 TOUED_LIB=to-ued_amd/exp/libtoued_H3_B_AUX_2.so $B && TOUED_EVAL_KEYS_EARLY=1 TOUED_LIB=to-ued_amd/exp/libtoued_H3_B_AUX_2.so $B" \
+  "e1b:200:TOUED_EVAL_KEYS_EARLY=1 $B" \
   "par:400:TOUED_EVAL_KEYS_EARLY=1 python -u -m pytest tests/test_gpu_meta.py tests/test_gpu_curve.py tests/test_gpu_c5.py -x -q --timeout 120 --timeout-method thread" \
-  "trace:300:TOUED_EVAL_KEYS_EARLY=1 bash tools/trace_step.sh r04e"
+  "trace:300:TOUED_EVAL_KEYS_EARLY=1 bash tools/trace_step.sh r04e" \
+  "trace2:300:TOUED_EVAL_KEYS_EARLY=1 TOUED_LIB=to-ued_amd/exp/libtoued_H3_B_AUX_2.so bash tools/trace_step.sh r04e_nt"
