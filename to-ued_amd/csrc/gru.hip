@@ -433,7 +433,12 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 #define F6_NFH (16 * 8 * 3 * 2)     // h-part fragments [ks][unit tile][gate r|z|hn][fp16 piece], 1 KiB each
 #define F6_NFA (8 * 4 * 3)          // augmented fragments [unit tile][gate r|z|hn|ni][bf16 piece]
 #define F6_SCALES ((F6_NFH + F6_NFA) * 256)   // float offset of the per-(gate, unit) weight scales 2^s [4][256]
-#define F6_FLOATS (F6_SCALES + 4 * HU)        // packed size in floats (1 KiB fragment = 256 floats)
+// f32 fragments of the augmented k-step (input weights and biases of r, z and the hn bias, scaled by 2^s):
+// [unit tile][gate r|z|hn][lane] float4 over kk = 0..3 of A[i = unit][k = 2 kk + (l >> 5)] (k < F: W_g[k][u],
+// k = 7: the bias), for the f32-MFMA input k-step (FWD_AUG32)
+#define F6_A32 (F6_SCALES + 4 * HU)
+#define F6_FLOATS (F6_A32 + 8 * 3 * 64 * 4)   // packed size in floats (1 KiB fragment = 256 floats)
+#define F6_NGRP (16 * 8 * 3 + 8 * 4 + 8 * 3)  // k_pack_fwd6's fragment groups: h part, bf16 augmented, f32 augmented
 #define HSCALE 16384.0f  // carry scale 2^14: |h| < 1 -> |2^14 h| < 2^14, inside the fp16 range
 
 template <typename V>
@@ -507,7 +512,7 @@ __global__ void k_pack_fwd6(const float* __restrict__ eta, EtaOff o, int F, bf16
   out += (long)blockIdx.y * out_stride16;
   const float* scl = reinterpret_cast<const float*>(out) + F6_SCALES;
   const int ngrp_h = 16 * 8 * 3, ngrp = ngrp_h + 8 * 4;
-  if (gid >= ngrp * 64) return;
+  if (gid >= F6_NGRP * 64) return;
   const int lane = gid & 63, grp = gid >> 6;
   if (grp < ngrp_h) {
     const int g = grp % 3, ut = (grp / 3) % 8, ks = grp / 24;
@@ -522,6 +527,25 @@ __global__ void k_pack_fwd6(const float* __restrict__ eta, EtaOff o, int F, bf16
     }
 #pragma unroll
     for (int q = 0; q < 2; ++q) out[(long)(grp * 2 + q) * 64 + lane] = __builtin_bit_cast(bf16x8, pc[q]);
+  } else if (grp >= ngrp) {
+    // the f32 augmented fragments (FWD_AUG32)
+    const int ga = grp - ngrp, g = ga % 3, ut = ga / 3;
+    const int u = 32 * ut + (lane & 31);
+    const float sg = scl[g * HU + u];
+    float v[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int k = 2 * kk + (lane >> 5);
+      float x = 0.0f;
+      if (k < F) {
+        if (g == 0) x = eta[o.ir_w + k * HU + u];
+        else if (g == 1) x = eta[o.iz_w + k * HU + u];
+      } else if (k == 7) {
+        x = g == 0 ? eta[o.ir_b + u] : g == 1 ? eta[o.iz_b + u] : eta[o.hn_b + u];
+      }
+      v[kk] = x * sg;   // a power of two: exact
+    }
+    reinterpret_cast<float4*>(out)[F6_A32 / 4 + (ut * 3 + g) * 64 + lane] = make_float4(v[0], v[1], v[2], v[3]);
   } else {
     const int ga = grp - ngrp_h, g = ga % 4, ut = ga / 4;
     const int u = 32 * ut + (lane & 31);
@@ -623,8 +647,12 @@ __device__ unsigned long long g_fwd_stamps[64 * 32 * 6];
 #define FWD_STAMP(ph) do {} while (0)
 #endif
 
+#ifndef FWD_AUG32
+#define FWD_AUG32 0
+#endif
 template <bool SAVE>
 __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
+  constexpr bool A32 = FWD_AUG32 && !SAVE;   // the per-candidate (ES) instance: f32-MFMA augmented k-step
   // carry image [row][unit]: slots 0, 1 the fp16 pieces of 2^14 h (MFMA B operand), slot 2 the bf16 residual
   __shared__ __attribute__((aligned(16))) __bf16 hB[3][64 * F6_HP];
   __shared__ __attribute__((aligned(16))) float wh[HU * 12];          // head weights [unit][pi | y0..y7 | pad]
@@ -751,6 +779,35 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     }
     kstep(14, A0, false);
     f16x8 (&A)[3][2] = A1;   // k-step 15
+    if (A32) {
+      // the augmented k-step on the f32 MFMA (exact products): A = the scaled input weights and biases (one 16-byte
+      // fragment per gate, 3 KB per wave-step instead of the bf16 triple's 12 KB: the ES candidates' per-step stream
+      // from the Infinity Cache is what this kernel waits on), B = 2^14 [x_k (k < F), 1 (k = 7)]
+      float4 a32[3];
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+        a32[g] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                rs_A, (int)vA, (F6_A32 + (wave * 3 + g) * 256) * 4, 0));
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) acc[g][h] = mfma3h(A[g], B[h], acc[g][h]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int k = 2 * kk + hi;
+        float bx[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) bx[h] = (k < F ? xv[h][k < 7 ? k : 6] : (k == 7 ? 1.0f : 0.0f)) * HSCALE;
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          const float av = kk == 0 ? a32[g].x : kk == 1 ? a32[g].y : kk == 2 ? a32[g].z : a32[g].w;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) acc[g][h] = mfma32(av, bx[h], acc[g][h]);
+        }
+      }
+    } else {
     // last carry k-step; each gate's augmented fragments (three bf16 pieces) load behind its MFMAs
     bf16x8 Aa[3][3], Ba[2][3];
 #pragma unroll
@@ -773,6 +830,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     for (int g = 0; g < 3; ++g) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) acc[g][h] = mfma6(Aa[g], Ba[h], acc[g][h]);
+    }
     }
     FWD_STAMP(1);
     lds_barrier();   // every wave done reading hB / xB: the carry and x(t-1) overwrite them in place
@@ -1649,7 +1707,7 @@ int toued_gru_pack(const float* eta, const int* off, int F, float* fwdA, float* 
   TOUED_REQUIRE(F >= 1 && F <= 7, "toued_gru_pack: F=%d", F);
   EtaOff o;
   memcpy(&o, off, sizeof(EtaOff));
-  const int n1 = NTILE_F * KQF * 64, n2 = 8 * 3 * 32 * 64, n3 = (16 * 8 * 3 + 8 * 4) * 64;
+  const int n1 = NTILE_F * KQF * 64, n2 = 8 * 3 * 32 * 64, n3 = F6_NGRP * 64;
   hipLaunchKernelGGL(k_pack_fwd, dim3((n1 + 255) / 256), dim3(256), 0, stream, eta, o, F,
                      reinterpret_cast<float4*>(fwdA), 0L, 0L);
   hipLaunchKernelGGL(k_fwd6_scales, dim3(16), dim3(256), 0, stream, eta, o, fwdA + (size_t)n1 * 4 + F6_SCALES, 0L, 0L);
@@ -1734,7 +1792,7 @@ int toued_gru_pack_fwd_multi(const float* eta, long eta_stride, int n, const int
   const long cstride = (long)toued_gru_packed_floats(2);   // floats per candidate
   hipLaunchKernelGGL(k_pack_fwd, dim3((n1 + 255) / 256, n), dim3(256), 0, stream, eta, o, F,
                      reinterpret_cast<float4*>(fwdA), eta_stride, cstride / 4);
-  const int n3 = (16 * 8 * 3 + 8 * 4) * 64;
+  const int n3 = F6_NGRP * 64;
   hipLaunchKernelGGL(k_fwd6_scales, dim3(16, n), dim3(256), 0, stream, eta, o, fwdA + (size_t)n1 * 4 + F6_SCALES,
                      eta_stride, cstride);
   hipLaunchKernelGGL(k_pack_fwd6, dim3((n3 + 255) / 256, n), dim3(256), 0, stream, eta, o, F,
