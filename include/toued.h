@@ -175,6 +175,10 @@ int toued_a2c_chain(EnvSpec spec, const int* levels, int N, int W, int T, int D,
 int toued_value_critic_update(int N, int W, int T, int D, float* vcrit, const int* tidx, const int* ttime,
                               const float* trew, const uint8_t* tdone, float gamma, float lam, float lr,
                               float max_norm, int* vstep, float* loss_out, hipStream_t stream);
+/* The register bitonic sort behind every sorted-segment kernel (no reference counterpart: it stands for XLA's
+ * deterministic scatter-add in a2c.py's gradient), exposed for its parity test: each of nblocks blocks sorts its 2048
+ * keys ascending with `threads` (256 or 512) threads; keys and out [nblocks][2048] may not alias. */
+int toued_sort_keys2048(const uint32_t* keys, uint32_t* out, int nblocks, int threads, hipStream_t stream);
 /* apply_gradients (clip_by_global_norm + SGD, models/optim.py:5-11) for actor and value critic,
  * kept only while step+1 <= levels[i].lifetime (a2c.py:71-75); zeroes Ga/Gv. */
 int toued_a2c_apply(int N, int D, float* theta, float* vcrit, float* Ga, float* Gv, float lr_a, float lr_c,

@@ -717,6 +717,17 @@ __global__ void __launch_bounds__(256) k_gae(int n, int W, int T, const float* _
   }
 }
 
+// The (row, sample) sort of the sorted-segment kernels on its own, for its parity test: block b sorts keys[b][2048]
+// with NT threads (256: the A2C kernels, 512: agent.hip's k_rows_sorted)
+template <int NT>
+__global__ void __launch_bounds__(NT) k_sort_keys2048(const uint32_t* __restrict__ keys, uint32_t* __restrict__ out) {
+  __shared__ uint32_t key[2048];
+  const size_t b = (size_t)blockIdx.x * 2048;
+  for (int i = threadIdx.x; i < 2048; i += NT) key[i] = keys[b + i];
+  sort2048_reg<NT>(key, threadIdx.x);
+  for (int i = threadIdx.x; i < 2048; i += NT) out[b + i] = key[i];
+}
+
 extern "C" {
 
 int toued_gae(int N, int W, int T, const float* value, const float* reward, const uint8_t* done, float gamma,
@@ -726,6 +737,19 @@ int toued_gae(int N, int W, int T, const float* value, const float* reward, cons
   if (n == 0) return 0;
   hipLaunchKernelGGL(k_gae, dim3((n + 255) / 256), dim3(256), 0, stream, n, W, T, value, reward, done, gamma,
                      gamma_lambda, adv, target);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_sort_keys2048(const uint32_t* keys, uint32_t* out, int nblocks, int threads, hipStream_t stream) {
+  TOUED_REQUIRE(nblocks >= 0 && (threads == 256 || threads == 512), "toued_sort_keys2048: nblocks=%d threads=%d",
+                nblocks, threads);
+  if (nblocks == 0) return 0;
+  TOUED_REQUIRE(keys && out, "toued_sort_keys2048: null buffer");
+  if (threads == 256)
+    hipLaunchKernelGGL(k_sort_keys2048<256>, dim3(nblocks), dim3(256), 0, stream, keys, out);
+  else
+    hipLaunchKernelGGL(k_sort_keys2048<512>, dim3(nblocks), dim3(512), 0, stream, keys, out);
   TOUED_CHECK_LAUNCH();
   return 0;
 }

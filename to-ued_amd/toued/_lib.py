@@ -74,6 +74,7 @@ _SIGS = {
                       _P, _P],
     "toued_gru_bwd_col_exp": [_I],
     "toued_gae": [_I, _I, _I, _P, _P, _P, _F, _F, _P, _P, _P],
+    "toued_sort_keys2048": [_P, _P, _I, _I, _P],
     "toued_gru_bwd_fused_fits": [_I, _I],
     "toued_gru_bwd_fused_work_floats": [_I, _I],
     "toued_gru_bwd_fused": [_I, _I, _I, _I, _P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _P, _P, _P, _P, _P,
