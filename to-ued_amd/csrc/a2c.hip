@@ -86,6 +86,28 @@ struct A2CStage {
   }
 };
 
+// S.vt[j] = V(obs j) + c_j V[D-1] for the NO staged observations, from S.ix / S.cc: each thread's up to VB gathers are
+// issued before the first is waited on (one memory round trip per update instead of one per loop trip).  Ends without
+// a barrier; the caller syncs.
+TOUED_DEV void gather_values(const A2CStage& S, const float* __restrict__ v, int D, int NO) {
+  constexpr int VB = 8;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const float vlast = v[D - 1];
+  for (int j0 = tid; j0 < NO; j0 += VB * nt) {
+    float g[VB];
+#pragma unroll
+    for (int q = 0; q < VB; ++q) {
+      const int j = j0 + q * nt;
+      g[q] = j < NO ? v[S.ix[j]] : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < VB; ++q) {
+      const int j = j0 + q * nt;
+      if (j < NO) S.vt[j] = g[q] + S.cc[j] * vlast;
+    }
+  }
+}
+
 // Latency structure: the agent's whole trajectory (obs rows and times, actions, rewards, dones) is staged into LDS
 // with coalesced loads, V(obs) gathered for every observation at once, and only then the per-worker GAE scans run
 // out of LDS -- a handful of dependent memory round trips per update instead of two per time step.  Ends with a
@@ -671,10 +693,7 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
     }
     if (u == U - 1) A2C_STAMP(7);
     __syncthreads();
-    {   // V(obs) for every observation (a2c_load's gather)
-      const float vlast = v[D - 1];
-      for (int j = tid; j < (T + 1) * W; j += blockDim.x) S.vt[j] = v[S.ix[j]] + S.cc[j] * vlast;
-    }
+    gather_values(S, v, D, (T + 1) * W);   // V(obs) for every observation (a2c_load's gather)
     __syncthreads();
     const float closs = a2c_gae(S, W, T, gamma, lam, sh.red);
     if (u == U - 1) A2C_STAMP(1);
