@@ -662,8 +662,14 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
   const int w = spread ? (tid >> 6) * (W / 4) + (tid & 63) : tid;
   const bool env = spread ? (tid & 63) < W / 4 : tid < W;
   const int i = a * W + w;
-  TrainWorker<NMAX, CAND> wk;
+  TrainWorker<NMAX, CAND, !CAND> wk;
   if (env) wk.init(sp, levels, a, theta, D, state, n, i);
+  if constexpr (!CAND) {   // the level's transition table after the update's LDS (toued_a2c_chain sizes it)
+    uint16_t* npt = reinterpret_cast<uint16_t*>(vec + (size_t)W * T * A2C_NV);
+    if (env) wk.build_npt(npt, w, W);
+    wk.npt = npt;
+    __syncthreads();
+  }
   for (int u = 0; u < U; ++u) {
     if (tid == 0) sh.has_last = 0;
     if (u == U - 1) A2C_STAMP(0);
@@ -847,10 +853,11 @@ int toued_a2c_chain(EnvSpec sp, const int* levels, int N, int W, int T, int D, i
   TOUED_REQUIRE((double)N * D * 20.0 < 4294967295.0, "toued_a2c_chain: actor tables (%d x %d rows) exceed 4 GiB", N, D);
   TOUED_REQUIRE(dstride >= (long)U * N * W, "toued_a2c_chain: draw stride %ld < %ld", dstride, (long)U * N * W);
   if (N == 0 || U == 0) return 0;
-  const size_t lds = a2c_update_lds(W, T);
   // the env chain's row gathers: the chosen row after the choice (default: 68k vs 94k cycles per 20-step chain,
   // profiles/r03/a2c_stamps_rows.log) or the five candidate rows ahead of it (TOUED_TRAIN_ROWS=cand; bit-identical)
   static const bool cand = getenv("TOUED_TRAIN_ROWS") && strcmp(getenv("TOUED_TRAIN_ROWS"), "cand") == 0;
+  // + the transition table of the default (non-candidate) worker: G2 x 5 u16
+  const size_t lds = a2c_update_lds(W, T) + (cand ? 0 : ((size_t)sp.max_grid * sp.max_grid * 5 * 2 + 3) / 4 * 4);
   static bool attr_set[2][6] = {};
 #define TOUED_A2C_CHAIN_LAUNCH(NM, CD)                                                                               \
   {                                                                                                                   \

@@ -139,6 +139,25 @@ TOUED_DEV float pexp(float x) {
   return nan ? x : (hi ? __builtin_inff() : (lo ? 0.0f : r));
 }
 
+// pexp on a softmax argument x - max (x <= 0, -inf or NaN): the same value as pexp(x) for every such x, with the
+// overflow test and the exponent clamps dropped -- for k = rint(x log2 e) in [-150, 0] (x >= -103.97) the +-200 and
+// [-126, 127] clamps are the identity and floor(k / 2) is k >> 1; below -103.97 the result is selected to 0 whatever
+// the core computed (k is floored at -200 first, so the conversion stays defined).  About 9 VALU fewer per call.
+TOUED_DEV float pexp_le0(float x) {
+  const float k = rintf(__fmul_rn(x, 1.44269504088896341f));
+  float r = __fsub_rn(x, __fmul_rn(k, 0.693145751953125f));
+  r = __fsub_rn(r, __fmul_rn(k, 1.428606765330187045e-06f));
+  const float C[8] = {1.0f, 1.0f, 0.5f, (float)(1.0 / 6.0), (float)(1.0 / 24.0), (float)(1.0 / 120.0),
+                      (float)(1.0 / 720.0), (float)(1.0 / 5040.0)};
+  float p = C[7];
+#pragma unroll
+  for (int i = 6; i >= 0; --i) p = __fadd_rn(__fmul_rn(p, r), C[i]);
+  const int ki = (int)fmaxf(k, -200.0f);
+  const int k1 = ki >> 1, k2 = ki - k1;
+  const float v = __fmul_rn(__fmul_rn(p, pow2i(k1)), pow2i(k2));
+  return x != x ? x : (x < -103.972084f ? 0.0f : v);
+}
+
 TOUED_DEV float plog(float x) {
   if (x != x) return x;
   if (x == 0.0f) return -__builtin_inff();

@@ -349,7 +349,7 @@ TOUED_DEV void actor_probs5(const float* __restrict__ tab, const float* last, in
   for (int j = 1; j < 5; ++j) m = fmaxf(m, l[j]);
   float e[5];
 #pragma unroll
-  for (int j = 0; j < 5; ++j) e[j] = pexp(__fsub_rn(l[j], m));
+  for (int j = 0; j < 5; ++j) e[j] = pexp_le0(__fsub_rn(l[j], m));
   float s = e[0];
 #pragma unroll
   for (int j = 1; j < 5; ++j) s = __fadd_rn(s, e[j]);
@@ -368,7 +368,7 @@ TOUED_DEV void actor_probs5_row(const float* row, const float* last, int t, floa
   for (int j = 1; j < 5; ++j) m = fmaxf(m, l[j]);
   float e[5];
 #pragma unroll
-  for (int j = 0; j < 5; ++j) e[j] = pexp(__fsub_rn(l[j], m));
+  for (int j = 0; j < 5; ++j) e[j] = pexp_le0(__fsub_rn(l[j], m));
   float s = e[0];
 #pragma unroll
   for (int j = 1; j < 5; ++j) s = __fadd_rn(s, e[j]);
@@ -411,7 +411,11 @@ typedef unsigned draw4 __attribute__((ext_vector_type(4)));
 // code path for both kernels, so their trajectories are bit-identical.  CAND = false (the default of both launchers):
 // no candidate gathers, the chosen next row is gathered after the step -- one dependent round trip per step beats
 // five 64-lane row gathers ahead of the choice here (W = 64 workers of one agent per wave; measured).
-template <int NMAX, bool CAND = true>
+//
+// NPT (the A2C chain): the move and the object test come from a per-level transition table in LDS, [G2][5] entries
+// next cell | (mask of the objects placed there) << 8, built once per launch by build_npt -- one LDS read per step
+// instead of next_pos_r's boundary tests, wall-word select and the object loop (~50 VALU); the same values.
+template <int NMAX, bool CAND = true, bool NPT = false>
 struct TrainWorker {
   LevR lev;
   EnvState s;
@@ -421,6 +425,7 @@ struct TrainWorker {
   float row[5], last[5], rrow[5];   // rrow: the auto-reset observation's row (a constant index per worker)
   __amdgpu_buffer_rsrc_t rs_t;
   unsigned tab_off;
+  const uint16_t* npt;   // NPT: the transition table (LDS)
 
   // worker i (agent a) of a batch of n workers; the state from state [S_FIELDS][n]
   TOUED_DEV void init(const EnvSpec& sp, const int* __restrict__ levels, int a, const float* __restrict__ theta, int D,
@@ -441,6 +446,19 @@ struct TrainWorker {
     for (int o = 0; o < NMAX; ++o) objpos[o] = s.obj[o] - lev_i(lev, L_OBJ_IDS + o) * G2;   // static in TAB
     idx = tab_index(sp, s);
     ridx = start + G2 * (used & ((1 << NMAX) - 1));
+  }
+
+  // NPT: entries c0, c0 + nc, ... of the transition table (all of a workgroup's workers share the level and so the
+  // static object cells objpos)
+  TOUED_DEV void build_npt(uint16_t* tbl, int c0, int nc) const {
+    for (int c = c0; c < G2 * 5; c += nc) {
+      const int p = next_pos_r(grid, wl, c / 5, c - (c / 5) * 5);
+      int m = 0;
+#pragma unroll
+      for (int o = 0; o < NMAX; ++o)
+        if (objpos[o] == p) m |= 1 << o;
+      tbl[c] = (uint16_t)(p | (m << 8));
+    }
   }
 
   // the actor rows a rollout starts from: the time row D-1, the current observation's row and the reset row
@@ -489,20 +507,27 @@ struct TrainWorker {
 #pragma unroll
           for (int j = 0; j < 5; ++j) row[j] = crow[act][j];
         }
+    } else if constexpr (NPT) {
+      const uint32_t e = npt[s.pos * 5 + action];
+      pos = (int)(e & 0xFFu);
+      collected = (int)(e >> 8) & s.exists;
     } else {
       pos = next_pos_r(grid, wl, s.pos, action);
 #pragma unroll
       for (int o = 0; o < NMAX; ++o)
         if (((s.exists >> o) & 1) && objpos[o] == pos) collected |= 1 << o;
     }
-    // step_env (gridworld.py:72-136), tabular: env_step's operation order
+    // step_env (gridworld.py:72-136), tabular: env_step's operation order.  Without a collection p_t only feeds the
+    // (false) hit test and rew stays 0, so the sums run under a branch most waves skip
     float p_t = 0.0f;
     rew = 0.0f;
+    if (collected) {
 #pragma unroll
-    for (int o = 0; o < NMAX; ++o) {
-      const float co = ((collected >> o) & 1) ? 1.0f : 0.0f;
-      p_t = __fadd_rn(p_t, __fmul_rn(lev_f(lev, L_PTERM + o), co));
-      if ((collected >> o) & 1) rew = __fadd_rn(rew, lev_f(lev, L_REW + o));
+      for (int o = 0; o < NMAX; ++o) {
+        const float co = ((collected >> o) & 1) ? 1.0f : 0.0f;
+        p_t = __fadd_rn(p_t, __fmul_rn(lev_f(lev, L_PTERM + o), co));
+        if ((collected >> o) & 1) rew = __fadd_rn(rew, lev_f(lev, L_REW + o));
+      }
     }
     const bool hit = collected != 0 && bits_to_unit(dr.y) < p_t;
     const int term = hit || s.early_term;
