@@ -182,8 +182,16 @@ TOUED_DEV float a2c_gae(const A2CStage& S, int W, int T, float gamma, float lam,
 // Sample i = t*W + w of the staged agent: actor row cotangent d[5] (policy term through the [T,T] broadcast plus
 // the entropy bonus of pi + 1e-8, a2c.py:52-63), critic row cotangent (returned), the row, the time coefficient
 // and this sample's actor-loss term.
+// The gradient maths run on the hardware transcendentals (v_exp_f32 / v_log_f32 / v_rcp_f32 without the library's
+// denormal range scaling: every argument here is a normal number or an exp underflow) with contraction on: about a
+// third fewer VALU per sample, within the update's float tolerance (tests/test_gpu_plr.py, 1e-4 of the float64 step);
+// the rollouts, which steer sampling, keep their exact portable maths.
+TOUED_DEV float hexp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
+TOUED_DEV float hlog(float x) { return __builtin_amdgcn_logf(x) * 0.693147180559945309f; }
+
 TOUED_DEV float a2c_sample(const A2CStage& S, int i, int W, int T, const float* thr, const float* lastA, float ent_coef,
                            float inv_n, float* d, float& c, float& al) {
+#pragma clang fp contract(fast)
   const int t = i / W, w = i - t * W;
   c = S.cc[i];
   const int act = S.act[i];
@@ -192,25 +200,25 @@ TOUED_DEV float a2c_sample(const A2CStage& S, int i, int W, int T, const float* 
   for (int j = 0; j < 5; ++j) { l[j] = thr[j] + c * lastA[j]; m = fmaxf(m, l[j]); }
   float z = 0.0f;
 #pragma unroll
-  for (int j = 0; j < 5; ++j) { p[j] = __expf(l[j] - m); z += p[j]; }
-  const float iz = 1.0f / z;
+  for (int j = 0; j < 5; ++j) { p[j] = hexp(l[j] - m); z += p[j]; }
+  const float iz = __builtin_amdgcn_rcpf(z);
   float pa = 0.0f, h = 0.0f, gl[5], pg = 0.0f;
 #pragma unroll
   for (int j = 0; j < 5; ++j) {
     p[j] *= iz;
     pa = (j == act) ? p[j] : pa;
-    const float lg = __logf(p[j] + EPSF);
+    const float lg = hlog(p[j] + EPSF);
     h -= (p[j] + EPSF) * lg;
     gl[j] = -(lg + 1.0f);
     pg += p[j] * gl[j];
   }
   const float ab = S.abar[w];
-  const float rho = pa / (pa + EPSF);
+  const float rho = pa * __builtin_amdgcn_rcpf(pa + EPSF);
   const float kap = -ab * inv_n;
   const float ke = -ent_coef * inv_n;
 #pragma unroll
   for (int j = 0; j < 5; ++j) d[j] = kap * rho * ((j == act ? 1.0f : 0.0f) - p[j]) + ke * p[j] * (gl[j] - pg);
-  al = -__logf(pa + EPSF) * ab - ent_coef * h;
+  al = -hlog(pa + EPSF) * ab - ent_coef * h;
   return -2.0f * S.dv[w * T + t] * inv_n;
 }
 
@@ -299,6 +307,8 @@ __global__ void __launch_bounds__(256) k_a2c_apply(int D, float* __restrict__ th
   const int st = step[a];
   const bool applied = (st + 1) <= levels[(size_t)a * LEVEL_WORDS + L_LIFETIME];
   const bool clip_a = !(gna < max_norm), clip_c = !(gnc < max_norm);
+  // optax's t / g_norm * max_norm as one scale per table (v_rcp_f32: within the update's float tolerance)
+  const float sc_a = max_norm * __builtin_amdgcn_rcpf(gna), sc_c = max_norm * __builtin_amdgcn_rcpf(gnc);
   float* pa = theta + (size_t)a * na;
   float* pc = vcrit + (size_t)a * D;
   for (size_t i = threadIdx.x; i < na; i += blockDim.x) {
@@ -559,6 +569,8 @@ TOUED_DEV void a2c_update_body(const A2CStage& S, uint32_t* key, float* vec, A2C
   block_sum_n<2>(nn, red);
   const float gna = sqrtf(nn[0]), gnc = sqrtf(nn[1]);
   const bool clip_a = !(gna < max_norm), clip_c = !(gnc < max_norm);
+  // optax's t / g_norm * max_norm as one scale per table (v_rcp_f32: within the update's float tolerance)
+  const float sc_a = max_norm * __builtin_amdgcn_rcpf(gna), sc_c = max_norm * __builtin_amdgcn_rcpf(gnc);
   A2C_STAMP(5);
   if (applied) {
 #pragma unroll
@@ -569,11 +581,11 @@ TOUED_DEV void a2c_update_body(const A2CStage& S, uint32_t* key, float* vec, A2C
         if (!CRITIC_ONLY) {
 #pragma unroll
           for (int j = 0; j < 5; ++j) {
-            const float gg = clip_a ? (g[j] / gna) * max_norm : g[j];
+            const float gg = clip_a ? g[j] * sc_a : g[j];
             th[r * 5 + j] = rth[e][j] + (-(lr_a * gg));
           }
         }
-        const float gg = clip_c ? (g[5] / gnc) * max_norm : g[5];
+        const float gg = clip_c ? g[5] * sc_c : g[5];
         v[r] = rv[e] + (-(lr_c * gg));
       }
     }
@@ -582,11 +594,11 @@ TOUED_DEV void a2c_update_body(const A2CStage& S, uint32_t* key, float* vec, A2C
       if (!CRITIC_ONLY) {
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
-          const float gg = clip_a ? (tot[j] / gna) * max_norm : tot[j];
+          const float gg = clip_a ? tot[j] * sc_a : tot[j];
           th[r * 5 + j] = th[r * 5 + j] + (-(lr_a * gg));
         }
       }
-      const float gg = clip_c ? (tot[5] / gnc) * max_norm : tot[5];
+      const float gg = clip_c ? tot[5] * sc_c : tot[5];
       v[r] = v[r] + (-(lr_c * gg));
     }
   }
