@@ -462,6 +462,7 @@ def test_level_sampler_alg_regret_end_to_end():
         rng = prng.split(rng, 2)[1].contiguous()
         # oracle replay of the buffer logic with the device's regret scores
         r, sub = jr.split(rng_np, 2)
+        sub_reset = sub
         ids, score, active, new = osp.reset_lowest_scoring(pre["score"].cpu().numpy(), pre["active"].cpu().numpy(),
                                                            pre["new"].cpu().numpy(), N)
         r, sub = jr.split(r, 2)
@@ -476,6 +477,10 @@ def test_level_sampler_alg_regret_end_to_end():
         new_ids = np.where(term, ch, old_ids)
         active[new_ids] = True
         assert np.array_equal(buf.levels[torch.from_numpy(ids).long().cuda(), L_BUFID].cpu().numpy(), ids)
+        # the reset levels themselves: gen(split(sub, N)) of the reset key (read on the side stream)
+        p_new, lt_new = olv.reset_env_params(jr.split(sub_reset, N), "mazes")
+        ref_new = olv.pack_levels(p_new, lt_new, olv.env_spec("mazes"), buffer_id=ids)
+        assert np.array_equal(buf.levels[torch.from_numpy(ids).long().cuda()].cpu().numpy(), ref_new), it
         assert np.array_equal(buf.score.cpu().numpy(), score), it
         assert np.array_equal(buf.active.cpu().numpy(), active), it
         assert np.array_equal(buf.new.cpu().numpy(), new), it
