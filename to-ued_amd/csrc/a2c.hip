@@ -183,21 +183,22 @@ TOUED_DEV float a2c_gae(const A2CStage& S, int W, int T, float gamma, float lam,
 // the entropy bonus of pi + 1e-8, a2c.py:52-63), critic row cotangent (returned), the row, the time coefficient
 // and this sample's actor-loss term.
 // The gradient maths run on the hardware transcendentals (v_exp_f32 / v_log_f32 / v_rcp_f32 without the library's
-// denormal range scaling: every argument here is a normal number or an exp underflow) with contraction on: about a
-// third fewer VALU per sample, within the update's float tolerance (tests/test_gpu_plr.py, 1e-4 of the float64 step);
-// the rollouts, which steer sampling, keep their exact portable maths.
+// denormal range scaling: every argument here is a normal number or an exp underflow) and explicit FMAs: about a
+// third fewer VALU per sample, within the update's float tolerance (tests/test_gpu_plr.py, 1e-4 of the float64 step).
+// The FMAs are written out, not left to contraction, which depends on the surrounding code: the chain kernel and the
+// one-update kernel inline this into different contexts and must stay bit-identical.  The rollouts, which steer
+// sampling, keep their exact portable maths.
 TOUED_DEV float hexp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
 TOUED_DEV float hlog(float x) { return __builtin_amdgcn_logf(x) * 0.693147180559945309f; }
 
 TOUED_DEV float a2c_sample(const A2CStage& S, int i, int W, int T, const float* thr, const float* lastA, float ent_coef,
                            float inv_n, float* d, float& c, float& al) {
-#pragma clang fp contract(fast)
   const int t = i / W, w = i - t * W;
   c = S.cc[i];
   const int act = S.act[i];
   float l[5], p[5], m = -__builtin_inff();
 #pragma unroll
-  for (int j = 0; j < 5; ++j) { l[j] = thr[j] + c * lastA[j]; m = fmaxf(m, l[j]); }
+  for (int j = 0; j < 5; ++j) { l[j] = fmaf(c, lastA[j], thr[j]); m = fmaxf(m, l[j]); }
   float z = 0.0f;
 #pragma unroll
   for (int j = 0; j < 5; ++j) { p[j] = hexp(l[j] - m); z += p[j]; }
@@ -208,17 +209,17 @@ TOUED_DEV float a2c_sample(const A2CStage& S, int i, int W, int T, const float* 
     p[j] *= iz;
     pa = (j == act) ? p[j] : pa;
     const float lg = hlog(p[j] + EPSF);
-    h -= (p[j] + EPSF) * lg;
+    h = fmaf(-(p[j] + EPSF), lg, h);
     gl[j] = -(lg + 1.0f);
-    pg += p[j] * gl[j];
+    pg = fmaf(p[j], gl[j], pg);
   }
   const float ab = S.abar[w];
   const float rho = pa * __builtin_amdgcn_rcpf(pa + EPSF);
-  const float kap = -ab * inv_n;
+  const float kr = -ab * inv_n * rho;
   const float ke = -ent_coef * inv_n;
 #pragma unroll
-  for (int j = 0; j < 5; ++j) d[j] = kap * rho * ((j == act ? 1.0f : 0.0f) - p[j]) + ke * p[j] * (gl[j] - pg);
-  al = -hlog(pa + EPSF) * ab - ent_coef * h;
+  for (int j = 0; j < 5; ++j) d[j] = fmaf(kr, (j == act ? 1.0f : 0.0f) - p[j], ke * p[j] * (gl[j] - pg));
+  al = fmaf(-hlog(pa + EPSF), ab, -ent_coef * h);
   return -2.0f * S.dv[w * T + t] * inv_n;
 }
 
@@ -674,9 +675,13 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
   const int w = spread ? (tid >> 6) * (W / 4) + (tid & 63) : tid;
   const bool env = spread ? (tid & 63) < W / 4 : tid < W;
   const int i = a * W + w;
-  TrainWorker<NMAX, CAND, !CAND> wk;
+#ifndef A2C_NPT
+#define A2C_NPT 1
+#endif
+  constexpr bool NPT = A2C_NPT && !CAND;   // the level's transition table in LDS (TrainWorker)
+  TrainWorker<NMAX, CAND, NPT> wk;
   if (env) wk.init(sp, levels, a, theta, D, state, n, i);
-  if constexpr (!CAND) {   // the level's transition table after the update's LDS (toued_a2c_chain sizes it)
+  if constexpr (NPT) {   // the level's transition table after the update's LDS (toued_a2c_chain sizes it)
     uint16_t* npt = reinterpret_cast<uint16_t*>(vec + (size_t)W * T * A2C_NV);
     if (env) wk.build_npt(npt, w, W);
     wk.npt = npt;

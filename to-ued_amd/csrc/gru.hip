@@ -648,7 +648,7 @@ __device__ unsigned long long g_fwd_stamps[64 * 32 * 6];
 #endif
 
 #ifndef FWD_AUG32
-#define FWD_AUG32 0
+#define FWD_AUG32 1
 #endif
 template <bool SAVE>
 __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {

@@ -3,10 +3,6 @@
 #pragma once
 #include "common.h"
 
-#ifndef SORT_MED3
-#define SORT_MED3 1
-#endif
-
 namespace {
 
 // DPP moves for patterns whose every source lane is valid (quad permutes, row rotates and mirrors): the old value
@@ -68,7 +64,6 @@ TOUED_DEV float wsum_dpp(float v) {
 // the stages with j >= WB exchange whole blocks through LDS between waves.  Every element keeps min or max of itself
 // and its partner i ^ j: min when (i & j == 0) == ascending, ascending = (i & k == 0).  The keep-min/keep-max choice
 // is a per-lane mask (0 / ~0u) and the exchange one umed3 per element.
-#if SORT_MED3
 template <int NT, int K, int J>
 TOUED_DEV void bitonic_stage(uint32_t (&x)[2048 / NT], uint32_t* key, int lane, int wv) {
   constexpr int KPL = 2048 / NT, WB = 64 * KPL, NQ = KPL / 4;
@@ -112,57 +107,6 @@ TOUED_DEV void bitonic_stage(uint32_t (&x)[2048 / NT], uint32_t* key, int lane, 
     __syncthreads();   // every partner read before the next stage's writes
   }
 }
-#else
-// round-3 form (min, max, select), kept for the timing A/B of SORT_MED3=0
-template <int NT, int K, int J>
-TOUED_DEV void bitonic_stage(uint32_t (&x)[2048 / NT], uint32_t* key, int lane, int wv) {
-  constexpr int KPL = 2048 / NT, WB = 64 * KPL, NQ = KPL / 4;
-  if constexpr (J < KPL) {
-#pragma unroll
-    for (int r = 0; r < KPL; ++r) {
-      if ((r & J) == 0) {
-        const int i = WB * wv + KPL * lane + r;
-        const bool asc = (i & K) == 0;
-        const uint32_t a = x[r], b = x[r | J];
-        const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
-        x[r] = asc ? lo : hi;
-        x[r | J] = asc ? hi : lo;
-      }
-    }
-  } else if constexpr (J < WB) {
-    const bool lowpos = (lane & (J / KPL)) == 0;
-#pragma unroll
-    for (int r = 0; r < KPL; ++r) {
-      const int i = WB * wv + KPL * lane + r;
-      const bool asc = (i & K) == 0;
-      const uint32_t p = lane_xor<J / KPL>(x[r], lane);
-      const uint32_t lo = x[r] < p ? x[r] : p, hi = x[r] < p ? p : x[r];
-      x[r] = lowpos == asc ? lo : hi;
-    }
-  } else {
-    uint4* kv = reinterpret_cast<uint4*>(key);
-    const int me = (WB * wv + KPL * lane) / 4, pa = (WB * (wv ^ (J / WB)) + KPL * lane) / 4;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) kv[me + q] = make_uint4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
-    __syncthreads();
-    uint32_t p[KPL];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const uint4 v = kv[pa + q];
-      p[4 * q] = v.x; p[4 * q + 1] = v.y; p[4 * q + 2] = v.z; p[4 * q + 3] = v.w;
-    }
-    const bool lowpos = (wv & (J / WB)) == 0;
-#pragma unroll
-    for (int r = 0; r < KPL; ++r) {
-      const int i = WB * wv + KPL * lane + r;
-      const bool asc = (i & K) == 0;
-      const uint32_t lo = x[r] < p[r] ? x[r] : p[r], hi = x[r] < p[r] ? p[r] : x[r];
-      x[r] = lowpos == asc ? lo : hi;
-    }
-    __syncthreads();
-  }
-}
-#endif
 
 template <int NT, int K, int J>
 TOUED_DEV void bitonic_merge(uint32_t (&x)[2048 / NT], uint32_t* key, int lane, int wv) {

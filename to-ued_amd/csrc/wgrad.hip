@@ -373,11 +373,6 @@ __device__ unsigned int g_h3_launch;
 
 // NW waves per workgroup, BT B tiles of 16 rows per wave: <4, 3> one wave per SIMD (acc 17 x 3, 512-register
 // budget), <8, 2> two waves per SIMD (acc 17 x 2 in 256 registers) so that one wave's waits are the other's issue.
-// cache policy of the B (cotangent) stream: 0 default; 2 = nt (streamed once: keeps the L2 for the A slabs and the
-// eval rollout's table gathers beside the kernel)
-#ifndef H3_B_AUX
-#define H3_B_AUX 0
-#endif
 template <int NW, int BT>
 __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict__ A, long lda, int ra,
                                                         int a_unit_rows, const int* __restrict__ rowmax_bits,
@@ -511,7 +506,7 @@ __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict
     for (int t = 0; t < BT; ++t)
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
-        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsB[t], (int)boff[t], 128 * s + 64 * hf, H3_B_AUX);
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsB[t], (int)boff[t], 128 * s + 64 * hf, 0);
         bq[t][hf] = make_float4(__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w));
       }
   };

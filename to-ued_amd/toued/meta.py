@@ -570,9 +570,10 @@ def create_lpg_train_state(rng: torch.Tensor, args) -> LpgTrainState:
 
 
 def eval_keys_early() -> bool:
-    """TOUED_EVAL_KEYS_EARLY=1: the meta-step's eval_agent key chain beside the reverse agent loop (else after the
-    backward, in front of the draws)."""
-    return os.environ.get("TOUED_EVAL_KEYS_EARLY", "0") == "1"
+    """The meta-step's eval_agent reset, key chain and draws beside the reverse agent loop (default; C2 20.07-20.09 ms
+    against 20.36-20.44 with them after the backward, where the weight-gradient reduction waited ~0.8 ms for them:
+    profiles/r04/c2_eval_keys_early_r04f.txt).  TOUED_EVAL_KEYS_EARLY=0: after the backward."""
+    return os.environ.get("TOUED_EVAL_KEYS_EARLY", "1") == "1"
 
 
 def make_lpg_train_step(args, level_sampler, n_agents: int | None = None, world=None, rank_slice=None, impl=None):
