@@ -60,9 +60,10 @@ GRU_BWD_FUSED_BYTES_PER_ELEM = {F: 4 * (4 * 256 + F + 3 * 256 + 17 + 2) + 1 for 
 # FLOP 2 * rows * 768 per column, issued as 3 fp16 products (block-floating-point pairs); algorithmic bytes = both
 # operands once (the A rows are re-read by 4 column tiles through L2)
 WGRAD_PRODUCTS = 3.0
-# the forward's packed fragments per (candidate, step): 16 carry k-steps x 8 unit tiles x 3 gates x 2 fp16 pieces +
-# 8 unit tiles x 4 gates x 3 bf16 pieces of the augmented k-step, 1 KiB each (csrc/gru.hip F6_NFH + F6_NFA)
-FWD6_FRAG_BYTES_PER_STEP = (16 * 8 * 3 * 2 + 8 * 4 * 3) * 1024
+# the forward's packed fragments a candidate's workgroup reads per step: 16 carry k-steps x 8 unit tiles x 3 gates x
+# 2 fp16 pieces + the augmented k-step's 8 unit tiles x 3 gates of 16-byte f32 fragments (FWD_AUG32, the default
+# since round 4), 1 KiB each (csrc/gru.hip F6_NFH, F6_A32); the bf16-triple form read 8 x 4 x 3 KiB instead
+FWD6_FRAG_BYTES_PER_STEP = (16 * 8 * 3 * 2 + 8 * 3) * 1024
 IC_RANDOM_ROWS_GBS = 8600.0        # MI355X_MICROARCH.md: uniformly random rows served by the Infinity Cache
 # train rollout: 34 B per agent-env-step (14 written: idx, time, action, reward, done; 20 read: the actor row)
 ROLLOUT_BYTES_PER_STEP = 34
