@@ -21,6 +21,17 @@
 
 #define EPSF 1e-8f
 
+#ifdef A2C_STAMPS_FINE
+// finer stamps inside the V gather + GAE phase (tools/a2c_stamps.py --fine): every update overwrites them
+__device__ unsigned long long g_a2c_fine[512 * 8];
+#define A2C_FINE(ph)                                                                                   \
+  do {                                                                                                 \
+    if (blockIdx.x < 512 && threadIdx.x == 0) g_a2c_fine[blockIdx.x * 8 + (ph)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define A2C_FINE(ph) do {} while (0)
+#endif
+
 namespace {
 
 TOUED_DEV float wave_sum(float v) { return wsum_dpp(v); }
@@ -158,9 +169,11 @@ TOUED_DEV float a2c_gae(const A2CStage& S, int W, int T, float gamma, float lam,
     }
     s_cl += cl / (float)T;
   }
+  A2C_FINE(2);
   const float n = (float)(W * T);
   float ms[2] = {s_adv, s_cl};
   block_sum_n<2>(ms, red);
+  A2C_FINE(3);
   const float mean = ms[0] / n;
   const float closs = ms[1] / (float)W;
   float s_var = 0.0f;
@@ -169,6 +182,7 @@ TOUED_DEV float a2c_gae(const A2CStage& S, int W, int T, float gamma, float lam,
     s_var += d * d;
   }
   const float inv_sd = 1.0f / (sqrtf(block_sum(s_var, red) / n) + EPSF);
+  A2C_FINE(4);
   for (int w = tid; w < W; w += blockDim.x) {
     float ab = 0.0f;
 #pragma unroll 4
@@ -716,9 +730,12 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
     }
     if (u == U - 1) A2C_STAMP(7);
     __syncthreads();
+    A2C_FINE(0);
     gather_values(S, v, D, (T + 1) * W);   // V(obs) for every observation (a2c_load's gather)
     __syncthreads();
+    A2C_FINE(1);
     const float closs = a2c_gae(S, W, T, gamma, lam, sh.red);
+    A2C_FINE(5);
     if (u == U - 1) A2C_STAMP(1);
     a2c_update_body<false>(S, key, vec, sh, closs, a, W, T, D, theta, vcrit, ent_coef, lr_a, lr_c, max_norm, step,
                            levels, loss_out);
@@ -796,6 +813,11 @@ int toued_sort_keys2048(const uint32_t* keys, uint32_t* out, int nblocks, int th
   return 0;
 }
 
+#ifdef A2C_STAMPS_FINE
+int toued_dbg_a2c_fine(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_a2c_fine), sizeof(g_a2c_fine)) == hipSuccess ? 0 : 1;
+}
+#endif
 #ifdef A2C_STAMPS
 int toued_dbg_a2c_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_a2c_stamps), sizeof(g_a2c_stamps)) == hipSuccess ? 0 : 1;

@@ -547,7 +547,15 @@ struct TrainWorker {
       s.exists = (s.exists | (int)dr.z) & ~collected & used;
       s.early_term = term;
       idx = tab_index(sp, s);   // == the candidate row's index: row already holds it
+#ifdef A2C_NOGATHER
+      // timing only (tools/a2c_stamps.py on an A2C_NOGATHER variant): the env chain without its row gathers
+      if (!CAND) {
+#pragma unroll
+        for (int j = 0; j < 5; ++j) row[j] = rrow[j];
+      }
+#else
       if (!CAND) load_row5(rs_t, tab_off + (unsigned)idx * 20u, row);
+#endif
     }
   }
 };

@@ -49,6 +49,18 @@ def main():
         res[n] = float((st[:, i + 2] - st[:, i + 1]).mean())
     res["update total"] = float((st[:, 6] - st[:, 0]).mean())
     print(json.dumps({k: round(v) for k, v in res.items()}), flush=True)
+    if hasattr(_lib.lib(), "toued_dbg_a2c_fine"):   # an A2C_STAMPS_FINE variant: inside the V gather + GAE phase
+        fb = np.zeros(512 * 8, np.uint64)
+        ff = _lib.lib().toued_dbg_a2c_fine
+        ff.argtypes = [ctypes.c_void_p]
+        assert ff(fb.ctypes.data) == 0
+        f = fb.reshape(512, 8).astype(np.int64)
+        names = ["barrier after the env chain", "V gather + barrier", "per-worker GAE scan", "mean / critic-loss sums",
+                 "variance sum", "abar + barrier"]
+        fine = {"env end -> F0": float((f[:, 0] - st[:, 7]).mean())}
+        for i, n in enumerate(names[1:]):
+            fine[n] = float((f[:, i + 1] - f[:, i]).mean())
+        print(json.dumps({"fine": {k: round(v) for k, v in fine.items()}}), flush=True)
 
 
 if __name__ == "__main__":
