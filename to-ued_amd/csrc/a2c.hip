@@ -97,28 +97,6 @@ struct A2CStage {
   }
 };
 
-// S.vt[j] = V(obs j) + c_j V[D-1] for the NO staged observations, from S.ix / S.cc: each thread's up to VB gathers are
-// issued before the first is waited on (one memory round trip per update instead of one per loop trip).  Ends without
-// a barrier; the caller syncs.
-TOUED_DEV void gather_values(const A2CStage& S, const float* __restrict__ v, int D, int NO) {
-  constexpr int VB = 8;
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const float vlast = v[D - 1];
-  for (int j0 = tid; j0 < NO; j0 += VB * nt) {
-    float g[VB];
-#pragma unroll
-    for (int q = 0; q < VB; ++q) {
-      const int j = j0 + q * nt;
-      g[q] = j < NO ? v[S.ix[j]] : 0.0f;
-    }
-#pragma unroll
-    for (int q = 0; q < VB; ++q) {
-      const int j = j0 + q * nt;
-      if (j < NO) S.vt[j] = g[q] + S.cc[j] * vlast;
-    }
-  }
-}
-
 // Latency structure: the agent's whole trajectory (obs rows and times, actions, rewards, dones) is staged into LDS
 // with coalesced loads, V(obs) gathered for every observation at once, and only then the per-worker GAE scans run
 // out of LDS -- a handful of dependent memory round trips per update instead of two per time step.  Ends with a
@@ -147,26 +125,36 @@ TOUED_DEV void a2c_load(const A2CStage& S, int a, int W, int T, int D, const flo
 
 // GAE on the staged trajectory.  Returns the critic loss mean((target - V)^2) (a2c.py:29-37); fills adv/dv/abar
 // (a2c.py:43 normalisation, the [T,T] broadcast's mean_t factor).  Ends with a barrier.
+// one worker's reverse GAE scan over the staged trajectory; the restrict-qualified views let the unrolled loop issue
+// a chunk's LDS loads ahead of the previous steps' adv / dv stores (with plain pointers into the one LDS stage each
+// step waited a load round trip: 4.0 k cycles per 20-step scan, profiles/r04/a2c_stamps_fine_r04h.log)
+TOUED_DEV void gae_scan(const float* __restrict__ vt, const float* __restrict__ nd, const float* __restrict__ rw,
+                        float* __restrict__ adv, float* __restrict__ dv, int W, int T, int w, float gamma, float lam,
+                        float& s_adv, float& cl) {
+  float vn = vt[T * W + w];
+  float g = 0.0f;
+#pragma unroll 10
+  for (int t = T - 1; t >= 0; --t) {
+    const float vv = vt[t * W + w];
+    const float ndt = nd[t * W + w];
+    const float delta = rw[t * W + w] + (gamma * vn * ndt - vv);
+    g = delta + gamma * lam * ndt * g;
+    const float e = (g + vv) - vv;
+    adv[w * T + t] = g;
+    dv[w * T + t] = e;
+    cl += e * e;
+    s_adv += g;
+    vn = vv;
+  }
+}
+
 TOUED_DEV float a2c_gae(const A2CStage& S, int W, int T, float gamma, float lam, float* red) {
   const int tid = threadIdx.x;
   // per-worker GAE (reverse scan over T, util/metrics.py:17-38)
   float s_adv = 0.0f, s_cl = 0.0f;
   for (int w = tid; w < W; w += blockDim.x) {
-    float vn = S.vt[T * W + w];
-    float g = 0.0f, cl = 0.0f;
-#pragma unroll 4
-    for (int t = T - 1; t >= 0; --t) {
-      const float vv = S.vt[t * W + w];
-      const float ndt = S.nd[t * W + w];
-      const float delta = S.rw[t * W + w] + (gamma * vn * ndt - vv);
-      g = delta + gamma * lam * ndt * g;
-      const float e = (g + vv) - vv;
-      S.adv[w * T + t] = g;
-      S.dv[w * T + t] = e;
-      cl += e * e;
-      s_adv += g;
-      vn = vv;
-    }
+    float cl = 0.0f;
+    gae_scan(S.vt, S.nd, S.rw, S.adv, S.dv, W, T, w, gamma, lam, s_adv, cl);
     s_cl += cl / (float)T;
   }
   A2C_FINE(2);
@@ -706,6 +694,10 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
     if (u == U - 1) A2C_STAMP(0);
     if (env) {
       wk.load_rows(tab, D);
+      // V(obs) of every observation loaded as the chain reaches it (issued behind the step's row gather, stored one
+      // step later, so its latency hides under the chain's): no separate gather phase and barrier after it
+      const float vlast = v[D - 1];
+      float vcur = v[wk.idx];
       const draw4* dr = reinterpret_cast<const draw4*>(draws) + (size_t)u * n + i;
       draw4 dr0 = {0u, 0u, 0u, 0u};
       if (T > 0) dr0 = dr[0];
@@ -719,20 +711,24 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
         float rew;
         bool done;
         wk.step(sp, tab, d, oi, ot, action, rew, done);
+        const float vnext = v[wk.idx];
+        const float c = (float)ot * 0.001f;
         S.ix[t * W + w] = oi;
-        S.cc[t * W + w] = (float)ot * 0.001f;
+        S.cc[t * W + w] = c;
+        S.vt[t * W + w] = vcur + c * vlast;   // a2c_load's expression
         S.act[t * W + w] = (uint8_t)action;
         S.rw[t * W + w] = rew;
         S.nd[t * W + w] = done ? 0.0f : 1.0f;
+        vcur = vnext;
       }
+      const float c = (float)wk.s.time * 0.001f;
       S.ix[T * W + w] = wk.idx;
-      S.cc[T * W + w] = (float)wk.s.time * 0.001f;
+      S.cc[T * W + w] = c;
+      S.vt[T * W + w] = vcur + c * vlast;
     }
     if (u == U - 1) A2C_STAMP(7);
     __syncthreads();
     A2C_FINE(0);
-    gather_values(S, v, D, (T + 1) * W);   // V(obs) for every observation (a2c_load's gather)
-    __syncthreads();
     A2C_FINE(1);
     const float closs = a2c_gae(S, W, T, gamma, lam, sh.red);
     A2C_FINE(5);
