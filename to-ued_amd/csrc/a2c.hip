@@ -97,6 +97,27 @@ struct A2CStage {
   }
 };
 
+// S.vt[j] = V(obs j) + c_j V[D-1] for the NO staged observations, from S.ix / S.cc: each thread's up to VB gathers are
+// issued before the first is waited on.  Ends without a barrier; the caller syncs.
+TOUED_DEV void gather_values(const A2CStage& S, const float* __restrict__ v, int D, int NO) {
+  constexpr int VB = 8;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const float vlast = v[D - 1];
+  for (int j0 = tid; j0 < NO; j0 += VB * nt) {
+    float g[VB];
+#pragma unroll
+    for (int q = 0; q < VB; ++q) {
+      const int j = j0 + q * nt;
+      g[q] = j < NO ? v[S.ix[j]] : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < VB; ++q) {
+      const int j = j0 + q * nt;
+      if (j < NO) S.vt[j] = g[q] + S.cc[j] * vlast;
+    }
+  }
+}
+
 // Latency structure: the agent's whole trajectory (obs rows and times, actions, rewards, dones) is staged into LDS
 // with coalesced loads, V(obs) gathered for every observation at once, and only then the per-worker GAE scans run
 // out of LDS -- a handful of dependent memory round trips per update instead of two per time step.  Ends with a
@@ -694,10 +715,6 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
     if (u == U - 1) A2C_STAMP(0);
     if (env) {
       wk.load_rows(tab, D);
-      // V(obs) of every observation loaded as the chain reaches it (issued behind the step's row gather, stored one
-      // step later, so its latency hides under the chain's): no separate gather phase and barrier after it
-      const float vlast = v[D - 1];
-      float vcur = v[wk.idx];
       const draw4* dr = reinterpret_cast<const draw4*>(draws) + (size_t)u * n + i;
       draw4 dr0 = {0u, 0u, 0u, 0u};
       if (T > 0) dr0 = dr[0];
@@ -711,24 +728,23 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
         float rew;
         bool done;
         wk.step(sp, tab, d, oi, ot, action, rew, done);
-        const float vnext = v[wk.idx];
-        const float c = (float)ot * 0.001f;
         S.ix[t * W + w] = oi;
-        S.cc[t * W + w] = c;
-        S.vt[t * W + w] = vcur + c * vlast;   // a2c_load's expression
+        S.cc[t * W + w] = (float)ot * 0.001f;
         S.act[t * W + w] = (uint8_t)action;
         S.rw[t * W + w] = rew;
         S.nd[t * W + w] = done ? 0.0f : 1.0f;
-        vcur = vnext;
       }
-      const float c = (float)wk.s.time * 0.001f;
       S.ix[T * W + w] = wk.idx;
-      S.cc[T * W + w] = c;
-      S.vt[T * W + w] = vcur + c * vlast;
+      S.cc[T * W + w] = (float)wk.s.time * 0.001f;
     }
     if (u == U - 1) A2C_STAMP(7);
     __syncthreads();
     A2C_FINE(0);
+    // V(obs) for every observation (a2c_load's gather) as its own phase: loading each step's V inside the env chain
+    // instead (behind the row gather, stored a step later) made the chain 48 -> 69 k cycles per update -- a second
+    // 64-lane gather per step doubles the chain's cache-line lookups (profiles/r04/a2c_stamps_fine_r04i.log)
+    gather_values(S, v, D, (T + 1) * W);
+    __syncthreads();
     A2C_FINE(1);
     const float closs = a2c_gae(S, W, T, gamma, lam, sh.red);
     A2C_FINE(5);

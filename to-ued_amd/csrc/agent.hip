@@ -1297,9 +1297,15 @@ struct HvpOp {   // k_hvp
   TOUED_DEV void finish(int, float, float) const {}
 };
 
+#ifndef ROWS_PRIO
+#define ROWS_PRIO 0
+#endif
 template <class Op>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k_rows_sorted(Op op) {
   constexpr int NA = Op::NA, NC = Op::NC, NV = NA + NC, NM = Op::NM;
+  // the reverse agent loop runs beside eval_agent's VALU-bound key chain (meta.py eval_keys_early): with a higher
+  // wave priority these latency-bound blocks take the issue slots first and the key chain fills the gaps
+  if (ROWS_PRIO > 0) __builtin_amdgcn_s_setprio(ROWS_PRIO);
   constexpr uint32_t NONE = 0xFFFFFFFFu, SMASK = 4095u;
   // unpadded vector stride (odd strides are bank-conflict free): 13-float rows keep a block's LDS at 75 KB,
   // so two agents' blocks share a CU and all N = 512 blocks are resident in one round
