@@ -171,6 +171,41 @@ TOUED_DEV void gae_scan(const float* __restrict__ vt, const float* __restrict__ 
 
 TOUED_DEV float a2c_gae(const A2CStage& S, int W, int T, float gamma, float lam, float* red) {
   const int tid = threadIdx.x;
+  const float n = (float)(W * T);
+  if (W <= 64) {
+    // every worker in wave 0: the scan, the advantage mean, the critic loss, the variance (two-pass over each
+    // worker's own advantages) and abar without a block reduction -- wave sums only, one barrier at the end (the
+    // block path's three reductions cost ~1.4 k cycles each, profiles/r04/a2c_stamps_fine_r04h.log).  The mean and
+    // the critic loss are the block path's values bit for bit (its other waves add zeros); the variance is summed
+    // per worker instead of strided over the block.
+    if (tid < 64) {
+      float sa = 0.0f, cl = 0.0f;
+      if (tid < W) gae_scan(S.vt, S.nd, S.rw, S.adv, S.dv, W, T, tid, gamma, lam, sa, cl);
+      A2C_FINE(2);
+      const float mean = wsum_dpp(sa) / n;
+      const float closs = wsum_dpp(tid < W ? cl / (float)T : 0.0f) / (float)W;
+      A2C_FINE(3);
+      float sv = 0.0f;
+      if (tid < W) {
+#pragma unroll 4
+        for (int t = 0; t < T; ++t) {
+          const float d = S.adv[tid * T + t] - mean;
+          sv += d * d;
+        }
+      }
+      const float inv_sd = 1.0f / (sqrtf(wsum_dpp(sv) / n) + EPSF);
+      A2C_FINE(4);
+      if (tid < W) {
+        float ab = 0.0f;
+#pragma unroll 4
+        for (int t = 0; t < T; ++t) ab += (S.adv[tid * T + t] - mean) * inv_sd;
+        S.abar[tid] = ab / (float)T;
+      }
+      if (tid == 0) red[0] = closs;
+    }
+    __syncthreads();
+    return red[0];
+  }
   // per-worker GAE (reverse scan over T, util/metrics.py:17-38)
   float s_adv = 0.0f, s_cl = 0.0f;
   for (int w = tid; w < W; w += blockDim.x) {
@@ -179,7 +214,6 @@ TOUED_DEV float a2c_gae(const A2CStage& S, int W, int T, float gamma, float lam,
     s_cl += cl / (float)T;
   }
   A2C_FINE(2);
-  const float n = (float)(W * T);
   float ms[2] = {s_adv, s_cl};
   block_sum_n<2>(ms, red);
   A2C_FINE(3);

@@ -1298,7 +1298,7 @@ struct HvpOp {   // k_hvp
 };
 
 #ifndef ROWS_PRIO
-#define ROWS_PRIO 0
+#define ROWS_PRIO 3   // C2 20.29-20.31 ms at 0, 19.96-20.00 at 3 (profiles/r04/c2_rows_prio_r04j.txt)
 #endif
 template <class Op>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k_rows_sorted(Op op) {
