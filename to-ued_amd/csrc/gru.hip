@@ -1402,30 +1402,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       al = acc;
     }
   };
-#ifndef BWD_NR
-#define BWD_NR 3
-#endif
-#ifndef BWD_PRE
-#define BWD_PRE 0
-#endif
-  constexpr int NR = BWD_NR;
-  // the memory part's load ring: NR slots, quads i+1 .. i+NR-1 in flight while quad i is processed (NR = 2: 10.11
-  // ms).  BWD_PRE: the next step's first NR-1 quads are issued at the end of the contraction (the dz / dhn registers
-  // are free there), so they land during the tail and the head cotangents instead of at the memory part's start.
-  float vr[NR][4][4];
-  auto load_q_at = [&](long c, int h, int g4, float (&v)[4][4]) {
-    const int ubq = 32 * wave + 4 * hi;
-    const unsigned vq = (unsigned)((((long)(ubq + (col & 3))) * p.M + r0 + RB * h + (col & 28)) * 4);
-    const unsigned so = (unsigned)(((long)8 * g4 * p.M + c) * 4);
-    ld4(rs_hin, vq, so, v[0]);
-    ld4(rs_r, vq, so, v[1]);
-    ld4(rs_z, vq, so, v[2]);
-    ld4(rs_hn, vq, so, v[3]);
-  };
-  if (BWD_PRE) {
-#pragma unroll
-    for (int qi = 0; qi < NR - 1; ++qi) load_q_at((long)k * T * R, qi >> 2, qi & 3, vr[qi]);
-  }
   for (int t = 0; t < T; ++t) {
     const long ctr = ((long)k * T + t) * R;
     BWD_STAMP(0);
@@ -1439,7 +1415,19 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     // LDS addresses below are re-derived from lane_now() where used (see lane_now)
     auto ubn = [&] { return 32 * wave + 4 * (lane_now() >> 5); };
     auto rown = [&](int h) { return RB * h + (lane_now() & 31); };
-    auto load_q = [&](int h, int g4, float (&v)[4][4]) { load_q_at(ctr, h, g4, v); };
+#ifndef BWD_NR
+#define BWD_NR 3
+#endif
+    constexpr int NR = BWD_NR;
+    float vr[NR][4][4];   // NR-slot ring: quads i+1 .. i+NR-1 in flight while quad i is processed (NR = 2: 10.11 ms)
+    auto load_q = [&](int h, int g4, float (&v)[4][4]) {
+      const unsigned vq = (unsigned)((((long)(ub + (col & 3))) * p.M + r0 + RB * h + (col & 28)) * 4);
+      const unsigned so = (unsigned)(((long)8 * g4 * p.M + ctr) * 4);
+      ld4(rs_hin, vq, so, v[0]);
+      ld4(rs_r, vq, so, v[1]);
+      ld4(rs_z, vq, so, v[2]);
+      ld4(rs_hn, vq, so, v[3]);
+    };
     // four units ub + 8 g4 .. +3 of this lane's row RB h + col (register quad g4 of tile h): per-unit dword
     // stores, lane = row (128-byte segments).  (Transposed back to 16-byte stores of four rows, as the loads are,
     // they measured no faster: 9.82-10.0 ms against 9.75-9.88.)
@@ -1465,10 +1453,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     floatx16 hacc;
     float dx3 = 0.0f, dx4 = 0.0f;
     float rmr[2] = {0.0f, 0.0f};   // running row maxima of |dr|
-    if (!BWD_PRE) {
 #pragma unroll
-      for (int qi = 0; qi < NR - 1; ++qi) load_q(qi >> 2, qi & 3, vr[qi]);
-    }
+    for (int qi = 0; qi < NR - 1; ++qi) load_q(qi >> 2, qi & 3, vr[qi]);
 #pragma unroll
     for (int qi = 0; qi < 8; ++qi) {
       const int h = qi >> 2, g4 = qi & 3;
@@ -1632,10 +1618,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     lds_barrier();
     BWD_STAMP(6);
     contract_h(2, 0);
-    if (BWD_PRE && t + 1 < T) {
-#pragma unroll
-      for (int qi = 0; qi < NR - 1; ++qi) load_q_at(ctr + R, qi >> 2, qi & 3, vr[qi]);
-    }
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const float4 w4 = *reinterpret_cast<const float4*>(&wsc[32 * wave + 4 * (lane_now() >> 5) + 8 * g4]);
