@@ -33,7 +33,9 @@ DRAW_RAMP = (4, 6, 9, 14, 21)
 def chunk_sizes(U: int) -> list[int]:
     """Update counts of the successive toued_a2c_chain launches of a U-update chain."""
     out, done = [], 0
-    ramp = DRAW_RAMP if os.environ.get("TOUED_A2C_RAMP", "1") != "0" else ()
+    env = os.environ.get("TOUED_A2C_RAMP", "1")
+    # "1": DRAW_RAMP; "0": none; a comma list: that ramp (timing studies)
+    ramp = DRAW_RAMP if env == "1" else () if env == "0" else tuple(int(x) for x in env.split(",") if x)
     for m in ramp:
         if done >= U:
             break
@@ -152,6 +154,9 @@ class A2CTrainer:
                                        stream=stream_ptr)
 
         d_ev, c_ev, pending = [], [], None
+        # the eval draws go on the side stream behind the draws of chunk len - ev_ahead + 1 (2: beside the last two
+        # chain launches)
+        ev_ahead = max(2, min(len(starts), int(os.environ.get("TOUED_A2C_EV_AHEAD", "2"))))
         if overlap:
             with torch.cuda.stream(side):
                 pending = draws_for(0, side.cuda_stream)
@@ -170,7 +175,7 @@ class A2CTrainer:
                     e = torch.cuda.Event()
                     e.record(side)
                     d_ev.append(e)
-                    if ev is not None and c + 2 == len(starts):
+                    if ev is not None and c + ev_ahead == len(starts):
                         with torch.cuda.stream(side):
                             ev()
                         ev_done = torch.cuda.Event()
