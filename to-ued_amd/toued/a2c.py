@@ -24,10 +24,12 @@ from .rollout import RolloutWrapper, Transition, split_rollouts
 
 # updates whose rollout draws are produced by one toued_rollout_draws call (32 x N x W x T x 16 B of scratch)
 DRAW_CHUNK = 32
-# chunk sizes of the chain path: the first chunk's draws are the only ones not made beside a chain launch, so the chunks
-# start short and grow ~1.5x (a chain launch of m updates covers the side stream's draws of ~1.6 m updates), then
-# DRAW_CHUNK (TOUED_A2C_RAMP=0: DRAW_CHUNK throughout)
-DRAW_RAMP = (4, 6, 9, 14, 21)
+# chunk sizes of the chain path: the first chunk's draws are the only ones not made beside a chain launch.  Round 3
+# started the chunks short and grew them ~1.5x (4, 6, 9, 14, 21, then DRAW_CHUNK) so the first chain launch started
+# early; since the round-4 chain speed-ups the short launches cost more than the wait they save (regret round 17.55 /
+# 17.69 ms without the ramp against 17.76 / 18.39 with it on the same boxes, profiles/r04/c3_ramp_r04p.txt), so the
+# default is no ramp (TOUED_A2C_RAMP: "1" this tuple, "0" none, or a comma list)
+DRAW_RAMP = ()
 
 
 def chunk_sizes(U: int) -> list[int]:
