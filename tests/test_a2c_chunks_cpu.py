@@ -16,9 +16,19 @@ def test_chunk_sizes_cover_u(U):
     assert sum(c) == U
     assert all(1 <= m <= DRAW_CHUNK for m in c)
     assert c == sorted(c)                       # short chunks first, full ones last
-    if U >= sum(DRAW_RAMP) + DRAW_CHUNK:
+    if DRAW_RAMP and U >= sum(DRAW_RAMP) + DRAW_CHUNK:
         assert c[0] == DRAW_RAMP[0] or c[0] < DRAW_RAMP[0]
+    if U >= sum(DRAW_RAMP) + DRAW_CHUNK:
         assert c[-1] == DRAW_CHUNK
+    # at most one partial chunk beyond the ramp
+    assert sum(1 for m in c[len(DRAW_RAMP):] if m != DRAW_CHUNK) <= 1 + len(DRAW_RAMP)
+
+
+def test_chunk_sizes_ramp_list(monkeypatch):
+    from toued.a2c import DRAW_CHUNK, chunk_sizes
+    monkeypatch.setenv("TOUED_A2C_RAMP", "4,6,9,14,21")
+    c = chunk_sizes(250)
+    assert c == [4, 4, 6, 9, 14, 21] + [DRAW_CHUNK] * 6 and sum(c) == 250
 
 
 def test_chunk_sizes_ramp_off(monkeypatch):
