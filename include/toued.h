@@ -11,10 +11,11 @@
  *
  * Conventions
  *   - Every buffer is a DEVICE pointer owned by the caller (torch tensors in
- *     the Python host).  Kernels never allocate; no hidden global state.
+ *     the Python host).  Kernels never allocate.
  *   - Every call is asynchronous on `stream` and returns 0 on success, <0 on
  *     error (-1 bad arguments, -2 launch failure); toued_last_error() returns
  *     a thread-local message.  Calls are re-entrant across streams.
+ *   - The only state kept between calls lives in an opaque context object (toued_ctx, below).
  *   - Keys are jax.random threefry keys: uint32[n][2].
  *   - Levels are packed int32[n][80] records (LEVEL_WORDS, layout in DESIGN.md
  *     §Data layout): scalars, raw obj_ids, static object cells, per-object
@@ -46,6 +47,18 @@ typedef struct {
 
 const char* toued_last_error(void);
 int toued_abi_version(void);
+
+/* Opaque context: the only state the library keeps between calls (today the weight-gradient plans' reserved-CU
+ * count, toued_set_reserved_cus).  A process-wide default context is current until a thread makes another one
+ * current; the setting is then per thread, so two host threads driving separate streams plan independently.
+ * toued_ctx_destroy of the calling thread's current context reverts that thread to the default (destroying a
+ * context another thread still has current is the caller's error).  Replaces no reference interface: the
+ * reference's equivalent state lives in its jitted closures. */
+typedef struct toued_ctx toued_ctx;
+toued_ctx* toued_ctx_create(void);
+int toued_ctx_destroy(toued_ctx* ctx);
+int toued_ctx_set_current(toued_ctx* ctx);   /* NULL selects the process default */
+toued_ctx* toued_ctx_current(void);
 
 /* ---- PRNG (jax 0.4.13 threefry, environments/* and meta/* call sites) ---- */
 /* out[i][j] = jax.random.split(keys[i], num)[j] */
@@ -317,7 +330,8 @@ int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit
 
 /* CUs the split-K weight-gradient plans leave free (default 0): a kernel running on a side stream beside them (the
  * eval_agent rollout) then occupies its own CUs instead of pushing one workgroup of every chunk into a second
- * round.  Workspace sizes queried before the change stay sufficient (fewer chunks).  Returns the previous value. */
+ * round.  Workspace sizes queried before the change stay sufficient (fewer chunks).  Sets the current context's
+ * value (toued_ctx_current) and returns its previous value. */
 int toued_set_reserved_cus(int n);
 
 /* toued_agent_grad + toued_agent_apply fused, in place, for an agent chain that never reads the gradient tables

@@ -45,3 +45,31 @@ def test_ctypes_signatures_match_header():
                     else "float" if a.startswith("float") else "int" if a.split()[0] in ("int", "uint32_t") else None)
             if want is not None and t in kinds:
                 assert kinds[t] == want, (name, a, kinds[t])
+
+
+def test_ctx_holds_reserved_cus_per_thread():
+    """toued_set_reserved_cus writes the current context: a created context starts at 0, a thread that never
+    made one current sees the process default, and destroying the current context reverts to the default."""
+    import threading
+    from toued import _lib
+    L = _lib.lib()
+    default = L.toued_ctx_current()
+    assert default
+    prev = L.toued_set_reserved_cus(7)
+    try:
+        ctx = L.toued_ctx_create()
+        assert ctx and ctx != default
+        assert L.toued_ctx_set_current(ctx) == 0
+        assert L.toued_ctx_current() == ctx
+        assert L.toued_set_reserved_cus(3) == 0          # fresh context
+        seen = []
+        t = threading.Thread(target=lambda: seen.append((L.toued_ctx_current(), L.toued_set_reserved_cus(7))))
+        t.start(); t.join()
+        assert seen == [(default, 7)]                   # other thread: the default, still 7
+        assert L.toued_set_reserved_cus(-5) == 3         # negative clamps to 0
+        assert L.toued_set_reserved_cus(0) == 0
+        assert L.toued_ctx_destroy(ctx) == 0
+        assert L.toued_ctx_current() == default
+        assert L.toued_ctx_set_current(None) == 0 and L.toued_ctx_destroy(None) == 0
+    finally:
+        assert L.toued_set_reserved_cus(prev) == 7

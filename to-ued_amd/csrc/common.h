@@ -205,8 +205,12 @@ TOUED_DEV float erfinv_giles(float x) {
 
 // ----------------------------------------------------------------------------
 // Error reporting for the C ABI
+struct toued_ctx {
+  int reserved_cus;   // CUs the weight-gradient reductions' split-K plans leave free (toued_set_reserved_cus)
+};
 namespace toued {
 void set_error(const char* fmt, ...);
+toued_ctx* current_ctx();   // the calling thread's current context, else the process default (capi.hip)
 }
 #define TOUED_CHECK_LAUNCH()                                                   \
   do {                                                                         \

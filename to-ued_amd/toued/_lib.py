@@ -112,8 +112,13 @@ _SIGS = {
     "toued_rowsum_into": [_I, _L, _P, _L, _P, _I, _P, ctypes.c_size_t, _P],
     "toued_last_error": [],
     "toued_abi_version": [],
+    "toued_ctx_create": [],
+    "toued_ctx_destroy": [_P],
+    "toued_ctx_set_current": [_P],
+    "toued_ctx_current": [],
 }
-_RESTYPES = {"toued_last_error": ctypes.c_char_p, "toued_mode_program_bytes": ctypes.c_size_t,
+_RESTYPES = {"toued_last_error": ctypes.c_char_p, "toued_ctx_create": ctypes.c_void_p,
+             "toued_ctx_current": ctypes.c_void_p, "toued_mode_program_bytes": ctypes.c_size_t,
              "toued_gru_packed_floats": ctypes.c_size_t, "toued_wgrad_workspace_floats": ctypes.c_size_t,
              "toued_gru_bwd_small_work_floats": ctypes.c_size_t, "toued_wgrad_bfp_workspace_floats": ctypes.c_size_t,
              "toued_rowsum_workspace_floats": ctypes.c_size_t,
