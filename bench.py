@@ -342,10 +342,15 @@ def workload_c3(a, cpu: bool):
         dom = _hbm_roofline("k_a2c_chain (A2C antagonist: env chain + fused update, %.2f updates per launch on "
                             "average)" % upl, int(steps_launch * upl * 40), chain_ms,
                             "latency-bound: per update a T-step dependent env chain, then the LDS sort/segment update")
-        draws_rf = _hbm_roofline("k_eval_keys + k_eval_draws (state-independent draws of %.2f updates on average)"
-                                 % upl, int(steps_launch * upl * 32), ks["a2c_draws"][1], "threefry VALU-bound")
-        secondary = {"a2c_chain": dom, "a2c_draws": draws_rf,
-                     "per_update_ms": round((chain_ms + ks["a2c_draws"][1]) / upl, 4)}
+        if "a2c_draws" in ks:
+            draws_rf = _hbm_roofline("k_eval_keys + k_eval_draws (state-independent draws of %.2f updates on average)"
+                                     % upl, int(steps_launch * upl * 32), ks["a2c_draws"][1], "threefry VALU-bound")
+            secondary = {"a2c_chain": dom, "a2c_draws": draws_rf,
+                         "per_update_ms": round((chain_ms + ks["a2c_draws"][1]) / upl, 4)}
+        else:   # toued_a2c_chain_self: the draws are made inside the chain launch
+            dom["kernel"] = ("k_a2c_chain<SELF> (A2C antagonist: env chain + fused update, the next update's draws in "
+                             "the idle waves; %.0f updates per launch)" % upl)
+            secondary = {"a2c_chain": dom, "per_update_ms": round(chain_ms / upl, 4)}
     else:
         roll_ms, upd_ms = ks["a2c_rollout"][1], ks["a2c_update"][1]
         traj_bytes = N * ((T + 1) * W * 8 + T * W * 6)

@@ -181,6 +181,13 @@ int toued_a2c_chain_fits(int W, int T, int D);
 int toued_a2c_chain(EnvSpec spec, const int* levels, int N, int W, int T, int D, int U, float* theta, float* vcrit,
                     int* state, const uint32_t* draws, long dstride, float gamma, float lam, float ent_coef, float lr_a,
                     float lr_c, float max_norm, int* step, float* loss_out, hipStream_t stream);
+/* The same scan making its own draws (W <= 64): from the U update keys (keys [U][N][2], toued_key_chain's output),
+ * each workgroup makes update u + 1's draws in the waves its env chain leaves idle during update u, into scratch
+ * u32 [N][2][T][W][4] (a per-agent double buffer).  Bit-identical to toued_rollout_draws + toued_a2c_chain over the
+ * same keys, with no draws pass in front of or beside the launch. */
+int toued_a2c_chain_self(EnvSpec spec, const int* levels, int N, int W, int T, int D, int U, float* theta, float* vcrit,
+                         int* state, const uint32_t* keys, uint32_t* scratch, float gamma, float lam, float ent_coef,
+                         float lr_a, float lr_c, float max_norm, int* step, float* loss_out, hipStream_t stream);
 /* --fix_value_critic: one update of the meta-gradient value critics vcrit [N][D] on a trajectory (meta/train.py:61-81
  * with the discarded `.replace` fixed): critic loss mean_w mean_t (target - V)^2 on stop-gradient GAE targets,
  * clip_by_global_norm + SGD (lr, max_norm), vstep[i] += 1; loss_out[i][1] += the loss before the update.

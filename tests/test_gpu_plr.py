@@ -141,13 +141,16 @@ def test_a2c_graph_replay_matches_eager_and_lifetime_discard():
     torch.testing.assert_close(vc_g, vc_e, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("self_draws", ["0", "1"])
 @pytest.mark.parametrize("mode,W,U", [("dense", 64, 40), ("all_shortlife", 32, 7), ("mazes", 64, 33)])
-def test_a2c_chain_matches_launch_per_update(mode, W, U):
+def test_a2c_chain_matches_launch_per_update(mode, W, U, self_draws, monkeypatch):
     """toued_a2c_chain (the whole update chain in one kernel per 32 updates, trajectories in LDS) against one
     toued_rollout_env + one toued_a2c_update launch per update: actor/critic tables, env state, step counters (with
-    lifetime discards) and losses bit-identical, over several draw chunks and a partial last chunk."""
+    lifetime discards) and losses bit-identical, over several draw chunks and a partial last chunk.  self_draws = 1:
+    toued_a2c_chain_self (one launch, the draws made in the env chain's idle waves)."""
     from toued.a2c import A2CHyperparams, A2CTrainer
     from toued.env import L_LIFETIME
+    monkeypatch.setenv("TOUED_A2C_SELF", self_draws)
     N, T = 4, 20
     ro, levels, p, lt, theta, vcrit, state, D = _a2c_setup(mode, N, W, T, seed=31)
     levels[:, L_LIFETIME] = torch.tensor([1, U // 2, 1000, U - 1], dtype=torch.int32, device="cuda")
@@ -158,6 +161,7 @@ def test_a2c_chain_matches_launch_per_update(mode, W, U):
         step = torch.zeros(N, dtype=torch.int32, device="cuda")
         tr = A2CTrainer(ro, A2CHyperparams(), _ahyp(mode), use_graph=False, chain=chain)
         assert tr.use_chain(W, T, D) == chain
+        assert tr.use_self_draws(W) == (self_draws == "1")
         loss = tr.train(rng, th, vc, step, levels, st, U)
         outs.append((th, vc, st, step, loss))
     for x, y, name in zip(outs[0], outs[1], ("theta", "vcrit", "state", "step", "loss")):

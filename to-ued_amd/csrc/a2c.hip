@@ -701,12 +701,18 @@ __global__ void __launch_bounds__(256) k_a2c_update(int W, int T, int D, float* 
 // obs_dim = 3201 table pair is 77 KB; two workgroups share a CU's LDS), read back by the next rollout after the
 // workgroup barrier.  Bit-identical to toued_rollout_env + toued_a2c_update per update
 // (tests/test_gpu_plr.py::test_a2c_chain_matches_launch_per_update).
-template <int NMAX, bool CAND>
+// SELF (toued_a2c_chain_self, W <= 64): the chain makes its own draws.  The env chain runs in wave 0 and waves 1-3
+// are idle there, so during update u they make update u + 1's (the key chain split_at(key_{u+1}, W, w) then two
+// splits per step, k_eval_keys' chain, each wave redundantly, and every third step's step_draws) into a per-agent
+// double buffer dscr [N][2][T][W] (global, L2-resident); update 0's are made by all four waves before the loop.
+// The same draws as toued_rollout_draws over the same keys, so the same trajectories.
+template <int NMAX, bool CAND, bool SELF>
 __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __restrict__ levels, int W, int T, int D,
                                                    int U, float* __restrict__ theta, float* __restrict__ vcrit,
                                                    int* __restrict__ state, const uint4* __restrict__ draws,
-                                                   long dstride, float gamma, float lam, float ent_coef, float lr_a,
-                                                   float lr_c, float max_norm, int* __restrict__ step,
+                                                   long dstride, const uint32_t* __restrict__ ukeys,
+                                                   uint4* __restrict__ dscr, float gamma, float lam, float ent_coef,
+                                                   float lr_a, float lr_c, float max_norm, int* __restrict__ step,
                                                    float* __restrict__ loss_out) {
   extern __shared__ float lds[];
   __shared__ A2CShared sh;
@@ -723,12 +729,14 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
   float* vec = reinterpret_cast<float*>(key + A2C_SORT_MAX);                    // [W*T][6]
   const float* tab = theta + (size_t)a * D * 5;
   const float* v = vcrit + (size_t)a * D;
-  // env workers spread over the four waves (W % 4 == 0: W/4 lanes of each wave), so each wave's row gather touches
-  // W/4 cache lines instead of W (A2C_ENV_SPREAD=0: all W workers in wave 0)
+  // env workers: all W in wave 0 (default), or spread over the four waves (A2C_ENV_SPREAD=1, W % 4 == 0: W/4 lanes of
+  // each wave, so each wave's row gather touches W/4 cache lines instead of W).  The spread paid before the level's
+  // transition table (NPT); since, one wave per agent costs a quarter of the issue slots and the chain runs faster
+  // (profiles/r04/a2c_env_spread_r04z.txt: 93.2 vs 95.2 k cycles per update, 1.37 vs 1.50 ms per 32-update launch)
 #ifndef A2C_ENV_SPREAD
-#define A2C_ENV_SPREAD 1
+#define A2C_ENV_SPREAD 0
 #endif
-  const bool spread = A2C_ENV_SPREAD && W % 4 == 0;
+  const bool spread = !SELF && A2C_ENV_SPREAD && W % 4 == 0;   // (SELF: the env chain in wave 0 always)
   const int w = spread ? (tid >> 6) * (W / 4) + (tid & 63) : tid;
   const bool env = spread ? (tid & 63) < W / 4 : tid < W;
   const int i = a * W + w;
@@ -744,20 +752,41 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
     wk.npt = npt;
     __syncthreads();
   }
+  const int wv = tid >> 6, ln = tid & 63;
+  // SELF: update uu's draws of steps t = part (mod nparts) for worker ln into buffer slot `slot`
+  auto make_draws = [&](int uu, int slot, int part, int nparts) {
+    if (ln >= W) return;
+    const uint32_t* kp = ukeys + ((size_t)uu * gridDim.x + a) * 2;
+    const int* levp = levels + (size_t)a * LEVEL_WORDS;
+    uint2 r = split_at(make_uint2(kp[0], kp[1]), (uint32_t)W, (uint32_t)ln);
+    draw4* out = reinterpret_cast<draw4*>(dscr) + (size_t)(a * 2 + slot) * T * W + ln;
+    for (int t = 0; t < T; ++t) {
+      uint2 sub, sub_env;
+      split2(r, r, sub);
+      split2(r, r, sub_env);
+      if (t % nparts == part) out[(size_t)t * W] = step_draws<NMAX>(levp, sub, sub_env);
+    }
+  };
+  if (SELF) {
+    make_draws(0, 0, wv, 4);
+    __syncthreads();
+  }
   for (int u = 0; u < U; ++u) {
     if (tid == 0) sh.has_last = 0;
     if (u == U - 1) A2C_STAMP(0);
     if (env) {
       wk.load_rows(tab, D);
-      const draw4* dr = reinterpret_cast<const draw4*>(draws) + (size_t)u * n + i;
+      const long ds = SELF ? (long)W : dstride;
+      const draw4* dr = SELF ? reinterpret_cast<const draw4*>(dscr) + (size_t)(a * 2 + (u & 1)) * T * W + w
+                             : reinterpret_cast<const draw4*>(draws) + (size_t)u * n + i;
       draw4 dr0 = {0u, 0u, 0u, 0u};
       if (T > 0) dr0 = dr[0];
       draw4 dr1 = dr0;
-      if (T > 1) dr1 = dr[dstride];
+      if (T > 1) dr1 = dr[ds];
       for (int t = 0; t < T; ++t) {
         const draw4 d = dr0;
         dr0 = dr1;
-        if (t + 2 < T) dr1 = dr[(size_t)(t + 2) * dstride];
+        if (t + 2 < T) dr1 = dr[(size_t)(t + 2) * ds];
         int oi, ot, action;
         float rew;
         bool done;
@@ -770,6 +799,8 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
       }
       S.ix[T * W + w] = wk.idx;
       S.cc[T * W + w] = (float)wk.s.time * 0.001f;
+    } else if (SELF && wv >= 1 && u + 1 < U) {
+      make_draws(u + 1, (u + 1) & 1, wv - 1, 3);   // beside wave 0's env chain
     }
     if (u == U - 1) A2C_STAMP(7);
     __syncthreads();
@@ -947,14 +978,14 @@ int toued_a2c_chain(EnvSpec sp, const int* levels, int N, int W, int T, int D, i
 #define TOUED_A2C_CHAIN_LAUNCH(NM, CD)                                                                               \
   {                                                                                                                   \
     if (!attr_set[CD][NM]) {                                                                                          \
-      TOUED_REQUIRE(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_a2c_chain<NM, CD>),                          \
+      TOUED_REQUIRE(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_a2c_chain<NM, CD, false>),                   \
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) == hipSuccess,        \
                     "toued_a2c_chain: cannot raise the dynamic LDS limit");                                           \
       attr_set[CD][NM] = true;                                                                                        \
     }                                                                                                                 \
-    hipLaunchKernelGGL((k_a2c_chain<NM, CD>), dim3(N), dim3(256), lds, stream, sp, levels, W, T, D, U, theta, vcrit, \
-                       state, reinterpret_cast<const uint4*>(draws), dstride, gamma, lam, ent_coef, lr_a, lr_c,       \
-                       max_norm, step, loss_out);                                                                     \
+    hipLaunchKernelGGL((k_a2c_chain<NM, CD, false>), dim3(N), dim3(256), lds, stream, sp, levels, W, T, D, U, theta,  \
+                       vcrit, state, reinterpret_cast<const uint4*>(draws), dstride, nullptr, nullptr, gamma, lam,    \
+                       ent_coef, lr_a, lr_c, max_norm, step, loss_out);                                               \
   }
 #define TOUED_A2C_CHAIN_CASE(NM)                                                                                     \
   case NM:                                                                                                            \
@@ -970,6 +1001,48 @@ int toued_a2c_chain(EnvSpec sp, const int* levels, int N, int W, int T, int D, i
   }
 #undef TOUED_A2C_CHAIN_LAUNCH
 #undef TOUED_A2C_CHAIN_CASE
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+// The same chain making its own draws from the U update keys (keys [U][N][2], toued_key_chain's output):
+// scratch = u32 [N][2][T][W][4].  W <= 64 (the env chain in one wave).  Bit-identical to toued_rollout_draws +
+// toued_a2c_chain over the same keys.
+int toued_a2c_chain_self(EnvSpec sp, const int* levels, int N, int W, int T, int D, int U, float* theta, float* vcrit,
+                         int* state, const uint32_t* keys, uint32_t* scratch, float gamma, float lam, float ent_coef,
+                         float lr_a, float lr_c, float max_norm, int* step, float* loss_out, hipStream_t stream) {
+  TOUED_REQUIRE(sp.tabular && sp.n_max >= 1 && sp.n_max <= 5 && sp.max_grid >= 1 && sp.max_grid * sp.max_grid <= 256,
+                "toued_a2c_chain_self: tabular env spec required");
+  TOUED_REQUIRE(N >= 0 && U >= 0 && W >= 1 && W <= 64 && toued_a2c_chain_fits(W, T, D),
+                "toued_a2c_chain_self: N=%d U=%d W=%d T=%d D=%d unsupported", N, U, W, T, D);
+  TOUED_REQUIRE(D == sp.max_grid * sp.max_grid * (1 << sp.n_max) + 1, "toued_a2c_chain_self: D=%d != obs_dim", D);
+  TOUED_REQUIRE((double)N * D * 20.0 < 4294967295.0, "toued_a2c_chain_self: actor tables (%d x %d rows) exceed 4 GiB",
+                N, D);
+  TOUED_REQUIRE(keys && scratch, "toued_a2c_chain_self: null keys / scratch");
+  if (N == 0 || U == 0) return 0;
+  const size_t lds = a2c_update_lds(W, T) + ((size_t)sp.max_grid * sp.max_grid * 5 * 2 + 3) / 4 * 4;
+  static bool attr_set[6] = {};
+#define TOUED_A2C_SELF_CASE(NM)                                                                                      \
+  case NM:                                                                                                            \
+    if (!attr_set[NM]) {                                                                                              \
+      TOUED_REQUIRE(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_a2c_chain<NM, false, true>),                 \
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) == hipSuccess,        \
+                    "toued_a2c_chain_self: cannot raise the dynamic LDS limit");                                      \
+      attr_set[NM] = true;                                                                                            \
+    }                                                                                                                 \
+    hipLaunchKernelGGL((k_a2c_chain<NM, false, true>), dim3(N), dim3(256), lds, stream, sp, levels, W, T, D, U, theta, \
+                       vcrit, state, nullptr, 0L, keys, reinterpret_cast<uint4*>(scratch), gamma, lam, ent_coef,      \
+                       lr_a, lr_c, max_norm, step, loss_out);                                                         \
+    break;
+  switch (sp.n_max) {
+    TOUED_A2C_SELF_CASE(1)
+    TOUED_A2C_SELF_CASE(2)
+    TOUED_A2C_SELF_CASE(3)
+    TOUED_A2C_SELF_CASE(4)
+    TOUED_A2C_SELF_CASE(5)
+    default: break;
+  }
+#undef TOUED_A2C_SELF_CASE
   TOUED_CHECK_LAUNCH();
   return 0;
 }

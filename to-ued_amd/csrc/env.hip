@@ -276,13 +276,8 @@ __global__ void __launch_bounds__(256) k_eval_draws(const int* __restrict__ leve
   const int i = (int)(j % n);
   const int* lev = levels + (size_t)((i / W) % na) * LEVEL_WORDS;
   const uint4 c = chain[j];
-  const uint32_t cbits = bits1(make_uint2(c.x, c.y));
-  // split(sub_env) blocks d0, d1; split(key_s, 3) blocks c0, c1, c2 (env_step's naming)
-  const uint2 d0 = threefry(c.z, c.w, 0u, 2u), d1 = threefry(c.z, c.w, 1u, 3u);
-  const uint2 c0 = threefry(d0.x, d1.x, 0u, 3u), c1 = threefry(d0.x, d1.x, 1u, 4u), c2 = threefry(d0.x, d1.x, 2u, 5u);
-  const int resp = respawn_draws<NMAX>(lev, (1 << NMAX) - 1, make_uint2(c2.x, c0.y));
-  const uint32_t tbits = threefry(c0.x, c1.x, 0u, 0u).x;
-  draws[j] = make_uint4(cbits, tbits, (uint32_t)resp, 0u);
+  const draw4 d = step_draws<NMAX>(lev, make_uint2(c.x, c.y), make_uint2(c.z, c.w));
+  draws[j] = make_uint4(d.x, d.y, d.z, d.w);
 }
 
 #ifdef H3_PLACE

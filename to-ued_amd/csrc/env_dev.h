@@ -404,6 +404,22 @@ TOUED_DEV int choice5(uint2 key, const float* p) {
 // copies in the two-ahead prefetch rotation went through scratch
 typedef unsigned draw4 __attribute__((ext_vector_type(4)));
 
+// One env step's four draw words from its two keys (sub: the action choice, sub_env: step_env's key), as
+// step_env would draw them (gridworld.py:72-136 over env_step's key splits): the choice bits, the termination
+// uniform's bits and the respawn bernoullis of every object, 0.  The state-independent half of a tabular step
+// (k_eval_draws and the A2C chain's own draws call this one function, so their draws are the same bits).
+template <int NMAX, typename LV>
+TOUED_DEV draw4 step_draws(const LV& lev, uint2 sub, uint2 sub_env) {
+  const uint32_t cbits = bits1(sub);
+  // split(sub_env) blocks d0, d1; split(key_s, 3) blocks c0, c1, c2 (env_step's naming)
+  const uint2 d0 = threefry(sub_env.x, sub_env.y, 0u, 2u), d1 = threefry(sub_env.x, sub_env.y, 1u, 3u);
+  const uint2 c0 = threefry(d0.x, d1.x, 0u, 3u), c1 = threefry(d0.x, d1.x, 1u, 4u), c2 = threefry(d0.x, d1.x, 2u, 5u);
+  const int resp = respawn_draws<NMAX>(lev, (1 << NMAX) - 1, make_uint2(c2.x, c0.y));
+  const uint32_t tbits = threefry(c0.x, c1.x, 0u, 0u).x;
+  draw4 r = {cbits, tbits, (unsigned)resp, 0u};
+  return r;
+}
+
 // One train-rollout worker on the state-independent draws of its steps (the env chain of the three-launch rollouts,
 // toued_rollout_env, and of the A2C chain, toued_a2c_chain): the level record in registers, the five candidate next
 // actor rows gathered before the choice (the next state of a step that does not end the episode is a function of

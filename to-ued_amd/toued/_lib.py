@@ -98,6 +98,7 @@ _SIGS = {
     "toued_entropy_clip": [_I, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _F, _F, _F, _P, _P],
     "toued_a2c_chain_fits": [_I, _I, _I],
     "toued_a2c_chain": [EnvSpecC, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _P, _P, _P],
+    "toued_a2c_chain_self": [EnvSpecC, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _F, _P, _P, _P],
     "toued_gru_pack_fwd_multi": [_P, _L, _I, _P, _I, _P, _P],
     "toued_gru_fwd_multi": [_I, _I, _I, _I, _I, _P, _L, _L, _P, _P, _P, _L, _P, _P, _P, _P],
     "toued_es_ask": [_P, _L, _L, _L, _L, _P, _F, _P, _P],

@@ -126,6 +126,28 @@ class A2CTrainer:
             return False
         return bool(_lib.lib().toued_a2c_chain_fits(W, T, D))
 
+    def use_self_draws(self, W: int) -> bool:
+        """The chain makes its own draws (toued_a2c_chain_self: the env chain's idle waves make the next update's) when
+        its env workers fit one wave and TOUED_A2C_SELF=1; otherwise the draws pass runs beside chunked launches."""
+        return W <= 64 and os.environ.get("TOUED_A2C_SELF", "0") == "1"
+
+    def _self_updates(self, b, n, D, W, T, U, tm, ev=None):
+        """All U updates in one toued_a2c_chain_self launch.  The eval draws `ev` (threefry, full chip) go first: beside
+        the chain's workgroups, which fill every register file, a kernel runs only where it held CUs when the launch
+        began (profiles/r04/c3_draws_overlap_r04st.txt)."""
+        L = _lib
+        if ev is not None:
+            ev()
+        if b.get("sscr") is None:   # the per-agent draw double buffer [n][2][T][W] uint32x4
+            b["sscr"] = torch.empty((n, 2, T, W, 4), dtype=torch.int32, device=b["theta"].device)
+        tok = tm.start("a2c_chain") if tm is not None else None
+        L.call("toued_a2c_chain_self", self.ro._c, L.ptr(b["levels"]), n, W, T, D, U, L.ptr(b["theta"]),
+               L.ptr(b["vcrit"]), L.ptr(b["state"]), L.ptr(b["chain"]), L.ptr(b["sscr"]), self.hyp.gamma,
+               self.hyp.gae_lambda, self.hyp.entropy_coeff, self.ah.actor_learning_rate, self.ah.critic_learning_rate,
+               self.ah.max_grad_norm, L.ptr(b["step"]), L.ptr(b["loss"]), L.stream_ptr())
+        if tm is not None:
+            tm.stop(tok)
+
     def _chain_updates(self, b, n, D, W, T, U, tm, ev=None):
         """All U updates as toued_a2c_chain launches of DRAW_CHUNK updates each, every chunk on its precomputed draws.
         Untimed, the next chunk's draws (threefry VALU work, no LDS, ~24 VGPRs) run on a side stream beside the
@@ -215,7 +237,10 @@ class A2CTrainer:
         L.call("toued_key_chain", L.ptr(b["rng"]), n, U, L.ptr(b["chain"]), st)
         tm = self.timers if self.timers is not None and self.timers.enabled else None
         if record is None and self.use_chain(W, T, D):
-            self._chain_updates(b, n, D, W, T, U, tm, ev)
+            if self.use_self_draws(W):
+                self._self_updates(b, n, D, W, T, U, tm, ev)
+            else:
+                self._chain_updates(b, n, D, W, T, U, tm, ev)
             return
         if ev is not None:   # the eval draws first: the per-update path below returns from inside its loop
             ev()
