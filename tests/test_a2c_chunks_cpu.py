@@ -52,10 +52,10 @@ def test_scatter_into_sink_drops_writes():
 
 
 def test_self_draws_selection(monkeypatch):
-    """toued_a2c_chain_self is used only on request (TOUED_A2C_SELF=1) and only when the env chain fits one wave."""
+    """toued_a2c_chain_self is the default when the env chain fits one wave (TOUED_A2C_SELF=0 turns it off)."""
     from toued.a2c import A2CTrainer
     monkeypatch.delenv("TOUED_A2C_SELF", raising=False)
-    assert not A2CTrainer.use_self_draws(None, 64)
+    assert A2CTrainer.use_self_draws(None, 64) and not A2CTrainer.use_self_draws(None, 128)
     monkeypatch.setenv("TOUED_A2C_SELF", "1")
     assert A2CTrainer.use_self_draws(None, 64) and A2CTrainer.use_self_draws(None, 32)
     assert not A2CTrainer.use_self_draws(None, 128)

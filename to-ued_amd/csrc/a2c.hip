@@ -415,6 +415,7 @@ struct A2CShared {
   int has_last;
   int scan_a[4];              // the segmented scan's per-wave totals
   float scan_b[4][A2C_NV];
+  int dflag[64];              // toued_a2c_chain_self: step t's keys of the update being drawn are in LDS (its number + 1)
 };
 
 // The fused update on a staged trajectory after its GAE (closs = the critic loss): per-sample row vectors, the sort,
@@ -767,7 +768,47 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
       if (t % nparts == part) out[(size_t)t * W] = step_draws<NMAX>(levp, sub, sub_env);
     }
   };
+  // SELF, during update u's env chain: wave 1 runs update uu = u + 1's key chain into LDS (the update's per-sample
+  // vectors, free until the update body), step by step behind a flag; waves 2 and 3 make the draws of alternate steps
+  // from it.  Flags hold uu + 1 (updates only grow, so a stale flag never matches); a wait that never ends stops
+  // after ~2^20 sleeps instead of hanging (wrong draws, not a hang: the bit-exact tests would fail).
+  uint4* kl = reinterpret_cast<uint4*>(vec);   // [T][W] (sub, sub_env)
+#ifndef A2C_SELF_PRIO
+#define A2C_SELF_PRIO 0
+#endif
+  auto make_draws_split = [&](int uu, int slot) {
+    // the draw waves below the env chain's priority: their threefry fills the issue slots its latency leaves
+    __builtin_amdgcn_s_setprio(A2C_SELF_PRIO);
+    if (wv == 1) {
+      const uint32_t* kp = ukeys + ((size_t)uu * gridDim.x + a) * 2;
+      uint2 r = split_at(make_uint2(kp[0], kp[1]), (uint32_t)W, (uint32_t)ln);
+      for (int t = 0; t < T; ++t) {
+        uint2 sub, sub_env;
+        split2(r, r, sub);
+        split2(r, r, sub_env);
+        if (ln < W) kl[t * W + ln] = make_uint4(sub.x, sub.y, sub_env.x, sub_env.y);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (ln == 0) __hip_atomic_store(&sh.dflag[t], uu + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    } else {
+      const int* levp = levels + (size_t)a * LEVEL_WORDS;
+      draw4* out = reinterpret_cast<draw4*>(dscr) + (size_t)(a * 2 + slot) * T * W + ln;
+      for (int t = wv - 2; t < T; t += 2) {
+        for (int it = 0; it < (1 << 20); ++it) {
+          if (__hip_atomic_load(&sh.dflag[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == uu + 1) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (ln < W) {
+          const uint4 k4 = kl[t * W + ln];
+          out[(size_t)t * W] = step_draws<NMAX>(levp, make_uint2(k4.x, k4.y), make_uint2(k4.z, k4.w));
+        }
+      }
+    }
+    __builtin_amdgcn_s_setprio(A2C_PRIO);
+  };
   if (SELF) {
+    for (int t = tid; t < 64; t += 256) sh.dflag[t] = 0;
     make_draws(0, 0, wv, 4);
     __syncthreads();
   }
@@ -800,7 +841,13 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
       S.ix[T * W + w] = wk.idx;
       S.cc[T * W + w] = (float)wk.s.time * 0.001f;
     } else if (SELF && wv >= 1 && u + 1 < U) {
-      make_draws(u + 1, (u + 1) & 1, wv - 1, 3);   // beside wave 0's env chain
+#ifndef A2C_SELF_SPLIT
+#define A2C_SELF_SPLIT 1
+#endif
+      if (A2C_SELF_SPLIT)
+        make_draws_split(u + 1, (u + 1) & 1);   // beside wave 0's env chain
+      else
+        make_draws(u + 1, (u + 1) & 1, wv - 1, 3);
     }
     if (u == U - 1) A2C_STAMP(7);
     __syncthreads();
@@ -1013,7 +1060,7 @@ int toued_a2c_chain_self(EnvSpec sp, const int* levels, int N, int W, int T, int
                          float lr_a, float lr_c, float max_norm, int* step, float* loss_out, hipStream_t stream) {
   TOUED_REQUIRE(sp.tabular && sp.n_max >= 1 && sp.n_max <= 5 && sp.max_grid >= 1 && sp.max_grid * sp.max_grid <= 256,
                 "toued_a2c_chain_self: tabular env spec required");
-  TOUED_REQUIRE(N >= 0 && U >= 0 && W >= 1 && W <= 64 && toued_a2c_chain_fits(W, T, D),
+  TOUED_REQUIRE(N >= 0 && U >= 0 && W >= 1 && W <= 64 && T <= 64 && toued_a2c_chain_fits(W, T, D),
                 "toued_a2c_chain_self: N=%d U=%d W=%d T=%d D=%d unsupported", N, U, W, T, D);
   TOUED_REQUIRE(D == sp.max_grid * sp.max_grid * (1 << sp.n_max) + 1, "toued_a2c_chain_self: D=%d != obs_dim", D);
   TOUED_REQUIRE((double)N * D * 20.0 < 4294967295.0, "toued_a2c_chain_self: actor tables (%d x %d rows) exceed 4 GiB",

@@ -128,8 +128,9 @@ class A2CTrainer:
 
     def use_self_draws(self, W: int) -> bool:
         """The chain makes its own draws (toued_a2c_chain_self: the env chain's idle waves make the next update's) when
-        its env workers fit one wave and TOUED_A2C_SELF=1; otherwise the draws pass runs beside chunked launches."""
-        return W <= 64 and os.environ.get("TOUED_A2C_SELF", "0") == "1"
+        its env workers fit one wave (TOUED_A2C_SELF=0: the draws pass beside chunked launches instead; regret round
+        14.7-15.1 vs 16.6-16.7 ms, profiles/r04/c3_self_prio_r04zd.txt)."""
+        return W <= 64 and os.environ.get("TOUED_A2C_SELF", "1") != "0"
 
     def _self_updates(self, b, n, D, W, T, U, tm, ev=None):
         """All U updates in one toued_a2c_chain_self launch.  The eval draws `ev` (threefry, full chip) go first: beside
