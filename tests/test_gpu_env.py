@@ -158,7 +158,8 @@ def test_rollout_large_properties():
 
 
 @pytest.mark.parametrize("mode,N,W", [("tabular", 96, 4), ("dense", 40, 4), ("longer", 24, 4), ("all_shortlife", 64, 4),
-                                      ("all_vrandlife", 64, 4), ("sparse", 33, 3), ("debug", 17, 5)])
+                                      ("all_vrandlife", 64, 4), ("sparse", 33, 3), ("debug", 17, 5),
+                                      ("all_shortlife", 6, 64), ("mazes", 5, 128)])   # W % 64 == 0: the table kernel
 def test_eval_returns_three_launches(mode, N, W):
     """eval_agent's returns-only rollout as key chain + parallel draws + env chain (toued_eval_keys/_draws/_returns)
     is bit-identical to the single-kernel returns-only mode (itself checked against the oracle below and in

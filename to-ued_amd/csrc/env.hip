@@ -286,13 +286,17 @@ __device__ unsigned g_evr_launch;
 __global__ void k_evr_next() { if (threadIdx.x == 0) atomicAdd(&g_evr_launch, 1u); }
 #endif
 
-template <int NMAX>
+// TBL (W a multiple of 64: every wave plays one agent's level): the five candidate moves and their object tests come
+// from a per-wave transition table in LDS, [G2][5] entries next cell | (mask of the objects placed there) << 8,
+// built once per launch -- five LDS reads per step instead of five next_pos_r and object loops; the same values.
+template <int NMAX, bool TBL>
 __global__ void __launch_bounds__(256) k_eval_returns(EnvSpec sp, const int* __restrict__ levels,
                                                       const float* __restrict__ theta, int D,
                                                       const int* __restrict__ state, int T, int W, int n,
                                                       const uint4* __restrict__ draws, float* __restrict__ cum_return) {
+  __shared__ uint16_t tbl[TBL ? 4 : 1][TBL ? 256 * 5 : 1];
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n) return;   // (TBL: n is a multiple of 64, so whole waves leave)
   const int a = i / W;
   const LevR lev = lev_regs(levels + (size_t)a * LEVEL_WORDS);
   const float* tab = theta + (size_t)a * D * 5;
@@ -314,6 +318,20 @@ __global__ void __launch_bounds__(256) k_eval_returns(EnvSpec sp, const int* __r
   int objpos[NMAX];
 #pragma unroll
   for (int o = 0; o < NMAX; ++o) objpos[o] = s.obj[o] - lev_i(lev, L_OBJ_IDS + o) * G2;   // static in TAB
+  uint16_t* tw = tbl[TBL ? (threadIdx.x >> 6) : 0];
+  if (TBL) {
+    for (int c = threadIdx.x & 63; c < G2 * 5; c += 64) {
+      const int p = next_pos_r(grid, wl, c / 5, c - (c / 5) * 5);
+      int m = 0;
+#pragma unroll
+      for (int o = 0; o < NMAX; ++o)
+        if (objpos[o] == p) m |= 1 << o;
+      tw[c] = (uint16_t)(p | (m << 8));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
   float row[5];
   {
     const int idx = tab_index(sp, s);
@@ -335,11 +353,17 @@ __global__ void __launch_bounds__(256) k_eval_returns(EnvSpec sp, const int* __r
     float crow[5][5];
 #pragma unroll
     for (int act = 0; act < 5; ++act) {
-      const int p = next_pos_r(grid, wl, s.pos, act);
-      int col = 0;
+      int p, col = 0;
+      if (TBL) {
+        const uint32_t e = tw[s.pos * 5 + act];
+        p = (int)(e & 0xFFu);
+        col = (int)(e >> 8) & s.exists;
+      } else {
+        p = next_pos_r(grid, wl, s.pos, act);
 #pragma unroll
-      for (int o = 0; o < NMAX; ++o)
-        if (((s.exists >> o) & 1) && objpos[o] == p) col |= 1 << o;
+        for (int o = 0; o < NMAX; ++o)
+          if (((s.exists >> o) & 1) && objpos[o] == p) col |= 1 << o;
+      }
       cpos[act] = p;
       cex[act] = col;
       const int ci = p + G2 * ((s.exists | (int)dr.z) & ~col & used);
@@ -557,9 +581,18 @@ int toued_eval_returns(EnvSpec sp, const int* levels, const float* theta, int D,
                 n_agents, D);
   const int n = n_agents * W;
   if (n == 0) return 0;
-  TOUED_DISPATCH_NMAX(sp.n_max, true, hipLaunchKernelGGL(k_eval_returns<NMAX>, dim3(nblk(n)), dim3(256), 0, stream, sp,
-                                                        levels, theta, D, state, T, W, n,
-                                                        reinterpret_cast<const uint4*>(draws), cum_return));
+  // the per-wave transition table when every wave plays one level (TOUED_EVAL_TBL=0: the register move maths)
+  static const bool tbl_env = !(getenv("TOUED_EVAL_TBL") && strcmp(getenv("TOUED_EVAL_TBL"), "0") == 0);
+  const bool tbl = tbl_env && W % 64 == 0 && sp.max_grid * sp.max_grid <= 256;
+  if (tbl) {
+    TOUED_DISPATCH_NMAX(sp.n_max, true, hipLaunchKernelGGL((k_eval_returns<NMAX, true>), dim3(nblk(n)), dim3(256), 0,
+                                                          stream, sp, levels, theta, D, state, T, W, n,
+                                                          reinterpret_cast<const uint4*>(draws), cum_return));
+  } else {
+    TOUED_DISPATCH_NMAX(sp.n_max, true, hipLaunchKernelGGL((k_eval_returns<NMAX, false>), dim3(nblk(n)), dim3(256), 0,
+                                                          stream, sp, levels, theta, D, state, T, W, n,
+                                                          reinterpret_cast<const uint4*>(draws), cum_return));
+  }
 #ifdef H3_PLACE
   hipLaunchKernelGGL(k_evr_next, dim3(1), dim3(64), 0, stream);
 #endif
