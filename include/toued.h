@@ -51,14 +51,30 @@ int toued_abi_version(void);
 /* Opaque context: the only state the library keeps between calls (today the weight-gradient plans' reserved-CU
  * count, toued_set_reserved_cus).  A process-wide default context is current until a thread makes another one
  * current; the setting is then per thread, so two host threads driving separate streams plan independently.
- * toued_ctx_destroy of the calling thread's current context reverts that thread to the default (destroying a
- * context another thread still has current is the caller's error).  Replaces no reference interface: the
+ * toued_ctx_destroy of the calling thread's current context reverts that thread to the default; destroying a
+ * context another thread still has current is refused (-1).  The settings are atomic, so threads sharing the
+ * default context do not race on them (each sees one of the values written).  Replaces no reference interface: the
  * reference's equivalent state lives in its jitted closures. */
 typedef struct toued_ctx toued_ctx;
 toued_ctx* toued_ctx_create(void);
 int toued_ctx_destroy(toued_ctx* ctx);
 int toued_ctx_set_current(toued_ctx* ctx);   /* NULL selects the process default */
 toued_ctx* toued_ctx_current(void);
+
+/* ---- device errors and debug hooks ---- */
+/* The device error word: kernels with a bounded wait (k_a2c_chain's draw-flag wait, toued_a2c_chain_self) set a bit
+ * in it when the wait expires instead of hanging.  wait = 1: synchronise with `stream` and report any error of the
+ * work enqueued before the call; wait = 0: never block -- report what the previous call's read-back saw (if it has
+ * landed) and enqueue a new read-back.  Returns -3 and sets toued_last_error() when a bit was set (the word is then
+ * cleared), 0 otherwise.  The first call allocates the word (do it outside graph capture: toued_a2c_chain_self
+ * refuses to launch before it).  Replaces no reference interface: XLA's scan cannot starve. */
+int toued_device_error_check(hipStream_t stream, int wait);
+/* --debug (experiments/parse_args.py:7, util/jax.py:12-14 `jax.disable_jit`): hipDeviceSynchronize + hipGetLastError,
+ * -1 with the HIP error in toued_last_error() when either fails.  The host calls it after every ABI call in debug mode. */
+int toued_sync_check(void);
+/* --debug_nans (util/jax.py:9-10 `jax_debug_nans`): *out += the number of NaN/inf floats in x[0..n), stream-ordered
+ * (one grid-stride reduction, one atomic per wave). */
+int toued_nonfinite_count(const float* x, long n, int* out, hipStream_t stream);
 
 /* ---- PRNG (jax 0.4.13 threefry, environments/* and meta/* call sites) ---- */
 /* out[i][j] = jax.random.split(keys[i], num)[j] */
@@ -178,13 +194,17 @@ int toued_a2c_update(int N, int W, int T, int D, float* theta, float* vcrit, con
  * updated in place, loss_out[N][2] accumulated.  Bit-identical, update by update, to toued_rollout_env +
  * toued_a2c_update.  Tabular envs, sizes where toued_a2c_chain_fits(W, T, D) is 1 (W <= 256, W*T <= 2048). */
 int toued_a2c_chain_fits(int W, int T, int D);
+/* 1 when toued_a2c_chain_self supports these sizes: toued_a2c_chain_fits, W <= 64 (one env wave), T <= 64 (one draw
+ * flag per step); else use toued_a2c_chain with toued_rollout_draws. */
+int toued_a2c_chain_self_fits(int W, int T, int D);
 int toued_a2c_chain(EnvSpec spec, const int* levels, int N, int W, int T, int D, int U, float* theta, float* vcrit,
                     int* state, const uint32_t* draws, long dstride, float gamma, float lam, float ent_coef, float lr_a,
                     float lr_c, float max_norm, int* step, float* loss_out, hipStream_t stream);
-/* The same scan making its own draws (W <= 64): from the U update keys (keys [U][N][2], toued_key_chain's output),
+/* The same scan making its own draws (toued_a2c_chain_self_fits): from the U update keys (keys [U][N][2], toued_key_chain's output),
  * each workgroup makes update u + 1's draws in the waves its env chain leaves idle during update u, into scratch
  * u32 [N][2][T][W][4] (a per-agent double buffer).  Bit-identical to toued_rollout_draws + toued_a2c_chain over the
- * same keys, with no draws pass in front of or beside the launch. */
+ * same keys, with no draws pass in front of or beside the launch.  A draw wave whose wait for the key wave expires
+ * sets a bit of the device error word (toued_device_error_check), which must have been allocated first. */
 int toued_a2c_chain_self(EnvSpec spec, const int* levels, int N, int W, int T, int D, int U, float* theta, float* vcrit,
                          int* state, const uint32_t* keys, uint32_t* scratch, float gamma, float lam, float ent_coef,
                          float lr_a, float lr_c, float max_norm, int* step, float* loss_out, hipStream_t stream);

@@ -52,12 +52,20 @@ def test_scatter_into_sink_drops_writes():
 
 
 def test_self_draws_selection(monkeypatch):
-    """toued_a2c_chain_self is the default when the env chain fits one wave (TOUED_A2C_SELF=0 turns it off)."""
+    """toued_a2c_chain_self is the default when the env chain fits one wave and the steps fit its draw flags
+    (toued_a2c_chain_self_fits: W <= 64, T <= 64; TOUED_A2C_SELF=0 turns it off).  A long rollout that the chunked
+    chain handles (T = 100, W = 16: W*T <= 2048) must fall back to it instead of failing in toued_a2c_chain_self."""
+    from toued import _lib
     from toued.a2c import A2CTrainer
+    D = 13 * 13 * 2 + 1
     monkeypatch.delenv("TOUED_A2C_SELF", raising=False)
-    assert A2CTrainer.use_self_draws(None, 64) and not A2CTrainer.use_self_draws(None, 128)
+    sd = lambda W, T: A2CTrainer.use_self_draws(None, W, T, D)
+    assert sd(64, 20) and not sd(128, 20)
     monkeypatch.setenv("TOUED_A2C_SELF", "1")
-    assert A2CTrainer.use_self_draws(None, 64) and A2CTrainer.use_self_draws(None, 32)
-    assert not A2CTrainer.use_self_draws(None, 128)
+    assert sd(64, 20) and sd(32, 20) and sd(32, 64)
+    assert not sd(128, 20)
+    assert not sd(16, 100) and not sd(16, 65)
+    assert _lib.lib().toued_a2c_chain_fits(16, 100, D) == 1      # the chunked chain takes T = 100
+    assert _lib.lib().toued_a2c_chain_self_fits(16, 100, D) == 0
     monkeypatch.setenv("TOUED_A2C_SELF", "0")
-    assert not A2CTrainer.use_self_draws(None, 64)
+    assert not sd(64, 20)

@@ -161,7 +161,7 @@ def test_a2c_chain_matches_launch_per_update(mode, W, U, self_draws, monkeypatch
         step = torch.zeros(N, dtype=torch.int32, device="cuda")
         tr = A2CTrainer(ro, A2CHyperparams(), _ahyp(mode), use_graph=False, chain=chain)
         assert tr.use_chain(W, T, D) == chain
-        assert tr.use_self_draws(W) == (self_draws == "1")
+        assert tr.use_self_draws(W, T, D) == (self_draws == "1")
         loss = tr.train(rng, th, vc, step, levels, st, U)
         outs.append((th, vc, st, step, loss))
     for x, y, name in zip(outs[0], outs[1], ("theta", "vcrit", "state", "step", "loss")):

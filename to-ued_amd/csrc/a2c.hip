@@ -714,7 +714,8 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
                                                    long dstride, const uint32_t* __restrict__ ukeys,
                                                    uint4* __restrict__ dscr, float gamma, float lam, float ent_coef,
                                                    float lr_a, float lr_c, float max_norm, int* __restrict__ step,
-                                                   float* __restrict__ loss_out) {
+                                                   float* __restrict__ loss_out, unsigned* __restrict__ err,
+                                                   int test_skip_publish) {
   extern __shared__ float lds[];
   __shared__ A2CShared sh;
 #ifndef A2C_PRIO
@@ -771,7 +772,9 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
   // SELF, during update u's env chain: wave 1 runs update uu = u + 1's key chain into LDS (the update's per-sample
   // vectors, free until the update body), step by step behind a flag; waves 2 and 3 make the draws of alternate steps
   // from it.  Flags hold uu + 1 (updates only grow, so a stale flag never matches); a wait that never ends stops
-  // after ~2^20 sleeps instead of hanging (wrong draws, not a hang: the bit-exact tests would fail).
+  // after ~2^20 sleeps instead of hanging and sets TOUED_DEVERR_A2C_DRAW_WAIT in the device error word `err`, which
+  // the host turns into an error (toued_device_error_check): the draws it then makes are from stale keys.
+  // test_skip_publish = 1 (tests only, TOUED_TEST_A2C_SKIP_PUBLISH): the key wave never publishes step 0 of update 1.
   uint4* kl = reinterpret_cast<uint4*>(vec);   // [T][W] (sub, sub_env)
 #ifndef A2C_SELF_PRIO
 #define A2C_SELF_PRIO 0
@@ -788,16 +791,20 @@ __global__ void __launch_bounds__(256) k_a2c_chain(EnvSpec sp, const int* __rest
         split2(r, r, sub_env);
         if (ln < W) kl[t * W + ln] = make_uint4(sub.x, sub.y, sub_env.x, sub_env.y);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (ln == 0) __hip_atomic_store(&sh.dflag[t], uu + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (ln == 0 && !(test_skip_publish && uu == 1 && t == 0))
+          __hip_atomic_store(&sh.dflag[t], uu + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     } else {
       const int* levp = levels + (size_t)a * LEVEL_WORDS;
       draw4* out = reinterpret_cast<draw4*>(dscr) + (size_t)(a * 2 + slot) * T * W + ln;
       for (int t = wv - 2; t < T; t += 2) {
-        for (int it = 0; it < (1 << 20); ++it) {
-          if (__hip_atomic_load(&sh.dflag[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == uu + 1) break;
-          __builtin_amdgcn_s_sleep(1);
+        bool seen = false;
+        for (int it = 0; it < (1 << 20) && !seen; ++it) {
+          seen = __hip_atomic_load(&sh.dflag[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == uu + 1;
+          if (!seen) __builtin_amdgcn_s_sleep(1);
         }
+        // a vector atomic from one lane (err is a plain device word; never a scalar-cache write)
+        if (!seen && ln == 0 && err) atomicOr(err, TOUED_DEVERR_A2C_DRAW_WAIT);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         if (ln < W) {
           const uint4 k4 = kl[t * W + ln];
@@ -1001,6 +1008,10 @@ int toued_a2c_update(int N, int W, int T, int D, float* theta, float* vcrit, con
 
 // 1 when toued_a2c_chain supports these sizes: the fused update's and W <= 256 workers (one per thread)
 int toued_a2c_chain_fits(int W, int T, int D) { return W <= 256 && toued_a2c_update_fits(W, T, D) ? 1 : 0; }
+// 1 when toued_a2c_chain_self does: the env chain in one wave (W <= 64) and one draw flag per step (T <= 64)
+int toued_a2c_chain_self_fits(int W, int T, int D) {
+  return W >= 1 && W <= 64 && T >= 1 && T <= 64 && toued_a2c_chain_fits(W, T, D) ? 1 : 0;
+}
 
 // U A2C updates (rollout + fused update each) of N antagonists in one launch: theta [N][D][5], vcrit [N][D], step
 // [N], state [S_FIELDS][N*W] updated in place, loss_out [N][2] accumulated; draws = toued_rollout_draws' output for
@@ -1032,7 +1043,7 @@ int toued_a2c_chain(EnvSpec sp, const int* levels, int N, int W, int T, int D, i
     }                                                                                                                 \
     hipLaunchKernelGGL((k_a2c_chain<NM, CD, false>), dim3(N), dim3(256), lds, stream, sp, levels, W, T, D, U, theta,  \
                        vcrit, state, reinterpret_cast<const uint4*>(draws), dstride, nullptr, nullptr, gamma, lam,    \
-                       ent_coef, lr_a, lr_c, max_norm, step, loss_out);                                               \
+                       ent_coef, lr_a, lr_c, max_norm, step, loss_out, nullptr, 0);                                   \
   }
 #define TOUED_A2C_CHAIN_CASE(NM)                                                                                     \
   case NM:                                                                                                            \
@@ -1060,13 +1071,17 @@ int toued_a2c_chain_self(EnvSpec sp, const int* levels, int N, int W, int T, int
                          float lr_a, float lr_c, float max_norm, int* step, float* loss_out, hipStream_t stream) {
   TOUED_REQUIRE(sp.tabular && sp.n_max >= 1 && sp.n_max <= 5 && sp.max_grid >= 1 && sp.max_grid * sp.max_grid <= 256,
                 "toued_a2c_chain_self: tabular env spec required");
-  TOUED_REQUIRE(N >= 0 && U >= 0 && W >= 1 && W <= 64 && T <= 64 && toued_a2c_chain_fits(W, T, D),
+  TOUED_REQUIRE(N >= 0 && U >= 0 && toued_a2c_chain_self_fits(W, T, D),
                 "toued_a2c_chain_self: N=%d U=%d W=%d T=%d D=%d unsupported", N, U, W, T, D);
   TOUED_REQUIRE(D == sp.max_grid * sp.max_grid * (1 << sp.n_max) + 1, "toued_a2c_chain_self: D=%d != obs_dim", D);
   TOUED_REQUIRE((double)N * D * 20.0 < 4294967295.0, "toued_a2c_chain_self: actor tables (%d x %d rows) exceed 4 GiB",
                 N, D);
   TOUED_REQUIRE(keys && scratch, "toued_a2c_chain_self: null keys / scratch");
+  unsigned* err = toued::dev_err_word();
+  TOUED_REQUIRE(err, "toued_a2c_chain_self: call toued_device_error_check once first (it allocates the device error "
+                "word, outside any graph capture)");
   if (N == 0 || U == 0) return 0;
+  const int skip_pub = getenv("TOUED_TEST_A2C_SKIP_PUBLISH") && atoi(getenv("TOUED_TEST_A2C_SKIP_PUBLISH"));
   const size_t lds = a2c_update_lds(W, T) + ((size_t)sp.max_grid * sp.max_grid * 5 * 2 + 3) / 4 * 4;
   static bool attr_set[6] = {};
 #define TOUED_A2C_SELF_CASE(NM)                                                                                      \
@@ -1079,7 +1094,7 @@ int toued_a2c_chain_self(EnvSpec sp, const int* levels, int N, int W, int T, int
     }                                                                                                                 \
     hipLaunchKernelGGL((k_a2c_chain<NM, false, true>), dim3(N), dim3(256), lds, stream, sp, levels, W, T, D, U, theta, \
                        vcrit, state, nullptr, 0L, keys, reinterpret_cast<uint4*>(scratch), gamma, lam, ent_coef,      \
-                       lr_a, lr_c, max_norm, step, loss_out);                                                         \
+                       lr_a, lr_c, max_norm, step, loss_out, err, skip_pub);                                          \
     break;
   switch (sp.n_max) {
     TOUED_A2C_SELF_CASE(1)

@@ -10,6 +10,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <atomic>
 
 #define TOUED_DEV __device__ __forceinline__
 
@@ -206,11 +207,16 @@ TOUED_DEV float erfinv_giles(float x) {
 // ----------------------------------------------------------------------------
 // Error reporting for the C ABI
 struct toued_ctx {
-  int reserved_cus;   // CUs the weight-gradient reductions' split-K plans leave free (toued_set_reserved_cus)
+  std::atomic<int> reserved_cus{0};   // CUs the weight-gradient reductions' split-K plans leave free (toued_set_reserved_cus)
+  std::atomic<int> users{0};          // host threads that have this context current (toued_ctx_set_current)
 };
+// Device error word (capi.hip): a kernel whose bounded wait expires ORs one of these bits into it instead of hanging;
+// the host reads it with toued_device_error_check, which turns a set bit into -3 + toued_last_error().
+#define TOUED_DEVERR_A2C_DRAW_WAIT 1u   // k_a2c_chain<SELF>: a draw wave's flag wait for the key wave gave up
 namespace toued {
 void set_error(const char* fmt, ...);
 toued_ctx* current_ctx();   // the calling thread's current context, else the process default (capi.hip)
+unsigned* dev_err_word();   // the device error word (allocated by the first toued_device_error_check; nullptr before)
 }
 #define TOUED_CHECK_LAUNCH()                                                   \
   do {                                                                         \

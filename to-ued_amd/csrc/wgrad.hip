@@ -701,7 +701,10 @@ static Plan plan(int ra, int rb, long K) {
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
     cus = 256;
-  cus = cus - toued::current_ctx()->reserved_cus > cus / 2 ? cus - toued::current_ctx()->reserved_cus : cus / 2;
+  {
+    const int rsv = toued::current_ctx()->reserved_cus.load();
+    cus = cus - rsv > cus / 2 ? cus - rsv : cus / 2;
+  }
   // x6: one workgroup per CU (104 KB LDS), as many K chunks as fill the CUs in one round.  f32 NRT = 17:
   // two workgroups per CU (125 VGPRs, 68 KB LDS each).  NRT = 1 is a bandwidth-bound stream over B: four
   // workgroups per CU keep enough loads in flight.
@@ -733,10 +736,7 @@ int toued_dbg_wgrad_stamps(unsigned long long* host) {
 #endif
 
 int toued_set_reserved_cus(int n) {
-  toued_ctx* c = toued::current_ctx();
-  const int prev = c->reserved_cus;
-  c->reserved_cus = n > 0 ? n : 0;
-  return prev;
+  return toued::current_ctx()->reserved_cus.exchange(n > 0 ? n : 0);
 }
 
 size_t toued_wgrad_workspace_floats(int ra, int rb, long K) {
@@ -864,7 +864,10 @@ static Plan plan_bfp(int ra, int rb, long K) {
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
     cus = 256;
-  cus = cus - toued::current_ctx()->reserved_cus > cus / 2 ? cus - toued::current_ctx()->reserved_cus : cus / 2;
+  {
+    const int rsv = toued::current_ctx()->reserved_cus.load();
+    cus = cus - rsv > cus / 2 ? cus - rsv : cus / 2;
+  }
   cus = cus - h3_slack() > cus / 2 ? cus - h3_slack() : cus / 2;
   int S = cus / p.ncol;
   if (S < 1) S = 1;

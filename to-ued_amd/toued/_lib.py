@@ -97,6 +97,10 @@ _SIGS = {
     "toued_meta_metrics": [_I, _I, _P, _F, _P, _F, _F, _F, _F, _P, _P],
     "toued_entropy_clip": [_I, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _F, _F, _F, _P, _P],
     "toued_a2c_chain_fits": [_I, _I, _I],
+    "toued_a2c_chain_self_fits": [_I, _I, _I],
+    "toued_device_error_check": [_P, _I],
+    "toued_sync_check": [],
+    "toued_nonfinite_count": [_P, _L, _P, _P],
     "toued_a2c_chain": [EnvSpecC, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _P, _P, _P],
     "toued_a2c_chain_self": [EnvSpecC, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _F, _P, _P, _P],
     "toued_gru_pack_fwd_multi": [_P, _L, _I, _P, _I, _P, _P],
@@ -162,13 +166,34 @@ def stream_ptr():
     return torch.cuda.current_stream().cuda_stream
 
 
+# --debug (util/jax.py:12-14): every ABI call is followed by a device synchronise and an error check, so an
+# asynchronous kernel fault is reported at the call that launched it (toued.debug.configure)
+_DEBUG_SYNC = False
+
+
+def set_debug_sync(on: bool) -> None:
+    global _DEBUG_SYNC
+    _DEBUG_SYNC = bool(on)
+
+
 def call(name: str, *args):
     fn = getattr(lib(), name)
     rc = fn(*args)
     if rc != 0:
         msg = lib().toued_last_error().decode(errors="replace")
         raise ToUEDError(f"{name} failed ({rc}): {msg}")
+    if _DEBUG_SYNC and not torch.cuda.is_current_stream_capturing():   # (a captured graph is checked at replay)
+        if lib().toued_sync_check() != 0:
+            msg = lib().toued_last_error().decode(errors="replace")
+            raise ToUEDError(f"{name}: {msg} (--debug: checked after the call)")
     return rc
+
+
+def check_device_errors(wait: bool = False) -> None:
+    """Raise ToUEDError if a kernel set the device error word (a bounded wait that expired, toued.h
+    toued_device_error_check).  wait=False never blocks: it reports the previous call's read-back and enqueues a new
+    one on the current stream; wait=True synchronises with the current stream first."""
+    call("toued_device_error_check", stream_ptr(), int(bool(wait)))
 
 
 def env_spec_c(spec) -> EnvSpecC:

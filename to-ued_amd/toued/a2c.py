@@ -17,6 +17,7 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
+from .debug import debug_sync
 from .agents import AgentHyperparams
 from .env import LEVEL_WORDS
 from .rollout import RolloutWrapper, Transition, split_rollouts
@@ -126,11 +127,13 @@ class A2CTrainer:
             return False
         return bool(_lib.lib().toued_a2c_chain_fits(W, T, D))
 
-    def use_self_draws(self, W: int) -> bool:
+    def use_self_draws(self, W: int, T: int, D: int) -> bool:
         """The chain makes its own draws (toued_a2c_chain_self: the env chain's idle waves make the next update's) when
-        its env workers fit one wave (TOUED_A2C_SELF=0: the draws pass beside chunked launches instead; regret round
-        14.7-15.1 vs 16.6-16.7 ms, profiles/r04/c3_self_prio_r04zd.txt)."""
-        return W <= 64 and os.environ.get("TOUED_A2C_SELF", "1") != "0"
+        its env workers fit one wave and its steps the draw flags (toued_a2c_chain_self_fits: W <= 64, T <= 64;
+        TOUED_A2C_SELF=0: the draws pass beside chunked launches instead; regret round 14.7-15.1 vs 16.6-16.7 ms,
+        profiles/r04/c3_self_prio_r04zd.txt)."""
+        return (os.environ.get("TOUED_A2C_SELF", "1") != "0"
+                and bool(_lib.lib().toued_a2c_chain_self_fits(W, T, D)))
 
     def _self_updates(self, b, n, D, W, T, U, tm, ev=None):
         """All U updates in one toued_a2c_chain_self launch.  The eval draws `ev` (threefry, full chip) go first: beside
@@ -238,7 +241,7 @@ class A2CTrainer:
         L.call("toued_key_chain", L.ptr(b["rng"]), n, U, L.ptr(b["chain"]), st)
         tm = self.timers if self.timers is not None and self.timers.enabled else None
         if record is None and self.use_chain(W, T, D):
-            if self.use_self_draws(W):
+            if self.use_self_draws(W, T, D):
                 self._self_updates(b, n, D, W, T, U, tm, ev)
             else:
                 self._chain_updates(b, n, D, W, T, U, tm, ev)
@@ -316,6 +319,9 @@ class A2CTrainer:
             b[name].copy_(src)
         ev = self._eval_bufs(b, eval_keys, eval_levels, W) if eval_keys is not None else None
         self.eval_draws_out = b["ev_draws"] if ev is not None else None
+        # the device error word (a draw wave's expired wait in toued_a2c_chain_self): allocated here, outside any
+        # capture, on the first call; reports what an earlier round's read-back saw without blocking
+        _lib.check_device_errors(wait=False)
         self._graph = self._graphs.get(ev is not None)
         if self.record is not None or (self.timers is not None and self.timers.enabled):
             self._updates(b, n, D, W, T, U, self.record, ev)
@@ -338,6 +344,8 @@ class A2CTrainer:
             self._graph.replay()
         else:
             self._updates(b, n, D, W, T, U, ev=ev)
+        # read the error word back behind this round (raised at the next round's check, or here under --debug)
+        _lib.check_device_errors(wait=debug_sync())
         theta.copy_(b["theta"])
         vcrit.copy_(b["vcrit"].reshape(vcrit.shape))
         step.copy_(b["step"])

@@ -25,6 +25,7 @@ import numpy as np
 import torch
 
 from . import _lib, prng
+from .debug import nan_checker
 from .agents import eval_agent, eval_agent_reset
 from .lpg import LPGLayout
 from .meta import lpg_inputs_fn
@@ -338,6 +339,7 @@ class ESTrainStep:
         else:
             fitness = eval_agent(self.ro, fit_keys, levels, self.theta[cur], W)
         self.fitness = fitness
+        nan_checker().check("es_fitness", fitness)
         # ---- rank per antithetic pair, winners (:199-211)
         first_greater = fitness[0::2] > fitness[1::2]
         rank = torch.empty_like(fitness)
@@ -353,6 +355,7 @@ class ESTrainStep:
         rank_all = self.world.all_gather_cat(rank) if multi else rank
         self.es.track_best(self.x, rank_all, 2 * lo, self.world if multi else None)
         self.es.tell(self.x, rank, self.world if multi else None)
+        nan_checker().check("es_mean_after_tell", self.es.mean)
         inv = 1.0 / (W * T * max(K, 1))
         m = self.met * inv
         fit_all = fitness if self.world is None or self.world.size == 1 else self.world.all_gather_cat(fitness)

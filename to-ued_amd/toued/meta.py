@@ -23,6 +23,7 @@ import torch
 
 from . import _lib, prng
 from .agents import AgentBatch
+from .debug import nan_checker
 from .lpg import LPGGRU, LPGLayout, Y
 from .rollout import RolloutWrapper, Transition, split_rollouts
 
@@ -244,9 +245,11 @@ class MetaGradStep:
         n_total = n_all
         if self.world is not None and self.world.size > 1:
             self.world.all_reduce_sum(self.grad)
+        nan_checker().check("meta_gradient", self.grad)
         adam.count += 1
         _lib.call("toued_adam", self.lay.size, _lib.ptr(eta), _lib.ptr(self.grad), _lib.ptr(adam.m), _lib.ptr(adam.v),
                   float(n_total), self.hyp.lpg_lr, 0.9, 0.999, 1e-8, adam.count, _lib.stream_ptr())
+        nan_checker().check("eta_after_adam", eta)
         if len(parts) == 1:
             return parts[0]
         return _cat_metrics(parts)
@@ -305,6 +308,7 @@ class MetaGradStep:
                 self.ro.batch_rollout(self.keys_roll[k], self.theta_h[k], agents.levels, state, out=tk,
                                       inplace_state=True)
             self.timers.stop(tok)
+            nan_checker().check("rollout_rewards", tk.reward)
             L.call(lpg_inputs_fn(R, W), N, W, T, D, self.F, ptr(self.theta_h[k]), ptr(self.phi_h[k]),
                    ptr(tk.obs_idx), ptr(tk.obs_time), ptr(tk.action), ptr(tk.reward), ptr(tk.done),
                    ptr(e1w), ptr(e1b), ptr(e2w), ptr(e2b), ptr(agents.step), ptr(agents.levels),
@@ -312,6 +316,7 @@ class MetaGradStep:
             tok = self.timers.start("gru_fwd")
             self.gru.forward(k, self.X, tk.done, eta, self.pi_hat, self.y_hat)
             self.timers.stop(tok)
+            nan_checker().check("lpg_outputs", self.pi_hat[k], self.y_hat[k])
             if self.fused_step:
                 main.wait_stream(self.side)
                 L.call("toued_agent_step", N, W, T, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]),
@@ -330,6 +335,7 @@ class MetaGradStep:
                        ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(self.gstat[k]), st)
             L.call("toued_entropy", N, W, T, D, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(tk.obs_idx),
                    ptr(tk.obs_time), ptr(self.met[k]), 0.0, 0.0, None, None, st)
+            nan_checker().check("agent_params", self.theta_h[k + 1], self.phi_h[k + 1])
         # ---------------- value critic on the train rollouts (--fix_value_critic), eval rollout, lpg loss
         if hyp.fix_value_critic:
             self.vc_loss.zero_()
@@ -456,6 +462,7 @@ class MetaGradStep:
         ea_cum = ea["cum"]
         ea_cum.record_stream(main)
         ea["state"].record_stream(main)
+        nan_checker().check("eval_returns", ea_cum)
         agents.theta.copy_(self.theta_h[K])
         agents.phi.copy_(self.phi_h[K])
         # (met * inv_wt).mean over the K updates and the regularised loss, one launch (toued_meta_metrics)

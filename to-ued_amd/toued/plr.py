@@ -25,6 +25,7 @@ import torch
 
 from . import _lib, prng
 from .a2c import A2CHyperparams, A2CTrainer
+from .debug import nan_checker
 from .agents import AgentBatch, create_agents, eval_agent, eval_agent_reset
 from .env import L_BUFID
 
@@ -143,6 +144,7 @@ def plr_sample(sampler, rng: torch.Tensor, buffer, agents: AgentBatch, term: tor
         if sel.numel():
             score[sel] = algorithmic_regret(sampler, keys[sel].contiguous(), agents.levels[sel].contiguous(),
                                             agents.theta[sel].contiguous())
+    nan_checker().check("regret_scores", score)
     old_ids = agents.levels[:, L_BUFID].contiguous()
     if world is not None and world.active:
         term_g = world.all_gather_cat(term.to(torch.int32)).bool()

@@ -19,7 +19,8 @@ import time
 import numpy as np
 import torch
 
-from . import prng
+from . import _lib, prng
+from .debug import configure as configure_debug
 from .dist import World, init_from_env
 from .level_sampler import LevelSampler
 from .lpg import flax_init_lpg_params
@@ -43,6 +44,8 @@ class Trainer:
     def __init__(self, args, world: World | None = None, device=None):
         check_supported(args)
         self.args = args
+        # util/jax.py:5-17: --debug_nans raises at the first non-finite stage, --debug checks every call synchronously
+        self.nans = configure_debug(debug=getattr(args, "debug", False), debug_nans=getattr(args, "debug_nans", False))
         self.world = world or World()
         self.dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         sl = self.world.agent_slice(args.num_agents) if self.world.size > 1 else None
@@ -87,7 +90,12 @@ class Trainer:
         ks = prng.split(self.rng, 2)
         self.rng, sub = ks[0].contiguous(), ks[1].contiguous()
         self.buffer, self.agents = self.sampler.sample(sub, self.buffer, self.agents, self.sl)
+        self.nans.raise_if_any()
         return metrics
+
+    def finish(self):
+        """End of training: report any device error a round left behind (synchronising once)."""
+        _lib.check_device_errors(wait=True)
 
 
 def reduce_metrics(m, world: World):
@@ -117,6 +125,7 @@ def main(cmd_args=None):
         history.append(m)
         if world.rank == 0:
             print(json.dumps({"step": i, "elapsed_s": round(time.time() - t0, 3), **m}), flush=True)
+    tr.finish()
     if args.checkpoint_dir and world.rank == 0:
         save_final_checkpoints(args.checkpoint_dir, tr, steps)
     return history
