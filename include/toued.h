@@ -360,6 +360,11 @@ int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit
  * round.  Workspace sizes queried before the change stay sufficient (fewer chunks).  Sets the current context's
  * value (toued_ctx_current) and returns its previous value. */
 int toued_set_reserved_cus(int n);
+/* Tests only: count every tile claim of the following toued_wgrad_bfp launches into visits[tile] (device int array of
+ * `capacity` entries, the caller zeroes it; capacity 0 switches counting off), and the tile count of the last launch.
+ * A tile claimed twice or never by k_wgrad_h3's per-XCD queues shows as a count != 1. */
+int toued_dbg_wgrad_visits(int* visits, int capacity);
+int toued_dbg_wgrad_last_ntiles(void);
 
 /* toued_agent_grad + toued_agent_apply fused, in place, for an agent chain that never reads the gradient tables
  * (the ES candidates): clip + SGD on theta [N][D][5] / phi [N][D][8] of the touched rows only (bit-identical to

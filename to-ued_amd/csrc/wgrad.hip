@@ -378,7 +378,8 @@ __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict
                                                         int a_unit_rows, const int* __restrict__ rowmax_bits,
                                                         const float* __restrict__ B, long ldb, int rb,
                                                         const int8_t* __restrict__ colexp, long K, long kchunk,
-                                                        float* __restrict__ part, int ntiles, int* __restrict__ qctr) {
+                                                        float* __restrict__ part, int ntiles, int* __restrict__ qctr,
+                                                        int* __restrict__ visits) {
   constexpr int NT = 64 * NW;
   constexpr int CT = 16 * BT * NW;                          // B rows per workgroup
   constexpr int NS = (X6_AQ + NT - 1) / NT;                 // A staging rounds per thread
@@ -412,6 +413,8 @@ __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict
       if (f + b < cnt) got = ncol * (q * per + (q < rem ? q : rem)) + (y == 0 ? f : cnt - 1 - b);
     }
     s_slot = got;
+    // tests only (toued_dbg_wgrad_visits): count each claimed tile, so a tile claimed twice or never shows
+    if (visits && got >= 0) atomicAdd(&visits[got], 1);
   }
   __syncthreads();
   const int L = s_slot;
@@ -879,6 +882,18 @@ static Plan plan_bfp(int ra, int rb, long K) {
   return p;
 }
 
+// tests only: per-tile claim counters of the next toued_wgrad_bfp launches (visits[tile] += 1 per claim; nullptr
+// switches it off), and the tile count of the last launch
+static int* g_dbg_visits = nullptr;
+static int g_dbg_visits_cap = 0;
+static int g_dbg_last_ntiles = 0;
+int toued_dbg_wgrad_visits(int* visits, int capacity) {
+  g_dbg_visits = capacity > 0 ? visits : nullptr;
+  g_dbg_visits_cap = capacity > 0 ? capacity : 0;
+  return 0;
+}
+int toued_dbg_wgrad_last_ntiles(void) { return g_dbg_last_ntiles; }
+
 size_t toued_wgrad_bfp_workspace_floats(int ra, int rb, long K) {
   if (ra <= 0 || rb <= 0 || K <= 0) return 0;
   const Plan p = plan_bfp(ra, rb, K);
@@ -910,12 +925,14 @@ int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit
     hipLaunchKernelGGL(k_wgrad_rowmax, dim3((unsigned)((K + kper - 1) / kper), nmeas), dim3(256), 0, stream, A, lda,
                        a_unit_rows, K, kper, bits);
   }
+  int* visits = g_dbg_visits && ntiles <= g_dbg_visits_cap ? g_dbg_visits : nullptr;
+  g_dbg_last_ntiles = ntiles;
   if (wgrad_h8())
     hipLaunchKernelGGL((k_wgrad_h3<8, 2>), dim3(grid), dim3(512), 0, stream, A, lda, ra, a_unit_rows, bits, B,
-                       ldb, rb, col_exp, K, p.kchunk, work, ntiles, qctr);
+                       ldb, rb, col_exp, K, p.kchunk, work, ntiles, qctr, visits);
   else
     hipLaunchKernelGGL((k_wgrad_h3<X6_NW, X6_BT>), dim3(grid), dim3(64 * X6_NW), 0, stream, A, lda, ra,
-                       a_unit_rows, bits, B, ldb, rb, col_exp, K, p.kchunk, work, ntiles, qctr);
+                       a_unit_rows, bits, B, ldb, rb, col_exp, K, p.kchunk, work, ntiles, qctr, visits);
 #ifdef H3_PLACE
   hipLaunchKernelGGL(k_h3_next, dim3(1), dim3(64), 0, stream);
 #endif

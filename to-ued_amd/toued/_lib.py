@@ -101,6 +101,8 @@ _SIGS = {
     "toued_device_error_check": [_P, _I],
     "toued_sync_check": [],
     "toued_nonfinite_count": [_P, _L, _P, _P],
+    "toued_dbg_wgrad_visits": [_P, _I],
+    "toued_dbg_wgrad_last_ntiles": [],
     "toued_a2c_chain": [EnvSpecC, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _P, _P, _P],
     "toued_a2c_chain_self": [EnvSpecC, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _F, _P, _P, _P],
     "toued_gru_pack_fwd_multi": [_P, _L, _I, _P, _I, _P, _P],
@@ -171,6 +173,13 @@ def stream_ptr():
 _DEBUG_SYNC = False
 
 
+def _capturing() -> bool:
+    try:
+        return torch.cuda.is_current_stream_capturing()
+    except RuntimeError:     # no device: nothing can be capturing
+        return False
+
+
 def set_debug_sync(on: bool) -> None:
     global _DEBUG_SYNC
     _DEBUG_SYNC = bool(on)
@@ -182,7 +191,7 @@ def call(name: str, *args):
     if rc != 0:
         msg = lib().toued_last_error().decode(errors="replace")
         raise ToUEDError(f"{name} failed ({rc}): {msg}")
-    if _DEBUG_SYNC and not torch.cuda.is_current_stream_capturing():   # (a captured graph is checked at replay)
+    if _DEBUG_SYNC and not _capturing():   # (a captured graph is checked at replay)
         if lib().toued_sync_check() != 0:
             msg = lib().toued_last_error().decode(errors="replace")
             raise ToUEDError(f"{name}: {msg} (--debug: checked after the call)")
