@@ -75,6 +75,9 @@ int toued_sync_check(void);
 /* --debug_nans (util/jax.py:9-10 `jax_debug_nans`): *out += the number of NaN/inf floats in x[0..n), stream-ordered
  * (one grid-stride reduction, one atomic per wave). */
 int toued_nonfinite_count(const float* x, long n, int* out, hipStream_t stream);
+/* the same over rows x cols floats with row pitch ld (a column block of an [rows][ld] operand, e.g. one inner update's
+ * GRU state saves) */
+int toued_nonfinite_count_2d(const float* x, long rows, long cols, long ld, int* out, hipStream_t stream);
 
 /* ---- PRNG (jax 0.4.13 threefry, environments/* and meta/* call sites) ---- */
 /* out[i][j] = jax.random.split(keys[i], num)[j] */

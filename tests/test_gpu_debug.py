@@ -1,8 +1,8 @@
 """GPU tests of the reference's debug hooks (util/jax.py:5-17) and of the device error word.
 
 * toued_nonfinite_count (--debug_nans' per-stage reduction) against torch.isfinite at several sizes;
-* --debug_nans: a NaN poisoned into eta raises FloatingPointError at the first stage it reaches (the LPG outputs of
-  inner update 0), a clean run raises nothing and matches the run without the flag bit for bit;
+* --debug_nans: a NaN poisoned into eta raises FloatingPointError at the first stage it reaches (the GRU states or
+  the LPG outputs of inner update 0), a clean run raises nothing and matches the run without the flag bit for bit;
 * --debug: the meta-step with a synchronise + error check after every ABI call equals the normal one;
 * toued_a2c_chain_self's bounded flag wait: with the key wave's publish of one step suppressed
   (TOUED_TEST_A2C_SKIP_PUBLISH, tests only) the expired wait is reported as ToUEDError through
@@ -38,6 +38,18 @@ def test_nonfinite_count_matches_torch(n):
     assert out.cpu().tolist() == [0, 2 * int((~torch.isfinite(x)).sum())]
 
 
+def test_nonfinite_count_2d_column_block():
+    from toued import _lib
+    x = torch.randn(40, 1000, device="cuda")
+    x[3, 10] = float("nan")     # inside the block
+    x[7, 600] = float("inf")    # inside
+    x[5, 999] = float("nan")    # outside (column 999 >= 100 + 700)
+    blk = x[:, 100:800]
+    out = torch.zeros(1, dtype=torch.int32, device="cuda")
+    _lib.call("toued_nonfinite_count_2d", blk.data_ptr(), 40, 700, 1000, _lib.ptr(out), _lib.stream_ptr())
+    assert int(out) == int((~torch.isfinite(blk)).sum()) == 1 + 0 * 0 + (1 if 600 - 100 < 700 else 0)
+
+
 def _trainer(extra=()):
     from toued.parse_args import parse_args
     from toued.train import Trainer
@@ -46,11 +58,15 @@ def _trainer(extra=()):
     return Trainer(args)
 
 
-def test_debug_nans_poisoned_eta_raises_at_lpg_outputs():
+@pytest.mark.parametrize("param,stage", [("hr_w", "lpg_gru_states"), ("pi_w", "lpg_outputs")])
+def test_debug_nans_poisoned_eta_raises_at_first_stage(param, stage):
+    """A NaN in a recurrent weight (or in the embedding MLP that feeds the GRU inputs) first shows in the GRU states
+    of inner update 0 (the heads read relu(h) = max(h, 0), which maps it to 0 on the device); one in a head weight in
+    the LPG outputs."""
     tr = _trainer(["--debug_nans"])
-    off = tr.step_fn.lay.offsets["hr_w"]          # a recurrent GRU weight: every LPG output of the step turns NaN
+    off = tr.step_fn.lay.offsets[param]
     tr.eta[off + 5] = float("nan")
-    with pytest.raises(FloatingPointError, match="stage 'lpg_outputs'"):
+    with pytest.raises(FloatingPointError, match=f"stage '{stage}'"):
         tr.meta_step()
 
 

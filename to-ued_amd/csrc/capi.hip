@@ -49,6 +49,18 @@ __global__ void __launch_bounds__(256) k_nonfinite_count(const float* __restrict
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
 }
+// the same over a row-strided block x[r * ld + c], r < rows, c < cols (blockIdx.y strides the rows)
+__global__ void __launch_bounds__(256) k_nonfinite_count_2d(const float* __restrict__ x, long rows, long cols, long ld,
+                                                             int* __restrict__ out) {
+  int c = 0;
+  for (long r = blockIdx.y; r < rows; r += gridDim.y)
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < cols; i += (long)gridDim.x * 256) {
+      const unsigned b = __float_as_uint(x[r * ld + i]);
+      c += (b & 0x7F800000u) == 0x7F800000u;
+    }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+}
 }  // namespace
 
 extern "C" {
@@ -141,6 +153,18 @@ int toued_nonfinite_count(const float* x, long n, int* out, hipStream_t stream) 
   if (n == 0) return 0;
   const long blocks = (n + 255) / 256;
   hipLaunchKernelGGL(k_nonfinite_count, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0, stream, x, n,
+                     out);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+// the same for a row-strided block: rows x cols floats, row pitch ld >= cols
+int toued_nonfinite_count_2d(const float* x, long rows, long cols, long ld, int* out, hipStream_t stream) {
+  TOUED_REQUIRE(rows >= 0 && cols >= 0 && ld >= cols && out && (rows * cols == 0 || x),
+                "toued_nonfinite_count_2d: bad arguments");
+  if (rows * cols == 0) return 0;
+  const long bx = (cols + 255) / 256;
+  const long gx = bx < 64 ? bx : 64, gy = rows < 256 ? rows : 256;
+  hipLaunchKernelGGL(k_nonfinite_count_2d, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, stream, x, rows, cols, ld,
                      out);
   TOUED_CHECK_LAUNCH();
   return 0;

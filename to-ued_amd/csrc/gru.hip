@@ -1171,8 +1171,17 @@ __device__ unsigned long long g_bwd_stamps[64 * 32 * 8];
     if (blockIdx.x < 64 && tid == 0 && t < 32)                                                         \
       g_bwd_stamps[(blockIdx.x * 32 + t) * 8 + (ph)] = __builtin_amdgcn_s_memtime();                   \
   } while (0)
+// per-wave stamps of the same workgroups: memory part start / end of every wave, and the wave's SIMD (HW_ID 5:4)
+__device__ unsigned long long g_bwd_wstamps[64 * 32 * 8 * 2];
+__device__ int g_bwd_wsimd[64 * 8];
+#define BWD_WSTAMP(ph)                                                                                 \
+  do {                                                                                                 \
+    if (blockIdx.x < 64 && lane_now() == 0 && t < 32)                                                  \
+      g_bwd_wstamps[((blockIdx.x * 32 + t) * 8 + wave) * 2 + (ph)] = __builtin_amdgcn_s_memtime();     \
+  } while (0)
 #else
 #define BWD_STAMP(ph) do {} while (0)
+#define BWD_WSTAMP(ph) do {} while (0)
 #endif
 
 // Backward in lockstep (k_gru_bwd6n): one 512-thread workgroup per (k, 64 rows), both 32-row tiles in
@@ -1216,6 +1225,10 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   const int k = blockIdx.x / nb;
   const int r0 = (blockIdx.x - k * nb) * RBT;
   const int R = p.R, T = p.T, W = p.W;
+#ifdef BWD_STAMPS
+  if (blockIdx.x < 64 && (tid & 63) == 0)
+    g_bwd_wsimd[blockIdx.x * 8 + wave] = __builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4);   // HW_ID SIMD_ID
+#endif
   for (int i = tid; i < 2 * 3 * HU; i += 512) {
     const int f = 3 + i / (3 * HU), g = (i / HU) % 3, u = i % HU;
     const int base = g == 0 ? p.o.ir_w : g == 1 ? p.o.iz_w : p.o.in_w;
@@ -1334,8 +1347,23 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #ifndef BWD_RD
 #define BWD_RD 4
 #endif
-  auto contract_h = [&](int g, int sb) {   // sb: the image slot of the first fp16 piece (the second at sb + 1)
+#ifndef BWD_SPREAD
+#define BWD_SPREAD 1
+#endif
+  // BWD_SPREAD: the pass's 32 DG stores per lane (one gate's cotangent of both row tiles, held in registers) go two per
+  // k-step between the MFMAs, where the vector memory pipe carries only the A ring, instead of as a burst in front of
+  // the pass (the store path takes ~11 B/clk per CU: a 64 KB burst per CU held the waves ~5.7 k cycles per gate).
+  // Slot s = 8 gi + i of group gi (i static): row tile h = gi >> 1, register q = 8 (gi & 1) + i; the queue qv is
+  // rotated by 8 after each rolled group so that its indices stay static.
+  auto store_slot = [&](int gst, long ctr_, int gi, int i, float v) {
+    const int h = gi >> 1, e = i & 3, g4 = 2 * (gi & 1) + (i >> 2);
+    const unsigned so = (unsigned)((((long)(e + 8 * g4) * p.M + ctr_) * 4) + 128 * h);
+    const int ln = lane_now();
+    st_u(rs_dg[gst], (unsigned)((((long)(32 * wave + 4 * (ln >> 5))) * p.M + r0 + (ln & 31)) * 4), so, v);
+  };
+  auto contract_h = [&](int g, int sb, float (&qv)[32], long ctr_) {   // sb: the image slot of the first fp16 piece
     constexpr int RD = BWD_RD;                    // A-fragment ring depth (k-steps in flight from L2)
+    static_assert(!BWD_SPREAD || RD == 4, "the spread stores assume 8 per ring group");
     f16x8 ring[RD][2], B[2][2];
 #pragma unroll
     for (int i = 0; i < RD; ++i)
@@ -1348,11 +1376,15 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     };
     ldB(0, 0);
     ldB(0, 1);
-    auto kstep = [&](int ks, f16x8 (&Ar)[2], bool reload) {
+    auto kstep = [&](int ks, f16x8 (&Ar)[2], bool reload, int gi, int j) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         acc[h] = mfma3h(Ar, B[h], acc[h]);
         if (ks + 1 < 16) ldB(ks + 1, h);
+        if (BWD_SPREAD && h == 0) {
+          store_slot(g, ctr_, gi, 2 * j, qv[2 * j]);
+          store_slot(g, ctr_, gi, 2 * j + 1, qv[2 * j + 1]);
+        }
       }
       if (reload) {
 #pragma unroll
@@ -1363,11 +1395,16 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     // whole groups of RD k-steps that all refill their slot (slots named statically), then the tail
     constexpr int NG = (16 - RD) / RD;
 #pragma nounroll
-    for (int gi = 0; gi < NG; ++gi)
+    for (int gi = 0; gi < NG; ++gi) {
 #pragma unroll
-      for (int j = 0; j < RD; ++j) kstep(gi * RD + j, ring[j], true);
+      for (int j = 0; j < RD; ++j) kstep(gi * RD + j, ring[j], true, gi, j);
+      if (BWD_SPREAD) {
 #pragma unroll
-    for (int ks = NG * RD; ks < 16; ++ks) kstep(ks, ring[ks % RD], ks + RD < 16);
+        for (int i = 0; i < 24; ++i) qv[i] = qv[i + 8];
+      }
+    }
+#pragma unroll
+    for (int ks = NG * RD; ks < 16; ++ks) kstep(ks, ring[ks % RD], ks + RD < 16, NG, ks - NG * RD);
   };
   // scaled fp16 pieces of the four units u0 .. u0 + 3 of row `row` into image slots 0, 1
   auto put4h = [&](int row, int u0, const float (&v)[4], float sc) {
@@ -1408,6 +1445,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     head_cot(t);
     lds_barrier();
     BWD_STAMP(1);
+    BWD_WSTAMP(0);
     // ---- memory part: the eight unit quads (two row tiles x four) as a software pipeline, quad i+1's five
     // 16-byte loads in flight while quad i is transposed and processed (twice the bytes in flight per wave)
     float dz_r[2][16], dhn_r[2][16];
@@ -1520,6 +1558,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       __builtin_amdgcn_sched_barrier(0);
     }
     BWD_STAMP(2);
+    BWD_WSTAMP(1);
     // row maxima of |dr|, |dz|, |dhn| over this wave's units (the fp16 B scale of the three passes)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1556,6 +1595,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     auto store_dg = [&](int g, int row, int g4, const float (&v)[4]) { st_q(rs_dg[g], row >= RB, g4, v); };
     // dr -> fp16 pieces: x0 straight into slot 0, x1 held until every lane has read its staged f32 values
     // (slot 1 overlaps the staging)
+    float qv[32];   // the pass's DG store queue (BWD_SPREAD): dr, then dz, then dhn, [h][4 g4 + e]
     {
       f16x4 x1h[2][4];
 #pragma unroll
@@ -1569,7 +1609,12 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) split2h(v4[e] * bs[h], x0, x1h[h][g4], e);
           *reinterpret_cast<f16x4*>(&dgB[0][row * PP + un + 8 * g4]) = x0;
-          store_dg(0, RB * h, g4, v4);
+          if (BWD_SPREAD) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) qv[16 * h + 4 * g4 + e] = v4[e];
+          } else {
+            store_dg(0, RB * h, g4, v4);
+          }
         }
       lds_barrier();
 #pragma unroll
@@ -1593,7 +1638,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         for (int e = 0; e < 4; ++e) acc[h][4 * g4 + e] = dh[h][4 * g4 + e] * (wv[e] * bs[h]);
     }
     BWD_STAMP(4);
-    contract_h(0, 0);
+    contract_h(0, 0, qv, ctr);
     lds_barrier();
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -1601,11 +1646,16 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       for (int g4 = 0; g4 < 4; ++g4) {
         const float v4[4] = {dz_r[h][4 * g4], dz_r[h][4 * g4 + 1], dz_r[h][4 * g4 + 2], dz_r[h][4 * g4 + 3]};
         put4h(rown(h), ubn() + 8 * g4, v4, bs[h]);
-        store_dg(1, RB * h, g4, v4);
+        if (BWD_SPREAD) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) qv[16 * h + 4 * g4 + e] = v4[e];
+        } else {
+          store_dg(1, RB * h, g4, v4);
+        }
       }
     lds_barrier();
     BWD_STAMP(5);
-    contract_h(1, 0);
+    contract_h(1, 0, qv, ctr);
     lds_barrier();
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -1613,11 +1663,16 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       for (int g4 = 0; g4 < 4; ++g4) {
         const float v4[4] = {dhn_r[h][4 * g4], dhn_r[h][4 * g4 + 1], dhn_r[h][4 * g4 + 2], dhn_r[h][4 * g4 + 3]};
         put4h(rown(h), ubn() + 8 * g4, v4, bs[h]);
-        store_dg(2, RB * h, g4, v4);
+        if (BWD_SPREAD) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) qv[16 * h + 4 * g4 + e] = v4[e];
+        } else {
+          store_dg(2, RB * h, g4, v4);
+        }
       }
     lds_barrier();
     BWD_STAMP(6);
-    contract_h(2, 0);
+    contract_h(2, 0, qv, ctr);
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const float4 w4 = *reinterpret_cast<const float4*>(&wsc[32 * wave + 4 * (lane_now() >> 5) + 8 * g4]);
@@ -1897,6 +1952,12 @@ int toued_dbg_fwd_stamps(unsigned long long* host) {
 #ifdef BWD_STAMPS
 int toued_dbg_bwd_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bwd_stamps), sizeof(g_bwd_stamps)) == hipSuccess ? 0 : 1;
+}
+int toued_dbg_bwd_wstamps(unsigned long long* host, int* simd) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bwd_wstamps), sizeof(g_bwd_wstamps)) == hipSuccess &&
+                 hipMemcpyFromSymbol(simd, HIP_SYMBOL(g_bwd_wsimd), sizeof(g_bwd_wsimd)) == hipSuccess
+             ? 0
+             : 1;
 }
 #endif
 

@@ -1,7 +1,9 @@
 """The reference's debug hooks (util/jax.py:5-17 jax_debug_wrapper, flags experiments/parse_args.py:7-12).
 
 * ``--debug_nans`` sets ``jax_debug_nans`` there: the first NaN raises.  Here every stage of a meta-step that the
-  reference's jitted program would produce a NaN in -- rollout rewards, the LPG outputs, the agent parameters after
+  reference's jitted program would produce a NaN in -- rollout rewards, the LPG's GRU states and outputs (the
+  forward's relu(h) = max(h, 0) maps a NaN state to 0, so a NaN in the recurrence shows in the states first; XLA's max
+  would propagate it), the agent parameters after
   the inner updates, the meta-gradient, eta after Adam, eval returns, regret scores, the ES fitness -- gets one
   device non-finite count (``toued_nonfinite_count``, stream-ordered, into its own slot of a small device array);
   the counts are read ONCE per meta-step (``NanChecker.raise_if_any``, one host sync) and the first stage in
@@ -49,6 +51,10 @@ class NanChecker:
                 continue
             if t.dtype != torch.float32:
                 raise TypeError(f"NanChecker.check({stage!r}): float32 tensors only, got {t.dtype}")
+            if t.dim() == 2 and not t.is_contiguous() and t.stride(1) == 1:   # a column block of a wider operand
+                _lib.call("toued_nonfinite_count_2d", t.data_ptr(), t.shape[0], t.shape[1], t.stride(0), out,
+                          _lib.stream_ptr())
+                continue
             x = t if t.is_contiguous() else t.contiguous()
             _lib.call("toued_nonfinite_count", x.data_ptr(), x.numel(), out, _lib.stream_ptr())
 

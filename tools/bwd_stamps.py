@@ -56,6 +56,33 @@ def main():
     res["tail (dx, carry, sync)"] = float(tail.mean())
     res["step total"] = float((st[:, 1:, 0] - st[:, :-1, 0]).mean())
     print(json.dumps({k: round(v) for k, v in res.items()}), flush=True)
+    # per-wave memory parts (BWD_WSTAMP): when each wave starts and ends its memory part relative to the workgroup's
+    # first start, by wave and by its SIMD, and how long the last wave trails the first
+    wf = getattr(_lib.lib(), "toued_dbg_bwd_wstamps", None)
+    if wf is not None:
+        wf.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        wb = np.zeros(64 * 32 * 8 * 2, np.uint64)
+        simd = np.zeros(64 * 8, np.int32)
+        assert wf(wb.ctypes.data, simd.ctypes.data) == 0
+        w = wb.reshape(64, 32, 8, 2)[:, :T].astype(np.int64)
+        t0 = w[:, :, :, 0].min(axis=2, keepdims=True)
+        start, end = w[:, :, :, 0] - t0, w[:, :, :, 1] - t0
+        dur = end - start
+        simd = simd.reshape(64, 8)
+        out = {"wave_start_mean": start.mean(axis=(0, 1)).round().tolist(),
+               "wave_end_mean": end.mean(axis=(0, 1)).round().tolist(),
+               "wave_dur_mean": dur.mean(axis=(0, 1)).round().tolist(),
+               "end_spread_mean (last - first wave)": float((end.max(axis=2) - end.min(axis=2)).mean()),
+               "simd_of_wave (wg 0..3)": simd[:4].tolist()}
+        # rank of each wave's end among the two waves on its SIMD: does the later one trail by the shared VALU?
+        pair_gap = []
+        for b_ in range(64):
+            for sm in range(4):
+                ws = np.nonzero(simd[b_] == sm)[0]
+                if len(ws) == 2:
+                    pair_gap.append(np.abs(end[b_, :, ws[0]] - end[b_, :, ws[1]]).mean())
+        out["same_simd_end_gap_mean"] = float(np.mean(pair_gap)) if pair_gap else None
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
