@@ -41,13 +41,14 @@ def test_nonfinite_count_matches_torch(n):
 def test_nonfinite_count_2d_column_block():
     from toued import _lib
     x = torch.randn(40, 1000, device="cuda")
-    x[3, 10] = float("nan")     # inside the block
+    x[3, 110] = float("nan")    # inside the block (columns 100 .. 799)
     x[7, 600] = float("inf")    # inside
-    x[5, 999] = float("nan")    # outside (column 999 >= 100 + 700)
+    x[5, 999] = float("nan")    # outside
+    x[6, 50] = float("nan")     # outside
     blk = x[:, 100:800]
     out = torch.zeros(1, dtype=torch.int32, device="cuda")
     _lib.call("toued_nonfinite_count_2d", blk.data_ptr(), 40, 700, 1000, _lib.ptr(out), _lib.stream_ptr())
-    assert int(out) == int((~torch.isfinite(blk)).sum()) == 1 + 0 * 0 + (1 if 600 - 100 < 700 else 0)
+    assert int(out) == int((~torch.isfinite(blk)).sum()) == 2
 
 
 def _trainer(extra=()):
