@@ -148,6 +148,9 @@ int toued_eval_draws(EnvSpec spec, const int* levels, int n_agents, int W, int T
                      uint32_t* draws, hipStream_t stream);
 int toued_eval_returns(EnvSpec spec, const int* levels, const float* theta, int D, const int* state, int n_agents,
                        int W, int T, const uint32_t* draws, float* cum_return, hipStream_t stream);
+/* CUs the non-table toued_eval_returns launch holds for n_workers eval workers (one workgroup each, TOUED_EVAL_BLOCK
+ * workers per workgroup): what the caller reserves beside the weight-gradient reduction (toued_set_reserved_cus). */
+int toued_eval_returns_cus(int n_workers);
 
 
 /* ---- Level sampler (environments/level_sampler.py) ---- */

@@ -654,15 +654,16 @@ def test_lpg_inputs_rows_bitexact(F, per_agent):
     assert torch.equal(a[m], b[m])
 
 
-@pytest.mark.parametrize("N,wscale", [(2, 4.0), (12, 1.0)])
-def test_gru_backward_fused_small_matches_unfused(N, wscale):
+@pytest.mark.parametrize("N,wscale,F", [(2, 4.0, 5), (12, 1.0, 5), (2, 1.0, 1), (2, 1.0, 6)])
+def test_gru_backward_fused_small_matches_unfused(N, wscale, F):
     """k_gru_bwd6n<true> (the two small weight-gradient products accumulated in the kernel on 16x16x4 f32 MFMAs,
     reduced from per-workgroup partials) against the unfused pair k_gru_bwd6n<false> + toued_gru_bwd_small: the
     contraction cotangents, column exponents and input cotangents bit-identical (the same gate maths), the small
     products GI within 2e-6 relative (exact f32 products, another summation order), the flat gradient within 1e-6
-    relative L2."""
+    relative L2.  F = 1 (the ones row at A-table row 1) and F = 6 (head cotangent rows up to row 15, the table's last)
+    are the edges of the A table's packing."""
     from toued.lpg import LPGGRU, LPGLayout, init_lpg_params
-    W, T, K, F = 64, 6, 2, 5
+    W, T, K = 64, 6, 2
     R = N * W
     lay = LPGLayout(F)
     eta = init_lpg_params(7, F)

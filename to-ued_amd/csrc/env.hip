@@ -289,6 +289,9 @@ __global__ void k_evr_next() { if (threadIdx.x == 0) atomicAdd(&g_evr_launch, 1u
 // TBL (W a multiple of 64: every wave plays one agent's level): the five candidate moves and their object tests come
 // from a per-wave transition table in LDS, [G2][5] entries next cell | (mask of the objects placed there) << 8,
 // built once per launch -- five LDS reads per step instead of five next_pos_r and object loops; the same values.
+#ifndef EVAL_CHOSEN_ROW
+#define EVAL_CHOSEN_ROW 0   // 1: gather only the chosen next row after the choice (timing study)
+#endif
 template <int NMAX, bool TBL>
 __global__ void __launch_bounds__(256) k_eval_returns(EnvSpec sp, const int* __restrict__ levels,
                                                       const float* __restrict__ theta, int D,
@@ -350,7 +353,7 @@ __global__ void __launch_bounds__(256) k_eval_returns(EnvSpec sp, const int* __r
     if (t + 2 < T) dr1 = dw[(size_t)(t + 2) * n + i];
     // next state of each action while the episode goes on: position, objects left
     int cpos[5], cex[5];
-    float crow[5][5];
+    float crow[EVAL_CHOSEN_ROW ? 1 : 5][5];
 #pragma unroll
     for (int act = 0; act < 5; ++act) {
       int p, col = 0;
@@ -366,8 +369,10 @@ __global__ void __launch_bounds__(256) k_eval_returns(EnvSpec sp, const int* __r
       }
       cpos[act] = p;
       cex[act] = col;
-      const int ci = p + G2 * ((s.exists | (int)dr.z) & ~col & used);
-      load_row5(rs_t, tab_off + (unsigned)ci * 20u, crow[act]);
+      if (!EVAL_CHOSEN_ROW) {
+        const int ci = p + G2 * ((s.exists | (int)dr.z) & ~col & used);
+        load_row5(rs_t, tab_off + (unsigned)ci * 20u, crow[EVAL_CHOSEN_ROW ? 0 : act]);
+      }
     }
     float p[5];
     actor_probs5_row(row, last, s.time, p);
@@ -378,9 +383,15 @@ __global__ void __launch_bounds__(256) k_eval_returns(EnvSpec sp, const int* __r
       if (act == action) {
         pos = cpos[act];
         collected = cex[act];
+        if (!EVAL_CHOSEN_ROW) {
 #pragma unroll
-        for (int j = 0; j < 5; ++j) row[j] = crow[act][j];
+          for (int j = 0; j < 5; ++j) row[j] = crow[act][j];
+        }
       }
+    if (EVAL_CHOSEN_ROW) {   // one gather of the chosen next row after the choice (its latency in the chain)
+      const int ci = pos + G2 * ((s.exists | (int)dr.z) & ~collected & used);
+      load_row5(rs_t, tab_off + (unsigned)ci * 20u, row);
+    }
     // step_env (gridworld.py:72-136), tabular: the same operation order as env_step
     float p_t = 0.0f, rew = 0.0f;
 #pragma unroll
@@ -571,6 +582,17 @@ int toued_eval_draws(EnvSpec sp, const int* levels, int n_agents, int W, int T, 
   return 0;
 }
 
+static int eval_block() {
+  static const int v = [] {
+    const char* e = getenv("TOUED_EVAL_BLOCK");
+    const int b = e ? atoi(e) : 256;
+    return b == 64 || b == 128 ? b : 256;
+  }();
+  return v;
+}
+// CUs toued_eval_returns' non-table launch holds for n_workers chains (one workgroup per CU)
+int toued_eval_returns_cus(int n_workers) { return (n_workers + eval_block() - 1) / eval_block(); }
+
 int toued_eval_returns(EnvSpec sp, const int* levels, const float* theta, int D, const int* state, int n_agents, int W,
                        int T, const uint32_t* draws, float* cum_return, hipStream_t stream) {
   if (int e = check_spec(sp)) return e;
@@ -589,8 +611,11 @@ int toued_eval_returns(EnvSpec sp, const int* levels, const float* theta, int D,
                                                           stream, sp, levels, theta, D, state, T, W, n,
                                                           reinterpret_cast<const uint4*>(draws), cum_return));
   } else {
-    TOUED_DISPATCH_NMAX(sp.n_max, true, hipLaunchKernelGGL((k_eval_returns<NMAX, false>), dim3(nblk(n)), dim3(256), 0,
-                                                          stream, sp, levels, theta, D, state, T, W, n,
+    // workgroup size (TOUED_EVAL_BLOCK: 64, 128 or 256): smaller blocks spread the chains over more CUs, each with
+    // fewer row gathers in flight on its TA (the caller reserves toued_eval_returns_cus() CUs beside the reduction)
+    const int bs = eval_block();
+    TOUED_DISPATCH_NMAX(sp.n_max, true, hipLaunchKernelGGL((k_eval_returns<NMAX, false>), dim3((n + bs - 1) / bs),
+                                                          dim3(bs), 0, stream, sp, levels, theta, D, state, T, W, n,
                                                           reinterpret_cast<const uint4*>(draws), cum_return));
   }
 #ifdef H3_PLACE

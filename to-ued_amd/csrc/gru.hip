@@ -1172,12 +1172,13 @@ __device__ unsigned long long g_bwd_stamps[64 * 32 * 8];
       g_bwd_stamps[(blockIdx.x * 32 + t) * 8 + (ph)] = __builtin_amdgcn_s_memtime();                   \
   } while (0)
 // per-wave stamps of the same workgroups: memory part start / end of every wave, and the wave's SIMD (HW_ID 5:4)
-__device__ unsigned long long g_bwd_wstamps[64 * 32 * 8 * 2];
+#define BWD_NWS 8
+__device__ unsigned long long g_bwd_wstamps[64 * 32 * 8 * BWD_NWS];
 __device__ int g_bwd_wsimd[64 * 8];
 #define BWD_WSTAMP(ph)                                                                                 \
   do {                                                                                                 \
     if (blockIdx.x < 64 && lane_now() == 0 && t < 32)                                                  \
-      g_bwd_wstamps[((blockIdx.x * 32 + t) * 8 + wave) * 2 + (ph)] = __builtin_amdgcn_s_memtime();     \
+      g_bwd_wstamps[((blockIdx.x * 32 + t) * 8 + wave) * BWD_NWS + (ph)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
 #define BWD_STAMP(ph) do {} while (0)
@@ -1638,8 +1639,11 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         for (int e = 0; e < 4; ++e) acc[h][4 * g4 + e] = dh[h][4 * g4 + e] * (wv[e] * bs[h]);
     }
     BWD_STAMP(4);
+    BWD_WSTAMP(2);
     contract_h(0, 0, qv, ctr);
+    BWD_WSTAMP(3);
     lds_barrier();
+    BWD_WSTAMP(4);
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -1655,8 +1659,11 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       }
     lds_barrier();
     BWD_STAMP(5);
+    BWD_WSTAMP(5);
     contract_h(1, 0, qv, ctr);
+    BWD_WSTAMP(6);
     lds_barrier();
+    BWD_WSTAMP(7);
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll

@@ -103,6 +103,7 @@ _SIGS = {
     "toued_nonfinite_count": [_P, _L, _P, _P],
     "toued_nonfinite_count_2d": [_P, _L, _L, _L, _P, _P],
     "toued_dbg_wgrad_visits": [_P, _I],
+    "toued_eval_returns_cus": [_I],
     "toued_dbg_wgrad_last_ntiles": [],
     "toued_a2c_chain": [EnvSpecC, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _P, _P, _P],
     "toued_a2c_chain_self": [EnvSpecC, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _F, _P, _P, _P],

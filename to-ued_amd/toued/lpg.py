@@ -42,8 +42,10 @@ def layout(F: int) -> "OrderedDict[str, tuple]":
 
 class LPGLayout:
     def __init__(self, F: int):
-        if F not in (5, 7):
-            raise ValueError(f"LPG input width F={F} (5, or 7 with lifetime conditioning)")
+        # the model's input width is 5, or 7 with lifetime conditioning; the GRU kernels take 1..7 (the augmented k-step
+        # holds x and the bias row in 8), which the kernel tests use for the edges of the fused small products' A table
+        if not 1 <= F <= 7:
+            raise ValueError(f"LPG input width F={F} (5, or 7 with lifetime conditioning; the kernels take 1..7)")
         self.F = F
         self.shapes = layout(F)
         self.offsets = {}

@@ -366,8 +366,8 @@ class MetaGradStep:
         # plans leave those CUs free.  (Beside the recurrent backward instead, whose 64-row workgroups fill exactly
         # K*R/64/256 rounds of the chip, any CU held pushes that kernel into one more round; beside the
         # latency-bound agent kernels the key chain slowed them by more than it took.)
-        eval_cus = -(-N * hyp.eval_workers // 256)
-        key_cus = 2 * eval_cus      # the key chain runs two lanes per eval worker (k_eval_keys_pairs)
+        key_cus = 2 * -(-N * hyp.eval_workers // 256)   # the key chain: two lanes per eval worker (k_eval_keys_pairs)
+        eval_cus = int(L.lib().toued_eval_returns_cus(N * hyp.eval_workers))
         ea = {}
 
         def launch_eval():

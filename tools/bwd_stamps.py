@@ -61,11 +61,18 @@ def main():
     wf = getattr(_lib.lib(), "toued_dbg_bwd_wstamps", None)
     if wf is not None:
         wf.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-        wb = np.zeros(64 * 32 * 8 * 2, np.uint64)
+        NWS = 8
+        wb = np.zeros(64 * 32 * 8 * NWS, np.uint64)
         simd = np.zeros(64 * 8, np.int32)
         assert wf(wb.ctypes.data, simd.ctypes.data) == 0
-        w = wb.reshape(64, 32, 8, 2)[:, :T].astype(np.int64)
+        w = wb.reshape(64, 32, 8, NWS)[:, :T].astype(np.int64)
         t0 = w[:, :, :, 0].min(axis=2, keepdims=True)
+        # the other per-wave points relative to the same origin: 2 pass dr start (after the dr split), 3 its last
+        # MFMA issued, 4 after the barrier behind it, 5 pass dz start (refill + barrier done), 6 its last MFMA, 7 barrier
+        names = {2: "pass_dr_start", 3: "pass_dr_issued", 4: "pass_dr_barrier", 5: "pass_dz_start",
+                 6: "pass_dz_issued", 7: "pass_dz_barrier"}
+        pts = {nm: (w[:, :, :, i] - t0[:, :, :]).mean(axis=(0, 1)).round().tolist() for i, nm in names.items()}
+        print(json.dumps(pts), flush=True)
         start, end = w[:, :, :, 0] - t0, w[:, :, :, 1] - t0
         dur = end - start
         simd = simd.reshape(64, 8)
