@@ -990,7 +990,7 @@ __global__ void __launch_bounds__(512, NT == 1 ? 4 : 1) k_gru_bwd(BwdArgs p) {
   for (int i = tid; i < 2 * 3 * HU; i += 512) {
     const int f = 3 + i / (3 * HU), g = (i / HU) % 3, u = i % HU;
     const int base = g == 0 ? p.o.ir_w : g == 1 ? p.o.iz_w : p.o.in_w;
-    wi34[i] = p.eta[base + f * HU + u];
+    wi34[i] = f < p.F ? p.eta[base + f * HU + u] : 0.0f;   // (inputs 3, 4 exist when F >= 5)
   }
   float dh[NT][16];
 #pragma unroll
@@ -1233,7 +1233,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   for (int i = tid; i < 2 * 3 * HU; i += 512) {
     const int f = 3 + i / (3 * HU), g = (i / HU) % 3, u = i % HU;
     const int base = g == 0 ? p.o.ir_w : g == 1 ? p.o.iz_w : p.o.in_w;
-    wi34[i] = p.eta[base + f * HU + u];
+    wi34[i] = f < p.F ? p.eta[base + f * HU + u] : 0.0f;   // (inputs 3, 4 exist when F >= 5)
   }
   for (int i = tid; i < HU; i += 512) wsc[i] = reinterpret_cast<const float*>(p.A6)[B6_SCALES + i];
   const int F = p.F;
