@@ -290,7 +290,7 @@ __global__ void k_evr_next() { if (threadIdx.x == 0) atomicAdd(&g_evr_launch, 1u
 // from a per-wave transition table in LDS, [G2][5] entries next cell | (mask of the objects placed there) << 8,
 // built once per launch -- five LDS reads per step instead of five next_pos_r and object loops; the same values.
 #ifndef EVAL_CHOSEN_ROW
-#define EVAL_CHOSEN_ROW 0   // 1: gather only the chosen next row after the choice (timing study)
+#define EVAL_CHOSEN_ROW 1   // gather only the chosen next row after the choice (0: the five candidates a step ahead)
 #endif
 template <int NMAX, bool TBL>
 __global__ void __launch_bounds__(256) k_eval_returns(EnvSpec sp, const int* __restrict__ levels,

@@ -650,6 +650,9 @@ __device__ unsigned long long g_fwd_stamps[64 * 32 * 6];
 #ifndef FWD_AUG32
 #define FWD_AUG32 1
 #endif
+#ifndef FWD_TST16
+#define FWD_TST16 0   // timing study: r, z, hn saved as 16-byte [M][256] rows (global stores)
+#endif
 template <bool SAVE>
 __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   constexpr bool A32 = FWD_AUG32 && !SAVE;   // the per-candidate (ES) instance: f32-MFMA augmented k-step
@@ -880,6 +883,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
         }
         f16x4 n0, n1;
         bf16x4 nr;
+        float sv[3][4];   // FWD_TST16: r, z, hn of the four units, one 16-byte store each
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int q = 4 * g4 + e;
@@ -893,15 +897,31 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
           const unsigned so = (unsigned)(((long)qunit(q) * p.M + cbase) * 4);
           if (SAVE) {
             st_u(rs_hin, vbyte, so, hin);
-            st_u(rs_r, vbyte, so, rg);
-            st_u(rs_z, vbyte, so, zg);
-            st_u(rs_hn, vbyte, so, hn);   // n is recomputed by the backward (gate_n)
+            if (FWD_TST16) {
+              sv[0][e] = rg; sv[1][e] = zg; sv[2][e] = hn;
+            } else {
+              st_u(rs_r, vbyte, so, rg);
+              st_u(rs_z, vbyte, so, zg);
+              st_u(rs_hn, vbyte, so, hn);   // n is recomputed by the backward (gate_n)
+            }
           }
           const float rl = fmaxf(hh, 0.0f);
           const float4 w0 = whl[qunit(q) * 3], w1 = whl[qunit(q) * 3 + 1], w2 = whl[qunit(q) * 3 + 2];
           hp_loc[0] += rl * w0.x; hp_loc[1] += rl * w0.y; hp_loc[2] += rl * w0.z;
           hp_loc[3] += rl * w0.w; hp_loc[4] += rl * w1.x; hp_loc[5] += rl * w1.y;
           hp_loc[6] += rl * w1.z; hp_loc[7] += rl * w1.w; hp_loc[8] += rl * w2.x;
+        }
+        if (SAVE && FWD_TST16) {   // [M][256] rows: four consecutive units of this row in 16 bytes (soffset 0)
+          const unsigned vb16 = (unsigned)(((cbase + r0 + row) * HU + ub + 8 * g4) * 4);
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(sv[0][0]), __float_as_uint(sv[0][1]),
+                                                       __float_as_uint(sv[0][2]), __float_as_uint(sv[0][3])},
+                                                 rs_r, (int)vb16, 0, GRU_ST_AUX);
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(sv[1][0]), __float_as_uint(sv[1][1]),
+                                                       __float_as_uint(sv[1][2]), __float_as_uint(sv[1][3])},
+                                                 rs_z, (int)vb16, 0, GRU_ST_AUX);
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(sv[2][0]), __float_as_uint(sv[2][1]),
+                                                       __float_as_uint(sv[2][2]), __float_as_uint(sv[2][3])},
+                                                 rs_hn, (int)vb16, 0, GRU_ST_AUX);
         }
         *reinterpret_cast<f16x4*>(&hB[0][ho]) = n0;
         *reinterpret_cast<f16x4*>(&hB[1][ho]) = n1;
@@ -1197,6 +1217,12 @@ __device__ int g_bwd_wsimd[64 * 8];
 //   SMALL (F <= 6): the two small weight-gradient products GI = [X; 1] . dn^T and DH . relu(h_out)^T accumulate in
 //     the kernel (16x16x4 f32 MFMA, exact f32 products) instead of streaming dn and relu(h_out) to HBM for a later
 //     reduction: see small_mfma below.
+#ifndef BWD_MPRIO
+#define BWD_MPRIO 0
+#endif
+#ifndef BWD_TNOTR
+#define BWD_TNOTR 0   // timing study only (wrong results): r, z, hn used without their lane-quad transposes
+#endif
 template <bool SMALL>
 __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   constexpr int RBT = 2 * RB;
@@ -1349,22 +1375,22 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #define BWD_RD 4
 #endif
 #ifndef BWD_SPREAD
-#define BWD_SPREAD 1
+#define BWD_SPREAD 0
 #endif
   // BWD_SPREAD: the pass's 32 DG stores per lane (one gate's cotangent of both row tiles, held in registers) go two per
   // k-step between the MFMAs, where the vector memory pipe carries only the A ring, instead of as a burst in front of
   // the pass (the store path takes ~11 B/clk per CU: a 64 KB burst per CU held the waves ~5.7 k cycles per gate).
-  // Slot s = 8 gi + i of group gi (i static): row tile h = gi >> 1, register q = 8 (gi & 1) + i; the queue qv is
-  // rotated by 8 after each rolled group so that its indices stay static.
+  // Slot s = 2 RD gi + i of ring group gi (i static): row tile h = s >> 4, register q = s & 15; the queue qv is rotated
+  // by 2 RD after each rolled group so that its indices stay static.
   auto store_slot = [&](int gst, long ctr_, int gi, int i, float v) {
-    const int h = gi >> 1, e = i & 3, g4 = 2 * (gi & 1) + (i >> 2);
+    const int s_ = 2 * BWD_RD * gi + i, h = s_ >> 4, e = s_ & 3, g4 = (s_ & 15) >> 2;
     const unsigned so = (unsigned)((((long)(e + 8 * g4) * p.M + ctr_) * 4) + 128 * h);
     const int ln = lane_now();
     st_u(rs_dg[gst], (unsigned)((((long)(32 * wave + 4 * (ln >> 5))) * p.M + r0 + (ln & 31)) * 4), so, v);
   };
   auto contract_h = [&](int g, int sb, float (&qv)[32], long ctr_) {   // sb: the image slot of the first fp16 piece
     constexpr int RD = BWD_RD;                    // A-fragment ring depth (k-steps in flight from L2)
-    static_assert(!BWD_SPREAD || RD == 4, "the spread stores assume 8 per ring group");
+    static_assert(!BWD_SPREAD || 16 % RD == 0, "the spread stores: 2 per k-step, 2 RD per ring group");
     f16x8 ring[RD][2], B[2][2];
 #pragma unroll
     for (int i = 0; i < RD; ++i)
@@ -1401,19 +1427,29 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       for (int j = 0; j < RD; ++j) kstep(gi * RD + j, ring[j], true, gi, j);
       if (BWD_SPREAD) {
 #pragma unroll
-        for (int i = 0; i < 24; ++i) qv[i] = qv[i + 8];
+        for (int i = 0; i < 32 - 2 * RD; ++i) qv[i] = qv[i + 2 * RD];
       }
     }
 #pragma unroll
     for (int ks = NG * RD; ks < 16; ++ks) kstep(ks, ring[ks % RD], ks + RD < 16, NG, ks - NG * RD);
   };
   // scaled fp16 pieces of the four units u0 .. u0 + 3 of row `row` into image slots 0, 1
+#ifndef BWD_TREFILL
+#define BWD_TREFILL 0   // timing studies only (wrong results): 1 = refills without LDS writes, 2 = without the split
+#endif
   auto put4h = [&](int row, int u0, const float (&v)[4], float sc) {
     f16x4 x0, x1;
+    if (BWD_TREFILL == 2) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) split2h(v[e] * sc, x0, x1, e);
-    *reinterpret_cast<f16x4*>(&dgB[0][row * PP + u0]) = x0;
-    *reinterpret_cast<f16x4*>(&dgB[1][row * PP + u0]) = x1;
+      for (int e = 0; e < 4; ++e) { x0[e] = (_Float16)0.0f; x1[e] = (_Float16)0.0f; }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) split2h(v[e] * sc, x0, x1, e);
+    }
+    if (BWD_TREFILL != 1) {
+      *reinterpret_cast<f16x4*>(&dgB[0][row * PP + u0]) = x0;
+      *reinterpret_cast<f16x4*>(&dgB[1][row * PP + u0]) = x1;
+    }
   };
   // SMALL: the wave's dn and relu(h_out) of one row tile and one 16-unit half go through a wave-private [row][unit]
   // f32 block in image slot 0 (free during the memory part) as the B operand B[k][j = unit] of 16x16x4 f32 MFMAs over
@@ -1497,6 +1533,13 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #pragma unroll
     for (int qi = 0; qi < 8; ++qi) {
       const int h = qi >> 2, g4 = qi & 3;
+      // BWD_MPRIO (timing study): the two waves of a SIMD (w, w + 4) take turns at the higher issue priority, one quad
+      // each (1), or the younger wave leads (2), instead of the older wave leading the whole memory part
+      if (BWD_MPRIO == 1) {
+        if (((qi + (wave >> 2)) & 1) == 0) __builtin_amdgcn_s_setprio(2); else __builtin_amdgcn_s_setprio(1);
+      } else if (BWD_MPRIO == 2 && qi == 0) {
+        if (wave >= 4) __builtin_amdgcn_s_setprio(2); else __builtin_amdgcn_s_setprio(1);
+      }
       float (&v)[4][4] = vr[qi % NR];
       if (qi + NR - 1 < 8) load_q((qi + NR - 1) >> 2, (qi + NR - 1) & 3, vr[(qi + NR - 1) % NR]);
       if (qi == 3) load_x(1, xb);
@@ -1518,7 +1561,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         dx4 = 0.0f;
       }
 #pragma unroll
-      for (int a = 0; a < 4; ++a) quad_transpose(v[a], lane);
+      for (int a = 0; a < (BWD_TNOTR ? 1 : 4); ++a) quad_transpose(v[a], lane);
       const float* wil = wi34 + ubn();
       float drq[4], rhq[4], dnq[4];
 #pragma unroll
@@ -1558,6 +1601,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+    if (BWD_MPRIO) __builtin_amdgcn_s_setprio(0);
     BWD_STAMP(2);
     BWD_WSTAMP(1);
     // row maxima of |dr|, |dz|, |dhn| over this wave's units (the fp16 B scale of the three passes)
