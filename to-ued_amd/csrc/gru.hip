@@ -650,6 +650,12 @@ __device__ unsigned long long g_fwd_stamps[64 * 32 * 6];
 #ifndef FWD_AUG32
 #define FWD_AUG32 1
 #endif
+#ifndef FWD_NOSAVE
+#define FWD_NOSAVE 0   // timing studies only: 1 = no saves, 2 = h_in only (the backward then reads stale data)
+#endif
+#ifndef FWD_ST16T
+#define FWD_ST16T 0   // the saves as 16-byte stores after lane-quad transposes (same layout)
+#endif
 #ifndef FWD_TST16
 #define FWD_TST16 0   // timing study: r, z, hn saved as 16-byte [M][256] rows (global stores)
 #endif
@@ -883,7 +889,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
         }
         f16x4 n0, n1;
         bf16x4 nr;
-        float sv[3][4];   // FWD_TST16: r, z, hn of the four units, one 16-byte store each
+        float sv[4][4];   // FWD_TST16 / FWD_ST16T: r, z, hn (, h_in) of the four units, one 16-byte store each
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int q = 4 * g4 + e;
@@ -895,7 +901,14 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
           const float hh = (1.0f - zg) * ng + zg * hin;
           split_carry(dn ? 0.0f : hh, n0, n1, nr, e);   // carry h_in(t-1) = where(d_{t-1}, 0, h_out(t))
           const unsigned so = (unsigned)(((long)qunit(q) * p.M + cbase) * 4);
-          if (SAVE) {
+          if (SAVE && FWD_ST16T) {
+            sv[0][e] = rg; sv[1][e] = zg; sv[2][e] = hn;
+            if (FWD_ST16T == 2) sv[3][e] = hin; else st_u(rs_hin, vbyte, so, hin);
+          } else if (SAVE && FWD_NOSAVE == 1) {
+            // timing study: no saves
+          } else if (SAVE && FWD_NOSAVE == 2) {
+            st_u(rs_hin, vbyte, so, hin);   // timing study: h_in only
+          } else if (SAVE) {
             st_u(rs_hin, vbyte, so, hin);
             if (FWD_TST16) {
               sv[0][e] = rg; sv[1][e] = zg; sv[2][e] = hn;
@@ -910,6 +923,22 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
           hp_loc[0] += rl * w0.x; hp_loc[1] += rl * w0.y; hp_loc[2] += rl * w0.z;
           hp_loc[3] += rl * w0.w; hp_loc[4] += rl * w1.x; hp_loc[5] += rl * w1.y;
           hp_loc[6] += rl * w1.z; hp_loc[7] += rl * w1.w; hp_loc[8] += rl * w2.x;
+        }
+        if (SAVE && FWD_ST16T) {
+          // lane-quad transposes (the backward's load in reverse): lane col then holds unit ub + 8 g4 + (col & 3) of
+          // rows (col & 28) .. +3 -- four consecutive columns of one unit row, one 16-byte store per array (a quarter
+          // of the dword store instructions; the address in the VGPR offset, soffset 0)
+          const int ln = lane_now();
+          const unsigned vq = (unsigned)((((long)(ub + (ln & 3))) * p.M + cbase + r0 + RB * h + (ln & 28)) * 4) +
+                              (unsigned)(8 * g4) * (unsigned)p.M * 4u;
+          __amdgpu_buffer_rsrc_t const rs4[4] = {rs_r, rs_z, rs_hn, rs_hin};
+#pragma unroll
+          for (int g = 0; g < (FWD_ST16T == 2 ? 4 : 3); ++g) {
+            quad_transpose(sv[g], ln);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(sv[g][0]), __float_as_uint(sv[g][1]),
+                                                         __float_as_uint(sv[g][2]), __float_as_uint(sv[g][3])},
+                                                   rs4[g], (int)vq, 0, GRU_ST_AUX);
+          }
         }
         if (SAVE && FWD_TST16) {   // [M][256] rows: four consecutive units of this row in 16 bytes (soffset 0)
           const unsigned vb16 = (unsigned)(((cbase + r0 + row) * HU + ub + 8 * g4) * 4);
@@ -958,6 +987,247 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     }
     FWD_STAMP(5);
   }
+}
+
+// Forward, half-row workgroups (k_gru_fwd6h, the SAVE instance: the meta-gradient's forward).  k_gru_fwd6 runs one
+// 512-thread workgroup of 64 rows per CU, all eight waves in the same phase: the contraction (matrix pipe) and then the
+// gate maths and saves (VALU), so one pipe idles at a time (stamps: 23 k + 24 k cycles of a 47 k step).  Here a
+// 256-thread workgroup holds ONE 32-row tile and wave w owns units [64 w, 64 w + 64) (two unit tiles); two workgroups
+// share a CU, each wave beside a wave of the other workgroup on its SIMD, so one workgroup's gate maths can run in
+// the other's contraction.  The price: each A fragment (L2) now feeds one row tile instead of two (twice the
+// fragment bytes per FLOP).  Same arithmetic as k_gru_fwd6 (the augmented k-step on the f32 MFMA, FWD_AUG32), the
+// same saves, bit-compatible outputs within the forward's tolerance.
+#ifndef FWD_H2
+#define FWD_H2 1
+#endif
+__global__ void __launch_bounds__(256, 2) k_gru_fwd6h(FwdArgs p) {
+  __shared__ __attribute__((aligned(16))) __bf16 hB[3][32 * F6_HP];   // carry image [piece][row][unit]: 50.7 KB
+  __shared__ __attribute__((aligned(16))) float wh[HU * 12];          // head weights [unit][pi | y0..y7 | pad]
+  __shared__ __attribute__((aligned(16))) float usc[3 * HU];          // accumulator unscale 2^-(s + 14) [gate][unit]
+  __shared__ float hp[4 * 9 * 32];      // head partials [wave][output][row]
+  __shared__ float wIs[8 * 4 * 64];     // gate_ain's W_in fragments [unit tile][kk][lane]
+  const int tid = threadIdx.x, lane = tid & 63, hi = lane >> 5, col = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r0 = blockIdx.x * RB;
+  const int R = p.R, T = p.T, W = p.W, F = p.F;
+  const int a_ = r0 / W;                  // (W % 32 == 0: the tile's rows are one agent's workers)
+  const int w_ = r0 + col - a_ * W;
+  const float* eta = p.eta;
+  const float* A6c = reinterpret_cast<const float*>(p.A6);
+  for (int i = tid; i < HU * 12; i += 256) {
+    const int u = i / 12, oo = i - u * 12;
+    wh[i] = oo == 0 ? eta[p.o.pi_w + u] : oo < 9 ? eta[p.o.y_w + u * 8 + (oo - 1)] : 0.0f;
+  }
+  for (int i = tid; i < 3 * HU; i += 256) usc[i] = 1.0f / (A6c[F6_SCALES + i] * HSCALE);   // powers of two: exact
+#pragma unroll
+  for (int ut = 0; ut < 2; ++ut) {
+    float wI[4];
+    load_win_frags(wI, eta, p.o, F, 2 * wave + ut, lane);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) wIs[((2 * wave + ut) * 4 + kk) * 64 + lane] = wI[kk];
+  }
+  {
+    uint4* z = reinterpret_cast<uint4*>(&hB[0][0]);
+    for (int i = tid; i < 3 * 32 * F6_HP / 8; i += 256) z[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  const __amdgpu_buffer_rsrc_t rs_X = rsrc_of(p.X);
+  const __amdgpu_buffer_rsrc_t rs_done = rsrc_of(reinterpret_cast<const float*>(p.done));
+  __syncthreads();
+  const float bpi = eta[p.o.pi_b];
+  const __amdgpu_buffer_rsrc_t rs_A = rsrc_of(A6c);
+  const unsigned vA = (unsigned)lane * 16;
+  auto ldAh = [&](int frag) {
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs_A, (int)vA, frag * 1024, 0);
+    return __builtin_bit_cast(f16x8, x);
+  };
+  const __amdgpu_buffer_rsrc_t rs_hin = rsrc_of(p.s_hin), rs_r = rsrc_of(p.s_r), rs_z = rsrc_of(p.s_z),
+                               rs_hn = rsrc_of(p.s_hn);
+  for (int s = 0; s < T; ++s) {
+    const int t = T - 1 - s;
+    floatx16 acc[3][2];   // r, z, W_hn h + b_hn of the wave's two unit tiles
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int ut = 0; ut < 2; ++ut)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[g][ut][q] = 0.0f;
+    // this lane's row inputs x(t) (the augmented k-step's B and gate_ain's)
+    float xv[7];
+#pragma unroll
+    for (int f = 0; f < 7; ++f) {
+      const int fc = f < F ? f : F - 1;
+      xv[f] = ld_u(rs_X, (unsigned)(col * p.xs_col * 4), (unsigned)((fc * p.xs_f + ((long)t * R + r0) * p.xs_col) * 4));
+    }
+    // A fragments (unit tile U = 2 wave + ut): FWD_H2_RING k-steps in flight (1: each fragment reloaded for the next
+    // k-step right after its MFMAs; the other workgroup's waves on the SIMD cover the latency); B (the carry, one row
+    // tile) double-buffered
+#ifndef FWD_H2_RING
+#define FWD_H2_RING 1
+#endif
+    f16x8 A0[3][2][2], A1[FWD_H2_RING == 2 ? 3 : 1][2][2], B[2][2];
+    auto fragA = [&](int ks, int g, int ut, int q) { return ((ks * 8 + 2 * wave + ut) * 3 + g) * 2 + q; };
+    auto load_B = [&](int ks, f16x8 (&b)[2]) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) b[q] = *reinterpret_cast<const f16x8*>(&hB[q][col * F6_HP + 16 * ks + 8 * hi]);
+    };
+    constexpr int RD = FWD_H2_RING;
+    auto slot = [&](int ks) -> f16x8 (&)[3][2][2] {
+      return (RD == 2 && (ks & 1)) ? reinterpret_cast<f16x8 (&)[3][2][2]>(A1) : A0;
+    };
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int ut = 0; ut < 2; ++ut)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          A0[g][ut][q] = ldAh(fragA(0, g, ut, q));
+          if (RD == 2) reinterpret_cast<f16x8 (&)[3][2][2]>(A1)[g][ut][q] = ldAh(fragA(1, g, ut, q));
+        }
+    load_B(0, B[0]);
+    auto kstep = [&](int ks, f16x8 (&Ar)[3][2][2], f16x8 (&Bc)[2], f16x8 (&Bn)[2], bool reload) {
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+#pragma unroll
+        for (int ut = 0; ut < 2; ++ut) {
+          acc[g][ut] = mfma3h(Ar[g][ut], Bc, acc[g][ut]);
+          if (reload) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) Ar[g][ut][q] = ldAh(fragA(ks + RD, g, ut, q));
+          }
+        }
+        if (g == 0 && ks + 1 < 16) load_B(ks + 1, Bn);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    // (rolled over k-step pairs: the ring slots and B buffers stay named statically)
+#pragma nounroll
+    for (int kp = 0; kp < 7; ++kp) {
+      kstep(2 * kp, slot(0), B[0], B[1], true);
+      kstep(2 * kp + 1, slot(1), B[1], B[0], 2 * kp + 1 + RD < 16);
+    }
+    kstep(14, slot(0), B[0], B[1], 14 + RD < 16);
+    f16x8 (&A1r)[3][2][2] = slot(1);   // k-step 15
+    {
+      // k-step 15, then the augmented k-step on the f32 MFMA (exact products): A = the scaled input weights and
+      // biases (one 16-byte fragment per gate and unit tile), B = 2^14 [x_k (k < F), 1 (k = 7)]
+      float4 a32[3][2];
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int ut = 0; ut < 2; ++ut)
+          a32[g][ut] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                      rs_A, (int)vA, (F6_A32 + ((2 * wave + ut) * 3 + g) * 256) * 4, 0));
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+#pragma unroll
+        for (int ut = 0; ut < 2; ++ut) acc[g][ut] = mfma3h(A1r[g][ut], B[1], acc[g][ut]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int k = 2 * kk + hi;
+        const float bx = (k < F ? xv[k < 7 ? k : 6] : (k == 7 ? 1.0f : 0.0f)) * HSCALE;
+#pragma unroll
+        for (int g = 0; g < 3; ++g)
+#pragma unroll
+          for (int ut = 0; ut < 2; ++ut) {
+            const float av = kk == 0 ? a32[g][ut].x : kk == 1 ? a32[g][ut].y : kk == 2 ? a32[g][ut].z : a32[g][ut].w;
+            acc[g][ut] = mfma32(av, bx, acc[g][ut]);
+          }
+      }
+    }
+    lds_barrier();   // every wave done reading hB: the carry overwrites it in place
+    // ---- gate maths (lane = row col, register q = unit 32 U + 4 hi + qunit(q))
+    const bool dn = (t >= 1) ? __builtin_amdgcn_raw_buffer_load_b8(
+                                   rs_done, lane_now() & 31, (int)(((long)a_ * T + (t - 1)) * W + r0 - a_ * W), 0) != 0
+                             : false;
+    const long cbase = (long)t * R;
+#pragma unroll
+    for (int ut = 0; ut < 2; ++ut) {
+      const int U = 2 * wave + ut;
+      float hp_loc[9];
+#pragma unroll
+      for (int oo = 0; oo < 9; ++oo) hp_loc[oo] = 0.0f;
+      float wI[4];
+      {
+        const int ln = lane_now();
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) wI[kk] = wIs[(U * 4 + kk) * 64 + ln];
+      }
+      const floatx16 ain = gate_ain(wI, F, hi, [&](int k) { return xv[k < 7 ? k : 6]; });
+      const int ub = 32 * U + 4 * hi;
+      const float4* whl = reinterpret_cast<const float4*>(wh + ub * 12);
+      const unsigned vbyte = (unsigned)(((long)ub * p.M + r0 + col) * 4);
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int ho = col * F6_HP + ub + 8 * g4;
+        const f16x4 h0 = *reinterpret_cast<const f16x4*>(&hB[0][ho]);
+        const f16x4 h1 = *reinterpret_cast<const f16x4*>(&hB[1][ho]);
+        const bf16x4 hr = *reinterpret_cast<const bf16x4*>(&hB[2][ho]);
+        float us[3][4];
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          const float4 v = *reinterpret_cast<const float4*>(&usc[g * HU + ub + 8 * g4]);
+          us[g][0] = v.x; us[g][1] = v.y; us[g][2] = v.z; us[g][3] = v.w;
+        }
+        f16x4 n0, n1;
+        bf16x4 nr;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int q = 4 * g4 + e;
+          const float rg = sigm_r(acc[0][ut][q] * us[0][e]);
+          const float zg = sigm_r(acc[1][ut][q] * us[1][e]);
+          const float hn = acc[2][ut][q] * us[2][e];
+          const float ng = gate_n(ain[q], rg, hn);
+          const float hin = (((float)h0[e] + (float)h1[e]) + (float)hr[e]) * (1.0f / HSCALE);   // exact
+          const float hh = (1.0f - zg) * ng + zg * hin;
+          split_carry(dn ? 0.0f : hh, n0, n1, nr, e);   // carry h_in(t-1) = where(d_{t-1}, 0, h_out(t))
+          const unsigned so = (unsigned)(((long)qunit(q) * p.M + cbase) * 4);
+          st_u(rs_hin, vbyte, so, hin);
+          st_u(rs_r, vbyte, so, rg);
+          st_u(rs_z, vbyte, so, zg);
+          st_u(rs_hn, vbyte, so, hn);   // n is recomputed by the backward (gate_n)
+          const float rl = fmaxf(hh, 0.0f);
+          const float4 w0 = whl[qunit(q) * 3], w1 = whl[qunit(q) * 3 + 1], w2 = whl[qunit(q) * 3 + 2];
+          hp_loc[0] += rl * w0.x; hp_loc[1] += rl * w0.y; hp_loc[2] += rl * w0.z;
+          hp_loc[3] += rl * w0.w; hp_loc[4] += rl * w1.x; hp_loc[5] += rl * w1.y;
+          hp_loc[6] += rl * w1.z; hp_loc[7] += rl * w1.w; hp_loc[8] += rl * w2.x;
+        }
+        *reinterpret_cast<f16x4*>(&hB[0][ho]) = n0;
+        *reinterpret_cast<f16x4*>(&hB[1][ho]) = n1;
+        *reinterpret_cast<bf16x4*>(&hB[2][ho]) = nr;
+      }
+      // lanes l and l + 32 hold the same row: fold the two halves; the second unit tile adds onto the first's (the
+      // same lane wrote it)
+#pragma unroll
+      for (int oo = 0; oo < 9; ++oo) {
+        const float o = __shfl_xor(hp_loc[oo], 32);
+        float* hq = &hp[(wave * 9 + oo) * 32 + lane_now()];
+        if (hi == 0) *hq = ut == 0 ? hp_loc[oo] + o : *hq + (hp_loc[oo] + o);
+      }
+    }
+    lds_barrier();   // head partials and the carry visible
+    if (tid < 32) {
+      const int tl = lane_now();   // == tid (wave 0)
+      float hv[9];
+#pragma unroll
+      for (int oo = 0; oo < 9; ++oo) {
+        float v = oo == 0 ? bpi : eta[p.o.y_b + oo - 1];
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) v += hp[(gq * 9 + oo) * 32 + tl];
+        hv[oo] = v;
+      }
+      const long ob = (long)t * R + r0 + tl;
+      p.pi_hat[ob] = hv[0];
+      float m = -__builtin_inff();
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, hv[j + 1]);
+      float e[8], ssum = 0.0f;
+      for (int j = 0; j < 8; ++j) { e[j] = __expf(hv[j + 1] - m); ssum += e[j]; }
+      const float inv = 1.0f / ssum;
+      for (int j = 0; j < 8; ++j) p.y_hat[((long)t * 8 + j) * R + r0 + tl] = e[j] * inv;
+    }
+  }
+  (void)w_;
 }
 
 // ------------------------------------------------------------------ backward
@@ -1862,7 +2132,11 @@ static int gru_fwd_launch(int R, int T, int W, int F, const float* X, long xs_f,
   // two row tiles per workgroup when the rows (and, for per-candidate parameters, each candidate's rows)
   // split into 64-row blocks
   const bool nt2 = R % (2 * RB) == 0 && (rpc == 0 || rpc % (2 * RB) == 0);
-  if (nt2 && !gru_f32_forced()) {
+  // the SAVE instance as two 32-row workgroups per CU (k_gru_fwd6h, TOUED_FWD_H2=1) or one 64-row workgroup
+  static const bool h2 = FWD_H2 && getenv("TOUED_FWD_H2") && getenv("TOUED_FWD_H2")[0] == '1';
+  if (save && h2 && !gru_f32_forced()) {
+    hipLaunchKernelGGL(k_gru_fwd6h, dim3(R / RB), dim3(256), 0, stream, p);
+  } else if (nt2 && !gru_f32_forced()) {
     if (save) hipLaunchKernelGGL(k_gru_fwd6<true>, dim3(R / (2 * RB)), dim3(512), 0, stream, p);
     else hipLaunchKernelGGL(k_gru_fwd6<false>, dim3(R / (2 * RB)), dim3(512), 0, stream, p);
   } else if (save) {
