@@ -2134,7 +2134,7 @@ static int gru_fwd_launch(int R, int T, int W, int F, const float* X, long xs_f,
   const bool nt2 = R % (2 * RB) == 0 && (rpc == 0 || rpc % (2 * RB) == 0);
   // the SAVE instance as two 32-row workgroups per CU (k_gru_fwd6h, TOUED_FWD_H2=1) or one 64-row workgroup
   static const bool h2 = FWD_H2 && getenv("TOUED_FWD_H2") && getenv("TOUED_FWD_H2")[0] == '1';
-  if (save && h2 && !gru_f32_forced()) {
+  if (save && h2 && nt2 && !gru_f32_forced()) {   // (the f32 fallback pair below keeps its own saves, n included)
     hipLaunchKernelGGL(k_gru_fwd6h, dim3(R / RB), dim3(256), 0, stream, p);
   } else if (nt2 && !gru_f32_forced()) {
     if (save) hipLaunchKernelGGL(k_gru_fwd6<true>, dim3(R / (2 * RB)), dim3(512), 0, stream, p);
