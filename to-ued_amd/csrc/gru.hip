@@ -1658,7 +1658,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     const int ln = lane_now();
     st_u(rs_dg[gst], (unsigned)((((long)(32 * wave + 4 * (ln >> 5))) * p.M + r0 + (ln & 31)) * 4), so, v);
   };
-  auto contract_h = [&](int g, int sb, float (&qv)[32], long ctr_) {   // sb: the image slot of the first fp16 piece
+  // pre: called once in the pass after its last ring reload (k-step 16 - RD): loads issued there stay outstanding
+  // behind every ring wait of the pass (vmcnt counts in issue order), so they cost the pass nothing
+  auto contract_h = [&](int g, int sb, float (&qv)[32], long ctr_, auto&& pre) {   // sb: the image slot of the first fp16 piece
     constexpr int RD = BWD_RD;                    // A-fragment ring depth (k-steps in flight from L2)
     static_assert(!BWD_SPREAD || 16 % RD == 0, "the spread stores: 2 per k-step, 2 RD per ring group");
     f16x8 ring[RD][2], B[2][2];
@@ -1701,7 +1703,13 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       }
     }
 #pragma unroll
-    for (int ks = NG * RD; ks < 16; ++ks) kstep(ks, ring[ks % RD], ks + RD < 16, NG, ks - NG * RD);
+    for (int ks = NG * RD; ks < 16; ++ks) {
+      kstep(ks, ring[ks % RD], ks + RD < 16, NG, ks - NG * RD);
+      if (ks == 16 - RD) {   // (16 - RD >= NG RD: always in the unrolled tail)
+        pre();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
   };
   // scaled fp16 pieces of the four units u0 .. u0 + 3 of row `row` into image slots 0, 1
 #ifndef BWD_TREFILL
@@ -1746,6 +1754,48 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       al = acc;
     }
   };
+#ifndef BWD_NR
+#define BWD_NR 3
+#endif
+  constexpr int NR = BWD_NR;
+  const int ub = 32 * wave + 4 * hi;               // lane's unit base (register q adds qunit(q))
+  float vr[NR][4][4];   // NR-slot ring: quads i+1 .. i+NR-1 in flight while quad i is processed (NR = 2: 10.11 ms)
+  auto load_q = [&](long ctr_, int h, int g4, float (&v)[4][4]) {
+    const unsigned vq = (unsigned)((((long)(ub + (col & 3))) * p.M + r0 + RB * h + (col & 28)) * 4);
+    const unsigned so = (unsigned)(((long)8 * g4 * p.M + ctr_) * 4);
+    ld4(rs_hin, vq, so, v[0]);
+    ld4(rs_r, vq, so, v[1]);
+    ld4(rs_z, vq, so, v[2]);
+    ld4(rs_hn, vq, so, v[3]);
+  };
+  // the rows' inputs x(t) as gate_ain's B fragments (lane = row RB h + col, k = 2 kk + hi): n is recomputed.
+  // Tile 0's go out with the first quads, tile 1's beside the ring loads of quad 3.
+  float xa[4], xb[4];
+  auto load_x = [&](long ctr_, int h, float (&x)[4]) {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int ln = lane_now(), k = 2 * kk + (ln >> 5);
+      // k (lane-dependent) goes in the VGPR offset: a lane-dependent soffset compiles to a waterfall loop
+      x[kk] = ld_u(rs_x, (unsigned)((((long)(k < F ? k : 0)) * p.M + RB * h + (ln & 31)) * 4), (unsigned)((ctr_ + r0) * 4));
+    }
+  };
+  // the first NR - 1 quads and tile 0's x of step t: quads [0, BWD_PF) (and x when BWD_PFX) in the previous step's dhn
+  // pass after its last ring reload, so that they land during that pass, the tail and the head; the rest at the top of
+  // the step's memory part
+#ifndef BWD_PF
+#define BWD_PF 0
+#endif
+#ifndef BWD_PFX
+#define BWD_PFX 0
+#endif
+  static_assert(BWD_PF >= 0 && BWD_PF <= NR - 1, "BWD_PF: at most the ring's NR - 1 leading quads");
+  auto load_first = [&](long ctr_, bool pre) {
+    if (pre == (bool)BWD_PFX) load_x(ctr_, 0, xa);
+#pragma unroll
+    for (int qi = 0; qi < NR - 1; ++qi)
+      if (pre == (qi < BWD_PF)) load_q(ctr_, qi >> 2, qi & 3, vr[qi]);
+  };
+  load_first((long)k * T * R, true);
   for (int t = 0; t < T; ++t) {
     const long ctr = ((long)k * T + t) * R;
     BWD_STAMP(0);
@@ -1756,23 +1806,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     // ---- memory part: the eight unit quads (two row tiles x four) as a software pipeline, quad i+1's five
     // 16-byte loads in flight while quad i is transposed and processed (twice the bytes in flight per wave)
     float dz_r[2][16], dhn_r[2][16];
-    const int ub = 32 * wave + 4 * hi;               // lane's unit base (register q adds qunit(q))
     // LDS addresses below are re-derived from lane_now() where used (see lane_now)
     auto ubn = [&] { return 32 * wave + 4 * (lane_now() >> 5); };
     auto rown = [&](int h) { return RB * h + (lane_now() & 31); };
-#ifndef BWD_NR
-#define BWD_NR 3
-#endif
-    constexpr int NR = BWD_NR;
-    float vr[NR][4][4];   // NR-slot ring: quads i+1 .. i+NR-1 in flight while quad i is processed (NR = 2: 10.11 ms)
-    auto load_q = [&](int h, int g4, float (&v)[4][4]) {
-      const unsigned vq = (unsigned)((((long)(ub + (col & 3))) * p.M + r0 + RB * h + (col & 28)) * 4);
-      const unsigned so = (unsigned)(((long)8 * g4 * p.M + ctr) * 4);
-      ld4(rs_hin, vq, so, v[0]);
-      ld4(rs_r, vq, so, v[1]);
-      ld4(rs_z, vq, so, v[2]);
-      ld4(rs_hn, vq, so, v[3]);
-    };
     // four units ub + 8 g4 .. +3 of this lane's row RB h + col (register quad g4 of tile h): per-unit dword
     // stores, lane = row (128-byte segments).  (Transposed back to 16-byte stores of four rows, as the loads are,
     // they measured no faster: 9.82-10.0 ms against 9.75-9.88.)
@@ -1782,24 +1818,11 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         st_u(rs, (unsigned)(((long)ub * p.M + r0 + RB * h + col) * 4),
              (unsigned)(((long)qunit(4 * g4 + e) * p.M + ctr) * 4), v[e]);
     };
-    // the rows' inputs x(t) as gate_ain's B fragments (lane = row RB h + col, k = 2 kk + hi): n is recomputed.
-    // Tile 0's go out now, tile 1's beside the ring loads of quad 3.
-    float xa[4], xb[4];
-    auto load_x = [&](int h, float (&x)[4]) {
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const int ln = lane_now(), k = 2 * kk + (ln >> 5);
-        // k (lane-dependent) goes in the VGPR offset: a lane-dependent soffset compiles to a waterfall loop
-        x[kk] = ld_u(rs_x, (unsigned)((((long)(k < F ? k : 0)) * p.M + RB * h + (ln & 31)) * 4), (unsigned)((ctr + r0) * 4));
-      }
-    };
-    load_x(0, xa);
+    load_first(ctr, false);
     floatx16 ain;
     floatx16 hacc;
     float dx3 = 0.0f, dx4 = 0.0f;
     float rmr[2] = {0.0f, 0.0f};   // running row maxima of |dr|
-#pragma unroll
-    for (int qi = 0; qi < NR - 1; ++qi) load_q(qi >> 2, qi & 3, vr[qi]);
 #pragma unroll
     for (int qi = 0; qi < 8; ++qi) {
       const int h = qi >> 2, g4 = qi & 3;
@@ -1811,8 +1834,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         if (wave >= 4) __builtin_amdgcn_s_setprio(2); else __builtin_amdgcn_s_setprio(1);
       }
       float (&v)[4][4] = vr[qi % NR];
-      if (qi + NR - 1 < 8) load_q((qi + NR - 1) >> 2, (qi + NR - 1) & 3, vr[(qi + NR - 1) % NR]);
-      if (qi == 3) load_x(1, xb);
+      if (qi + NR - 1 < 8) load_q(ctr, (qi + NR - 1) >> 2, (qi + NR - 1) & 3, vr[(qi + NR - 1) % NR]);
+      if (qi == 3) load_x(ctr, 1, xb);
       __builtin_amdgcn_sched_barrier(0);
       if (g4 == 0) {
         // head VJP W_heads . hv on MFMA for this row tile (lane = row, register = unit)
@@ -1954,7 +1977,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     }
     BWD_STAMP(4);
     BWD_WSTAMP(2);
-    contract_h(0, 0, qv, ctr);
+    contract_h(0, 0, qv, ctr, [] {});
     BWD_WSTAMP(3);
     lds_barrier();
     BWD_WSTAMP(4);
@@ -1974,7 +1997,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     lds_barrier();
     BWD_STAMP(5);
     BWD_WSTAMP(5);
-    contract_h(1, 0, qv, ctr);
+    contract_h(1, 0, qv, ctr, [] {});
     BWD_WSTAMP(6);
     lds_barrier();
     BWD_WSTAMP(7);
@@ -1993,7 +2016,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       }
     lds_barrier();
     BWD_STAMP(6);
-    contract_h(2, 0, qv, ctr);
+    contract_h(2, 0, qv, ctr, [&] {
+      if (t + 1 < T) load_first(ctr + R, true);
+    });
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const float4 w4 = *reinterpret_cast<const float4*>(&wsc[32 * wave + 4 * (lane_now() >> 5) + 8 * g4]);
