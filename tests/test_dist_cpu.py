@@ -115,3 +115,16 @@ def _worker8(rank, size, port, q):
     q.put((rank, (lo, hi, n), bool(torch.equal(full, torch.arange(n, dtype=torch.int32))), float(s[0])))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def test_nccl_rank_without_a_gpu_fails_clearly(monkeypatch):
+    """More nccl (RCCL) ranks on a node than GPUs: init_from_env refuses before RCCL's communicator init, naming the
+    cause (here: local rank 1 on a one-GPU node)."""
+    from toued import dist as tdist
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "1")
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    monkeypatch.setattr(tdist.dist, "init_process_group", lambda **kw: pytest.fail("reached init_process_group"))
+    with pytest.raises(RuntimeError, match="no GPU of its own"):
+        tdist.init_from_env("nccl")

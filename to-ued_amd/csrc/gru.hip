@@ -144,7 +144,8 @@ TOUED_DEV floatx16 gate_ain(const float (&wI)[4], int F, int hi, XK xk) {
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) {
     const int k = 2 * kk + hi;
-    a = mfma32(wI[kk], k < F ? xk(k) : k == 7 ? 1.0f : 0.0f, a);
+    const float xkv = hi ? xk(2 * kk + 1) : xk(2 * kk);   // static indices (a lane-dependent one puts xk's array in scratch)
+    a = mfma32(wI[kk], k < F ? xkv : k == 7 ? 1.0f : 0.0f, a);
   }
   return a;
 }
@@ -659,6 +660,12 @@ __device__ unsigned long long g_fwd_stamps[64 * 32 * 6];
 #ifndef FWD_TST16
 #define FWD_TST16 0   // timing study: r, z, hn saved as 16-byte [M][256] rows (global stores)
 #endif
+#ifndef FWD_PF
+#define FWD_PF 0
+#endif
+#ifndef FWD_XFIRST
+#define FWD_XFIRST 0   // comparison runs: x(t) issued before the ring's lead fragments (the round-4 order)
+#endif
 template <bool SAVE>
 __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   constexpr bool A32 = FWD_AUG32 && !SAVE;   // the per-candidate (ES) instance: f32-MFMA augmented k-step
@@ -669,6 +676,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   __shared__ float hp[8 * 9 * 64];      // head partials [wave][output][row]
   __shared__ float hout[9 * 64];
   __shared__ float wIs[8 * 4 * 64];     // gate_ain's W_in fragments [wave][kk][lane] (registers are the bound)
+  __shared__ float hbias[9];            // pi_b, y_b[0..7]: no global load in the head reduce (FWD_PF's loads in flight)
   const int tid = threadIdx.x, lane = tid & 63, hi = lane >> 5, col = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r0 = blockIdx.x * 64;
@@ -688,6 +696,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     wh[i] = oo == 0 ? eta[p.o.pi_w + u] : oo < 9 ? eta[p.o.y_w + u * 8 + (oo - 1)] : 0.0f;
   }
   for (int i = tid; i < 4 * HU; i += 512) usc[i] = 1.0f / (A6c[F6_SCALES + i] * HSCALE);   // powers of two: exact
+  if (tid < 9) hbias[tid] = tid == 0 ? eta[p.o.pi_b] : eta[p.o.y_b + tid - 1];
   {
     float wI[4];
     load_win_frags(wI, eta, p.o, F, wave, lane);
@@ -704,7 +713,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   const __amdgpu_buffer_rsrc_t rs_X = rsrc_of(p.X);
   const __amdgpu_buffer_rsrc_t rs_done = rsrc_of(reinterpret_cast<const float*>(p.done));
   __syncthreads();
-  const float bpi = eta[p.o.pi_b];
   const __amdgpu_buffer_rsrc_t rs_A = rsrc_of(A6c);
   const unsigned vA = (unsigned)lane * 16;
   auto ldA = [&](int frag) {
@@ -722,6 +730,38 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   // half a step late so the two halves contract at different times (later rounds inherit the offset)
   if (p.stagger > 0 && blockIdx.x < 256 && ((blockIdx.x >> 3) & 1))
     for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
+  // the step's rows' inputs x(t) for the augmented k-step [x_0 .. x_{F-1}, 1, 0 ...] (F <= 7), split into B
+  // fragments at the end of the contraction (lanes 32-63 hold k = 8..15: zero); A fragments through a two-k-step ring
+  // (A0: even k-steps, A1: odd): each L2 fragment load has a whole k-step of the wave's MFMAs (plus the partner
+  // wave's) to land instead of one gate's
+  float xv[2][7];
+  f16x8 A0[3][2], A1[3][2], B[2][2];
+  auto fragA = [&](int ks, int g, int q) { return ((ks * 8 + wave) * 3 + g) * 2 + q; };
+  auto fragAug = [&](int g, int q) { return F6_NFH + (wave * 4 + g) * 3 + q; };
+  // the ring's first two k-steps, then x(t) (HBM, behind them: the first ring wait does not wait for x).  FWD_PF: issued
+  // for step t - 1 after step t's gate maths, so that they land during the head reduce instead of after it
+  auto load_lead = [&](int t_) {
+    auto ring = [&] {
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          A0[g][q] = ldAh(fragA(0, g, q));
+          A1[g][q] = ldAh(fragA(1, g, q));
+        }
+    };
+    if (!FWD_XFIRST) ring();
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int f = 0; f < 7; ++f) {
+        const int fc = f < F ? f : F - 1;
+        xv[h][f] = ld_u(rs_X, (unsigned)((RB * h + col) * p.xs_col * 4),
+                        (unsigned)((fc * p.xs_f + ((long)t_ * R + r0) * p.xs_col) * 4));
+      }
+    if (FWD_XFIRST) ring();
+  };
+  if (FWD_PF) load_lead(T - 1);
   for (int s = 0; s < T; ++s) {
     const int t = T - 1 - s;
     FWD_STAMP(0);
@@ -735,34 +775,12 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     // ---- contraction: 16 fp16 k-steps over the carry + one augmented bf16 k-step.  Each gate's A fragments
     // (unit tile `wave`) are refilled for the next k-step right after their last MFMA, each row tile's B
     // fragments right after theirs; the partner wave on the SIMD covers what latency remains.
-    // this lane's row inputs x(t) for the augmented k-step [x_0 .. x_{F-1}, 1, 0 ...] (F <= 7), loaded now
-    // and split into B fragments at the end of the contraction (lanes 32-63 hold k = 8..15: zero)
-    float xv[2][7];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int f = 0; f < 7; ++f) {
-        const int fc = f < F ? f : F - 1;
-        xv[h][f] = ld_u(rs_X, (unsigned)((RB * h + col) * p.xs_col * 4),
-                        (unsigned)((fc * p.xs_f + ((long)t * R + r0) * p.xs_col) * 4));
-      }
-    // A fragments through a two-k-step ring (A0: even k-steps, A1: odd): each L2 fragment load has a whole k-step
-    // of the wave's MFMAs (plus the partner wave's) to land instead of one gate's
-    f16x8 A0[3][2], A1[3][2], B[2][2];
-    auto fragA = [&](int ks, int g, int q) { return ((ks * 8 + wave) * 3 + g) * 2 + q; };
-    auto fragAug = [&](int g, int q) { return F6_NFH + (wave * 4 + g) * 3 + q; };
+    if (!FWD_PF) load_lead(t);
     auto load_B = [&](int ks, int h) {
 #pragma unroll
       for (int q = 0; q < 2; ++q)
         B[h][q] = *reinterpret_cast<const f16x8*>(&hB[q][(RB * h + col) * F6_HP + 16 * ks + 8 * hi]);
     };
-#pragma unroll
-    for (int g = 0; g < 3; ++g)
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        A0[g][q] = ldAh(fragA(0, g, q));
-        A1[g][q] = ldAh(fragA(1, g, q));
-      }
     load_B(0, 0);
     load_B(0, 1);
     auto kstep = [&](int ks, f16x8 (&Ar)[3][2], bool reload) {
@@ -964,11 +982,16 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
       }
     }
     FWD_STAMP(3);
+    if (FWD_PF && s + 1 < T) {
+      __builtin_amdgcn_sched_barrier(0);
+      load_lead(t - 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     lds_barrier();   // head partials, the carry and x(t-1) visible
     FWD_STAMP(4);
     for (int i = 64 * wave + lane_now(); i < 9 * 64; i += 512) {
       const int oo = i >> 6, c = i & 63;
-      float v = oo == 0 ? bpi : eta[p.o.y_b + oo - 1];
+      float v = hbias[oo];
 #pragma unroll
       for (int gq = 0; gq < 8; ++gq) v += hp[(gq * 9 + oo) * 64 + c];
       hout[i] = v;
@@ -1248,6 +1271,7 @@ struct BwdArgs {
                     // reduction (2^CE[m] max over dr, dz, dhn of column m < 2^14; 127 = all zero)
   int F;            // LPG input width (lockstep kernel: x rows at s_hin + 256 M, n recomputed by gate_n)
   float* SP;        // fused small products (k_gru_bwd6n<true>): per-workgroup partials [n_wg][SP_FLOATS]
+  int stagger, stagger_mode;   // k_gru_bwd6n: s_sleep(127) quanta some first-round workgroups wait at start
 };
 // fused small weight-gradient products: per workgroup C[16][256] (rows 0..F-1: X . dn^T, row F: the ones row,
 // rows F+1..F+9: DH . relu(h_out)^T) then the head cotangents' row sums [9][64 rows]
@@ -1795,6 +1819,12 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     for (int qi = 0; qi < NR - 1; ++qi)
       if (pre == (qi < BWD_PF)) load_q(ctr_, qi >> 2, qi & 3, vr[qi]);
   };
+  // TOUED_BWD_STAGGER (study): first-round workgroups start late by phase * stagger quanta (~8 k cycles each), phase
+  // by mode: 0 = alternate CUs of every XCD, 1 = alternate XCDs, 2 = four phases over the CUs of every XCD
+  if (p.stagger > 0 && blockIdx.x < 256) {
+    const int ph = p.stagger_mode == 0 ? (blockIdx.x >> 3) & 1 : p.stagger_mode == 1 ? blockIdx.x & 1 : (blockIdx.x >> 3) & 3;
+    for (int i = 0; i < ph * p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   load_first((long)k * T * R, true);
   for (int t = 0; t < T; ++t) {
     const long ctr = ((long)k * T + t) * R;
@@ -2228,7 +2258,7 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
   TOUED_REQUIRE(R % RB == 0 && W % RB == 0, "toued_gru_bwd: rows R=%d and workers W=%d must be multiples of 32", R, W);
   TOUED_REQUIRE((double)M * 264.0 * 4.0 < 4294967295.0, "toued_gru_bwd: M=%ld columns exceed the 4 GiB buffer range",
                 M);
-  BwdArgs p;
+  BwdArgs p{};
   p.R = R; p.T = T; p.W = W; p.K = K; p.done = done; p.done_stride_k = done_stride_k;
   p.A = reinterpret_cast<const float4*>(bwdA); p.eta = eta;
   p.A6 = bwdA + (size_t)8 * 3 * 32 * 64 * 4;
@@ -2272,7 +2302,7 @@ int toued_gru_bwd_fused(int R, int T, int W, int K, const uint8_t* done, long do
   TOUED_REQUIRE(work_floats >= toued_gru_bwd_fused_work_floats(R, K), "toued_gru_bwd_fused: workspace %zu < %zu",
                 work_floats, toued_gru_bwd_fused_work_floats(R, K));
   TOUED_REQUIRE(col_exp != nullptr, "toued_gru_bwd_fused: col_exp is required");
-  BwdArgs p;
+  BwdArgs p{};
   p.R = R; p.T = T; p.W = W; p.K = K; p.done = done; p.done_stride_k = done_stride_k;
   p.A = reinterpret_cast<const float4*>(bwdA); p.eta = eta;
   p.A6 = bwdA + (size_t)8 * 3 * 32 * 64 * 4;
@@ -2284,6 +2314,11 @@ int toued_gru_bwd_fused(int R, int T, int W, int K, const uint8_t* done, long do
   TOUED_REQUIRE(p.F >= 1 && p.F <= 6 && p.o.ir_b - p.o.in_w == p.F * HU, "toued_gru_bwd_fused: LPG layout F=%d", p.F);
   const int n_wg = K * (R / (2 * RB)), n_chunk = (n_wg + SR_CHUNK - 1) / SR_CHUNK;
   p.SP = work;
+  {
+    static const char* e = getenv("TOUED_BWD_STAGGER");   // "quanta[,mode]" (study; default off)
+    p.stagger = e ? atoi(e) : 0;
+    p.stagger_mode = e && strchr(e, ',') ? atoi(strchr(e, ',') + 1) : 0;
+  }
   float* part2 = work + (size_t)n_wg * SP_FLOATS;
   hipLaunchKernelGGL(k_gru_bwd6n<true>, dim3(n_wg), dim3(512), 0, stream, p);
   hipLaunchKernelGGL(k_small_part, dim3((SP_FLOATS + 255) / 256, n_chunk), dim3(256), 0, stream, work, n_wg, part2);

@@ -371,6 +371,11 @@ __device__ unsigned long long g_h3_place[64 * 256 * 4];
 __device__ unsigned int g_h3_launch;
 #endif
 
+// cache policy of the streamed B loads (buffer aux bits; 2 = nt): B is read once, A (each slab read by the chunk's
+// column tiles, ideally from L2) is what should stay in L2
+#ifndef H3_B_AUX
+#define H3_B_AUX 0
+#endif
 // NW waves per workgroup, BT B tiles of 16 rows per wave: <4, 3> one wave per SIMD (acc 17 x 3, 512-register
 // budget), <8, 2> two waves per SIMD (acc 17 x 2 in 256 registers) so that one wave's waits are the other's issue.
 template <int NW, int BT>
@@ -509,7 +514,7 @@ __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict
     for (int t = 0; t < BT; ++t)
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
-        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsB[t], (int)boff[t], 128 * s + 64 * hf, 0);
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsB[t], (int)boff[t], 128 * s + 64 * hf, H3_B_AUX);
         bq[t][hf] = make_float4(__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w));
       }
   };

@@ -69,9 +69,14 @@ def init_from_env(backend: str | None = None) -> World:
     local = int(os.environ.get("LOCAL_RANK", rank))
     if backend is None:
         backend = os.environ.get("TOUED_DIST_BACKEND") or ("nccl" if torch.cuda.device_count() > 0 else "gloo")
-    if torch.cuda.device_count() > 0:
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and local >= ndev:
+        # RCCL needs one device per rank: fail here with the cause instead of inside RCCL's communicator init
+        raise RuntimeError(f"backend nccl (RCCL): local rank {local} has no GPU of its own ({ndev} visible); "
+                           f"run at most {ndev} ranks per node, or TOUED_DIST_BACKEND=gloo to share devices")
+    if ndev > 0:
         # one GPU per rank; ranks beyond the device count share devices (gloo only)
-        torch.cuda.set_device(local % torch.cuda.device_count())
+        torch.cuda.set_device(local % ndev)
     if not dist.is_initialized():
         dist.init_process_group(backend=backend)
     return World(rank, ws, local, backend)
