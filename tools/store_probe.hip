@@ -1,0 +1,93 @@
+// Store-path probe (round 5): is a CU's stream of the GRU kernels' per-unit dword stores (lane = row, two 128-byte
+// row segments per wave instruction into [unit][M] arrays) limited per CU or by HBM when every CU stores at once?
+//   hipcc -O3 --offload-arch=gfx950 tools/store_probe.hip -o /tmp/store_probe && /tmp/store_probe
+// Each workgroup (512 threads, one per CU) writes ITER blocks of 64 columns x 256 units (64 KB) into its own column
+// range of a [256][M] f32 array, as k_gru_fwd6's saves / k_gru_bwd6n's DG stores do; grids of 8 (one per XCD), 32,
+// 128 and 256 workgroups; dword stores (lane = row) and 16-byte stores (four consecutive columns per lane), and the
+// backward memory part's 16-byte loads (half the units per block: 32 KB).
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
+
+template <int MODE>
+__global__ void __launch_bounds__(512, 1) k_store(float* __restrict__ out, long M, int iters, unsigned long long* cyc) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hi = lane >> 5, col = lane & 31;
+  const long c0 = (long)blockIdx.x * iters * 64;
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < iters; ++it) {
+    const long cb = c0 + 64L * it;
+    if (MODE == 0) {
+      // 32 dword stores per lane: unit 32 wave + 4 hi + (q & 3) + 8 (q >> 2) (q < 16), rows RB h + col (h = 0, 1)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int u = 32 * wave + 4 * hi + (q & 3) + 8 * (q >> 2);
+          __builtin_nontemporal_store((float)(it + q), out + (long)u * M + cb + 32 * h + col);
+        }
+    } else if (MODE == 2) {
+      // the backward memory part's loads: 16 bytes per lane = four consecutive rows of unit 32 wave + 4 hi + (col & 3)
+      // + 8 g4, rows RB h + (col & 28); 16 per lane per 64-column block (k_gru_bwd6n load_q x 4 arrays x 8 quads / 2)
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      f4v acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int u = 32 * wave + 4 * hi + (col & 3) + 8 * g4;
+          acc += __builtin_nontemporal_load(reinterpret_cast<const f4v*>(out + (long)u * M + cb + 32 * h + (col & 28)));
+        }
+      if (acc.x == 1.2345e-30f) out[tid] = acc.y;   // keeps the loads (never true)
+    } else {
+      // 8 16-byte stores per lane: lane l covers columns 4 (l & 15) .. +3 of unit 32 wave + 4 j + (l >> 4)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int u = 32 * wave + 4 * j + (lane >> 4);
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v v = {(float)it, (float)j, 0.0f, 1.0f};
+        __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(out + (long)u * M + cb + 4 * (lane & 15)));
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (tid == 0) cyc[blockIdx.x] = __builtin_amdgcn_s_memtime() - t0;
+}
+
+int main() {
+  const int iters = 200;
+  const long M = 256L * iters * 64;   // columns: 256 workgroups x iters x 64
+  float* out;
+  unsigned long long* cyc;
+  CHECK(hipMalloc(&out, 256L * M * 4));
+  CHECK(hipMalloc(&cyc, 256 * 8));
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  const int grids[] = {8, 32, 128, 256};
+  for (int mode = 0; mode < 3; ++mode)
+    for (int g : grids) {
+      float best = 1e30f;
+      for (int rep = 0; rep < 3; ++rep) {
+        CHECK(hipEventRecord(a));
+        if (mode == 0) hipLaunchKernelGGL(k_store<0>, dim3(g), dim3(512), 0, 0, out, M, iters, cyc);
+        else if (mode == 1) hipLaunchKernelGGL(k_store<1>, dim3(g), dim3(512), 0, 0, out, M, iters, cyc);
+        else hipLaunchKernelGGL(k_store<2>, dim3(g), dim3(512), 0, 0, out, M, iters, cyc);
+        CHECK(hipEventRecord(b));
+        CHECK(hipEventSynchronize(b));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, a, b));
+        if (ms < best) best = ms;
+      }
+      unsigned long long h[256];
+      CHECK(hipMemcpy(h, cyc, g * 8, hipMemcpyDeviceToHost));
+      double mc = 0;
+      for (int i = 0; i < g; ++i) mc += (double)h[i] / g;
+      const double bytes_wg = (double)iters * 64 * 256 * 4 * (mode == 2 ? 0.5 : 1.0);
+      printf("{\"mode\": \"%s\", \"workgroups\": %d, \"ms\": %.4f, \"GBps\": %.1f, \"cycles_per_wg\": %.0f, "
+             "\"B_per_clk_per_cu\": %.2f}\n", mode == 2 ? "load_b128" : mode ? "b128" : "dword", g, best, bytes_wg * g / best / 1e6, mc,
+             bytes_wg / mc);
+    }
+  return 0;
+}
