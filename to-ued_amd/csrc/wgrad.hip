@@ -376,6 +376,9 @@ __device__ unsigned int g_h3_launch;
 #ifndef H3_B_AUX
 #define H3_B_AUX 0
 #endif
+#ifndef H3_BR2
+#define H3_BR2 1
+#endif
 // NW waves per workgroup, BT B tiles of 16 rows per wave: <4, 3> one wave per SIMD (acc 17 x 3, 512-register
 // budget), <8, 2> two waves per SIMD (acc 17 x 2 in 256 registers) so that one wave's waits are the other's issue.
 template <int NW, int BT>
@@ -582,6 +585,89 @@ __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict
     WG_STAMP(s, 3);
   };
 
+#if H3_BR2
+  // B's raw slabs through a two-buffer register ring instead of split-ahead pieces (same registers: raw x 2 + one
+  // piece set instead of raw + two piece sets): slab s+2's loads go out at tile 1 of slab s and are split at the end of
+  // slab s+1, two slabs in flight instead of one; the split of the next slab's pieces sits after the last tile's MFMAs
+  float4 bq2[2][BT][2];
+  auto issue_into = [&](float4 (&dst)[BT][2], int s) {
+#pragma unroll
+    for (int t = 0; t < BT; ++t)
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsB[t], (int)boff[t], 128 * s + 64 * hf, H3_B_AUX);
+        dst[t][hf] = make_float4(__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w));
+      }
+  };
+  auto split_from = [&](const float4 (&src)[BT][2], f16x8 (&dst)[BT][2]) {
+#pragma unroll
+    for (int t = 0; t < BT; ++t)
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) split2_f16s(f4(src[t][hf], e), bsc, dst[t][0], dst[t][1], 4 * hf + e);
+  };
+  auto slab2 = [&](int s, f16x8 (&bp)[BT][2], const float4 (&nxt)[BT][2], float4 (&fill)[BT][2]) {
+    const int buf = s & 1;
+    load_a(s + 1 < nslab ? s + 1 : s);
+    const f16x8* a0p = As[buf][0];
+    const f16x8* a1p = As[buf][1];
+    constexpr int LA = NW == 4 ? 2 : 1;
+    f16x8 fr[LA + 1][2];
+#pragma unroll
+    for (int d = 0; d < LA; ++d) {
+      const int slot = x6_slot(16 * d + q16, oct);
+      fr[d][0] = a0p[slot]; fr[d][1] = a1p[slot];
+    }
+#pragma unroll
+    for (int i = 0; i < 17; ++i) {
+      if (i + LA < 17) {
+        const int slot = x6_slot(16 * (i + LA) + q16, oct);
+        fr[(i + LA) % (LA + 1)][0] = a0p[slot]; fr[(i + LA) % (LA + 1)][1] = a1p[slot];
+      }
+      const f16x8(&a)[2] = fr[i % (LA + 1)];
+#pragma unroll
+      for (int t = 0; t < BT; ++t) {
+        floatx4 c = acc[i][t];
+        c = mfma_h(a[1], bp[t][0], c);
+        c = mfma_h(a[0], bp[t][1], c);
+        c = mfma_h(a[0], bp[t][0], c);
+        acc[i][t] = c;
+      }
+      if (i == 1) issue_into(fill, s + 2 < nslab ? s + 2 : nslab - 1);
+      if (i >= 17 - NS) write_a(buf ^ 1, i - (17 - NS));
+      if (i == 16) split_from(nxt, bp);   // the last tile's MFMAs have read bp
+      if (i + LA < 17) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+#pragma unroll
+      for (int m = 0; m < 3 * BT; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    lds_barrier();
+  };
+#pragma unroll
+  for (int j = 0; j < NS; ++j) asr[j] = asc[a_index(j) >> 3];
+  f16x8 bpc[BT][2];
+  if (nslab > 0) {
+    load_a(0);
+    issue_into(bq2[0], 0);
+    issue_into(bq2[1], nslab > 1 ? 1 : 0);
+#pragma unroll
+    for (int j = 0; j < NS; ++j) write_a(0, j);
+    split_from(bq2[0], bpc);
+  }
+  __syncthreads();
+  int s2 = 0;
+  for (; s2 + 1 < nslab; s2 += 2) {
+    slab2(s2, bpc, bq2[1], bq2[0]);
+    slab2(s2 + 1, bpc, bq2[0], bq2[1]);
+  }
+  if (s2 < nslab) slab2(s2, bpc, bq2[1], bq2[0]);
+#else
   f16x8 bpa[BT][2], bpb[BT][2];
 #pragma unroll
   for (int j = 0; j < NS; ++j) asr[j] = asc[a_index(j) >> 3];
@@ -602,6 +688,7 @@ __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict
 #pragma unroll
       for (int pc = 0; pc < 2; ++pc) bpa[t][pc] = bpb[t][pc];
   }
+#endif
   // D map: lane l, reg r -> C[16i + 4 oct + r][brow]; unscale by 2^-(s_row + c) (two exact steps)
   const int rbp = ncol * CT;
   float* out = part + (long)sc * X6_RA * rbp;

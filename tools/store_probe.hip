@@ -11,7 +11,8 @@
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
 
 template <int MODE>
-__global__ void __launch_bounds__(512, 1) k_store(float* __restrict__ out, long M, int iters, unsigned long long* cyc) {
+__global__ void __launch_bounds__(512, 1) k_store(float* __restrict__ out, long M, int iters, unsigned long long* cyc,
+                                                  long us, long bs) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hi = lane >> 5, col = lane & 31;
   const long c0 = (long)blockIdx.x * iters * 64;
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -36,7 +37,10 @@ __global__ void __launch_bounds__(512, 1) k_store(float* __restrict__ out, long 
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           const int u = 32 * wave + 4 * hi + (col & 3) + 8 * g4;
-          acc += __builtin_nontemporal_load(reinterpret_cast<const f4v*>(out + (long)u * M + cb + 32 * h + (col & 28)));
+          // element (unit u, column c) at u * us + (c / 64) * bs + c % 64: us = M, bs = 64 is the [256][M] layout;
+          // us = 64, bs = 256 * 64 the blocked [M / 64][256][64] one
+          acc += __builtin_nontemporal_load(
+              reinterpret_cast<const f4v*>(out + (long)u * us + (cb / 64) * bs + 32 * h + (col & 28)));
         }
       if (acc.x == 1.2345e-30f) out[tid] = acc.y;   // keeps the loads (never true)
     } else {
@@ -66,14 +70,18 @@ int main() {
   CHECK(hipEventCreate(&a));
   CHECK(hipEventCreate(&b));
   const int grids[] = {8, 32, 128, 256};
-  for (int mode = 0; mode < 3; ++mode)
+  // loads: [256][M] (unit stride 13 MB), blocked [M/64][256][64] (unit stride 256 B), unit stride 64 KB
+  const long lus[3] = {M, 64L, 16384L};
+  const long lbs[3] = {64L, 256L * 64, 64L};
+  const char* lname[3] = {"load_b128 [256][M]", "load_b128 blocked [M/64][256][64]", "load_b128 unit stride 64 KB"};
+  for (int mode = 0; mode < 5; ++mode)
     for (int g : grids) {
       float best = 1e30f;
       for (int rep = 0; rep < 3; ++rep) {
         CHECK(hipEventRecord(a));
-        if (mode == 0) hipLaunchKernelGGL(k_store<0>, dim3(g), dim3(512), 0, 0, out, M, iters, cyc);
-        else if (mode == 1) hipLaunchKernelGGL(k_store<1>, dim3(g), dim3(512), 0, 0, out, M, iters, cyc);
-        else hipLaunchKernelGGL(k_store<2>, dim3(g), dim3(512), 0, 0, out, M, iters, cyc);
+        if (mode == 0) hipLaunchKernelGGL(k_store<0>, dim3(g), dim3(512), 0, 0, out, M, iters, cyc, M, 64L);
+        else if (mode == 1) hipLaunchKernelGGL(k_store<1>, dim3(g), dim3(512), 0, 0, out, M, iters, cyc, M, 64L);
+        else hipLaunchKernelGGL(k_store<2>, dim3(g), dim3(512), 0, 0, out, M, iters, cyc, lus[mode - 2], lbs[mode - 2]);
         CHECK(hipEventRecord(b));
         CHECK(hipEventSynchronize(b));
         float ms;
@@ -84,9 +92,9 @@ int main() {
       CHECK(hipMemcpy(h, cyc, g * 8, hipMemcpyDeviceToHost));
       double mc = 0;
       for (int i = 0; i < g; ++i) mc += (double)h[i] / g;
-      const double bytes_wg = (double)iters * 64 * 256 * 4 * (mode == 2 ? 0.5 : 1.0);
+      const double bytes_wg = (double)iters * 64 * 256 * 4 * (mode >= 2 ? 0.5 : 1.0);
       printf("{\"mode\": \"%s\", \"workgroups\": %d, \"ms\": %.4f, \"GBps\": %.1f, \"cycles_per_wg\": %.0f, "
-             "\"B_per_clk_per_cu\": %.2f}\n", mode == 2 ? "load_b128" : mode ? "b128" : "dword", g, best, bytes_wg * g / best / 1e6, mc,
+             "\"B_per_clk_per_cu\": %.2f}\n", mode >= 2 ? lname[mode - 2] : mode ? "b128" : "dword", g, best, bytes_wg * g / best / 1e6, mc,
              bytes_wg / mc);
     }
   return 0;
