@@ -1272,6 +1272,7 @@ struct BwdArgs {
   int F;            // LPG input width (lockstep kernel: x rows at s_hin + 256 M, n recomputed by gate_n)
   float* SP;        // fused small products (k_gru_bwd6n<true>): per-workgroup partials [n_wg][SP_FLOATS]
   int stagger, stagger_mode;   // k_gru_bwd6n: s_sleep(127) quanta some first-round workgroups wait at start
+  int wg_base;                 // k_gru_bwd6n: this launch's first workgroup in the whole grid (TOUED_BWD_HALVES)
 };
 // fused small weight-gradient products: per workgroup C[16][256] (rows 0..F-1: X . dn^T, row F: the ones row,
 // rows F+1..F+9: DH . relu(h_out)^T) then the head cotangents' row sums [9][64 rows]
@@ -1543,8 +1544,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, hi = lane >> 5, col = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nb = p.R / RBT;
-  const int k = blockIdx.x / nb;
-  const int r0 = (blockIdx.x - k * nb) * RBT;
+  const int bid = blockIdx.x + p.wg_base;
+  const int k = bid / nb;
+  const int r0 = (bid - k * nb) * RBT;
   const int R = p.R, T = p.T, W = p.W;
 #ifdef BWD_STAMPS
   if (blockIdx.x < 64 && (tid & 63) == 0)
@@ -1684,14 +1686,30 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   };
   // pre: called once in the pass after its last ring reload (k-step 16 - RD): loads issued there stay outstanding
   // behind every ring wait of the pass (vmcnt counts in issue order), so they cost the pass nothing
-  auto contract_h = [&](int g, int sb, float (&qv)[32], long ctr_, auto&& pre) {   // sb: the image slot of the first fp16 piece
-    constexpr int RD = BWD_RD;                    // A-fragment ring depth (k-steps in flight from L2)
-    static_assert(!BWD_SPREAD || 16 % RD == 0, "the spread stores: 2 per k-step, 2 RD per ring group");
-    f16x8 ring[RD][2], B[2][2];
+  // BWD_SPLACE: where the DG stores go.  vmcnt counts loads and stores in issue order, so a ring load issued behind a
+  // 64 KB store burst is waited for only once the burst has drained (HBM-write-bound when every CU stores at once):
+  // with the stores right in front of a pass, its first MFMAs waited for them.  Here each pass's first RD ring slots
+  // are loaded ahead of the stores -- in the previous pass's last RD k-steps, into the slots those k-steps free (no
+  // extra registers), or before the dr split's stores -- and the dz / dhn stores go out at the end of the previous
+  // pass (dz_r, dhn_r are live there anyway), so a burst drains during the barrier, the refill and RD k-steps.
+#ifndef BWD_SPLACE
+#define BWD_SPLACE 0
+#endif
+  static_assert(!BWD_SPLACE || (!BWD_SPREAD && 16 % BWD_RD == 0), "BWD_SPLACE: burst stores, RD dividing 16");
+  f16x8 ring[BWD_RD][2];
+  auto preload_ring = [&](int g) {
 #pragma unroll
-    for (int i = 0; i < RD; ++i)
+    for (int i = 0; i < BWD_RD; ++i)
 #pragma unroll
       for (int q = 0; q < 2; ++q) ring[i][q] = ldAh(i, g, q);
+  };
+  // nextg >= 0 (BWD_SPLACE): the last RD k-steps load pass nextg's first RD slots; post() runs after the last k-step
+  auto contract_h = [&](int g, int sb, float (&qv)[32], long ctr_, auto&& pre, bool preloaded, int nextg,
+                        auto&& post) {   // sb: the image slot of the first fp16 piece
+    constexpr int RD = BWD_RD;                    // A-fragment ring depth (k-steps in flight from L2)
+    static_assert(!BWD_SPREAD || 16 % RD == 0, "the spread stores: 2 per k-step, 2 RD per ring group");
+    f16x8 B[2][2];
+    if (!preloaded) preload_ring(g);
     const int ln = lane_now(), bl = (ln & 31) * PP + 8 * (ln >> 5);
     auto ldB = [&](int ks, int h) {
 #pragma unroll
@@ -1733,7 +1751,13 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         pre();
         __builtin_amdgcn_sched_barrier(0);
       }
+      if (BWD_SPLACE && nextg >= 0 && ks >= 16 - RD) {   // this k-step's slot is free: pass nextg's slot ks - (16 - RD)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) ring[ks % RD][q] = ldAh(ks - (16 - RD), nextg, q);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
+    post();
   };
   // scaled fp16 pieces of the four units u0 .. u0 + 3 of row `row` into image slots 0, 1
 #ifndef BWD_TREFILL
@@ -1964,6 +1988,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     // dr -> fp16 pieces: x0 straight into slot 0, x1 held until every lane has read its staged f32 values
     // (slot 1 overlaps the staging)
     float qv[32];   // the pass's DG store queue (BWD_SPREAD): dr, then dz, then dhn, [h][4 g4 + e]
+    if (BWD_SPLACE) preload_ring(0);   // ahead of the dr stores below
     {
       f16x4 x1h[2][4];
 #pragma unroll
@@ -2007,7 +2032,17 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     }
     BWD_STAMP(4);
     BWD_WSTAMP(2);
-    contract_h(0, 0, qv, ctr, [] {});
+    contract_h(0, 0, qv, ctr, [] {}, (bool)BWD_SPLACE, BWD_SPLACE ? 1 : -1, [&] {
+      if (BWD_SPLACE) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) {
+            const float v4[4] = {dz_r[h][4 * g4], dz_r[h][4 * g4 + 1], dz_r[h][4 * g4 + 2], dz_r[h][4 * g4 + 3]};
+            store_dg(1, RB * h, g4, v4);
+          }
+      }
+    });
     BWD_WSTAMP(3);
     lds_barrier();
     BWD_WSTAMP(4);
@@ -2020,14 +2055,24 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         if (BWD_SPREAD) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) qv[16 * h + 4 * g4 + e] = v4[e];
-        } else {
+        } else if (!BWD_SPLACE) {
           store_dg(1, RB * h, g4, v4);
         }
       }
     lds_barrier();
     BWD_STAMP(5);
     BWD_WSTAMP(5);
-    contract_h(1, 0, qv, ctr, [] {});
+    contract_h(1, 0, qv, ctr, [] {}, (bool)BWD_SPLACE, BWD_SPLACE ? 2 : -1, [&] {
+      if (BWD_SPLACE) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) {
+            const float v4[4] = {dhn_r[h][4 * g4], dhn_r[h][4 * g4 + 1], dhn_r[h][4 * g4 + 2], dhn_r[h][4 * g4 + 3]};
+            store_dg(2, RB * h, g4, v4);
+          }
+      }
+    });
     BWD_WSTAMP(6);
     lds_barrier();
     BWD_WSTAMP(7);
@@ -2040,7 +2085,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         if (BWD_SPREAD) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) qv[16 * h + 4 * g4 + e] = v4[e];
-        } else {
+        } else if (!BWD_SPLACE) {
           store_dg(2, RB * h, g4, v4);
         }
       }
@@ -2048,7 +2093,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     BWD_STAMP(6);
     contract_h(2, 0, qv, ctr, [&] {
       if (t + 1 < T) load_first(ctr + R, true);
-    });
+    }, (bool)BWD_SPLACE, -1, [] {});
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const float4 w4 = *reinterpret_cast<const float4*>(&wsc[32 * wave + 4 * (lane_now() >> 5) + 8 * g4]);
@@ -2082,7 +2127,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   }
   if (SMALL) {
     // this workgroup's partials: C[i = 4 (l >> 4) + r][unit 32 wave + 16 uh + (l & 15)], then the head rows' sums
-    float* out = p.SP + (size_t)blockIdx.x * SP_FLOATS;
+    float* out = p.SP + (size_t)bid * SP_FLOATS;
     const int ln = lane_now();
 #pragma unroll
     for (int uh = 0; uh < 2; ++uh) {
@@ -2092,6 +2137,11 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     }
     for (int i = tid; i < 9 * RBT; i += 512) out[SP_C + i] = hvs[i];
   }
+}
+
+// TOUED_BWD_HALVES: holds its stream for q s_sleep(127) quanta
+__global__ void k_sleep_quanta(int q) {
+  for (int i = 0; i < q; ++i) __builtin_amdgcn_s_sleep(127);
 }
 
 // Sum of the fused small products' per-workgroup partials in a fixed order (deterministic): level 1, block (chunk c of
@@ -2320,7 +2370,39 @@ int toued_gru_bwd_fused(int R, int T, int W, int K, const uint8_t* done, long do
     p.stagger_mode = e && strchr(e, ',') ? atoi(strchr(e, ',') + 1) : 0;
   }
   float* part2 = work + (size_t)n_wg * SP_FLOATS;
-  hipLaunchKernelGGL(k_gru_bwd6n<true>, dim3(n_wg), dim3(512), 0, stream, p);
+  // TOUED_BWD_HALVES=q (study): the grid as two launches on two CU-masked streams (alternate CUs), the second half q
+  // s_sleep quanta (~8 k cycles each) late, so the two halves' memory parts and passes stay out of phase
+  static const int halves = getenv("TOUED_BWD_HALVES") ? atoi(getenv("TOUED_BWD_HALVES")) : -1;
+  if (halves >= 0 && n_wg >= 2) {
+    static hipStream_t sh[2] = {nullptr, nullptr};
+    static hipEvent_t ev[3];
+    if (!sh[0]) {
+      int dev = 0, ncu = 0;
+      TOUED_REQUIRE(hipGetDevice(&dev) == hipSuccess &&
+                        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess,
+                    "toued_gru_bwd_fused: device query failed");
+      uint32_t m[2][16] = {};
+      for (int c = 0; c < ncu && c < 512; ++c) m[c & 1][c >> 5] |= 1u << (c & 31);
+      const uint32_t nw = (uint32_t)((ncu + 31) / 32);
+      for (int h = 0; h < 2; ++h)
+        TOUED_REQUIRE(hipExtStreamCreateWithCUMask(&sh[h], nw, m[h]) == hipSuccess, "CU-masked stream");
+      for (int i = 0; i < 3; ++i) TOUED_REQUIRE(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) == hipSuccess, "ev");
+    }
+    (void)hipEventRecord(ev[0], stream);
+    const int n1 = n_wg / 2;
+    for (int h = 0; h < 2; ++h) {
+      (void)hipStreamWaitEvent(sh[h], ev[0], 0);
+      BwdArgs q = p;
+      q.wg_base = h ? n1 : 0;
+      q.stagger = 0;
+      if (h && halves > 0) hipLaunchKernelGGL(k_sleep_quanta, dim3(1), dim3(64), 0, sh[h], halves);
+      hipLaunchKernelGGL(k_gru_bwd6n<true>, dim3(h ? n_wg - n1 : n1), dim3(512), 0, sh[h], q);
+      (void)hipEventRecord(ev[1 + h], sh[h]);
+      (void)hipStreamWaitEvent(stream, ev[1 + h], 0);
+    }
+  } else {
+    hipLaunchKernelGGL(k_gru_bwd6n<true>, dim3(n_wg), dim3(512), 0, stream, p);
+  }
   hipLaunchKernelGGL(k_small_part, dim3((SP_FLOATS + 255) / 256, n_chunk), dim3(256), 0, stream, work, n_wg, part2);
   hipLaunchKernelGGL(k_small_final, dim3((8 * HU + 9 * (HU + 1) + 255) / 256), dim3(256), 0, stream, part2, n_chunk,
                      p.F, GI);
