@@ -57,7 +57,7 @@ int run(const float* in, float* sink, long M, int iters, unsigned long long* cyc
   CHECK(hipMemcpy(h, cyc, g * 8, hipMemcpyDeviceToHost));
   double mc = 0;
   for (int i = 0; i < g; ++i) mc += (double)h[i] / g;
-  const double bytes_wg = (double)iters * 64 * 256 * 4 * 0.5;
+  const double bytes_wg = (double)iters * 64 * 256 * 4;
   printf("{\"depth_kb_per_wave\": %d, \"aux\": %d, \"workgroups\": %d, \"ms\": %.4f, \"GBps\": %.1f, "
          "\"B_per_clk_per_cu\": %.2f, \"cycles_per_wait\": %.0f}\n", 8 * DEPTH, AUX, g, best, bytes_wg * g / best / 1e6,
          bytes_wg / mc, mc / (iters / DEPTH));

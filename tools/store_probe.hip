@@ -4,7 +4,7 @@
 // Each workgroup (512 threads, one per CU) writes ITER blocks of 64 columns x 256 units (64 KB) into its own column
 // range of a [256][M] f32 array, as k_gru_fwd6's saves / k_gru_bwd6n's DG stores do; grids of 8 (one per XCD), 32,
 // 128 and 256 workgroups; dword stores (lane = row) and 16-byte stores (four consecutive columns per lane), and the
-// backward memory part's 16-byte loads (half the units per block: 32 KB).
+// backward memory part's 16-byte loads (all 256 units of each 64-column block: 64 KB).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 
@@ -92,7 +92,7 @@ int main() {
       CHECK(hipMemcpy(h, cyc, g * 8, hipMemcpyDeviceToHost));
       double mc = 0;
       for (int i = 0; i < g; ++i) mc += (double)h[i] / g;
-      const double bytes_wg = (double)iters * 64 * 256 * 4 * (mode >= 2 ? 0.5 : 1.0);
+      const double bytes_wg = (double)iters * 64 * 256 * 4;
       printf("{\"mode\": \"%s\", \"workgroups\": %d, \"ms\": %.4f, \"GBps\": %.1f, \"cycles_per_wg\": %.0f, "
              "\"B_per_clk_per_cu\": %.2f}\n", mode >= 2 ? lname[mode - 2] : mode ? "b128" : "dword", g, best, bytes_wg * g / best / 1e6, mc,
              bytes_wg / mc);
