@@ -36,8 +36,12 @@ def kernel_stats(db: Path):
     tot = sum(sum(v) for v in agg.values())
     rows = []
     for k, v in agg.items():
+        # median beside the mean: the bench's first (warmup) launches under the profiler run cold and slow
+        srt = sorted(v)
+        med = srt[len(srt) // 2] if len(srt) % 2 else 0.5 * (srt[len(srt) // 2 - 1] + srt[len(srt) // 2])
         rows.append({"kernel": k, "calls": len(v), "total_ns": round(sum(v)), "avg_ns": round(sum(v) / len(v), 1),
-                     "min_ns": round(min(v)), "max_ns": round(max(v)), "percent": round(100 * sum(v) / tot, 3)})
+                     "median_ns": round(med, 1), "min_ns": round(min(v)), "max_ns": round(max(v)),
+                     "percent": round(100 * sum(v) / tot, 3)})
     rows.sort(key=lambda r: -r["total_ns"])
     return rows
 
