@@ -325,9 +325,10 @@ int toued_gru_bwd_fused_fits(int R, int F);
 /* floats of `work` toued_gru_bwd_fused needs: per-workgroup partials of the small products + their chunk sums */
 size_t toued_gru_bwd_fused_work_floats(int R, int K);
 /* the VJP with the small weight-gradient products fused (replaces toued_gru_bwd + toued_gru_bwd_small where it fits):
- * DG3 [3][256][M] = dr, dz, d(W_hn h + b_hn) (the main reduction's B operand), dX3/dX4, col_exp (required), and GI as
- * toued_gru_bwd_small writes it; dn, relu(h_out) and the head cotangents stay on chip (no s_n: n is recomputed).
- * Deterministic: per-workgroup partials summed in a fixed order. */
+ * DG3 = dr, dz, d(W_hn h + b_hn) (the main reduction's B operand, for toued_wgrad_bfp_slab), each gate in 32-column
+ * slab blocks [M/32][256][32] (element (u, m) of gate g at g*256*M + ((m >> 5)*256 + u)*32 + (m & 31)), dX3/dX4,
+ * col_exp (required), and GI as toued_gru_bwd_small writes it; dn, relu(h_out) and the head cotangents stay on chip
+ * (no s_n: n is recomputed).  Deterministic: per-workgroup partials summed in a fixed order. */
 int toued_gru_bwd_fused(int R, int T, int W, int K, const uint8_t* done, long done_stride_k, const float* bwdA,
                         const float* eta, const int* off, const float* y_hat, const float* d_pi_hat,
                         const float* d_y_hat, const float* s_hin, const float* s_r, const float* s_z,
@@ -360,6 +361,10 @@ int toued_rowsum_into(int ra, long K, const float* A, long lda, float* C, int ld
 size_t toued_wgrad_bfp_workspace_floats(int ra, int rb, long K);
 int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit_rows, const float* B, long ldb,
                     const int8_t* col_exp, float* C, float* work, size_t work_floats, hipStream_t stream);
+/* the same with B in 32-column slab blocks of 256 rows, [rb/256][K/32][256][32] (toued_gru_bwd_fused's DG3: each
+ * workgroup's B slab is 32 KB of contiguous memory); rb a multiple of 256; workspace as toued_wgrad_bfp */
+int toued_wgrad_bfp_slab(int ra, int rb, long K, const float* A, long lda, int a_unit_rows, const float* B,
+                         const int8_t* col_exp, float* C, float* work, size_t work_floats, hipStream_t stream);
 
 /* CUs the split-K weight-gradient plans leave free (default 0): a kernel running on a side stream beside them (the
  * eval_agent rollout) then occupies its own CUs instead of pushing one workgroup of every chunk into a second

@@ -63,7 +63,7 @@ def test_fullsize_main_wgrad_matches_float64(c2_step):
     F, M = gru.lay.F, gru.M
     ra = 256 + F + 1
     A = gru.A[:ra]                                # [h_in; x; 1]  [262][M]
-    B = gru.DG.view(3 * 256, M)                   # [dr; dz; dhn] [768][M]
+    B = gru.dg_rows().reshape(3 * 256, M)         # [dr; dz; dhn] [768][M] (rows of the slab blocks)
     ref = torch.zeros(ra, 768, dtype=torch.float64, device="cuda")
     mag = torch.zeros_like(ref)
     step = 1 << 18
@@ -132,9 +132,10 @@ def test_fullsize_backward_sampled_rows_match_float64(c2_step):
     y_ref = torch.softmax(hs @ P["y_w"] + P["y_b"], -1)
     ((pi_ref * dpi).sum() + (y_ref * dy).sum()).backward()
     errs = {}
+    DG = gru.dg_rows()
     for g, name in enumerate(("dr_pre", "dz_pre", "dhn")):
         ref = torch.stack([pres[t][g].grad for t in range(T)], 1)                            # [n, T, 256]
-        got = gru.DG[g][:, cols].permute(1, 2, 0).double()
+        got = DG[g][:, cols].permute(1, 2, 0).double()
         errs[name] = float(torch.linalg.norm(got - ref) / torch.linalg.norm(ref))
     for f, dX in ((3, gru.dX3), (4, gru.dX4)):
         got = dX.view(K * T, R)[torch.from_numpy(ks * T).cuda()[:, None] + torch.arange(T, device="cuda")[None, :],

@@ -689,7 +689,8 @@ def test_gru_backward_fused_small_matches_unfused(N, wscale, F):
         grad = torch.zeros(lay.size, device="cuda")
         gru.backward(done_t, eta, y_hat, d_pi, d_y, gru.X, grad)
         torch.cuda.synchronize()
-        outs.append((gru.DG[:3].clone(), gru.CE.clone(), gru.dX3.clone(), gru.dX4.clone(), gru.GI.clone(), grad))
+        outs.append((gru.dg_rows()[:3].clone(), gru.CE.clone(), gru.dX3.clone(), gru.dX4.clone(), gru.GI.clone(),
+                     grad))
     (dg0, ce0, x30, x40, gi0, g0), (dg1, ce1, x31, x41, gi1, g1) = outs
     assert torch.equal(dg0, dg1) and torch.equal(ce0, ce1)
     assert torch.equal(x30, x31) and torch.equal(x40, x41)

@@ -153,3 +153,10 @@ def test_wgrad_bfp_matches_float64(K, spread):
            work.numel(), L.stream_ptr())
     torch.cuda.synchronize()
     assert torch.equal(C, C2)
+    # B in 32-column slab blocks of 256 rows (the fused backward's DG layout): the same products, the same result
+    Bs = B.view(rb // 256, 256, K // 32, 32).permute(0, 2, 1, 3).contiguous()
+    C3 = torch.full_like(C, float("nan"))
+    L.call("toued_wgrad_bfp_slab", ra, rb, K, L.ptr(A), K, 256, L.ptr(Bs), L.ptr(CE), L.ptr(C3), L.ptr(work),
+           work.numel(), L.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(C, C3)

@@ -1678,11 +1678,22 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   // the pass (the store path takes ~11 B/clk per CU: a 64 KB burst per CU held the waves ~5.7 k cycles per gate).
   // Slot s = 2 RD gi + i of ring group gi (i static): row tile h = s >> 4, register q = s & 15; the queue qv is rotated
   // by 2 RD after each rolled group so that its indices stay static.
+  // SMALL (the fused path, read only by toued_wgrad_bfp_slab): each gate's cotangent DG_g in 32-column slab blocks,
+  // [M / 32][256][32] (element (u, c) at ((c >> 5) * 256 + u) * 32 + (c & 31)): a reduction workgroup's B slab (256
+  // rows x 32 columns) is then 32 KB of contiguous HBM instead of 256 rows x 128 bytes 4 M bytes apart, which HBM
+  // serves at ~4.0 instead of ~5.9 TB/s (tools/load_probe2.hip).  Else [256][M] rows.  Offsets of unit u's 4 bytes at
+  // row r0 + RB h + col of this step: lane part (unit base ub_, col) and uniform part (unit offset uq, tile h)
+  auto dg_vbyte = [&](int ub_, int col_) {
+    return SMALL ? (unsigned)(ub_ * 128 + col_ * 4) : (unsigned)(((long)ub_ * p.M + r0 + col_) * 4);
+  };
+  auto dg_soff = [&](long ctr_, int uq, int h) {
+    return SMALL ? (unsigned)((((ctr_ + r0) >> 5) + h) * 32768L + uq * 128)
+                 : (unsigned)((((long)uq * p.M + ctr_) * 4) + 128 * h);
+  };
   auto store_slot = [&](int gst, long ctr_, int gi, int i, float v) {
     const int s_ = 2 * BWD_RD * gi + i, h = s_ >> 4, e = s_ & 3, g4 = (s_ & 15) >> 2;
-    const unsigned so = (unsigned)((((long)(e + 8 * g4) * p.M + ctr_) * 4) + 128 * h);
     const int ln = lane_now();
-    st_u(rs_dg[gst], (unsigned)((((long)(32 * wave + 4 * (ln >> 5))) * p.M + r0 + (ln & 31)) * 4), so, v);
+    st_u(rs_dg[gst], dg_vbyte(32 * wave + 4 * (ln >> 5), ln & 31), dg_soff(ctr_, e + 8 * g4, h), v);
   };
   // pre: called once in the pass after its last ring reload (k-step 16 - RD): loads issued there stay outstanding
   // behind every ring wait of the pass (vmcnt counts in issue order), so they cost the pass nothing
@@ -1984,7 +1995,11 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     }
     // a lane's four units ub + 8 g4 .. +3 of batch row `row` of gate cotangent g to DG, issued beside the
     // contraction's MFMAs where the memory pipe is otherwise idle
-    auto store_dg = [&](int g, int row, int g4, const float (&v)[4]) { st_q(rs_dg[g], row >= RB, g4, v); };
+    auto store_dg = [&](int g, int row, int g4, const float (&v)[4]) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        st_u(rs_dg[g], dg_vbyte(ub, col), dg_soff(ctr, qunit(4 * g4 + e), row >= RB ? 1 : 0), v[e]);
+    };
     // dr -> fp16 pieces: x0 straight into slot 0, x1 held until every lane has read its staged f32 values
     // (slot 1 overlaps the staging)
     float qv[32];   // the pass's DG store queue (BWD_SPREAD): dr, then dz, then dhn, [h][4 g4 + e]

@@ -381,7 +381,9 @@ __device__ unsigned int g_h3_launch;
 #endif
 // NW waves per workgroup, BT B tiles of 16 rows per wave: <4, 3> one wave per SIMD (acc 17 x 3, 512-register
 // budget), <8, 2> two waves per SIMD (acc 17 x 2 in 256 registers) so that one wave's waits are the other's issue.
-template <int NW, int BT>
+// BSL: B in 32-column slab blocks of 256 rows (toued_wgrad_bfp_slab; k_gru_bwd6n<true>'s DG): row r of block
+// r >> 8, column k at (r >> 8) * 256 K + ((k >> 5) * 256 + (r & 255)) * 32 + (k & 31) floats
+template <int NW, int BT, bool BSL>
 __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict__ A, long lda, int ra,
                                                         int a_unit_rows, const int* __restrict__ rowmax_bits,
                                                         const float* __restrict__ B, long ldb, int rb,
@@ -390,6 +392,7 @@ __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict
                                                         int* __restrict__ visits) {
   constexpr int NT = 64 * NW;
   constexpr int CT = 16 * BT * NW;                          // B rows per workgroup
+  static_assert(!BSL || CT == 256, "slab-block B: one 256-row block per column tile");
   constexpr int NS = (X6_AQ + NT - 1) / NT;                 // A staging rounds per thread
   static_assert(NS <= 17 && 2 * BT < 17 - NS, "side-work schedule: B splits, B issue, then the staging rounds");
   const int ncol = (rb + CT - 1) / CT;
@@ -472,8 +475,14 @@ __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict
     const int tbc = tb < rb ? tb : rb - 1;
     brow[t] = tb + q16;
     const int rr = brow[t] < rb ? brow[t] : rb - 1;
-    rsB[t] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B + (long)tbc * ldb + kb), 0, -1, 0x00020000);
-    boff[t] = (unsigned)(((long)(rr - tbc) * ldb + 4 * oct) * 4);
+    if (BSL) {   // the tile's rows within its block's slab (128 bytes each); the slab in the scalar offset
+      rsB[t] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B + (long)ct * 256 * K + (kb >> 5) * 256 * 32), 0,
+                                                 -1, 0x00020000);
+      boff[t] = (unsigned)((rr - ct * 256) * 128 + 16 * oct);
+    } else {
+      rsB[t] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B + (long)tbc * ldb + kb), 0, -1, 0x00020000);
+      boff[t] = (unsigned)(((long)(rr - tbc) * ldb + 4 * oct) * 4);
+    }
   }
   float4 ast[NS];
   auto a_index = [&](int j) {
@@ -517,7 +526,8 @@ __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict
     for (int t = 0; t < BT; ++t)
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
-        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsB[t], (int)boff[t], 128 * s + 64 * hf, H3_B_AUX);
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsB[t], (int)boff[t], (BSL ? 32768 : 128) * s + 64 * hf,
+                                                              H3_B_AUX);
         bq[t][hf] = make_float4(__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w));
       }
   };
@@ -595,7 +605,8 @@ __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict
     for (int t = 0; t < BT; ++t)
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
-        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsB[t], (int)boff[t], 128 * s + 64 * hf, H3_B_AUX);
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsB[t], (int)boff[t], (BSL ? 32768 : 128) * s + 64 * hf,
+                                                              H3_B_AUX);
         dst[t][hf] = make_float4(__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w));
       }
   };
@@ -992,8 +1003,10 @@ size_t toued_wgrad_bfp_workspace_floats(int ra, int rb, long K) {
   return (size_t)p.S * 17 * 16 * p.ncol * p.ct + X6_RA + 8;
 }
 
-int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit_rows, const float* B, long ldb,
-                    const int8_t* col_exp, float* C, float* work, size_t work_floats, hipStream_t stream) {
+}  // extern "C"
+
+static int wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit_rows, const float* B, long ldb,
+                     bool bslab, const int8_t* col_exp, float* C, float* work, size_t work_floats, hipStream_t stream) {
   TOUED_REQUIRE(ra > 16 && ra <= X6_RA && rb >= 1 && a_unit_rows >= 0 && a_unit_rows <= ra,
                 "toued_wgrad_bfp: ra=%d (17..%d) rb=%d a_unit_rows=%d", ra, X6_RA, rb, a_unit_rows);
   TOUED_REQUIRE(K > 0 && K % 32 == 0, "toued_wgrad_bfp: K=%ld must be a positive multiple of 32", K);
@@ -1019,11 +1032,14 @@ int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit
   }
   int* visits = g_dbg_visits && ntiles <= g_dbg_visits_cap ? g_dbg_visits : nullptr;
   g_dbg_last_ntiles = ntiles;
-  if (wgrad_h8())
-    hipLaunchKernelGGL((k_wgrad_h3<8, 2>), dim3(grid), dim3(512), 0, stream, A, lda, ra, a_unit_rows, bits, B,
+  if (bslab)
+    hipLaunchKernelGGL((k_wgrad_h3<8, 2, true>), dim3(grid), dim3(512), 0, stream, A, lda, ra, a_unit_rows, bits, B,
+                       ldb, rb, col_exp, K, p.kchunk, work, ntiles, qctr, visits);
+  else if (wgrad_h8())
+    hipLaunchKernelGGL((k_wgrad_h3<8, 2, false>), dim3(grid), dim3(512), 0, stream, A, lda, ra, a_unit_rows, bits, B,
                        ldb, rb, col_exp, K, p.kchunk, work, ntiles, qctr, visits);
   else
-    hipLaunchKernelGGL((k_wgrad_h3<X6_NW, X6_BT>), dim3(grid), dim3(64 * X6_NW), 0, stream, A, lda, ra,
+    hipLaunchKernelGGL((k_wgrad_h3<X6_NW, X6_BT, false>), dim3(grid), dim3(64 * X6_NW), 0, stream, A, lda, ra,
                        a_unit_rows, bits, B, ldb, rb, col_exp, K, p.kchunk, work, ntiles, qctr, visits);
 #ifdef H3_PLACE
   hipLaunchKernelGGL(k_h3_next, dim3(1), dim3(64), 0, stream);
@@ -1033,6 +1049,22 @@ int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit
                      p.ncol * p.ct, ra, rb, C, rb);
   TOUED_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" {
+int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit_rows, const float* B, long ldb,
+                    const int8_t* col_exp, float* C, float* work, size_t work_floats, hipStream_t stream) {
+  return wgrad_bfp(ra, rb, K, A, lda, a_unit_rows, B, ldb, false, col_exp, C, work, work_floats, stream);
+}
+
+// The same with B in 32-column slab blocks of 256 rows, [rb / 256][K / 32][256][32] (the fused backward's DG):
+// rb a multiple of 256, the two-waves-per-SIMD kernel
+int toued_wgrad_bfp_slab(int ra, int rb, long K, const float* A, long lda, int a_unit_rows, const float* B,
+                         const int8_t* col_exp, float* C, float* work, size_t work_floats, hipStream_t stream) {
+  TOUED_REQUIRE(rb % 256 == 0 && rb > 0, "toued_wgrad_bfp_slab: rb=%d must be a positive multiple of 256", rb);
+  TOUED_REQUIRE(wgrad_h8(), "toued_wgrad_bfp_slab: slab-block B needs the 256-row tiles (not TOUED_WGRAD_NW4=1)");
+  TOUED_REQUIRE((double)K * 256.0 * 4.0 < 4294967295.0, "toued_wgrad_bfp_slab: a 256-row block of K=%ld exceeds 4 GiB", K);
+  return wgrad_bfp(ra, rb, K, A, lda, a_unit_rows, B, 4, true, col_exp, C, work, work_floats, stream);
 }
 
 }  // extern "C"

@@ -164,7 +164,8 @@ class LPGGRU:
         # unfused kernel + toued_gru_bwd_small)
         fits = bool(L.toued_gru_bwd_fused_fits(R, lay.F))
         self.fused = (fits and os.environ.get("TOUED_BWD_FUSED", "1") != "0") if fused is None else (fused and fits)
-        # dr_pre, dz_pre, d(hn) (+ dn_pre when unfused)
+        # dr_pre, dz_pre, d(hn) (+ dn_pre when unfused); fused: each gate in 32-column slab blocks [M/32][256][32]
+        # (toued_gru_bwd_fused -> toued_wgrad_bfp_slab), else [256][M] rows -- dg_rows() gives rows either way
         self.DG = torch.empty((3 if self.fused else 4, H, M), dtype=f32, device=dev)
         if self.fused:
             self.RH = self.DH = None
@@ -193,6 +194,14 @@ class LPGGRU:
                    int(L.toued_wgrad_bfp_workspace_floats(H + lay.F + 1, 3 * H, M)),
                    int(L.toued_gru_bwd_fused_work_floats(R, K)) if self.fused else int(L.toued_gru_bwd_small_work_floats(M)))
         self.wg_work = torch.empty(max(need, 1), dtype=f32, device=dev)
+
+    def dg_rows(self):
+        """The gate cotangents as [gates][256][M] rows: DG itself (unfused), or a row-major copy of the fused
+        backward's slab blocks (tests, comparison paths)."""
+        if not self.fused:
+            return self.DG
+        g, H, M = self.DG.shape
+        return self.DG.view(g, M // 32, H, 32).permute(0, 2, 1, 3).reshape(g, H, M)
 
     def _scatter_indices(self, dev):
         """(src into G|GI, dst into eta) for the blocks the backward accumulates, the same element pairs as the
@@ -303,12 +312,17 @@ class LPGGRU:
         if before_main_wgrad is not None:
             before_main_wgrad()
         tok_main = timers.start("wgrad_main") if timers is not None else None
-        if self.bfp:
-            _lib.call("toued_wgrad_bfp", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, H, _lib.ptr(DG), M,
+        if self.bfp and self.fused and os.environ.get("TOUED_WGRAD_NW4") != "1":
+            _lib.call("toued_wgrad_bfp_slab", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, H, _lib.ptr(DG),
                       _lib.ptr(self.CE), _lib.ptr(G), ws, wn, st)
         else:
-            _lib.call("toued_wgrad", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, _lib.ptr(DG), M, _lib.ptr(G), ws, wn,
-                      st)
+            B = self.dg_rows()   # (comparison paths with the fused backward: a row-major copy of its slab blocks)
+            if self.bfp:
+                _lib.call("toued_wgrad_bfp", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, H, _lib.ptr(B), M,
+                          _lib.ptr(self.CE), _lib.ptr(G), ws, wn, st)
+            else:
+                _lib.call("toued_wgrad", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, _lib.ptr(B), M, _lib.ptr(G), ws,
+                          wn, st)
         if tok_main is not None:
             timers.stop(tok_main)
         # every block of G (dW_h, dW_i, biases) and GI (dW_in, b_in, head kernels and biases) into eta's layout:
