@@ -237,6 +237,16 @@ TOUED_DEV void store_gate_lds(const float* buf, __amdgpu_buffer_rsrc_t rs, long 
   }
 }
 
+// The split-precision pair's saved r, z, W_hn h + b_hn (k_gru_fwd6 / k_gru_fwd6h write them, k_gru_bwd6n reads them)
+// live in 32-column slab blocks, [M / 32][256][32] per array (element (u, c) at ((c >> 5) * 256 + u) * 32 + (c & 31);
+// the forward's pointers at its update's first block): the backward's per-quad loads (eight consecutive units x 32
+// rows) are then 1 KB of contiguous memory instead of eight 128-byte rows 4 M bytes apart, and a wave's stores fill
+// 4 KB regions (HBM serves 128-byte row segments at ~4.0 TB/s, contiguous KBs at ~5.9: tools/load_probe2.hip).  h_in
+// stays in [256][M] rows: it is also the main weight-gradient reduction's A operand.  Byte offsets of unit
+// ub_ + uq, column c0 + 32 h + col_ (c0 a multiple of 32): lane part vslab, uniform part slab_soff.
+TOUED_DEV unsigned slab_vbyte(int ub_, int col_) { return (unsigned)(ub_ * 128 + col_ * 4); }
+TOUED_DEV unsigned slab_soff(long c0, int h, int uq) { return (unsigned)(((c0 >> 5) + h) * 32768L + uq * 128); }
+
 // ------------------------------------------------------------------ forward
 struct FwdArgs {
   int R, T, W, F;
@@ -654,12 +664,6 @@ __device__ unsigned long long g_fwd_stamps[64 * 32 * 6];
 #ifndef FWD_NOSAVE
 #define FWD_NOSAVE 0   // timing studies only: 1 = no saves, 2 = h_in only (the backward then reads stale data)
 #endif
-#ifndef FWD_ST16T
-#define FWD_ST16T 0   // the saves as 16-byte stores after lane-quad transposes (same layout)
-#endif
-#ifndef FWD_TST16
-#define FWD_TST16 0   // timing study: r, z, hn saved as 16-byte [M][256] rows (global stores)
-#endif
 #ifndef FWD_PF
 #define FWD_PF 0
 #endif
@@ -889,6 +893,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
       const int row = RB * h + col;
       const bool dn = dnf[h];
       const unsigned vbyte = (unsigned)(((long)ub * p.M + r0 + row) * 4);
+      const unsigned vslab = slab_vbyte(ub, col);
       float hp_loc[9];
 #pragma unroll
       for (int oo = 0; oo < 9; ++oo) hp_loc[oo] = 0.0f;
@@ -907,7 +912,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
         }
         f16x4 n0, n1;
         bf16x4 nr;
-        float sv[4][4];   // FWD_TST16 / FWD_ST16T: r, z, hn (, h_in) of the four units, one 16-byte store each
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int q = 4 * g4 + e;
@@ -919,56 +923,23 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
           const float hh = (1.0f - zg) * ng + zg * hin;
           split_carry(dn ? 0.0f : hh, n0, n1, nr, e);   // carry h_in(t-1) = where(d_{t-1}, 0, h_out(t))
           const unsigned so = (unsigned)(((long)qunit(q) * p.M + cbase) * 4);
-          if (SAVE && FWD_ST16T) {
-            sv[0][e] = rg; sv[1][e] = zg; sv[2][e] = hn;
-            if (FWD_ST16T == 2) sv[3][e] = hin; else st_u(rs_hin, vbyte, so, hin);
-          } else if (SAVE && FWD_NOSAVE == 1) {
+          if (SAVE && FWD_NOSAVE == 1) {
             // timing study: no saves
           } else if (SAVE && FWD_NOSAVE == 2) {
             st_u(rs_hin, vbyte, so, hin);   // timing study: h_in only
           } else if (SAVE) {
             st_u(rs_hin, vbyte, so, hin);
-            if (FWD_TST16) {
-              sv[0][e] = rg; sv[1][e] = zg; sv[2][e] = hn;
-            } else {
-              st_u(rs_r, vbyte, so, rg);
-              st_u(rs_z, vbyte, so, zg);
-              st_u(rs_hn, vbyte, so, hn);   // n is recomputed by the backward (gate_n)
-            }
+            // r, z, hn in slab blocks (see slab_soff)
+            const unsigned ss = slab_soff(cbase + r0, h, qunit(q));
+            st_u(rs_r, vslab, ss, rg);
+            st_u(rs_z, vslab, ss, zg);
+            st_u(rs_hn, vslab, ss, hn);   // n is recomputed by the backward (gate_n)
           }
           const float rl = fmaxf(hh, 0.0f);
           const float4 w0 = whl[qunit(q) * 3], w1 = whl[qunit(q) * 3 + 1], w2 = whl[qunit(q) * 3 + 2];
           hp_loc[0] += rl * w0.x; hp_loc[1] += rl * w0.y; hp_loc[2] += rl * w0.z;
           hp_loc[3] += rl * w0.w; hp_loc[4] += rl * w1.x; hp_loc[5] += rl * w1.y;
           hp_loc[6] += rl * w1.z; hp_loc[7] += rl * w1.w; hp_loc[8] += rl * w2.x;
-        }
-        if (SAVE && FWD_ST16T) {
-          // lane-quad transposes (the backward's load in reverse): lane col then holds unit ub + 8 g4 + (col & 3) of
-          // rows (col & 28) .. +3 -- four consecutive columns of one unit row, one 16-byte store per array (a quarter
-          // of the dword store instructions; the address in the VGPR offset, soffset 0)
-          const int ln = lane_now();
-          const unsigned vq = (unsigned)((((long)(ub + (ln & 3))) * p.M + cbase + r0 + RB * h + (ln & 28)) * 4) +
-                              (unsigned)(8 * g4) * (unsigned)p.M * 4u;
-          __amdgpu_buffer_rsrc_t const rs4[4] = {rs_r, rs_z, rs_hn, rs_hin};
-#pragma unroll
-          for (int g = 0; g < (FWD_ST16T == 2 ? 4 : 3); ++g) {
-            quad_transpose(sv[g], ln);
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(sv[g][0]), __float_as_uint(sv[g][1]),
-                                                         __float_as_uint(sv[g][2]), __float_as_uint(sv[g][3])},
-                                                   rs4[g], (int)vq, 0, GRU_ST_AUX);
-          }
-        }
-        if (SAVE && FWD_TST16) {   // [M][256] rows: four consecutive units of this row in 16 bytes (soffset 0)
-          const unsigned vb16 = (unsigned)(((cbase + r0 + row) * HU + ub + 8 * g4) * 4);
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(sv[0][0]), __float_as_uint(sv[0][1]),
-                                                       __float_as_uint(sv[0][2]), __float_as_uint(sv[0][3])},
-                                                 rs_r, (int)vb16, 0, GRU_ST_AUX);
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(sv[1][0]), __float_as_uint(sv[1][1]),
-                                                       __float_as_uint(sv[1][2]), __float_as_uint(sv[1][3])},
-                                                 rs_z, (int)vb16, 0, GRU_ST_AUX);
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(sv[2][0]), __float_as_uint(sv[2][1]),
-                                                       __float_as_uint(sv[2][2]), __float_as_uint(sv[2][3])},
-                                                 rs_hn, (int)vb16, 0, GRU_ST_AUX);
         }
         *reinterpret_cast<f16x4*>(&hB[0][ho]) = n0;
         *reinterpret_cast<f16x4*>(&hB[1][ho]) = n1;
@@ -1181,6 +1152,7 @@ __global__ void __launch_bounds__(256, 2) k_gru_fwd6h(FwdArgs p) {
       const int ub = 32 * U + 4 * hi;
       const float4* whl = reinterpret_cast<const float4*>(wh + ub * 12);
       const unsigned vbyte = (unsigned)(((long)ub * p.M + r0 + col) * 4);
+      const unsigned vslab = slab_vbyte(ub, col);
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const int ho = col * F6_HP + ub + 8 * g4;
@@ -1207,9 +1179,10 @@ __global__ void __launch_bounds__(256, 2) k_gru_fwd6h(FwdArgs p) {
           split_carry(dn ? 0.0f : hh, n0, n1, nr, e);   // carry h_in(t-1) = where(d_{t-1}, 0, h_out(t))
           const unsigned so = (unsigned)(((long)qunit(q) * p.M + cbase) * 4);
           st_u(rs_hin, vbyte, so, hin);
-          st_u(rs_r, vbyte, so, rg);
-          st_u(rs_z, vbyte, so, zg);
-          st_u(rs_hn, vbyte, so, hn);   // n is recomputed by the backward (gate_n)
+          const unsigned ss = slab_soff(cbase + r0, 0, qunit(q));   // r, z, hn in slab blocks
+          st_u(rs_r, vslab, ss, rg);
+          st_u(rs_z, vslab, ss, zg);
+          st_u(rs_hn, vslab, ss, hn);   // n is recomputed by the backward (gate_n)
           const float rl = fmaxf(hh, 0.0f);
           const float4 w0 = whl[qunit(q) * 3], w1 = whl[qunit(q) * 3 + 1], w2 = whl[qunit(q) * 3 + 2];
           hp_loc[0] += rl * w0.x; hp_loc[1] += rl * w0.y; hp_loc[2] += rl * w0.z;
@@ -1823,9 +1796,11 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     const unsigned vq = (unsigned)((((long)(ub + (col & 3))) * p.M + r0 + RB * h + (col & 28)) * 4);
     const unsigned so = (unsigned)(((long)8 * g4 * p.M + ctr_) * 4);
     ld4(rs_hin, vq, so, v[0]);
-    ld4(rs_r, vq, so, v[1]);
-    ld4(rs_z, vq, so, v[2]);
-    ld4(rs_hn, vq, so, v[3]);
+    // r, z, hn from their slab blocks (slab_soff): eight consecutive units x 32 rows, 1 KB contiguous
+    const unsigned vs = slab_vbyte(ub + (col & 3), col & 28), ss = slab_soff(ctr_ + r0, h, 8 * g4);
+    ld4(rs_r, vs, ss, v[1]);
+    ld4(rs_z, vs, ss, v[2]);
+    ld4(rs_hn, vs, ss, v[3]);
   };
   // the rows' inputs x(t) as gate_ain's B fragments (lane = row RB h + col, k = 2 kk + hi): n is recomputed.
   // Tile 0's go out with the first quads, tile 1's beside the ring loads of quad 3.
@@ -2341,6 +2316,9 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
   TOUED_CHECK_LAUNCH();
   return 0;
 }
+
+// 1 when the forward / backward for R rows keep r, z, W_hn h + b_hn in 32-column slab blocks (the split-precision pair)
+int toued_gru_slab_saves(int R) { return toued_gru_bwd_col_exp(R); }
 
 // 1 when toued_gru_bwd_fused applies: the lockstep kernel (R a multiple of 64) with F + 10 <= 16 A rows
 int toued_gru_bwd_fused_fits(int R, int F) { return toued_gru_bwd_col_exp(R) && F >= 1 && F <= 6 ? 1 : 0; }

@@ -159,6 +159,8 @@ class LPGGRU:
         self.A[H + lay.F].fill_(1.0)
         self.X = self.A[H:H + lay.F].view(lay.F, K, T, R)
         self.S = torch.empty((4, H, M), dtype=f32, device=dev)          # r, z, n (f32 fallback only), hn
+        # the split-precision pair keeps r, z, hn in 32-column slab blocks [M/32][256][32] (s_rows() gives rows)
+        self.slab = bool(L.toued_gru_slab_saves(R))
         # the small weight-gradient products fused into the backward (toued_gru_bwd_fused) where the lockstep kernel
         # runs and F <= 6: then dn_pre, relu(h_out) and the head cotangents never reach HBM (TOUED_BWD_FUSED=0: the
         # unfused kernel + toued_gru_bwd_small)
@@ -194,6 +196,13 @@ class LPGGRU:
                    int(L.toued_wgrad_bfp_workspace_floats(H + lay.F + 1, 3 * H, M)),
                    int(L.toued_gru_bwd_fused_work_floats(R, K)) if self.fused else int(L.toued_gru_bwd_small_work_floats(M)))
         self.wg_work = torch.empty(max(need, 1), dtype=f32, device=dev)
+
+    def s_rows(self, i: int):
+        """Saved array i (0 r, 1 z, 2 n, 3 hn) as [256][M] rows (a copy of its slab blocks for r, z, hn)."""
+        if not self.slab or i == 2:
+            return self.S[i]
+        H, M = self.S.shape[1], self.S.shape[2]
+        return self.S[i].view(M // 32, H, 32).permute(1, 0, 2).reshape(H, M)
 
     def dg_rows(self):
         """The gate cotangents as [gates][256][M] rows: DG itself (unfused), or a row-major copy of the fused
@@ -235,11 +244,13 @@ class LPGGRU:
         col = k * T * R
         Xk = X[:, k]
         S = self.S
+        # this update's first column: [256][M] rows (h_in; every save of the f32 pair) or its first slab block
+        sc = H * col if self.slab else col
         _lib.call("toued_gru_fwd", R, T, self.W, self.lay.F, _lib.ptr(X) + 4 * col, M, 1, _lib.ptr(done_k),
                   _lib.ptr(self.fwdA), _lib.ptr(eta), self.lay.c_offsets, _lib.ptr(pi_hat[k]), _lib.ptr(y_hat[k]),
-                  _lib.ptr(self.A) + 4 * col, _lib.ptr(S) + 4 * (0 * H * M + col),
-                  _lib.ptr(S) + 4 * (1 * H * M + col), _lib.ptr(S) + 4 * (2 * H * M + col),
-                  _lib.ptr(S) + 4 * (3 * H * M + col), M, _lib.stream_ptr())
+                  _lib.ptr(self.A) + 4 * col, _lib.ptr(S) + 4 * (0 * H * M + sc),
+                  _lib.ptr(S) + 4 * (1 * H * M + sc), _lib.ptr(S) + 4 * (2 * H * M + col),
+                  _lib.ptr(S) + 4 * (3 * H * M + sc), M, _lib.stream_ptr())
         del Xk
 
     def relu_out(self) -> torch.Tensor:
