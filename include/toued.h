@@ -366,10 +366,14 @@ int toued_rowsum_into(int ra, long K, const float* A, long lda, float* C, int ld
 size_t toued_wgrad_bfp_workspace_floats(int ra, int rb, long K);
 int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit_rows, const float* B, long ldb,
                     const int8_t* col_exp, float* C, float* work, size_t work_floats, hipStream_t stream);
-/* the same with B in 32-column slab blocks of 256 rows, [rb/256][K/32][256][32] (toued_gru_bwd_fused's DG3: each
- * workgroup's B slab is 32 KB of contiguous memory); rb a multiple of 256; workspace as toued_wgrad_bfp */
-int toued_wgrad_bfp_slab(int ra, int rb, long K, const float* A, long lda, int a_unit_rows, const float* B,
-                         const int8_t* col_exp, float* C, float* work, size_t work_floats, hipStream_t stream);
+/* the same with operands in 32-column slab blocks (the split-precision GRU pair's layouts, toued_gru_slab_saves):
+ * layout bit 0 = A's rows [0, 256) (h_in) in slab blocks [K/32][256][32] at A, its rows 256.. in [ra][lda] rows
+ * after them (needs ra > 256, a_unit_rows == 256); bit 1 = B in slab blocks of 256 rows [rb/256][K/32][256][32]
+ * (toued_gru_bwd_fused's DG3; rb % 256 == 0; ldb unused).  Each workgroup's slabs are then contiguous 32 KB pieces
+ * instead of 128-byte row segments.  Workspace as toued_wgrad_bfp. */
+int toued_wgrad_bfp_slab(int ra, int rb, long K, const float* A, long lda, int a_unit_rows, const float* B, long ldb,
+                         int layout, const int8_t* col_exp, float* C, float* work, size_t work_floats,
+                         hipStream_t stream);
 
 /* CUs the split-K weight-gradient plans leave free (default 0): a kernel running on a side stream beside them (the
  * eval_agent rollout) then occupies its own CUs instead of pushing one workgroup of every chunk into a second

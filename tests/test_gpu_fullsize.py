@@ -62,7 +62,7 @@ def test_fullsize_main_wgrad_matches_float64(c2_step):
     gru = tr.step_fn.gru
     F, M = gru.lay.F, gru.M
     ra = 256 + F + 1
-    A = gru.A[:ra]                                # [h_in; x; 1]  [262][M]
+    A = gru.a_rows()[:ra]                         # [h_in; x; 1]  [262][M] (rows of h_in's slab blocks)
     B = gru.dg_rows().reshape(3 * 256, M)         # [dr; dz; dhn] [768][M] (rows of the slab blocks)
     ref = torch.zeros(ra, 768, dtype=torch.float64, device="cuda")
     mag = torch.zeros_like(ref)

@@ -175,7 +175,7 @@ def test_gru_forward_matches_oracle():
         return a.reshape(256, T, R).transpose(1, 2, 0)
     # (the split-precision pair k_gru_fwd6 / k_gru_bwd6n saves no n: the backward recomputes it, gru.hip gate_n)
     from toued import _lib
-    saves = [("hin", tr(gru.A[:256].cpu().numpy())), ("r", tr(gru.s_rows(0).cpu().numpy())),
+    saves = [("hin", tr(gru.hin_rows().cpu().numpy())), ("r", tr(gru.s_rows(0).cpu().numpy())),
              ("z", tr(gru.s_rows(1).cpu().numpy())), ("hn", tr(gru.s_rows(3).cpu().numpy()))]
     if not _lib.lib().toued_gru_bwd_col_exp(R):
         saves.append(("n", tr(gru.S[2].cpu().numpy())))

@@ -156,7 +156,15 @@ def test_wgrad_bfp_matches_float64(K, spread):
     # B in 32-column slab blocks of 256 rows (the fused backward's DG layout): the same products, the same result
     Bs = B.view(rb // 256, 256, K // 32, 32).permute(0, 2, 1, 3).contiguous()
     C3 = torch.full_like(C, float("nan"))
-    L.call("toued_wgrad_bfp_slab", ra, rb, K, L.ptr(A), K, 256, L.ptr(Bs), L.ptr(CE), L.ptr(C3), L.ptr(work),
+    L.call("toued_wgrad_bfp_slab", ra, rb, K, L.ptr(A), K, 256, L.ptr(Bs), K, 2, L.ptr(CE), L.ptr(C3), L.ptr(work),
            work.numel(), L.stream_ptr())
     torch.cuda.synchronize()
     assert torch.equal(C, C3)
+    # and A's rows 0..255 in slab blocks too (the split-precision GRU pair's h_in), alone and with B's
+    As = torch.cat([A[:256].view(256, K // 32, 32).permute(1, 0, 2).reshape(256, K), A[256:]]).contiguous()
+    for layout, b in ((1, B), (3, Bs)):
+        C4 = torch.full_like(C, float("nan"))
+        L.call("toued_wgrad_bfp_slab", ra, rb, K, L.ptr(As), K, 256, L.ptr(b), K, layout, L.ptr(CE), L.ptr(C4),
+               L.ptr(work), work.numel(), L.stream_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(C, C4), layout

@@ -237,13 +237,14 @@ TOUED_DEV void store_gate_lds(const float* buf, __amdgpu_buffer_rsrc_t rs, long 
   }
 }
 
-// The split-precision pair's saved r, z, W_hn h + b_hn (k_gru_fwd6 / k_gru_fwd6h write them, k_gru_bwd6n reads them)
-// live in 32-column slab blocks, [M / 32][256][32] per array (element (u, c) at ((c >> 5) * 256 + u) * 32 + (c & 31);
-// the forward's pointers at its update's first block): the backward's per-quad loads (eight consecutive units x 32
-// rows) are then 1 KB of contiguous memory instead of eight 128-byte rows 4 M bytes apart, and a wave's stores fill
-// 4 KB regions (HBM serves 128-byte row segments at ~4.0 TB/s, contiguous KBs at ~5.9: tools/load_probe2.hip).  h_in
-// stays in [256][M] rows: it is also the main weight-gradient reduction's A operand.  Byte offsets of unit
-// ub_ + uq, column c0 + 32 h + col_ (c0 a multiple of 32): lane part vslab, uniform part slab_soff.
+// The split-precision pair's saves h_in, r, z, W_hn h + b_hn (k_gru_fwd6 / k_gru_fwd6h write them, k_gru_bwd6n reads
+// them; h_in is also the main weight-gradient reduction's A operand, toued_wgrad_bfp_slab layout bit 0) live in
+// 32-column slab blocks, [M / 32][256][32] per array (element (u, c) at ((c >> 5) * 256 + u) * 32 + (c & 31); the
+// forward's pointers at its update's first block; the input rows x that follow h_in stay [F][M] rows): the backward's
+// per-quad loads (eight consecutive units x 32 rows) are then 1 KB of contiguous memory instead of eight 128-byte rows
+// 4 M bytes apart, and a wave's stores fill 4 KB regions (HBM serves 128-byte row segments at ~4.0 TB/s, contiguous
+// KBs at ~5.9: tools/load_probe2.hip).  Byte offsets of unit ub_ + uq, column c0 + 32 h + col_ (c0 a multiple of
+// 32): lane part slab_vbyte, uniform part slab_soff.
 TOUED_DEV unsigned slab_vbyte(int ub_, int col_) { return (unsigned)(ub_ * 128 + col_ * 4); }
 TOUED_DEV unsigned slab_soff(long c0, int h, int uq) { return (unsigned)(((c0 >> 5) + h) * 32768L + uq * 128); }
 
@@ -892,7 +893,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     for (int h = 0; h < 2; ++h) {
       const int row = RB * h + col;
       const bool dn = dnf[h];
-      const unsigned vbyte = (unsigned)(((long)ub * p.M + r0 + row) * 4);
       const unsigned vslab = slab_vbyte(ub, col);
       float hp_loc[9];
 #pragma unroll
@@ -922,15 +922,14 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
           const float hin = (((float)h0[e] + (float)h1[e]) + (float)hr[e]) * (1.0f / HSCALE);   // exact
           const float hh = (1.0f - zg) * ng + zg * hin;
           split_carry(dn ? 0.0f : hh, n0, n1, nr, e);   // carry h_in(t-1) = where(d_{t-1}, 0, h_out(t))
-          const unsigned so = (unsigned)(((long)qunit(q) * p.M + cbase) * 4);
           if (SAVE && FWD_NOSAVE == 1) {
             // timing study: no saves
           } else if (SAVE && FWD_NOSAVE == 2) {
-            st_u(rs_hin, vbyte, so, hin);   // timing study: h_in only
+            st_u(rs_hin, vslab, slab_soff(cbase + r0, h, qunit(q)), hin);   // timing study: h_in only
           } else if (SAVE) {
-            st_u(rs_hin, vbyte, so, hin);
-            // r, z, hn in slab blocks (see slab_soff)
+            // h_in, r, z, hn in slab blocks (see slab_soff)
             const unsigned ss = slab_soff(cbase + r0, h, qunit(q));
+            st_u(rs_hin, vslab, ss, hin);
             st_u(rs_r, vslab, ss, rg);
             st_u(rs_z, vslab, ss, zg);
             st_u(rs_hn, vslab, ss, hn);   // n is recomputed by the backward (gate_n)
@@ -1151,7 +1150,6 @@ __global__ void __launch_bounds__(256, 2) k_gru_fwd6h(FwdArgs p) {
       const floatx16 ain = gate_ain(wI, F, hi, [&](int k) { return xv[k < 7 ? k : 6]; });
       const int ub = 32 * U + 4 * hi;
       const float4* whl = reinterpret_cast<const float4*>(wh + ub * 12);
-      const unsigned vbyte = (unsigned)(((long)ub * p.M + r0 + col) * 4);
       const unsigned vslab = slab_vbyte(ub, col);
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
@@ -1177,9 +1175,8 @@ __global__ void __launch_bounds__(256, 2) k_gru_fwd6h(FwdArgs p) {
           const float hin = (((float)h0[e] + (float)h1[e]) + (float)hr[e]) * (1.0f / HSCALE);   // exact
           const float hh = (1.0f - zg) * ng + zg * hin;
           split_carry(dn ? 0.0f : hh, n0, n1, nr, e);   // carry h_in(t-1) = where(d_{t-1}, 0, h_out(t))
-          const unsigned so = (unsigned)(((long)qunit(q) * p.M + cbase) * 4);
-          st_u(rs_hin, vbyte, so, hin);
-          const unsigned ss = slab_soff(cbase + r0, 0, qunit(q));   // r, z, hn in slab blocks
+          const unsigned ss = slab_soff(cbase + r0, 0, qunit(q));   // h_in, r, z, hn in slab blocks
+          st_u(rs_hin, vslab, ss, hin);
           st_u(rs_r, vslab, ss, rg);
           st_u(rs_z, vslab, ss, zg);
           st_u(rs_hn, vslab, ss, hn);   // n is recomputed by the backward (gate_n)
@@ -1793,11 +1790,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   const int ub = 32 * wave + 4 * hi;               // lane's unit base (register q adds qunit(q))
   float vr[NR][4][4];   // NR-slot ring: quads i+1 .. i+NR-1 in flight while quad i is processed (NR = 2: 10.11 ms)
   auto load_q = [&](long ctr_, int h, int g4, float (&v)[4][4]) {
-    const unsigned vq = (unsigned)((((long)(ub + (col & 3))) * p.M + r0 + RB * h + (col & 28)) * 4);
-    const unsigned so = (unsigned)(((long)8 * g4 * p.M + ctr_) * 4);
-    ld4(rs_hin, vq, so, v[0]);
-    // r, z, hn from their slab blocks (slab_soff): eight consecutive units x 32 rows, 1 KB contiguous
+    // h_in, r, z, hn from their slab blocks (slab_soff): eight consecutive units x 32 rows, 1 KB contiguous
     const unsigned vs = slab_vbyte(ub + (col & 3), col & 28), ss = slab_soff(ctr_ + r0, h, 8 * g4);
+    ld4(rs_hin, vs, ss, v[0]);
     ld4(rs_r, vs, ss, v[1]);
     ld4(rs_z, vs, ss, v[2]);
     ld4(rs_hn, vs, ss, v[3]);

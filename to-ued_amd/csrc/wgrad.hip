@@ -381,9 +381,10 @@ __device__ unsigned int g_h3_launch;
 #endif
 // NW waves per workgroup, BT B tiles of 16 rows per wave: <4, 3> one wave per SIMD (acc 17 x 3, 512-register
 // budget), <8, 2> two waves per SIMD (acc 17 x 2 in 256 registers) so that one wave's waits are the other's issue.
-// BSL: B in 32-column slab blocks of 256 rows (toued_wgrad_bfp_slab; k_gru_bwd6n<true>'s DG): row r of block
-// r >> 8, column k at (r >> 8) * 256 K + ((k >> 5) * 256 + (r & 255)) * 32 + (k & 31) floats
-template <int NW, int BT, bool BSL>
+// LAY (toued_wgrad_bfp_slab): bit 1 = B in 32-column slab blocks of 256 rows (k_gru_bwd6n<true>'s DG): row r of block
+// r >> 8, column k at (r >> 8) * 256 K + ((k >> 5) * 256 + (r & 255)) * 32 + (k & 31) floats; bit 0 = A's rows 0..255
+// (the GRU's h_in) in slab blocks at A, ((k >> 5) * 256 + r) * 32 + (k & 31), its rows 256.. in [ra][lda] rows
+template <int NW, int BT, int LAY>
 __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict__ A, long lda, int ra,
                                                         int a_unit_rows, const int* __restrict__ rowmax_bits,
                                                         const float* __restrict__ B, long ldb, int rb,
@@ -392,6 +393,7 @@ __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict
                                                         int* __restrict__ visits) {
   constexpr int NT = 64 * NW;
   constexpr int CT = 16 * BT * NW;                          // B rows per workgroup
+  constexpr bool BSL = (LAY & 2) != 0, ASL = (LAY & 1) != 0;
   static_assert(!BSL || CT == 256, "slab-block B: one 256-row block per column tile");
   constexpr int NS = (X6_AQ + NT - 1) / NT;                 // A staging rounds per thread
   static_assert(NS <= 17 && 2 * BT < 17 - NS, "side-work schedule: B splits, B issue, then the staging rounds");
@@ -492,17 +494,24 @@ __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict
   // A through a buffer descriptor: per round one 32-bit lane offset (row, k-quad), the slab's column in the scalar
   // offset (64-bit row pointers per round, loop-invariant, were spilled and reloaded every slab)
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A), 0, -1, 0x00020000);
+  // ASL: rounds j < JS stage rows 0..255 (uniform per round: round j holds rows j NT / 8 .. (j + 1) NT / 8 - 1) from the
+  // slab blocks: the chunk's first block in the descriptor, the slab's block in the scalar offset
+  constexpr int JS = ASL ? 2048 / NT : 0;
+  static_assert(!ASL || (2048 % NT == 0 && JS <= NS - 1), "slab-block A: rounds split at row 256");
+  const __amdgpu_buffer_rsrc_t rsAs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A + (ASL ? (kb >> 5) * 256 * 32 : 0)), 0, -1, 0x00020000);
   unsigned avo[NS];
 #pragma unroll
   for (int j = 0; j < NS; ++j) {
     const int i = a_index(j);
     const int row = (i >> 3) < ra ? (i >> 3) : ra - 1;
-    avo[j] = (unsigned)(((long)row * lda + 4 * (i & 7)) * 4);
+    avo[j] = j < JS ? (unsigned)((row * 32 + 4 * (i & 7)) * 4) : (unsigned)(((long)row * lda + 4 * (i & 7)) * 4);
   }
   auto load_a = [&](int s) {
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
-      const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)avo[j], (int)((kb + 32L * s) * 4), 0);
+      const u32x4 x = j < JS ? __builtin_amdgcn_raw_buffer_load_b128(rsAs, (int)avo[j], 32768 * s, 0)
+                             : __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)avo[j], (int)((kb + 32L * s) * 4), 0);
       ast[j] = make_float4(__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w));
     }
   };
@@ -1006,7 +1015,7 @@ size_t toued_wgrad_bfp_workspace_floats(int ra, int rb, long K) {
 }  // extern "C"
 
 static int wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit_rows, const float* B, long ldb,
-                     bool bslab, const int8_t* col_exp, float* C, float* work, size_t work_floats, hipStream_t stream) {
+                     int layout, const int8_t* col_exp, float* C, float* work, size_t work_floats, hipStream_t stream) {
   TOUED_REQUIRE(ra > 16 && ra <= X6_RA && rb >= 1 && a_unit_rows >= 0 && a_unit_rows <= ra,
                 "toued_wgrad_bfp: ra=%d (17..%d) rb=%d a_unit_rows=%d", ra, X6_RA, rb, a_unit_rows);
   TOUED_REQUIRE(K > 0 && K % 32 == 0, "toued_wgrad_bfp: K=%ld must be a positive multiple of 32", K);
@@ -1032,14 +1041,20 @@ static int wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_uni
   }
   int* visits = g_dbg_visits && ntiles <= g_dbg_visits_cap ? g_dbg_visits : nullptr;
   g_dbg_last_ntiles = ntiles;
-  if (bslab)
-    hipLaunchKernelGGL((k_wgrad_h3<8, 2, true>), dim3(grid), dim3(512), 0, stream, A, lda, ra, a_unit_rows, bits, B,
+  if (layout == 3)
+    hipLaunchKernelGGL((k_wgrad_h3<8, 2, 3>), dim3(grid), dim3(512), 0, stream, A, lda, ra, a_unit_rows, bits, B,
+                       ldb, rb, col_exp, K, p.kchunk, work, ntiles, qctr, visits);
+  else if (layout == 2)
+    hipLaunchKernelGGL((k_wgrad_h3<8, 2, 2>), dim3(grid), dim3(512), 0, stream, A, lda, ra, a_unit_rows, bits, B,
+                       ldb, rb, col_exp, K, p.kchunk, work, ntiles, qctr, visits);
+  else if (layout == 1)
+    hipLaunchKernelGGL((k_wgrad_h3<8, 2, 1>), dim3(grid), dim3(512), 0, stream, A, lda, ra, a_unit_rows, bits, B,
                        ldb, rb, col_exp, K, p.kchunk, work, ntiles, qctr, visits);
   else if (wgrad_h8())
-    hipLaunchKernelGGL((k_wgrad_h3<8, 2, false>), dim3(grid), dim3(512), 0, stream, A, lda, ra, a_unit_rows, bits, B,
+    hipLaunchKernelGGL((k_wgrad_h3<8, 2, 0>), dim3(grid), dim3(512), 0, stream, A, lda, ra, a_unit_rows, bits, B,
                        ldb, rb, col_exp, K, p.kchunk, work, ntiles, qctr, visits);
   else
-    hipLaunchKernelGGL((k_wgrad_h3<X6_NW, X6_BT, false>), dim3(grid), dim3(64 * X6_NW), 0, stream, A, lda, ra,
+    hipLaunchKernelGGL((k_wgrad_h3<X6_NW, X6_BT, 0>), dim3(grid), dim3(64 * X6_NW), 0, stream, A, lda, ra,
                        a_unit_rows, bits, B, ldb, rb, col_exp, K, p.kchunk, work, ntiles, qctr, visits);
 #ifdef H3_PLACE
   hipLaunchKernelGGL(k_h3_next, dim3(1), dim3(64), 0, stream);
@@ -1054,17 +1069,25 @@ static int wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_uni
 extern "C" {
 int toued_wgrad_bfp(int ra, int rb, long K, const float* A, long lda, int a_unit_rows, const float* B, long ldb,
                     const int8_t* col_exp, float* C, float* work, size_t work_floats, hipStream_t stream) {
-  return wgrad_bfp(ra, rb, K, A, lda, a_unit_rows, B, ldb, false, col_exp, C, work, work_floats, stream);
+  return wgrad_bfp(ra, rb, K, A, lda, a_unit_rows, B, ldb, 0, col_exp, C, work, work_floats, stream);
 }
 
-// The same with B in 32-column slab blocks of 256 rows, [rb / 256][K / 32][256][32] (the fused backward's DG):
-// rb a multiple of 256, the two-waves-per-SIMD kernel
-int toued_wgrad_bfp_slab(int ra, int rb, long K, const float* A, long lda, int a_unit_rows, const float* B,
-                         const int8_t* col_exp, float* C, float* work, size_t work_floats, hipStream_t stream) {
-  TOUED_REQUIRE(rb % 256 == 0 && rb > 0, "toued_wgrad_bfp_slab: rb=%d must be a positive multiple of 256", rb);
-  TOUED_REQUIRE(wgrad_h8(), "toued_wgrad_bfp_slab: slab-block B needs the 256-row tiles (not TOUED_WGRAD_NW4=1)");
+// The same with operands in 32-column slab blocks (the split-precision GRU pair's layouts): layout bit 0 = A's rows
+// [0, 256) in slab blocks at A ([K/32][256][32]; its rows 256.. stay [ra][lda] rows at A), bit 1 = B in slab blocks
+// of 256 rows, [rb/256][K/32][256][32] (ldb unused).  The two-waves-per-SIMD kernel; bit 1 needs rb % 256 == 0,
+// bit 0 ra > 256 and a_unit_rows == 256.
+int toued_wgrad_bfp_slab(int ra, int rb, long K, const float* A, long lda, int a_unit_rows, const float* B, long ldb,
+                         int layout, const int8_t* col_exp, float* C, float* work, size_t work_floats,
+                         hipStream_t stream) {
+  TOUED_REQUIRE(layout >= 0 && layout <= 3, "toued_wgrad_bfp_slab: layout=%d (0..3)", layout);
+  TOUED_REQUIRE(!(layout & 2) || (rb % 256 == 0 && rb > 0), "toued_wgrad_bfp_slab: rb=%d must be a multiple of 256", rb);
+  TOUED_REQUIRE(!(layout & 1) || (ra > 256 && a_unit_rows == 256),
+                "toued_wgrad_bfp_slab: slab-block A needs ra > 256 (got %d) and a_unit_rows == 256 (got %d)", ra,
+                a_unit_rows);
+  TOUED_REQUIRE(layout == 0 || wgrad_h8(), "toued_wgrad_bfp_slab: slab blocks need the 256-row tiles (not TOUED_WGRAD_NW4=1)");
   TOUED_REQUIRE((double)K * 256.0 * 4.0 < 4294967295.0, "toued_wgrad_bfp_slab: a 256-row block of K=%ld exceeds 4 GiB", K);
-  return wgrad_bfp(ra, rb, K, A, lda, a_unit_rows, B, 4, true, col_exp, C, work, work_floats, stream);
+  return wgrad_bfp(ra, rb, K, A, lda, a_unit_rows, B, (layout & 2) ? 4 : ldb, layout, col_exp, C, work, work_floats,
+                   stream);
 }
 
 }  // extern "C"

@@ -82,7 +82,7 @@ _SIGS = {
     "toued_set_reserved_cus": [_I],
     "toued_wgrad_bfp_workspace_floats": [_I, _I, _L],
     "toued_wgrad_bfp": [_I, _I, _L, _P, _L, _I, _P, _L, _P, _P, _P, ctypes.c_size_t, _P],
-    "toued_wgrad_bfp_slab": [_I, _I, _L, _P, _L, _I, _P, _P, _P, _P, ctypes.c_size_t, _P],
+    "toued_wgrad_bfp_slab": [_I, _I, _L, _P, _L, _I, _P, _L, _I, _P, _P, _P, ctypes.c_size_t, _P],
     "toued_gru_slab_saves": [_I],
     "toued_gru_bwd_small_work_floats": [_L],
     "toued_gru_bwd_small": [_L, _P, _P, _P, _P, _P, _P, ctypes.c_size_t, _P],

@@ -159,7 +159,8 @@ class LPGGRU:
         self.A[H + lay.F].fill_(1.0)
         self.X = self.A[H:H + lay.F].view(lay.F, K, T, R)
         self.S = torch.empty((4, H, M), dtype=f32, device=dev)          # r, z, n (f32 fallback only), hn
-        # the split-precision pair keeps r, z, hn in 32-column slab blocks [M/32][256][32] (s_rows() gives rows)
+        # the split-precision pair keeps h_in (A's first 256 rows' region) and r, z, hn in 32-column slab blocks
+        # [M/32][256][32] (hin_rows(), a_rows(), s_rows() give rows); A's rows 256.. (x, ones) stay rows
         self.slab = bool(L.toued_gru_slab_saves(R))
         # the small weight-gradient products fused into the backward (toued_gru_bwd_fused) where the lockstep kernel
         # runs and F <= 6: then dn_pre, relu(h_out) and the head cotangents never reach HBM (TOUED_BWD_FUSED=0: the
@@ -196,6 +197,23 @@ class LPGGRU:
                    int(L.toued_wgrad_bfp_workspace_floats(H + lay.F + 1, 3 * H, M)),
                    int(L.toued_gru_bwd_fused_work_floats(R, K)) if self.fused else int(L.toued_gru_bwd_small_work_floats(M)))
         self.wg_work = torch.empty(max(need, 1), dtype=f32, device=dev)
+
+    def hin_rows(self):
+        """The saved h_in as [256][M] rows (a copy of its slab blocks on the split-precision pair)."""
+        H, M = 256, self.M
+        if not self.slab:
+            return self.A[:H]
+        return self.A[:H].reshape(-1).view(M // 32, H, 32).permute(1, 0, 2).reshape(H, M)
+
+    def a_rows(self):
+        """The main reduction's A operand [h_in; x; 1; pad] as [264][M] rows (a copy when h_in is in slab blocks)."""
+        return torch.cat([self.hin_rows(), self.A[256:]]) if self.slab else self.A
+
+    def hin_block(self, k: int):
+        """Update k's saved h_in (for --debug_nans): a [256][T*R] column block of the rows, or its contiguous slab
+        blocks."""
+        c0, n = k * self.T * self.R, self.T * self.R
+        return self.A.view(-1)[256 * c0:256 * (c0 + n)] if self.slab else self.A[:256, c0:c0 + n]
 
     def s_rows(self, i: int):
         """Saved array i (0 r, 1 z, 2 n, 3 hn) as [256][M] rows (a copy of its slab blocks for r, z, hn)."""
@@ -244,11 +262,11 @@ class LPGGRU:
         col = k * T * R
         Xk = X[:, k]
         S = self.S
-        # this update's first column: [256][M] rows (h_in; every save of the f32 pair) or its first slab block
+        # this update's first column: [256][M] rows (the f32 pair) or its first slab block (the split-precision pair)
         sc = H * col if self.slab else col
         _lib.call("toued_gru_fwd", R, T, self.W, self.lay.F, _lib.ptr(X) + 4 * col, M, 1, _lib.ptr(done_k),
                   _lib.ptr(self.fwdA), _lib.ptr(eta), self.lay.c_offsets, _lib.ptr(pi_hat[k]), _lib.ptr(y_hat[k]),
-                  _lib.ptr(self.A) + 4 * col, _lib.ptr(S) + 4 * (0 * H * M + sc),
+                  _lib.ptr(self.A) + 4 * sc, _lib.ptr(S) + 4 * (0 * H * M + sc),
                   _lib.ptr(S) + 4 * (1 * H * M + sc), _lib.ptr(S) + 4 * (2 * H * M + col),
                   _lib.ptr(S) + 4 * (3 * H * M + sc), M, _lib.stream_ptr())
         del Xk
@@ -323,17 +341,18 @@ class LPGGRU:
         if before_main_wgrad is not None:
             before_main_wgrad()
         tok_main = timers.start("wgrad_main") if timers is not None else None
-        if self.bfp and self.fused and os.environ.get("TOUED_WGRAD_NW4") != "1":
-            _lib.call("toued_wgrad_bfp_slab", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, H, _lib.ptr(DG),
-                      _lib.ptr(self.CE), _lib.ptr(G), ws, wn, st)
+        if self.bfp and self.slab and os.environ.get("TOUED_WGRAD_NW4") != "1":
+            # h_in in slab blocks (layout bit 0); the fused backward's DG too (bit 1), the unfused one's in rows
+            _lib.call("toued_wgrad_bfp_slab", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, H, _lib.ptr(DG), M,
+                      3 if self.fused else 1, _lib.ptr(self.CE), _lib.ptr(G), ws, wn, st)
         else:
-            B = self.dg_rows()   # (comparison paths with the fused backward: a row-major copy of its slab blocks)
+            # (comparison paths on the split-precision pair: row-major copies of the slab blocks)
+            A, B = self.a_rows(), self.dg_rows()
             if self.bfp:
-                _lib.call("toued_wgrad_bfp", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, H, _lib.ptr(B), M,
+                _lib.call("toued_wgrad_bfp", H + F + 1, 3 * H, M, _lib.ptr(A), M, H, _lib.ptr(B), M,
                           _lib.ptr(self.CE), _lib.ptr(G), ws, wn, st)
             else:
-                _lib.call("toued_wgrad", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, _lib.ptr(B), M, _lib.ptr(G), ws,
-                          wn, st)
+                _lib.call("toued_wgrad", H + F + 1, 3 * H, M, _lib.ptr(A), M, _lib.ptr(B), M, _lib.ptr(G), ws, wn, st)
         if tok_main is not None:
             timers.stop(tok_main)
         # every block of G (dW_h, dW_i, biases) and GI (dW_in, b_in, head kernels and biases) into eta's layout:

@@ -317,7 +317,7 @@ class MetaGradStep:
             self.gru.forward(k, self.X, tk.done, eta, self.pi_hat, self.y_hat)
             self.timers.stop(tok)
             if nan_checker().enabled:   # the update's saved GRU states h_in [256][T*R] (a column block of the operand)
-                nan_checker().check("lpg_gru_states", self.gru.A[:256, k * T * R:(k + 1) * T * R])
+                nan_checker().check("lpg_gru_states", self.gru.hin_block(k))
             nan_checker().check("lpg_outputs", self.pi_hat[k], self.y_hat[k])
             if self.fused_step:
                 main.wait_stream(self.side)

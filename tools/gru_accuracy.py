@@ -53,7 +53,7 @@ def main():
     hs = torch.relu(torch.stack(outs, 1))
     pi_ref = (hs @ P["pi_w"] + P["pi_b"])[..., 0].numpy()
     y_ref = torch.softmax(hs @ P["y_w"] + P["y_b"], -1).numpy()
-    hin_gpu = gru.A[:256].cpu().numpy().reshape(256, T, R).transpose(2, 1, 0)
+    hin_gpu = gru.hin_rows().cpu().numpy().reshape(256, T, R).transpose(2, 1, 0)
     hin_ref = torch.stack(hins, 1).numpy()
     res = {"kernel": "f32" if os.environ.get("TOUED_GRU_F32") == "1" else "default",
            "pi_hat_max_abs": float(np.abs(pi_hat[0].cpu().numpy().T - pi_ref).max()),
