@@ -487,9 +487,11 @@ __global__ void __launch_bounds__(64 * NW, 1) k_wgrad_h3(const float* __restrict
     }
   }
   float4 ast[NS];
+  // the last round's threads past the slab's 272 rows redo row 271's k-quads (identical values, benign duplicate LDS
+  // writes); they must stay in rows >= 256 so that a round is uniformly slab-block or row-major A (ASL)
   auto a_index = [&](int j) {
     const int i = tid + NT * j;
-    return j < NS - 1 || i < X6_AQ ? i : i - NT;
+    return j < NS - 1 || i < X6_AQ ? i : X6_AQ - 8 + (i & 7);
   };
   // A through a buffer descriptor: per round one 32-bit lane offset (row, k-quad), the slab's column in the scalar
   // offset (64-bit row pointers per round, loop-invariant, were spilled and reloaded every slab)
