@@ -325,6 +325,8 @@ int toued_gru_bwd_col_exp(int R);
 /* 1 when the forward and backward for R rows keep r, z, W_hn h + b_hn in 32-column slab blocks (see toued_gru_fwd):
  * the split-precision pair's 1 KB-contiguous loads and stores instead of 128-byte rows */
 int toued_gru_slab_saves(int R);
+/* 1 when those slab blocks include h_in (A's first 256 rows' region; 0 only in HIN_SLAB=0 comparison builds) */
+int toued_gru_hin_slab(void);
 /* 1 when toued_gru_bwd_fused applies: the lockstep kernel for R rows and LPG input width F <= 6 */
 int toued_gru_bwd_fused_fits(int R, int F);
 /* floats of `work` toued_gru_bwd_fused needs: per-workgroup partials of the small products + their chunk sums */

@@ -245,6 +245,10 @@ TOUED_DEV void store_gate_lds(const float* buf, __amdgpu_buffer_rsrc_t rs, long 
 // 4 M bytes apart, and a wave's stores fill 4 KB regions (HBM serves 128-byte row segments at ~4.0 TB/s, contiguous
 // KBs at ~5.9: tools/load_probe2.hip).  Byte offsets of unit ub_ + uq, column c0 + 32 h + col_ (c0 a multiple of
 // 32): lane part slab_vbyte, uniform part slab_soff.
+// HIN_SLAB=0 (comparison builds): h_in in [256][M] rows (toued_gru_hin_slab() reports it to the host)
+#ifndef HIN_SLAB
+#define HIN_SLAB 1
+#endif
 TOUED_DEV unsigned slab_vbyte(int ub_, int col_) { return (unsigned)(ub_ * 128 + col_ * 4); }
 TOUED_DEV unsigned slab_soff(long c0, int h, int uq) { return (unsigned)(((c0 >> 5) + h) * 32768L + uq * 128); }
 
@@ -929,7 +933,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
           } else if (SAVE) {
             // h_in, r, z, hn in slab blocks (see slab_soff)
             const unsigned ss = slab_soff(cbase + r0, h, qunit(q));
-            st_u(rs_hin, vslab, ss, hin);
+            if (HIN_SLAB) st_u(rs_hin, vslab, ss, hin);
+            else st_u(rs_hin, (unsigned)(((long)ub * p.M + r0 + row) * 4), (unsigned)(((long)qunit(q) * p.M + cbase) * 4), hin);
             st_u(rs_r, vslab, ss, rg);
             st_u(rs_z, vslab, ss, zg);
             st_u(rs_hn, vslab, ss, hn);   // n is recomputed by the backward (gate_n)
@@ -1176,7 +1181,8 @@ __global__ void __launch_bounds__(256, 2) k_gru_fwd6h(FwdArgs p) {
           const float hh = (1.0f - zg) * ng + zg * hin;
           split_carry(dn ? 0.0f : hh, n0, n1, nr, e);   // carry h_in(t-1) = where(d_{t-1}, 0, h_out(t))
           const unsigned ss = slab_soff(cbase + r0, 0, qunit(q));   // h_in, r, z, hn in slab blocks
-          st_u(rs_hin, vslab, ss, hin);
+          if (HIN_SLAB) st_u(rs_hin, vslab, ss, hin);
+          else st_u(rs_hin, (unsigned)(((long)ub * p.M + r0 + col) * 4), (unsigned)(((long)qunit(q) * p.M + cbase) * 4), hin);
           st_u(rs_r, vslab, ss, rg);
           st_u(rs_z, vslab, ss, zg);
           st_u(rs_hn, vslab, ss, hn);   // n is recomputed by the backward (gate_n)
@@ -1792,7 +1798,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   auto load_q = [&](long ctr_, int h, int g4, float (&v)[4][4]) {
     // h_in, r, z, hn from their slab blocks (slab_soff): eight consecutive units x 32 rows, 1 KB contiguous
     const unsigned vs = slab_vbyte(ub + (col & 3), col & 28), ss = slab_soff(ctr_ + r0, h, 8 * g4);
-    ld4(rs_hin, vs, ss, v[0]);
+    if (HIN_SLAB) ld4(rs_hin, vs, ss, v[0]);
+    else ld4(rs_hin, (unsigned)((((long)(ub + (col & 3))) * p.M + r0 + RB * h + (col & 28)) * 4),
+             (unsigned)(((long)8 * g4 * p.M + ctr_) * 4), v[0]);
     ld4(rs_r, vs, ss, v[1]);
     ld4(rs_z, vs, ss, v[2]);
     ld4(rs_hn, vs, ss, v[3]);
@@ -2314,6 +2322,8 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
 
 // 1 when the forward / backward for R rows keep r, z, W_hn h + b_hn in 32-column slab blocks (the split-precision pair)
 int toued_gru_slab_saves(int R) { return toued_gru_bwd_col_exp(R); }
+// 1 when the slab saves include h_in (A's first 256 rows' region; 0 only in HIN_SLAB=0 comparison builds)
+int toued_gru_hin_slab(void) { return HIN_SLAB; }
 
 // 1 when toued_gru_bwd_fused applies: the lockstep kernel (R a multiple of 64) with F + 10 <= 16 A rows
 int toued_gru_bwd_fused_fits(int R, int F) { return toued_gru_bwd_col_exp(R) && F >= 1 && F <= 6 ? 1 : 0; }

@@ -84,6 +84,7 @@ _SIGS = {
     "toued_wgrad_bfp": [_I, _I, _L, _P, _L, _I, _P, _L, _P, _P, _P, ctypes.c_size_t, _P],
     "toued_wgrad_bfp_slab": [_I, _I, _L, _P, _L, _I, _P, _L, _I, _P, _P, _P, ctypes.c_size_t, _P],
     "toued_gru_slab_saves": [_I],
+    "toued_gru_hin_slab": [],
     "toued_gru_bwd_small_work_floats": [_L],
     "toued_gru_bwd_small": [_L, _P, _P, _P, _P, _P, _P, ctypes.c_size_t, _P],
     "toued_choice_cdf": [_P, _P, _I, _I, _P, _P],

@@ -162,6 +162,7 @@ class LPGGRU:
         # the split-precision pair keeps h_in (A's first 256 rows' region) and r, z, hn in 32-column slab blocks
         # [M/32][256][32] (hin_rows(), a_rows(), s_rows() give rows); A's rows 256.. (x, ones) stay rows
         self.slab = bool(L.toued_gru_slab_saves(R))
+        self.hin_slab = self.slab and bool(L.toued_gru_hin_slab())
         # the small weight-gradient products fused into the backward (toued_gru_bwd_fused) where the lockstep kernel
         # runs and F <= 6: then dn_pre, relu(h_out) and the head cotangents never reach HBM (TOUED_BWD_FUSED=0: the
         # unfused kernel + toued_gru_bwd_small)
@@ -201,19 +202,19 @@ class LPGGRU:
     def hin_rows(self):
         """The saved h_in as [256][M] rows (a copy of its slab blocks on the split-precision pair)."""
         H, M = 256, self.M
-        if not self.slab:
+        if not self.hin_slab:
             return self.A[:H]
         return self.A[:H].reshape(-1).view(M // 32, H, 32).permute(1, 0, 2).reshape(H, M)
 
     def a_rows(self):
         """The main reduction's A operand [h_in; x; 1; pad] as [264][M] rows (a copy when h_in is in slab blocks)."""
-        return torch.cat([self.hin_rows(), self.A[256:]]) if self.slab else self.A
+        return torch.cat([self.hin_rows(), self.A[256:]]) if self.hin_slab else self.A
 
     def hin_block(self, k: int):
         """Update k's saved h_in (for --debug_nans): a [256][T*R] column block of the rows, or its contiguous slab
         blocks."""
         c0, n = k * self.T * self.R, self.T * self.R
-        return self.A.view(-1)[256 * c0:256 * (c0 + n)] if self.slab else self.A[:256, c0:c0 + n]
+        return self.A.view(-1)[256 * c0:256 * (c0 + n)] if self.hin_slab else self.A[:256, c0:c0 + n]
 
     def s_rows(self, i: int):
         """Saved array i (0 r, 1 z, 2 n, 3 hn) as [256][M] rows (a copy of its slab blocks for r, z, hn)."""
@@ -266,7 +267,7 @@ class LPGGRU:
         sc = H * col if self.slab else col
         _lib.call("toued_gru_fwd", R, T, self.W, self.lay.F, _lib.ptr(X) + 4 * col, M, 1, _lib.ptr(done_k),
                   _lib.ptr(self.fwdA), _lib.ptr(eta), self.lay.c_offsets, _lib.ptr(pi_hat[k]), _lib.ptr(y_hat[k]),
-                  _lib.ptr(self.A) + 4 * sc, _lib.ptr(S) + 4 * (0 * H * M + sc),
+                  _lib.ptr(self.A) + 4 * (sc if self.hin_slab else col), _lib.ptr(S) + 4 * (0 * H * M + sc),
                   _lib.ptr(S) + 4 * (1 * H * M + sc), _lib.ptr(S) + 4 * (2 * H * M + col),
                   _lib.ptr(S) + 4 * (3 * H * M + sc), M, _lib.stream_ptr())
         del Xk
@@ -344,7 +345,8 @@ class LPGGRU:
         if self.bfp and self.slab and os.environ.get("TOUED_WGRAD_NW4") != "1":
             # h_in in slab blocks (layout bit 0); the fused backward's DG too (bit 1), the unfused one's in rows
             _lib.call("toued_wgrad_bfp_slab", H + F + 1, 3 * H, M, _lib.ptr(self.A), M, H, _lib.ptr(DG), M,
-                      3 if self.fused else 1, _lib.ptr(self.CE), _lib.ptr(G), ws, wn, st)
+                      (1 if self.hin_slab else 0) | (2 if self.fused else 0), _lib.ptr(self.CE), _lib.ptr(G), ws, wn,
+                      st)
         else:
             # (comparison paths on the split-precision pair: row-major copies of the slab blocks)
             A, B = self.a_rows(), self.dg_rows()
