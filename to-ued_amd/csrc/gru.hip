@@ -672,6 +672,9 @@ __device__ unsigned long long g_fwd_stamps[64 * 32 * 6];
 #ifndef FWD_PF
 #define FWD_PF 0
 #endif
+#ifndef FWD_HDEFER
+#define FWD_HDEFER 1   // the head reduce + softmax of step s at the end of step s + 1's contraction (wave 0)
+#endif
 #ifndef FWD_XFIRST
 #define FWD_XFIRST 0   // comparison runs: x(t) issued before the ring's lead fragments (the round-4 order)
 #endif
@@ -682,8 +685,10 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   __shared__ __attribute__((aligned(16))) __bf16 hB[3][64 * F6_HP];
   __shared__ __attribute__((aligned(16))) float wh[HU * 12];          // head weights [unit][pi | y0..y7 | pad]
   __shared__ __attribute__((aligned(16))) float usc[4 * HU];          // accumulator unscale 2^-(s + 14) [gate][unit]
-  __shared__ float hp[8 * 9 * 64];      // head partials [wave][output][row]
-  __shared__ float hout[9 * 64];
+  // head partials [wave][output][row]; FWD_HDEFER: two buffers (step parity), reduced by wave 0 at the end of the next
+  // step's contraction, where it waits for the other waves' MFMAs anyway
+  __shared__ float hp[(FWD_HDEFER ? 2 : 1) * 8 * 9 * 64];
+  __shared__ float hout[FWD_HDEFER ? 1 : 9 * 64];
   __shared__ float wIs[8 * 4 * 64];     // gate_ain's W_in fragments [wave][kk][lane] (registers are the bound)
   __shared__ float hbias[9];            // pi_b, y_b[0..7]: no global load in the head reduce (FWD_PF's loads in flight)
   const int tid = threadIdx.x, lane = tid & 63, hi = lane >> 5, col = lane & 31;
@@ -769,6 +774,26 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
                         (unsigned)((fc * p.xs_f + ((long)t_ * R + r0) * p.xs_col) * 4));
       }
     if (FWD_XFIRST) ring();
+  };
+  // FWD_HDEFER: step s_'s heads from its partials (wave 0, lane = row): the bias plus the eight waves' partials in
+  // wave order, then pi_hat and the softmax of the eight y logits -- the arithmetic of the reduce below, in one lane
+  auto head_out = [&](int s_) {
+    const int tl = lane_now(), t_ = T - 1 - s_;
+    const float* hb = hp + (s_ & 1) * 4608;
+    float v[9];
+#pragma unroll
+    for (int oo = 0; oo < 9; ++oo) {
+      v[oo] = hbias[oo];
+#pragma unroll
+      for (int gq = 0; gq < 8; ++gq) v[oo] += hb[(gq * 9 + oo) * 64 + tl];
+    }
+    p.pi_hat[(long)t_ * R + r0 + tl] = v[0];
+    float m = -__builtin_inff();
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, v[j + 1]);
+    float e[8], ssum = 0.0f;
+    for (int j = 0; j < 8; ++j) { e[j] = __expf(v[j + 1] - m); ssum += e[j]; }
+    const float inv = 1.0f / ssum;
+    for (int j = 0; j < 8; ++j) p.y_hat[((long)t_ * 8 + j) * R + r0 + tl] = e[j] * inv;
   };
   if (FWD_PF) load_lead(T - 1);
   for (int s = 0; s < T; ++s) {
@@ -868,6 +893,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
       for (int h = 0; h < 2; ++h) acc[g][h] = mfma6(Aa[g], Ba[h], acc[g][h]);
     }
     }
+    if (FWD_HDEFER && s > 0 && wave == 0) head_out(s - 1);   // (wave 0 leads its SIMD: it waits here anyway)
     FWD_STAMP(1);
     lds_barrier();   // every wave done reading hB / xB: the carry and x(t-1) overwrite them in place
     FWD_STAMP(2);
@@ -953,7 +979,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
 #pragma unroll
       for (int oo = 0; oo < 9; ++oo) {
         const float o = __shfl_xor(hp_loc[oo], 32);
-        if (hi == 0) hp[(wave * 9 + oo) * 64 + row] = hp_loc[oo] + o;
+        if (hi == 0) hp[(FWD_HDEFER ? (s & 1) * 4608 : 0) + (wave * 9 + oo) * 64 + row] = hp_loc[oo] + o;
       }
     }
     FWD_STAMP(3);
@@ -964,6 +990,10 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     }
     lds_barrier();   // head partials, the carry and x(t-1) visible
     FWD_STAMP(4);
+    if (FWD_HDEFER) {
+      FWD_STAMP(5);
+      continue;
+    }
     for (int i = 64 * wave + lane_now(); i < 9 * 64; i += 512) {
       const int oo = i >> 6, c = i & 63;
       float v = hbias[oo];
@@ -985,6 +1015,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     }
     FWD_STAMP(5);
   }
+  if (FWD_HDEFER && wave == 0) head_out(T - 1);   // the last step's heads (its partials visible: the loop's barrier)
 }
 
 // Forward, half-row workgroups (k_gru_fwd6h, the SAVE instance: the meta-gradient's forward).  k_gru_fwd6 runs one
