@@ -1722,8 +1722,10 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       for (int q = 0; q < 2; ++q) ring[i][q] = ldAh(i, g, q);
   };
   // nextg >= 0 (BWD_SPLACE): the last RD k-steps load pass nextg's first RD slots; post() runs after the last k-step
-  auto contract_h = [&](int g, int sb, float (&qv)[32], long ctr_, auto&& pre, bool preloaded, int nextg,
-                        auto&& post) {   // sb: the image slot of the first fp16 piece
+  // inpass(j): called after each of the last four k-steps (j = 0..3, the unrolled tail without ring reloads), where the
+  // matrix pipe paces the wave and VALU / LDS work rides beside it (BWD_INPASS: the next gate's first piece)
+  auto contract_h = [&](int g, int sb, int sb1, float (&qv)[32], long ctr_, auto&& pre, bool preloaded, int nextg,
+                        auto&& post, auto&& inpass) {   // sb, sb1: the image slots of the two fp16 pieces
     constexpr int RD = BWD_RD;                    // A-fragment ring depth (k-steps in flight from L2)
     static_assert(!BWD_SPREAD || 16 % RD == 0, "the spread stores: 2 per k-step, 2 RD per ring group");
     f16x8 B[2][2];
@@ -1731,7 +1733,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     const int ln = lane_now(), bl = (ln & 31) * PP + 8 * (ln >> 5);
     auto ldB = [&](int ks, int h) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q) B[h][q] = *reinterpret_cast<const f16x8*>(&dgB[sb + q][bl + RB * h * PP + 16 * ks]);
+      for (int q = 0; q < 2; ++q) B[h][q] = *reinterpret_cast<const f16x8*>(&dgB[q ? sb1 : sb][bl + RB * h * PP + 16 * ks]);
     };
     ldB(0, 0);
     ldB(0, 1);
@@ -1774,10 +1776,17 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         for (int q = 0; q < 2; ++q) ring[ks % RD][q] = ldAh(ks - (16 - RD), nextg, q);
         __builtin_amdgcn_sched_barrier(0);
       }
+      if (ks >= 12) {
+        inpass(ks - 12);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     post();
   };
   // scaled fp16 pieces of the four units u0 .. u0 + 3 of row `row` into image slots 0, 1
+#ifndef BWD_INPASS
+#define BWD_INPASS 0
+#endif
 #ifndef BWD_TREFILL
 #define BWD_TREFILL 0   // timing studies only (wrong results): 1 = refills without LDS writes, 2 = without the split
 #endif
@@ -1794,6 +1803,13 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       *reinterpret_cast<f16x4*>(&dgB[0][row * PP + u0]) = x0;
       *reinterpret_cast<f16x4*>(&dgB[1][row * PP + u0]) = x1;
     }
+  };
+  // BWD_INPASS: one of the two pieces (which) into image slot `slot`
+  auto put1h = [&](int slot, int which, int row, int u0, const float (&v)[4], float sc) {
+    f16x4 x0, x1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split2h(v[e] * sc, x0, x1, e);
+    *reinterpret_cast<f16x4*>(&dgB[slot][row * PP + u0]) = which ? x1 : x0;
   };
   // SMALL: the wave's dn and relu(h_out) of one row tile and one 16-unit half go through a wave-private [row][unit]
   // f32 block in image slot 0 (free during the memory part) as the B operand B[k][j = unit] of 16x16x4 f32 MFMAs over
@@ -2056,7 +2072,17 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     }
     BWD_STAMP(4);
     BWD_WSTAMP(2);
-    contract_h(0, 0, qv, ctr, [] {}, (bool)BWD_SPLACE, BWD_SPLACE ? 1 : -1, [&] {
+    // BWD_INPASS: dz's first piece goes to the idle slot 2 during pass dr, dhn's to slot 1 (dr's second piece, read
+    // through) during pass dz; the refills write only the second pieces: pass dz reads slots (2, 0), pass dhn (1, 2)
+    auto inpass_put = [&](int j, int slot, const float (&src)[2][16]) {
+#pragma unroll
+      for (int i = 2 * j; i < 2 * j + 2; ++i) {   // (h, g4) = (i >> 2, i & 3): eight quads over the four k-steps
+        const int h = i >> 2, g4 = i & 3;
+        const float v4[4] = {src[h][4 * g4], src[h][4 * g4 + 1], src[h][4 * g4 + 2], src[h][4 * g4 + 3]};
+        put1h(slot, 0, rown(h), ubn() + 8 * g4, v4, bs[h]);
+      }
+    };
+    contract_h(0, 0, 1, qv, ctr, [] {}, (bool)BWD_SPLACE, BWD_SPLACE ? 1 : -1, [&] {
       if (BWD_SPLACE) {
 #pragma unroll
         for (int h = 0; h < 2; ++h)
@@ -2066,6 +2092,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
             store_dg(1, RB * h, g4, v4);
           }
       }
+    }, [&](int j) {
+      if (BWD_INPASS) inpass_put(j, 2, dz_r);
     });
     BWD_WSTAMP(3);
     lds_barrier();
@@ -2075,7 +2103,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const float v4[4] = {dz_r[h][4 * g4], dz_r[h][4 * g4 + 1], dz_r[h][4 * g4 + 2], dz_r[h][4 * g4 + 3]};
-        put4h(rown(h), ubn() + 8 * g4, v4, bs[h]);
+        if (BWD_INPASS) put1h(0, 1, rown(h), ubn() + 8 * g4, v4, bs[h]);
+        else put4h(rown(h), ubn() + 8 * g4, v4, bs[h]);
         if (BWD_SPREAD) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) qv[16 * h + 4 * g4 + e] = v4[e];
@@ -2086,7 +2115,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     lds_barrier();
     BWD_STAMP(5);
     BWD_WSTAMP(5);
-    contract_h(1, 0, qv, ctr, [] {}, (bool)BWD_SPLACE, BWD_SPLACE ? 2 : -1, [&] {
+    contract_h(1, BWD_INPASS ? 2 : 0, BWD_INPASS ? 0 : 1, qv, ctr, [] {}, (bool)BWD_SPLACE, BWD_SPLACE ? 2 : -1, [&] {
       if (BWD_SPLACE) {
 #pragma unroll
         for (int h = 0; h < 2; ++h)
@@ -2096,6 +2125,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
             store_dg(2, RB * h, g4, v4);
           }
       }
+    }, [&](int j) {
+      if (BWD_INPASS) inpass_put(j, 1, dhn_r);
     });
     BWD_WSTAMP(6);
     lds_barrier();
@@ -2105,7 +2136,8 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const float v4[4] = {dhn_r[h][4 * g4], dhn_r[h][4 * g4 + 1], dhn_r[h][4 * g4 + 2], dhn_r[h][4 * g4 + 3]};
-        put4h(rown(h), ubn() + 8 * g4, v4, bs[h]);
+        if (BWD_INPASS) put1h(2, 1, rown(h), ubn() + 8 * g4, v4, bs[h]);
+        else put4h(rown(h), ubn() + 8 * g4, v4, bs[h]);
         if (BWD_SPREAD) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) qv[16 * h + 4 * g4 + e] = v4[e];
@@ -2115,9 +2147,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       }
     lds_barrier();
     BWD_STAMP(6);
-    contract_h(2, 0, qv, ctr, [&] {
+    contract_h(2, BWD_INPASS ? 1 : 0, BWD_INPASS ? 2 : 1, qv, ctr, [&] {
       if (t + 1 < T) load_first(ctr + R, true);
-    }, (bool)BWD_SPLACE, -1, [] {});
+    }, (bool)BWD_SPLACE, -1, [] {}, [](int) {});
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const float4 w4 = *reinterpret_cast<const float4*>(&wsc[32 * wave + 4 * (lane_now() >> 5) + 8 * g4]);
