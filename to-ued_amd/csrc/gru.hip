@@ -669,9 +669,6 @@ __device__ unsigned long long g_fwd_stamps[64 * 32 * 6];
 #ifndef FWD_NOSAVE
 #define FWD_NOSAVE 0   // timing studies only: 1 = no saves, 2 = h_in only (the backward then reads stale data)
 #endif
-#ifndef FWD_PF
-#define FWD_PF 0
-#endif
 #ifndef FWD_HDEFER
 #define FWD_HDEFER 1   // the head reduce + softmax of step s at the end of step s + 1's contraction (wave 0)
 #endif
@@ -690,7 +687,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   __shared__ float hp[(FWD_HDEFER ? 2 : 1) * 8 * 9 * 64];
   __shared__ float hout[FWD_HDEFER ? 1 : 9 * 64];
   __shared__ float wIs[8 * 4 * 64];     // gate_ain's W_in fragments [wave][kk][lane] (registers are the bound)
-  __shared__ float hbias[9];            // pi_b, y_b[0..7]: no global load in the head reduce (FWD_PF's loads in flight)
+  __shared__ float hbias[9];            // pi_b, y_b[0..7] (the head reduce reads them from LDS)
   const int tid = threadIdx.x, lane = tid & 63, hi = lane >> 5, col = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r0 = blockIdx.x * 64;
@@ -744,37 +741,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   // half a step late so the two halves contract at different times (later rounds inherit the offset)
   if (p.stagger > 0 && blockIdx.x < 256 && ((blockIdx.x >> 3) & 1))
     for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
-  // the step's rows' inputs x(t) for the augmented k-step [x_0 .. x_{F-1}, 1, 0 ...] (F <= 7), split into B
-  // fragments at the end of the contraction (lanes 32-63 hold k = 8..15: zero); A fragments through a two-k-step ring
-  // (A0: even k-steps, A1: odd): each L2 fragment load has a whole k-step of the wave's MFMAs (plus the partner
-  // wave's) to land instead of one gate's
-  float xv[2][7];
-  f16x8 A0[3][2], A1[3][2], B[2][2];
-  auto fragA = [&](int ks, int g, int q) { return ((ks * 8 + wave) * 3 + g) * 2 + q; };
-  auto fragAug = [&](int g, int q) { return F6_NFH + (wave * 4 + g) * 3 + q; };
-  // the ring's first two k-steps, then x(t) (HBM, behind them: the first ring wait does not wait for x).  FWD_PF: issued
-  // for step t - 1 after step t's gate maths, so that they land during the head reduce instead of after it
-  auto load_lead = [&](int t_) {
-    auto ring = [&] {
-#pragma unroll
-      for (int g = 0; g < 3; ++g)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          A0[g][q] = ldAh(fragA(0, g, q));
-          A1[g][q] = ldAh(fragA(1, g, q));
-        }
-    };
-    if (!FWD_XFIRST) ring();
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int f = 0; f < 7; ++f) {
-        const int fc = f < F ? f : F - 1;
-        xv[h][f] = ld_u(rs_X, (unsigned)((RB * h + col) * p.xs_col * 4),
-                        (unsigned)((fc * p.xs_f + ((long)t_ * R + r0) * p.xs_col) * 4));
-      }
-    if (FWD_XFIRST) ring();
-  };
   // FWD_HDEFER: step s_'s heads from its partials (wave 0, lane = row): the bias plus the eight waves' partials in
   // wave order, then pi_hat and the softmax of the eight y logits -- the arithmetic of the reduce below, in one lane
   auto head_out = [&](int s_) {
@@ -795,7 +761,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     const float inv = 1.0f / ssum;
     for (int j = 0; j < 8; ++j) p.y_hat[((long)t_ * 8 + j) * R + r0 + tl] = e[j] * inv;
   };
-  if (FWD_PF) load_lead(T - 1);
   for (int s = 0; s < T; ++s) {
     const int t = T - 1 - s;
     FWD_STAMP(0);
@@ -809,7 +774,37 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     // ---- contraction: 16 fp16 k-steps over the carry + one augmented bf16 k-step.  Each gate's A fragments
     // (unit tile `wave`) are refilled for the next k-step right after their last MFMA, each row tile's B
     // fragments right after theirs; the partner wave on the SIMD covers what latency remains.
-    if (!FWD_PF) load_lead(t);
+    // this lane's row inputs x(t) for the augmented k-step [x_0 .. x_{F-1}, 1, 0 ...] (F <= 7), split into B fragments
+    // at the end of the contraction (lanes 32-63 hold k = 8..15: zero); A fragments through a two-k-step ring (A0: even
+    // k-steps, A1: odd): each L2 fragment load has a whole k-step of the wave's MFMAs (plus the partner wave's) to land
+    // instead of one gate's.  (Declared in the step: hoisted out of the loop, the C4 per-candidate instance ran 2.61-2.69
+    // instead of 2.22 ms.)  The ring's first two k-steps go out ahead of x (FWD_XFIRST=0: the first ring wait does not
+    // wait for x's HBM loads; 1.207-1.216 ms either order at C2)
+    float xv[2][7];
+    f16x8 A0[3][2], A1[3][2], B[2][2];
+    auto fragA = [&](int ks, int g, int q) { return ((ks * 8 + wave) * 3 + g) * 2 + q; };
+    auto fragAug = [&](int g, int q) { return F6_NFH + (wave * 4 + g) * 3 + q; };
+    {
+      auto ring = [&] {
+#pragma unroll
+        for (int g = 0; g < 3; ++g)
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            A0[g][q] = ldAh(fragA(0, g, q));
+            A1[g][q] = ldAh(fragA(1, g, q));
+          }
+      };
+      if (!FWD_XFIRST) ring();
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int f = 0; f < 7; ++f) {
+          const int fc = f < F ? f : F - 1;
+          xv[h][f] = ld_u(rs_X, (unsigned)((RB * h + col) * p.xs_col * 4),
+                          (unsigned)((fc * p.xs_f + ((long)t * R + r0) * p.xs_col) * 4));
+        }
+      if (FWD_XFIRST) ring();
+    }
     auto load_B = [&](int ks, int h) {
 #pragma unroll
       for (int q = 0; q < 2; ++q)
@@ -860,7 +855,12 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
         const int k = 2 * kk + hi;
         float bx[2];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) bx[h] = (k < F ? xv[h][k < 7 ? k : 6] : (k == 7 ? 1.0f : 0.0f)) * HSCALE;
+        for (int h = 0; h < 2; ++h) {
+          // static indices: the lane's k = 2 kk + hi picks between two registers (a lane-dependent index puts xv in
+          // scratch: 64 bytes per lane, C4's forward 2.22 -> 2.65 ms while xv lived outside the step loop)
+          const float xs = hi ? xv[h][2 * kk + 1 < 7 ? 2 * kk + 1 : 6] : xv[h][2 * kk];
+          bx[h] = (k < F ? xs : (k == 7 ? 1.0f : 0.0f)) * HSCALE;
+        }
 #pragma unroll
         for (int g = 0; g < 3; ++g) {
           const float av = kk == 0 ? a32[g].x : kk == 1 ? a32[g].y : kk == 2 ? a32[g].z : a32[g].w;
@@ -983,11 +983,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
       }
     }
     FWD_STAMP(3);
-    if (FWD_PF && s + 1 < T) {
-      __builtin_amdgcn_sched_barrier(0);
-      load_lead(t - 1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
     lds_barrier();   // head partials, the carry and x(t-1) visible
     FWD_STAMP(4);
     if (FWD_HDEFER) {
