@@ -409,6 +409,14 @@ int toued_agent_step(int N, int W, int T, int D, const float* theta, const float
                      const int* tidx, const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
                      const float* pi_hat, const float* y_hat, float alpha_y, float lr_a, float lr_c, float max_norm,
                      float* Gth, float* Gph, float* met, int* step, const int* levels, float* gstat, hipStream_t stream);
+/* toued_agent_step, then toued_entropy's metric mode on the updated tables theta1 / phi1 (met slots 3 and 4) in the
+ * same launch: bit-identical to toued_agent_step followed by toued_entropy(..., theta1, phi1, ..., met, 0, 0, NULL,
+ * NULL) (lpg_agent.py:119-120's batch_rollout_entropy of the new policy on rollout k). */
+int toued_agent_step_entropy(int N, int W, int T, int D, const float* theta, const float* phi, float* theta1,
+                             float* phi1, const int* tidx, const int* ttime, const uint8_t* tact, const float* trew,
+                             const uint8_t* tdone, const float* pi_hat, const float* y_hat, float alpha_y, float lr_a,
+                             float lr_c, float max_norm, float* Gth, float* Gph, float* met, int* step,
+                             const int* levels, float* gstat, hipStream_t stream);
 /* The per-agent metrics of a meta-step (meta/train.py:101-117) from met [K][N][8] (k_agent_grad / k_entropy slots) and
  * loss_out [N][2]: out [6][N] = reg_lpg_loss, policy_l2, policy_entropy, critic_loss, critic_l2, critic_entropy */
 int toued_meta_metrics(int N, int K, const float* met, float inv_wt, const float* loss_out, float pec, float pl2,

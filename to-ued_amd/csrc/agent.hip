@@ -19,6 +19,7 @@
 // A tabular observation (idx, t) contributes logits table[idx] + (0.001 t) * table[D-1].
 #include <string.h>
 #include <algorithm>
+#include <type_traits>
 #include "common.h"
 #include "wave_dev.h"
 
@@ -495,40 +496,50 @@ __global__ void __launch_bounds__(256) k_entropy(int N, int W, int T, int D, con
 
 // Metric mode of the entropies (train_lpg_agent's batch_rollout_entropy, lpg_agent.py:119-120): one block per
 // agent, fixed summation order (per-thread strided partials, then a block reduction), one writer per metric.
-__global__ void __launch_bounds__(256) k_entropy_metric(int W, int T, int D, const float* __restrict__ theta,
-                                                        const float* __restrict__ phi, const int* __restrict__ tidx,
-                                                        const int* __restrict__ ttime, float* __restrict__ met) {
-  __shared__ float red[2][4];
-  const int a = blockIdx.x, tid = threadIdx.x;
-  const float* th = theta + (size_t)a * D * 5;
-  const float* ph = phi + (size_t)a * D * 8;
-  float lastA[5], lastC[8];
+// The body for agent a on threads 0..255 of the calling block (every thread of the block calls it: one barrier); red
+// is 8 floats of LDS.  Shared with toued_agent_step_entropy's k_rows_sorted<GradStepEntOp>, so both sum the same
+// partials in the same order (bit-identical).
+TOUED_DEV void entropy_metric_agent(int a, int tid, int W, int T, int D, const float* __restrict__ theta,
+                                    const float* __restrict__ phi, const int* __restrict__ tidx,
+                                    const int* __restrict__ ttime, float* __restrict__ met, float (*red)[4]) {
+  if (tid < 256) {
+    const float* th = theta + (size_t)a * D * 5;
+    const float* ph = phi + (size_t)a * D * 8;
+    float lastA[5], lastC[8];
 #pragma unroll
-  for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
+    for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
-  float ha = 0.0f, hc = 0.0f;
-  for (int i = tid; i < T * W; i += 256) {
-    const int t = i / W, w = i - t * W;
-    const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
-    const int idx = tidx[o0];
-    const float c = (float)ttime[o0] * 0.001f;
-    float p[5], y[8];
-    probs_of<5>(th, lastA, idx, c, p);
-    probs_of<8>(ph, lastC, idx, c, y);
+    for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
+    float ha = 0.0f, hc = 0.0f;
+    for (int i = tid; i < T * W; i += 256) {
+      const int t = i / W, w = i - t * W;
+      const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
+      const int idx = tidx[o0];
+      const float c = (float)ttime[o0] * 0.001f;
+      float p[5], y[8];
+      probs_of<5>(th, lastA, idx, c, p);
+      probs_of<8>(ph, lastC, idx, c, y);
 #pragma unroll
-    for (int j = 0; j < 5; ++j) ha -= (p[j] + EPSF) * __logf(p[j] + EPSF);
+      for (int j = 0; j < 5; ++j) ha -= (p[j] + EPSF) * __logf(p[j] + EPSF);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) hc -= (y[j] + EPSF) * __logf(y[j] + EPSF);
+      for (int j = 0; j < 8; ++j) hc -= (y[j] + EPSF) * __logf(y[j] + EPSF);
+    }
+    ha = wave_sum(ha);
+    hc = wave_sum(hc);
+    if ((tid & 63) == 0) { red[0][tid >> 6] = ha; red[1][tid >> 6] = hc; }
   }
-  ha = wave_sum(ha);
-  hc = wave_sum(hc);
-  if ((tid & 63) == 0) { red[0][tid >> 6] = ha; red[1][tid >> 6] = hc; }
   __syncthreads();
   if (tid == 0) {
     met[a * 8 + 3] += (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
     met[a * 8 + 4] += (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
   }
+}
+
+__global__ void __launch_bounds__(256) k_entropy_metric(int W, int T, int D, const float* __restrict__ theta,
+                                                        const float* __restrict__ phi, const int* __restrict__ tidx,
+                                                        const int* __restrict__ ttime, float* __restrict__ met) {
+  __shared__ float red[2][4];
+  entropy_metric_agent(blockIdx.x, threadIdx.x, W, T, D, theta, phi, tidx, ttime, met, red);
 }
 
 // ---------------------------------------------------------------------------- eval loss
@@ -855,6 +866,12 @@ __global__ void __launch_bounds__(256) k_hvp(int N, int W, int T, int D, int K, 
 }
 
 // ---------------------------------------------------------------------------- embedding MLP backward
+#ifndef EMBED_V
+#define EMBED_V 3   // k_embed_bwd3 (one lane per sample, e1_w / e1_b on the matrix cores); 1: k_embed_bwd
+#endif
+#ifndef EMBED_WPE
+#define EMBED_WPE 3   // k_embed_bwd3's waves per SIMD (its register budget: 512 / EMBED_WPE)
+#endif
 // grad layout (161 floats): e1_b[16], e1_w[8*16], e2_b[1], e2_w[16] (flat-eta order within MLP_0)
 // Inputs: y_t / y_tp1 recomputed from phi_k; cotangents dX3 (pyt), dX4 (pyt1, masked by done).
 // Four lanes per sample, each owning four of the 16 hidden units (41 accumulators per lane instead of 161:
@@ -977,6 +994,193 @@ __global__ void __launch_bounds__(256) k_embed_bwd(int N, int W, int T, int D, i
   {
     const float vc = qsum(ac);
     if (lane == 0) red[wv][144] = vc;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 161; i += blockDim.x) {
+    float v = 0.0f;
+    for (int qq = 0; qq < (int)(blockDim.x >> 6); ++qq) v += red[qq][i];
+    partial[(size_t)blockIdx.x * 161 + i] = v;
+  }
+}
+
+// probs_of on a row already in registers (the same operations in the same order: bit-identical)
+template <int K>
+TOUED_DEV void probs_regs(const float* row, const float* last, float c, float* p) {
+  float l[K];
+  float m = -__builtin_inff();
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    l[j] = row[j] + c * last[j];
+    m = fmaxf(m, l[j]);
+  }
+  float s = 0.0f;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    p[j] = __expf(l[j] - m);
+    s += p[j];
+  }
+  const float inv = 1.0f / s;
+#pragma unroll
+  for (int j = 0; j < K; ++j) p[j] *= inv;
+}
+
+// The same gradient with one lane per sample and the e1_w / e1_b reduction on the matrix cores.  A wave takes 64
+// consecutive samples per round (each load instruction covers 64 samples: 256 contiguous bytes of an index or
+// cotangent array, where k_embed_bwd's quad-per-sample layout covered 16 and repeated the loads and the softmax in
+// four lanes); a lane computes its sample's critic outputs y and, per observation, the 16 hidden units (e1_w / e1_b /
+// e2_w broadcast from LDS: no per-lane weight registers), accumulates e2_w / e2_b itself, and writes the item's
+// rows a = [y, 1] and d = dh (the hidden cotangents) to the wave's LDS tile; sixteen v_mfma_f32_16x16x4_f32 then add
+// A^T D over the 64 items into a 16 x 16 accumulator (rows 0..7 e1_w, row 8 e1_b) -- 4 accumulator registers
+// instead of 41 per lane, so the kernel runs at 6 waves per SIMD.  The next round's index / time / cotangent loads
+// are issued before this round's maths.  f32 products and sums, in another order than k_embed_bwd.
+template <bool UNIF>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EMBED_WPE))) k_embed_bwd3(int N, int W, int T, int D, int K, const float* __restrict__ phi_hist,
+                                                    long phi_stride, const int* __restrict__ tidx_hist, long tidx_stride,
+                                                    const int* __restrict__ ttime_hist, const uint8_t* __restrict__ tdone_hist,
+                                                    long tstep_stride, const float* __restrict__ dX3,
+                                                    const float* __restrict__ dX4, long dx_stride_k,
+                                                    const float* __restrict__ e1w, const float* __restrict__ e1b,
+                                                    const float* __restrict__ e2w, float* __restrict__ partial) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __shared__ float4 sw1[8][4];                   // e1_w [8][16] as float4 rows of four units
+  __shared__ float4 sb1[4], sw2[4];              // e1_b, e2_w
+  __shared__ float4 tA[4][64][3];                // per wave: item rows [y0..y7, 1, 0, 0, 0] (12 floats)
+  __shared__ float4 tD[4][64][4];                // per wave: item rows dh[16]
+  __shared__ float red[4][161];
+  if (threadIdx.x < 32) sw1[threadIdx.x >> 2][threadIdx.x & 3] = reinterpret_cast<const float4*>(e1w)[threadIdx.x];
+  if (threadIdx.x < 4) {
+    sb1[threadIdx.x] = reinterpret_cast<const float4*>(e1b)[threadIdx.x];
+    sw2[threadIdx.x] = reinterpret_cast<const float4*>(e2w)[threadIdx.x];
+  }
+  __syncthreads();
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+  float a2[16], ac = 0.0f;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) a2[u] = 0.0f;
+  const int NTW = N * T * W;
+  const int total = K * NTW;
+  const int R = N * W;
+  const int stride = gridDim.x * blockDim.x;     // samples per round of the grid
+  struct In {
+    const float* ph;
+    int ix[2];
+    float cx[2], cg[2];
+  };
+  auto load_in = [&](int g) {
+    In v;
+    const bool live = g < total;
+    g = live ? g : total - 1;
+    const int k = (unsigned)g / (unsigned)NTW;
+    const int s = g - k * NTW;
+    const int at = (unsigned)s / (unsigned)W;
+    const int w = s - at * W;
+    const int a = (unsigned)at / (unsigned)T;
+    const int t = at - a * T;
+    const int r = a * W + w;
+    const int* tidx = tidx_hist + k * tidx_stride;
+    const int* ttime = ttime_hist + k * tidx_stride;
+    const uint8_t* tdone = tdone_hist + k * tstep_stride;
+    v.ph = phi_hist + k * phi_stride + (size_t)a * D * 8;
+    const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
+    const size_t o = (size_t)k * dx_stride_k + (size_t)t * R + r;
+    v.ix[0] = tidx[o0];
+    v.ix[1] = tidx[o0 + W];
+    v.cx[0] = (float)ttime[o0] * 0.001f;
+    v.cx[1] = (float)ttime[o0 + W] * 0.001f;
+    v.cg[0] = live ? dX3[o] : 0.0f;
+    v.cg[1] = (!live || tdone[s]) ? 0.0f : dX4[o];
+    return v;
+  };
+  float4 (*A)[3] = tA[wv];
+  float4 (*Dt)[4] = tD[wv];
+  const float* Af = reinterpret_cast<const float*>(A);
+  const float* Df = reinterpret_cast<const float*>(Dt);
+  // MFMA operands: lane l supplies A[m = l & 15][k = l >> 4] and B[k][n = l & 15]; feature rows m >= 12 re-read row
+  // 11's zero (their accumulator rows are not used)
+  const int am = (lane & 15) < 12 ? (lane & 15) : 11, kq = lane >> 4, bn = lane & 15;
+  const int g0 = blockIdx.x * blockDim.x + threadIdx.x;
+  In nx = load_in(g0);
+  for (int gb = g0 - lane; gb < total; gb += stride) {   // gb: the wave's first sample this round (wave-uniform)
+    const In cur = nx;
+    nx = load_in(gb + lane + stride);
+    float last[8], row[2][8];
+    {
+      const float4* lp = reinterpret_cast<const float4*>(cur.ph + (size_t)(D - 1) * 8);
+      const float4 l0 = lp[0], l1 = lp[1];
+      last[0] = l0.x; last[1] = l0.y; last[2] = l0.z; last[3] = l0.w;
+      last[4] = l1.x; last[5] = l1.y; last[6] = l1.z; last[7] = l1.w;
+#pragma unroll
+      for (int which = 0; which < 2; ++which) {
+        const float4* rp = reinterpret_cast<const float4*>(cur.ph + (size_t)cur.ix[which] * 8);
+        const float4 r0 = rp[0], r1 = rp[1];
+        row[which][0] = r0.x; row[which][1] = r0.y; row[which][2] = r0.z; row[which][3] = r0.w;
+        row[which][4] = r1.x; row[which][5] = r1.y; row[which][6] = r1.z; row[which][7] = r1.w;
+      }
+    }
+#pragma unroll
+    for (int which = 0; which < 2; ++which) {
+      float y[8];
+      probs_regs<8>(row[which], last, cur.cx[which], y);
+      const float cg = cur.cg[which];
+      ac += cg;                                          // e2_b
+      // keep the weights in LDS (hoisted copies would take 160 registers per lane)
+      __asm__ volatile("" ::: "memory");
+      float dh[16];
+#pragma unroll
+      for (int uq = 0; uq < 4; ++uq) {
+        const float4 bb = sb1[uq], ww = sw2[uq];
+        float pre[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float4 wv4 = sw1[i][uq];
+          pre[0] += y[i] * wv4.x;
+          pre[1] += y[i] * wv4.y;
+          pre[2] += y[i] * wv4.z;
+          pre[3] += y[i] * wv4.w;
+        }
+        const float w2v[4] = {ww.x, ww.y, ww.z, ww.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          a2[4 * uq + u] += fmaxf(pre[u], 0.0f) * cg;     // e2_w
+          dh[4 * uq + u] = pre[u] > 0.0f ? w2v[u] * cg : 0.0f;
+        }
+        __builtin_amdgcn_sched_barrier(0);   // one group's weights live at a time
+      }
+      A[lane][0] = make_float4(y[0], y[1], y[2], y[3]);
+      A[lane][1] = make_float4(y[4], y[5], y[6], y[7]);
+      A[lane][2] = make_float4(1.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) Dt[lane][c] = make_float4(dh[4 * c], dh[4 * c + 1], dh[4 * c + 2], dh[4 * c + 3]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int kg = 0; kg < 16; ++kg) {
+        const int it = 4 * kg + kq;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[it * 12 + am], Df[it * 16 + bn], acc, 0, 0, 0);
+        if ((kg & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // operands of four products in flight at a time
+      }
+      // the tile's reads are in registers before the next item's writes (in-order LDS within the wave)
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_sched_barrier(0);   // one observation's values live at a time
+    }
+  }
+  // accumulator: lane l holds C[m = 4 (l >> 4) + r][n = l & 15], r = 0..3 (m < 8: e1_w[m][n], m = 8: e1_b[n])
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = 4 * kq + r;
+    if (m < 8) red[wv][16 + m * 16 + bn] = acc[r];
+    else if (m == 8) red[wv][bn] = acc[r];
+  }
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const float v = wsum_dpp(a2[u]);
+    if (lane == 0) red[wv][145 + u] = v;
+  }
+  {
+    const float v = wsum_dpp(ac);
+    if (lane == 0) red[wv][144] = v;
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 161; i += blockDim.x) {
@@ -1110,6 +1314,17 @@ struct GradApplyOp : GradOp {
 struct GradStepOp : GradApplyOp {
   static constexpr bool WRITE_G = true;
 };
+
+// toued_agent_step_entropy: GradStepOp, then the metric-mode entropies of the new policy (theta_{k+1} / phi_{k+1},
+// toued_entropy with met) on the same block -- the rows they read are the rows the block just wrote (its samples'
+// rows and the time row) or theta_k's copies, so one barrier orders them; one launch less per inner update.
+struct GradStepEntOp : GradStepOp {
+  static constexpr bool ENTROPY_AFTER = true;
+};
+template <class Op, class = void>
+struct entropy_after : std::false_type {};
+template <class Op>
+struct entropy_after<Op, std::void_t<decltype(Op::ENTROPY_AFTER)>> : std::bool_constant<Op::ENTROPY_AFTER> {};
 
 struct EntropyBwdOp {   // k_entropy, gradient mode
   static constexpr int NA = 5, NC = 8, NM = 1;
@@ -1590,6 +1805,11 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
       op.finish(a, x, y);
     }
   }
+  if constexpr (entropy_after<Op>::value) {
+    __syncthreads();   // the rewritten rows (and red's last readers) before the entropies read them
+    entropy_metric_agent(a, tid, W, T, D, op.theta_w, op.phi_w, op.tidx, op.ttime, op.met,
+                         reinterpret_cast<float (*)[4]>(&red[0][0]));
+  }
 }
 
 // launch the sorted variant when one agent's samples fit (T*W <= SORT_MAX_TW, D < 2^19); false otherwise
@@ -1715,10 +1935,11 @@ int toued_agent_update(int N, int W, int T, int D, float* theta, float* phi, con
 // (bit-identical to toued_agent_apply), the touched gradient rows go to Gth / Gph (bit-identical to toued_agent_grad
 // there; the other rows are not written and must not be read: toued_entropy_clip and toued_hvp read touched rows
 // only).  step advanced when applied, met accumulated, gstat written.
-int toued_agent_step(int N, int W, int T, int D, const float* theta, const float* phi, float* theta1, float* phi1,
-                     const int* tidx, const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
-                     const float* pi_hat, const float* y_hat, float alpha_y, float lr_a, float lr_c, float max_norm,
-                     float* Gth, float* Gph, float* met, int* step, const int* levels, float* gstat, hipStream_t stream) {
+static int agent_step(int N, int W, int T, int D, const float* theta, const float* phi, float* theta1, float* phi1,
+                      const int* tidx, const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
+                      const float* pi_hat, const float* y_hat, float alpha_y, float lr_a, float lr_c, float max_norm,
+                      float* Gth, float* Gph, float* met, int* step, const int* levels, float* gstat, bool with_entropy,
+                      hipStream_t stream) {
   TOUED_REQUIRE(step && levels && gstat && met && Gth && Gph && theta1 && phi1,
                 "toued_agent_step: every output is required");
   TOUED_REQUIRE(toued_agent_update_fits(W, T, D), "toued_agent_step: W=%d T=%d D=%d unsupported (T*W <= %d)", W, T, D,
@@ -1734,9 +1955,33 @@ int toued_agent_step(int N, int W, int T, int D, const float* theta, const float
   op.lr_c = lr_c;
   op.max_norm = max_norm;
   op.step_w = step;
-  TOUED_REQUIRE(launch_sorted(op, N, stream), "toued_agent_step: cannot launch the sorted kernel");
+  if (with_entropy) {
+    GradStepEntOp eop;
+    static_cast<GradStepOp&>(eop) = op;
+    TOUED_REQUIRE(launch_sorted(eop, N, stream), "toued_agent_step_entropy: cannot launch the sorted kernel");
+  } else {
+    TOUED_REQUIRE(launch_sorted(op, N, stream), "toued_agent_step: cannot launch the sorted kernel");
+  }
   TOUED_CHECK_LAUNCH();
   return 0;
+}
+
+int toued_agent_step(int N, int W, int T, int D, const float* theta, const float* phi, float* theta1, float* phi1,
+                     const int* tidx, const int* ttime, const uint8_t* tact, const float* trew, const uint8_t* tdone,
+                     const float* pi_hat, const float* y_hat, float alpha_y, float lr_a, float lr_c, float max_norm,
+                     float* Gth, float* Gph, float* met, int* step, const int* levels, float* gstat, hipStream_t stream) {
+  return agent_step(N, W, T, D, theta, phi, theta1, phi1, tidx, ttime, tact, trew, tdone, pi_hat, y_hat, alpha_y, lr_a,
+                    lr_c, max_norm, Gth, Gph, met, step, levels, gstat, false, stream);
+}
+
+// toued_agent_step followed by toued_entropy's metric mode on theta1 / phi1 (met slots 3, 4), in the same launch
+int toued_agent_step_entropy(int N, int W, int T, int D, const float* theta, const float* phi, float* theta1,
+                             float* phi1, const int* tidx, const int* ttime, const uint8_t* tact, const float* trew,
+                             const uint8_t* tdone, const float* pi_hat, const float* y_hat, float alpha_y, float lr_a,
+                             float lr_c, float max_norm, float* Gth, float* Gph, float* met, int* step,
+                             const int* levels, float* gstat, hipStream_t stream) {
+  return agent_step(N, W, T, D, theta, phi, theta1, phi1, tidx, ttime, tact, trew, tdone, pi_hat, y_hat, alpha_y, lr_a,
+                    lr_c, max_norm, Gth, Gph, met, step, levels, gstat, true, stream);
 }
 
 // toued_entropy's gradient mode followed by toued_clip_dot over the touched rows, in one kernel (the reverse pass of toued_agent_step's
@@ -1880,14 +2125,15 @@ int toued_embed_bwd(int N, int W, int T, int D, int K, const float* phi_hist, lo
   if ((long)K * N * T * W == 0) return 0;
   TOUED_REQUIRE((long)K * N * (T + 1) * W < (1L << 31), "toued_embed_bwd: K*N*(T+1)*W = %ld samples exceed 2^31",
                 (long)K * N * (T + 1) * W);
-  if (W % 64 == 0)
-    hipLaunchKernelGGL(k_embed_bwd<true>, dim3(n_blocks), dim3(256), 0, stream, N, W, T, D, K, phi_hist, phi_stride,
-                       tidx_hist, tidx_stride, ttime_hist, tdone_hist, tstep_stride, dX3, dX4, dx_stride_k, e1w, e1b,
-                       e2w, partial);
-  else
-    hipLaunchKernelGGL(k_embed_bwd<false>, dim3(n_blocks), dim3(256), 0, stream, N, W, T, D, K, phi_hist, phi_stride,
-                       tidx_hist, tidx_stride, ttime_hist, tdone_hist, tstep_stride, dX3, dX4, dx_stride_k, e1w, e1b,
-                       e2w, partial);
+#define L_(KER) hipLaunchKernelGGL(KER, dim3(n_blocks), dim3(256), 0, stream, N, W, T, D, K, phi_hist, phi_stride,     \
+                                   tidx_hist, tidx_stride, ttime_hist, tdone_hist, tstep_stride, dX3, dX4, dx_stride_k, \
+                                   e1w, e1b, e2w, partial)
+  if (EMBED_V == 3) {
+    if (W % 64 == 0) L_(k_embed_bwd3<true>); else L_(k_embed_bwd3<false>);
+  } else {
+    if (W % 64 == 0) L_(k_embed_bwd<true>); else L_(k_embed_bwd<false>);
+  }
+#undef L_
   TOUED_CHECK_LAUNCH();
   return 0;
 }

@@ -88,16 +88,16 @@ def lecun_tables_into(keys: torch.Tensor, out: torch.Tensor, mask: torch.Tensor)
 
 def create_agents_into(agent_keys: torch.Tensor, theta: torch.Tensor, phi: torch.Tensor, mask: torch.Tensor):
     """``create_agents`` for the agents with ``mask`` set, in place into theta [n, D, 5] / phi [n, D, Y]."""
-    ks = prng.split(agent_keys, 2)
-    lecun_tables_into(ks[:, 0].contiguous(), theta, mask)
-    lecun_tables_into(ks[:, 1].contiguous(), phi, mask)
+    ks = prng.split_planar(agent_keys, 2)   # ks[j] = split(agent_keys, 2)[:, j], contiguous
+    lecun_tables_into(ks[0], theta, mask)
+    lecun_tables_into(ks[1], phi, mask)
 
 
 def create_agents(agent_keys: torch.Tensor, D: int, Y: int):
     """create_agent (agents/agents.py:31-56) for each key: actor_rng, critic_rng = split(agent_rng)."""
-    ks = prng.split(agent_keys, 2)
-    theta = lecun_tables(ks[:, 0].contiguous(), D, 5)
-    phi = lecun_tables(ks[:, 1].contiguous(), D, Y)
+    ks = prng.split_planar(agent_keys, 2)
+    theta = lecun_tables(ks[0], D, 5)
+    phi = lecun_tables(ks[1], D, Y)
     return theta, phi
 
 

@@ -116,9 +116,9 @@ class LevelSampler:
     def _create_agents(self, rng, levels, n_total, sl, create_value_critics_too: bool):
         """vmap(_create_agent) (level_sampler.py:273-291): worker_rng, agent_rng = split(rng_i)."""
         keys = self._slice(prng.split(rng, n_total), sl)
-        ks = prng.split(keys, 2)
-        (_, _), state = self.rollout_manager.batch_reset(ks[:, 0].contiguous(), levels)
-        theta, phi = create_agents(ks[:, 1].contiguous(), self.obs_dim, self.Y)
+        ks = prng.split_planar(keys, 2)    # ks[j] = split(keys, 2)[:, j], contiguous
+        (_, _), state = self.rollout_manager.batch_reset(ks[0], levels)
+        theta, phi = create_agents(ks[1], self.obs_dim, self.Y)
         return theta, phi, state
 
     # ------------------------------------------------------------------ API
@@ -156,8 +156,8 @@ class LevelSampler:
 
     @staticmethod
     def _split2(rng):
-        ks = prng.split(rng, 2)
-        return ks[0].contiguous(), ks[1].contiguous()
+        ks = prng.split_planar(rng.view(1, 2), 2)
+        return ks[0, 0], ks[1, 0]
 
     def sample(self, rng, level_buffer, agents: AgentBatch, sl=None):
         """level_sampler.py:134-266: new levels/agents for agents whose step >= lifetime.
@@ -182,9 +182,9 @@ class LevelSampler:
             agents.levels = torch.where(term[:, None], new_levels, agents.levels)
         # vmap(_create_agent) (level_sampler.py:273-291): worker_rng, agent_rng = split(rng_i)
         rng, sub = self._split2(rng)
-        ks = prng.split(self._slice(prng.split(sub, n_total), sl), 2)
-        self.rollout_manager.batch_reset_into(ks[:, 0].contiguous(), agents.levels, agents.state, mask)
-        create_agents_into(ks[:, 1].contiguous(), agents.theta, agents.phi, mask)
+        ks = prng.split_planar(self._slice(prng.split(sub, n_total), sl), 2)
+        self.rollout_manager.batch_reset_into(ks[0], agents.levels, agents.state, mask)
+        create_agents_into(ks[1], agents.theta, agents.phi, mask)
         agents.step = torch.where(term, torch.zeros_like(agents.step), agents.step)
         if agents.vcrit is not None:
             rng, sub = self._split2(rng)

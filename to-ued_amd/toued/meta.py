@@ -176,6 +176,9 @@ class MetaGradStep:
         # TOUED_META_FUSED_STEP=0 keeps the dense grad + apply + entropy + clip_dot path
         self.fused_step = (os.environ.get("TOUED_META_FUSED_STEP", "1") != "0"
                            and bool(_lib.lib().toued_agent_update_fits(W, T, D)))
+        # the update's entropy metrics in the same launch (toued_agent_step_entropy); TOUED_STEP_ENTROPY=0: a separate
+        # toued_entropy launch (bit-identical)
+        self.step_entropy = os.environ.get("TOUED_STEP_ENTROPY", "1") != "0"
         self.gstat = z(K, N, 4)
         self.met = z(K, N, 8)
         self.traj = Transition(z(K + 1, N, T + 1, W, dt=i32), z(K + 1, N, T + 1, W, dt=i32),
@@ -191,8 +194,10 @@ class MetaGradStep:
         self.adj_th = [z(N, D, 5)]       # adjoint tables, accumulated in place over k (toued_hvp)
         self.adj_ph = [z(N, D, Y)]
         self.coef = z(N, 4)
-        self.keys_roll = z(K, N, 2, dt=i32)
-        self.keys_eval = z(N, 2, dt=i32)
+        # the K train rollouts' keys and the eval rollout's, one buffer (the step's draws take all K + 1 at once)
+        self.keys_train = z(K + 1, N, 2, dt=i32)
+        self.keys_roll = self.keys_train[:K]
+        self.keys_eval = self.keys_train[K]
         self.keys_ea_reset = z(N, 2, dt=i32)
         self.keys_ea_roll = z(N, 2, dt=i32)
         self.gru = LPGGRU(self.lay, R, T, K, W, dev)
@@ -290,7 +295,7 @@ class MetaGradStep:
             if self._draws is None:    # the step's own (chain scratch, draws) pair: [T][(K + 1) * N * W][4]
                 self._draws = tuple(torch.empty((T, (K + 1) * N * W, 4), dtype=torch.int32, device=self.dev)
                                     for _ in range(2))
-            draws = self.ro.train_draws(torch.cat([self.keys_roll, self.keys_eval.unsqueeze(0)]), agents.levels, W,
+            draws = self.ro.train_draws(self.keys_train, agents.levels, W,
                                         self._draws)
         # ---------------- forward: K inner updates (agents/lpg_agent.py:88-140)
         for k in range(K):
@@ -320,13 +325,17 @@ class MetaGradStep:
                 nan_checker().check("lpg_gru_states", self.gru.hin_block(k))
             nan_checker().check("lpg_outputs", self.pi_hat[k], self.y_hat[k])
             if self.fused_step:
+                # the update and the new policy's entropy metrics (toued_entropy's metric mode) in one launch
                 main.wait_stream(self.side)
-                L.call("toued_agent_step", N, W, T, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]),
+                L.call("toued_agent_step_entropy" if self.step_entropy else "toued_agent_step", N, W, T, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]),
                        ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(tk.obs_idx), ptr(tk.obs_time),
                        ptr(tk.action), ptr(tk.reward), ptr(tk.done), ptr(self.pi_hat[k]), ptr(self.y_hat[k]),
                        hyp.agent_target_coeff, hyp.actor_lr, hyp.critic_lr, hyp.max_grad_norm, ptr(self.G_th[k]),
                        ptr(self.G_ph[k]), ptr(self.met[k]), ptr(agents.step), ptr(agents.levels), ptr(self.gstat[k]),
                        st)
+                if not self.step_entropy:
+                    L.call("toued_entropy", N, W, T, D, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]),
+                           ptr(tk.obs_idx), ptr(tk.obs_time), ptr(self.met[k]), 0.0, 0.0, None, None, st)
             else:
                 L.call("toued_agent_grad", N, W, T, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(tk.obs_idx),
                        ptr(tk.obs_time), ptr(tk.action), ptr(tk.reward), ptr(tk.done), ptr(self.pi_hat[k]),
@@ -335,8 +344,8 @@ class MetaGradStep:
                 L.call("toued_agent_apply", N, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(self.G_th[k]),
                        ptr(self.G_ph[k]), hyp.actor_lr, hyp.critic_lr, hyp.max_grad_norm, ptr(agents.step),
                        ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(self.gstat[k]), st)
-            L.call("toued_entropy", N, W, T, D, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(tk.obs_idx),
-                   ptr(tk.obs_time), ptr(self.met[k]), 0.0, 0.0, None, None, st)
+                L.call("toued_entropy", N, W, T, D, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]),
+                       ptr(tk.obs_idx), ptr(tk.obs_time), ptr(self.met[k]), 0.0, 0.0, None, None, st)
             nan_checker().check("agent_params", self.theta_h[k + 1], self.phi_h[k + 1])
         # ---------------- value critic on the train rollouts (--fix_value_critic), eval rollout, lpg loss
         if hyp.fix_value_critic:

@@ -84,11 +84,12 @@ class Trainer:
 
     def meta_step(self):
         """_meta_train_loop (train.py:36-54): LPG update, then level_sampler.sample."""
-        ks = prng.split(self.rng, 2)
-        self.rng, sub = ks[0].contiguous(), ks[1].contiguous()
+        # split(rng) with the key axis first: both halves contiguous, no copy launches
+        ks = prng.split_planar(self.rng.view(1, 2), 2)
+        self.rng, sub = ks[0, 0], ks[1, 0]
         self.train_state, self.agents, _, metrics = self.train_step(sub, self.train_state, self.agents)
-        ks = prng.split(self.rng, 2)
-        self.rng, sub = ks[0].contiguous(), ks[1].contiguous()
+        ks = prng.split_planar(self.rng.view(1, 2), 2)
+        self.rng, sub = ks[0, 0], ks[1, 0]
         self.buffer, self.agents = self.sampler.sample(sub, self.buffer, self.agents, self.sl)
         self.nans.raise_if_any()
         return metrics
