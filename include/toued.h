@@ -177,6 +177,14 @@ int toued_init_tables(const uint32_t* keys, int n, int cols, int D, float lo, fl
 /* only the tables i with mask[i] != 0 are written (in place) */
 int toued_init_tables_masked(const uint32_t* keys, int n, int cols, int D, float lo, float hi, float stddev,
                              float* out, const uint8_t* mask, hipStream_t stream);
+/* level_sampler.sample with score_function=random (level_sampler.py:134-194): the termination test and all key
+ * derivations for this rank's n agents (global indices lo .. lo+n-1 of n_total) in one launch.  mask [n] (u8) =
+ * step >= levels[:, lifetime]; step (and vstep, when not NULL) zeroed where set; keys [4 or 5][n][2]: the new level's
+ * key, the env reset key, the actor and critic table keys already folded with dense_hash (lecun_tables' Dense_0), and
+ * with vstep the value critic's folded key.  rng [2] is the sampler's key (jax.random.split chains as in the
+ * reference). */
+int toued_sample_random_keys(const uint32_t* rng, int n_total, int lo, int n, int* step, const int* levels, int* vstep,
+                             uint32_t dense_hash, uint8_t* mask, uint32_t* keys, hipStream_t stream);
 
 /* ---- A2C antagonist (agents/a2c.py:19-125) ---- */
 /* out[u][i] = the u-th `_rng` of `rng, _rng = split(rng)` chained from keys[i] (a2c.py:97). */
@@ -425,6 +433,16 @@ int toued_entropy_clip(int N, int W, int T, int D, const float* theta, const flo
                        const int* ttime, float coef_a, float coef_c, float* adj_th, float* adj_ph, const float* Gth,
                        const float* Gph, const float* gstat, float lr_a, float lr_c, float max_norm, float* coef,
                        hipStream_t stream);
+
+/* The reverse pass's step k (meta/train.py:174's scan body) in one launch: toued_entropy_clip on theta1 / phi1
+ * (theta_{k+1}, phi_{k+1}), then toued_hvp on theta / phi (theta_k, phi_k) in place on adj_th / adj_ph, reading the
+ * coef the first part wrote; the rollout's samples are sorted once.  Bit-identical to the two calls. */
+int toued_entropy_clip_hvp(int N, int W, int T, int D, int K, const float* theta1, const float* phi1,
+                           const float* theta, const float* phi, const int* tidx, const int* ttime, const uint8_t* tact,
+                           const float* pi_hat, const float* y_hat, float coef_a, float coef_c, float* adj_th,
+                           float* adj_ph, const float* Gth, const float* Gph, const float* gstat, float lr_a,
+                           float lr_c, float max_norm, float* coef, float alpha_y, float b2, float b3, float* d_pi_hat,
+                           float* d_y_hat, hipStream_t stream);
 
 /* ES inference path: pack n candidates' forward fragments (candidate c at eta + c*eta_stride) */
 int toued_gru_pack_fwd_multi(const float* eta, long eta_stride, int n, const int* off, int F, float* fwdA,

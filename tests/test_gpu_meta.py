@@ -534,6 +534,46 @@ def test_fused_agent_step_matches_dense_path(monkeypatch, mode, N, lc):
         assert rel < 1e-6
 
 
+@pytest.mark.parametrize("mode,N,lc", [("tabular", 512, False), ("all_vrandlife", 16, True)])
+def test_one_launch_update_and_reverse_step_bit_identical(monkeypatch, mode, N, lc):
+    """toued_agent_step_entropy (the inner update and its entropy metrics in one launch) and toued_entropy_clip_hvp
+    (the reverse pass's entropy-clip and HVP of step k in one launch, one sort) against the separate launches
+    (TOUED_STEP_ENTROPY=0, TOUED_REVERSE_PAIR=0), over two consecutive meta-steps: the meta-gradient, every
+    theta_k / phi_k, the adjoint's cotangents d_pi_hat / d_y_hat, the agents and the metrics bit-identical."""
+    from toued.lpg import init_lpg_params
+    from toued.meta import AdamState, LpgHyperparams, MetaGradStep
+    W, T, K = 64, 20, 5
+    ro, ag0 = _agents_for(mode, N, W, T, 92)
+    eta0 = init_lpg_params(93, 7 if lc else 5)
+    out = []
+    for one in ("0", "1"):
+        monkeypatch.setenv("TOUED_STEP_ENTROPY", one)
+        monkeypatch.setenv("TOUED_REVERSE_PAIR", one)
+        ag = _clone_agents(ag0)
+        step = MetaGradStep(ro, N, LpgHyperparams(num_agent_updates=K), lc)
+        assert step.fused_step and step.step_entropy == (one == "1") and step.reverse_pair == (one == "1")
+        hist = []
+        for i in range(2):
+            eta = eta0.clone()
+            met = step(torch.tensor([7, 30 + i], dtype=torch.int32, device="cuda"), eta,
+                       AdamState(eta.numel(), "cuda"), ag)
+            torch.cuda.synchronize()
+            hist.append((step.theta_h.clone(), step.phi_h.clone(), step.d_pi_hat.clone(), step.d_y_hat.clone(),
+                         step.grad.clone(), met))
+        out.append((ag, hist))
+    (a0, h0), (a1, h1) = out
+    for name in ("theta", "phi", "step", "state", "vstep"):
+        assert torch.equal(getattr(a0, name), getattr(a1, name)), name
+    for x0, x1 in zip(h0, h1):
+        for j in range(5):
+            assert torch.equal(x0[j], x1[j]), j
+        m0, m1 = x0[5], x1[5]
+        for k in m0["lpg_agent"]:
+            assert torch.equal(m0["lpg_agent"][k], m1["lpg_agent"][k]), k
+        for k in ("lpg_loss", "reg_lpg_loss", "lpg_agent_return"):
+            assert torch.equal(m0[k], m1[k]), k
+
+
 def test_1024_agents_two_mini_batches_on_one_gpu():
     """A reference-legal --num_agents 1024 --num_mini_batches 2 on one GPU (one 512-agent batch alone is the
     bench's size; 1024 at once exceeds the GRU kernels' 4 GiB operand range, so --num_mini_batches 1 runs the same

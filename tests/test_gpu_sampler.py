@@ -77,9 +77,15 @@ def _check_agents(spec, agents, lv, th, ph, st, vc, step):
     np.testing.assert_array_equal(agents.step.cpu().numpy(), step)
 
 
+@pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("score_function,mode", [("random", "all_shortlife"), ("frozen", "all_shortlife"),
                                                  ("random", "tabular"), ("frozen", "mazes")])
-def test_sample_nonplr_matches_oracle(score_function, mode):
+def test_sample_nonplr_matches_oracle(monkeypatch, score_function, mode, fused):
+    """sample() against the oracle; the random branch both as toued_sample_random_keys + the masked generators
+    (TOUED_SAMPLE_FUSED=1, default) and launch per operation (0)."""
+    if fused == "0" and score_function != "random":
+        pytest.skip("the flag only selects the random branch's path")
+    monkeypatch.setenv("TOUED_SAMPLE_FUSED", fused)
     from toued import prng
     from toued.env import L_LIFETIME
     from toued.level_sampler import LevelSampler

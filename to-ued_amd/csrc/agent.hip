@@ -1515,12 +1515,12 @@ struct HvpOp {   // k_hvp
 #ifndef ROWS_PRIO
 #define ROWS_PRIO 3   // C2 20.29-20.31 ms at 0, 19.96-20.00 at 3 (profiles/r04/c2_rows_prio_r04j.txt)
 #endif
-template <class Op>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k_rows_sorted(Op op) {
+// One agent's block (k_rows_sorted below).  PRESORTED: `key` already holds the block's sorted sample keys from an
+// earlier body over the same samples (every sample kept by both ops, as EntropyClipOp and HvpOp do), so only the row
+// vectors and partial sums are rebuilt and the sort is skipped.
+template <class Op, bool PRESORTED>
+TOUED_DEV void rows_sorted_body(const Op& op) {
   constexpr int NA = Op::NA, NC = Op::NC, NV = NA + NC, NM = Op::NM;
-  // the reverse agent loop runs beside eval_agent's VALU-bound key chain (meta.py eval_keys_early): with a higher
-  // wave priority these latency-bound blocks take the issue slots first and the key chain fills the gaps
-  if (ROWS_PRIO > 0) __builtin_amdgcn_s_setprio(ROWS_PRIO);
   constexpr uint32_t NONE = 0xFFFFFFFFu, SMASK = 4095u;
   // unpadded vector stride (odd strides are bank-conflict free): 13-float rows keep a block's LDS at 75 KB,
   // so two agents' blocks share a CU and all N = 512 blocks are resident in one round
@@ -1557,7 +1557,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
 #pragma unroll
       for (int j = 0; j < NM; ++j) part[NV + j] += m[j];
     }
-    key[sl] = kk;
+    if (!PRESORTED) key[sl] = kk;
   }
 #pragma unroll
   for (int j = 0; j < NV + NM; ++j) {
@@ -1571,7 +1571,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
     tot[tid] = r;
   }
   // 2) sort by (row, sample)
-  sort2048_reg<512>(key, tid);
+  if constexpr (PRESORTED) __syncthreads();   // (tot and the row vectors before phase 3)
+  else sort2048_reg<512>(key, tid);
   // 3) segmented row sums, deterministic (a fixed combination tree): thread t owns the sorted entries
   //    [CH t, CH t + CH) as runs of equal rows; the part of a segment in earlier chunks (the carry) reaches the chunk
   //    where the segment ends through a segmented scan over the 512 chunks (carry_t = a_t carry_{t-1} + b_t, b_t the
@@ -1812,6 +1813,24 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   }
 }
 
+template <class Op>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k_rows_sorted(Op op) {
+  // the reverse agent loop runs beside eval_agent's VALU-bound key chain (meta.py eval_keys_early): with a higher
+  // wave priority these latency-bound blocks take the issue slots first and the key chain fills the gaps
+  if (ROWS_PRIO > 0) __builtin_amdgcn_s_setprio(ROWS_PRIO);
+  rows_sorted_body<Op, false>(op);
+}
+
+// Two ops over the same samples in one block: the second reuses the first's sort (and reads what the first wrote:
+// its rows and, through global memory, anything its thread 0 wrote -- the barrier orders them within the block).
+template <class Op1, class Op2>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k_rows_sorted2(Op1 op1, Op2 op2) {
+  if (ROWS_PRIO > 0) __builtin_amdgcn_s_setprio(ROWS_PRIO);
+  rows_sorted_body<Op1, false>(op1);
+  __syncthreads();
+  rows_sorted_body<Op2, true>(op2);
+}
+
 // launch the sorted variant when one agent's samples fit (T*W <= SORT_MAX_TW, D < 2^19); false otherwise
 template <class Op>
 static bool launch_sorted(const Op& op, int N, hipStream_t stream) {
@@ -1826,6 +1845,23 @@ static bool launch_sorted(const Op& op, int N, hipStream_t stream) {
     attr_set = true;
   }
   hipLaunchKernelGGL(k_rows_sorted<Op>, dim3(N), dim3(512), bytes, stream, op);
+  return true;
+}
+
+template <class Op1, class Op2>
+static bool launch_sorted2(const Op1& op1, const Op2& op2, int N, hipStream_t stream) {
+  static_assert(Op1::NA + Op1::NC == Op2::NA + Op2::NC, "launch_sorted2: the ops' row vectors differ in size");
+  const int TW = op1.T * op1.W;
+  if (TW > SORT_MAX_TW || TW <= 0 || op1.D >= (1 << 20)) return false;
+  const size_t bytes = 2048 * 4 + (size_t)TW * (Op1::NA + Op1::NC) * 4;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rows_sorted2<Op1, Op2>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024) != hipSuccess)
+      return false;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((k_rows_sorted2<Op1, Op2>), dim3(N), dim3(512), bytes, stream, op1, op2);
   return true;
 }
 
@@ -2016,6 +2052,32 @@ int toued_entropy_clip(int N, int W, int T, int D, const float* theta, const flo
   return 0;
 }
 
+// The reverse pass's step k as one launch: toued_entropy_clip on (theta1, phi1) = theta_{k+1} / phi_{k+1}, then
+// toued_hvp on (theta, phi) = theta_k / phi_k reading the adjoint and coef the first part wrote, in place on adj_th /
+// adj_ph; the rollout's samples are sorted once.  Same operations as the two launches (bit-identical).
+int toued_entropy_clip_hvp(int N, int W, int T, int D, int K, const float* theta1, const float* phi1,
+                           const float* theta, const float* phi, const int* tidx, const int* ttime, const uint8_t* tact,
+                           const float* pi_hat, const float* y_hat, float coef_a, float coef_c, float* adj_th,
+                           float* adj_ph, const float* Gth, const float* Gph, const float* gstat, float lr_a,
+                           float lr_c, float max_norm, float* coef, float alpha_y, float b2, float b3, float* d_pi_hat,
+                           float* d_y_hat, hipStream_t stream) {
+  TOUED_REQUIRE(toued_agent_update_fits(W, T, D), "toued_entropy_clip_hvp: W=%d T=%d D=%d unsupported", W, T, D);
+  if (N == 0) return 0;
+  EntropyClipOp ec;
+  static_cast<EntropyBwdOp&>(ec) = EntropyBwdOp{theta1, phi1, tidx, ttime, coef_a, coef_c, adj_th, adj_ph, N, W, T, D};
+  ec.Gth = Gth;
+  ec.Gph = Gph;
+  ec.gstat = gstat;
+  ec.lr_a = lr_a;
+  ec.lr_c = lr_c;
+  ec.max_norm = max_norm;
+  ec.coef = coef;
+  const HvpOp hv{theta, phi, tidx, ttime, tact, pi_hat, y_hat, Gth, Gph, adj_th, adj_ph, coef, lr_a, lr_c, alpha_y,
+                 b2, b3, adj_th, adj_ph, d_pi_hat, d_y_hat, N, W, T, D, K};
+  TOUED_REQUIRE(launch_sorted2(ec, hv, N, stream), "toued_entropy_clip_hvp: cannot launch the sorted kernel");
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
 
 int toued_agent_apply(int N, int D, const float* th0, const float* ph0, const float* Gth, const float* Gph,
                       float lr_a, float lr_c, float max_norm, int* step, float* th1, float* ph1, const float* gstat,

@@ -56,9 +56,64 @@ __global__ void __launch_bounds__(256) k_normal(const uint32_t* __restrict__ key
   out[t] = __fmul_rn(1.41421354f, erfinv_giles(u));
 }
 
+// level_sampler.sample with score_function=random (level_sampler.py:134-194 with _sample_random_levels :268-271 and
+// _create_agent :273-291), its key plumbing and termination test for agent i of this rank (global index lo + i of
+// n_total) in one thread instead of ~20 launches of splits, copies and elementwise ops:
+//   term = step >= lifetime; mask = term; step (and vstep) = term ? 0 : step
+//   (rng1, s1) = split(rng):  keys[0] = split(s1, n_total)[lo + i]                     (the new level)
+//   (rng2, s2) = split(rng1): (reset, agent) = split(split(s2, n_total)[lo + i])
+//                             keys[1] = reset; (actor, critic) = split(agent)
+//                             keys[2] = fold_in(actor, h), keys[3] = fold_in(critic, h)  (lecun_tables' Dense_0 key)
+//   vstep given:  (_, s3) = split(rng2): keys[4] = fold_in(split(s3, n_total)[lo + i], h) (the value critic)
+__global__ void __launch_bounds__(256) k_sample_random_keys(const uint32_t* __restrict__ rng, int n_total, int lo, int n,
+                                                            int* __restrict__ step, const int* __restrict__ levels,
+                                                            int* __restrict__ vstep, uint32_t h,
+                                                            uint8_t* __restrict__ mask, uint32_t* __restrict__ keys) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int st = step[i];
+  const bool term = st >= levels[(size_t)i * LEVEL_WORDS + L_LIFETIME];
+  mask[i] = term ? 1 : 0;
+  if (term) {
+    step[i] = 0;
+    if (vstep) vstep[i] = 0;
+  }
+  auto put = [&](int j, uint2 k) {
+    keys[((size_t)j * n + i) * 2] = k.x;
+    keys[((size_t)j * n + i) * 2 + 1] = k.y;
+  };
+  const uint32_t g = (uint32_t)(lo + i);
+  uint2 rng1, s1, rng2, s2, s3, reset, agent, actor, critic;
+  split2(make_uint2(rng[0], rng[1]), rng1, s1);
+  put(0, split_at(s1, (uint32_t)n_total, g));
+  split2(rng1, rng2, s2);
+  split2(split_at(s2, (uint32_t)n_total, g), reset, agent);
+  put(1, reset);
+  split2(agent, actor, critic);
+  put(2, threefry(actor.x, actor.y, 0u, h));
+  put(3, threefry(critic.x, critic.y, 0u, h));
+  if (vstep) {
+    uint2 rng3;
+    split2(rng2, rng3, s3);
+    const uint2 v = split_at(s3, (uint32_t)n_total, g);
+    put(4, threefry(v.x, v.y, 0u, h));
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int toued_sample_random_keys(const uint32_t* rng, int n_total, int lo, int n, int* step, const int* levels, int* vstep,
+                             uint32_t dense_hash, uint8_t* mask, uint32_t* keys, hipStream_t stream) {
+  TOUED_REQUIRE(n >= 0 && lo >= 0 && lo + n <= n_total, "toued_sample_random_keys: lo=%d n=%d n_total=%d", lo, n,
+                n_total);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_sample_random_keys, dim3((n + 255) / 256), dim3(256), 0, stream, rng, n_total, lo, n, step,
+                     levels, vstep, dense_hash, mask, keys);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
 
 int toued_split(const uint32_t* keys, int n, int num, uint32_t* out, hipStream_t stream) {
   TOUED_REQUIRE(n >= 0 && num >= 1, "toued_split: n=%d num=%d", n, num);

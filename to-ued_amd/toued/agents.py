@@ -86,6 +86,15 @@ def lecun_tables_into(keys: torch.Tensor, out: torch.Tensor, mask: torch.Tensor)
     return out
 
 
+def lecun_tables_into_folded(pkeys: torch.Tensor, out: torch.Tensor, mask: torch.Tensor):
+    """``lecun_tables_into`` with the keys already folded with DENSE0_HASH (toued_sample_random_keys)."""
+    n, D, cols = out.shape
+    std = float(np.float32(np.sqrt(np.float32(1.0 / D))) / np.float32(0.87962566103423978))
+    _lib.call("toued_init_tables_masked", _lib.ptr(pkeys), n, cols, D, TN_LO, TN_HI, std, _lib.ptr(out),
+              _lib.ptr(mask), _lib.stream_ptr())
+    return out
+
+
 def create_agents_into(agent_keys: torch.Tensor, theta: torch.Tensor, phi: torch.Tensor, mask: torch.Tensor):
     """``create_agents`` for the agents with ``mask`` set, in place into theta [n, D, 5] / phi [n, D, Y]."""
     ks = prng.split_planar(agent_keys, 2)   # ks[j] = split(agent_keys, 2)[:, j], contiguous

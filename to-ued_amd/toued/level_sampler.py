@@ -10,14 +10,15 @@ reference's vmapped ``jnp.where`` (the masked-out work has no observable effect)
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import numpy as np
 import torch
 
 from . import _lib, prng
-from .agents import (AgentBatch, AgentHyperparams, create_agents, create_agents_into, create_value_critics,
-                     lecun_tables_into)
+from .agents import (DENSE0_HASH, AgentBatch, AgentHyperparams, create_agents, create_agents_into,
+                     create_value_critics, lecun_tables_into, lecun_tables_into_folded)
 from .env import L_BUFID, L_LIFETIME, LevelGenerator, get_env_spec
 from .rollout import RolloutWrapper
 
@@ -166,6 +167,8 @@ class LevelSampler:
         (``where(term, new, old)``); here the generators write the terminated agents' rows in place (same
         keys, same values) and leave the others untouched."""
         n_total = agents.n if sl is None else sl[2]
+        if self.score_function == "random" and os.environ.get("TOUED_SAMPLE_FUSED", "1") != "0":
+            return level_buffer, self._sample_random_fused(rng, agents, n_total, 0 if sl is None else sl[0])
         term = agents.step >= agents.levels[:, L_LIFETIME]
         mask = term.to(torch.uint8)
         if self.score_function == "random":
@@ -192,6 +195,29 @@ class LevelSampler:
             lecun_tables_into(self._slice(prng.split(sub, n_total), sl), agents.vcrit.view(n, self.obs_dim, 1), mask)
             agents.vstep = torch.where(term, torch.zeros_like(agents.vstep), agents.vstep)
         return level_buffer, agents
+
+    def _sample_random_fused(self, rng, agents: AgentBatch, n_total: int, lo: int) -> AgentBatch:
+        """The random branch of ``sample`` with its termination test and key derivations in one launch
+        (toued_sample_random_keys: the same keys and masks as the split / fold_in chain below, bit-identical), then
+        the masked level generator, env reset and table inits; step / vstep are zeroed in place where terminated.
+        TOUED_SAMPLE_FUSED=0 takes the launch-per-operation path."""
+        n = agents.n
+        nk = 5 if agents.vcrit is not None else 4
+        if getattr(self, "_rk", None) is None or self._rk[0].shape != (nk, n, 2):
+            self._rk = (torch.empty((nk, n, 2), dtype=torch.int32, device=self.dev),
+                        torch.empty((n,), dtype=torch.uint8, device=self.dev))
+        keys, mask = self._rk
+        vstep = agents.vstep if agents.vcrit is not None else None
+        _lib.call("toued_sample_random_keys", _lib.ptr(rng.contiguous()), n_total, lo, n, _lib.ptr(agents.step),
+                  _lib.ptr(agents.levels), _lib.ptr(vstep), DENSE0_HASH, _lib.ptr(mask), _lib.ptr(keys),
+                  _lib.stream_ptr())
+        self.gen.regenerate(keys[0], agents.levels, mask)
+        self.rollout_manager.batch_reset_into(keys[1], agents.levels, agents.state, mask)
+        lecun_tables_into_folded(keys[2], agents.theta, mask)
+        lecun_tables_into_folded(keys[3], agents.phi, mask)
+        if agents.vcrit is not None:
+            lecun_tables_into_folded(keys[4], agents.vcrit.view(n, self.obs_dim, 1), mask)
+        return agents
 
     def _frozen_ids(self, rng, n):
         """random.choice(arange(B), p=uniform, shape=(N,), replace=True) (level_sampler.py:157-165)."""

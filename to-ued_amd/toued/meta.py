@@ -179,6 +179,9 @@ class MetaGradStep:
         # the update's entropy metrics in the same launch (toued_agent_step_entropy); TOUED_STEP_ENTROPY=0: a separate
         # toued_entropy launch (bit-identical)
         self.step_entropy = os.environ.get("TOUED_STEP_ENTROPY", "1") != "0"
+        # the reverse pass's entropy-clip and HVP of step k in one launch (toued_entropy_clip_hvp);
+        # TOUED_REVERSE_PAIR=0: two launches (bit-identical)
+        self.reverse_pair = os.environ.get("TOUED_REVERSE_PAIR", "1") != "0"
         self.gstat = z(K, N, 4)
         self.met = z(K, N, 8)
         self.traj = Transition(z(K + 1, N, T + 1, W, dt=i32), z(K + 1, N, T + 1, W, dt=i32),
@@ -426,6 +429,16 @@ class MetaGradStep:
         for k in range(K - 1, -1, -1):
             tk = self._t(k)
             # d(-b0*H_pi - b1*H_y)/K at (theta_{k+1}, phi_{k+1}) on rollout k, then the clip-VJP coefficients
+            if self.fused_step and self.reverse_pair:
+                # entropy adjoint + clip coefficients, then the HVP rows, in one launch (one sort of rollout k)
+                L.call("toued_entropy_clip_hvp", N, W, T, D, K, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]),
+                       ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(tk.obs_idx), ptr(tk.obs_time), ptr(tk.action),
+                       ptr(self.pi_hat[k]), ptr(self.y_hat[k]), -hyp.policy_entropy_coeff / K,
+                       -hyp.target_entropy_coeff / K, ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]),
+                       ptr(self.G_th[k]), ptr(self.G_ph[k]), ptr(self.gstat[k]), hyp.actor_lr, hyp.critic_lr,
+                       hyp.max_grad_norm, ptr(self.coef), hyp.agent_target_coeff, hyp.policy_l2_coeff,
+                       hyp.target_l2_coeff, ptr(self.d_pi_hat[k]), ptr(self.d_y_hat[k]), st)
+                continue
             if self.fused_step:
                 # one kernel: the entropy gradient's rows are the rows update k touched, so their owners add
                 # <G_k, adjoint> as they write them (toued_clip_dot's dot up to the summation order)
