@@ -289,8 +289,10 @@ int toued_hvp(int N, int W, int T, int D, int K, const float* theta, const float
               const float* Gph, const float* adj_th_in, const float* adj_ph_in, const float* coef, float lr_a,
               float lr_c, float alpha_y, float b2, float b3, float* adj_th_out, float* adj_ph_out, float* d_pi_hat,
               float* d_y_hat, hipStream_t stream);
-/* embedding-MLP (models/lpg.py:36-46) parameter gradient from the GRU input cotangents */
-int toued_embed_bwd(int N, int W, int T, int D, int K, const float* phi_hist, long phi_stride, const int* tidx_hist,
+/* embedding-MLP (models/lpg.py:36-46) parameter gradient from the GRU input cotangents.  phi_hist: K + 1 critic-table
+ * slots phi_stride floats apart, update k's phi_k in slot (phi_slot0 + k) % (K + 1) (a ring of the step's history) */
+int toued_embed_bwd(int N, int W, int T, int D, int K, const float* phi_hist, long phi_stride, int phi_slot0,
+                    const int* tidx_hist,
                     long tidx_stride, const int* ttime_hist, const uint8_t* tdone_hist, long tstep_stride,
                     const float* dX3, const float* dX4, long dx_stride_k, const float* e1w, const float* e1b,
                     const float* e2w, float* partial, int n_blocks, hipStream_t stream);

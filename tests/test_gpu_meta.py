@@ -542,8 +542,13 @@ def test_one_launch_update_and_reverse_step_bit_identical(monkeypatch, mode, N, 
     theta_k / phi_k, the adjoint's cotangents d_pi_hat / d_y_hat, the agents and the metrics bit-identical."""
     from toued.lpg import init_lpg_params
     from toued.meta import AdamState, LpgHyperparams, MetaGradStep
+    from toued.env import L_LIFETIME
     W, T, K = 64, 20, 5
     ro, ag0 = _agents_for(mode, N, W, T, 92)
+    # every third agent two updates short of its lifetime: its later updates are not applied (HvpOp then keeps none
+    # of its samples, the case where the one-launch reverse step's second op drops what the first op sorted)
+    life = ag0.levels[:, L_LIFETIME]
+    ag0.step[::3] = (life[::3] - 2).clamp(min=0).to(ag0.step.dtype)
     eta0 = init_lpg_params(93, 7 if lc else 5)
     out = []
     for one in ("0", "1"):

@@ -879,7 +879,7 @@ __global__ void __launch_bounds__(256) k_hvp(int N, int W, int T, int D, int K, 
 // of a wave with cross-lane adds, then over the block; partial[block][161] in the flat layout below.
 template <bool UNIF>
 __global__ void __launch_bounds__(256) k_embed_bwd(int N, int W, int T, int D, int K, const float* __restrict__ phi_hist,
-                                                   long phi_stride, const int* __restrict__ tidx_hist, long tidx_stride,
+                                                   long phi_stride, int phi_slot0, const int* __restrict__ tidx_hist, long tidx_stride,
                                                    const int* __restrict__ ttime_hist, const uint8_t* __restrict__ tdone_hist,
                                                    long tstep_stride, const float* __restrict__ dX3,
                                                    const float* __restrict__ dX4, long dx_stride_k,
@@ -925,7 +925,8 @@ __global__ void __launch_bounds__(256) k_embed_bwd(int N, int W, int T, int D, i
     const int* tidx = tidx_hist + k * tidx_stride;
     const int* ttime = ttime_hist + k * tidx_stride;
     const uint8_t* tdone = tdone_hist + k * tstep_stride;
-    v.ph = phi_hist + k * phi_stride + (size_t)a * D * 8;
+    const int slot = k + phi_slot0 > K ? k + phi_slot0 - (K + 1) : k + phi_slot0;   // ring of K + 1 slots
+    v.ph = phi_hist + slot * phi_stride + (size_t)a * D * 8;
     const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
 #pragma unroll
     for (int j = 0; j < 8; ++j) v.lastC[j] = v.ph[(size_t)(D - 1) * 8 + j];
@@ -1035,7 +1036,7 @@ TOUED_DEV void probs_regs(const float* row, const float* last, float c, float* p
 // are issued before this round's maths.  f32 products and sums, in another order than k_embed_bwd.
 template <bool UNIF>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EMBED_WPE))) k_embed_bwd3(int N, int W, int T, int D, int K, const float* __restrict__ phi_hist,
-                                                    long phi_stride, const int* __restrict__ tidx_hist, long tidx_stride,
+                                                    long phi_stride, int phi_slot0, const int* __restrict__ tidx_hist, long tidx_stride,
                                                     const int* __restrict__ ttime_hist, const uint8_t* __restrict__ tdone_hist,
                                                     long tstep_stride, const float* __restrict__ dX3,
                                                     const float* __restrict__ dX4, long dx_stride_k,
@@ -1081,7 +1082,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EMBED_
     const int* tidx = tidx_hist + k * tidx_stride;
     const int* ttime = ttime_hist + k * tidx_stride;
     const uint8_t* tdone = tdone_hist + k * tstep_stride;
-    v.ph = phi_hist + k * phi_stride + (size_t)a * D * 8;
+    const int slot = k + phi_slot0 > K ? k + phi_slot0 - (K + 1) : k + phi_slot0;   // ring of K + 1 slots
+    v.ph = phi_hist + slot * phi_stride + (size_t)a * D * 8;
     const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
     const size_t o = (size_t)k * dx_stride_k + (size_t)t * R + r;
     v.ix[0] = tidx[o0];
@@ -1231,6 +1233,24 @@ __global__ void __launch_bounds__(256) k_init_tables(const uint32_t* __restrict_
   float z = 1.41421356237f * erfinv_giles(u);
   z = fminf(fmaxf(z, -1.99999988f), 1.99999988f);
   out[e] = z * stddev;
+}
+
+// The masked form for the level sampler (few tables of many rewritten per call): one block per table looping over
+// its D * cols elements, so the unmasked tables cost one exiting block each instead of ceil(D * cols / 256); the
+// same element values as k_init_tables.
+__global__ void __launch_bounds__(256) k_init_tables_blk(const uint32_t* __restrict__ keys, int n, int cols, int D,
+                                                         float lo, float hi, float stddev, float* __restrict__ out,
+                                                         const uint8_t* __restrict__ mask) {
+  const int i = blockIdx.x;
+  if (i >= n || !mask[i]) return;
+  const long per = (long)D * cols;
+  const uint2 key = make_uint2(keys[2 * i], keys[2 * i + 1]);
+  for (long j = threadIdx.x; j < per; j += blockDim.x) {
+    const float u = uniform_from_bits(random_bits_at(key, (uint32_t)per, (uint32_t)j), lo, hi);
+    float z = 1.41421356237f * erfinv_giles(u);
+    z = fminf(fmaxf(z, -1.99999988f), 1.99999988f);
+    out[(long)i * per + j] = z * stddev;
+  }
 }
 
 }  // namespace
@@ -1530,13 +1550,14 @@ TOUED_DEV void rows_sorted_body(const Op& op) {
   __shared__ float red[8][NV + NM];
   __shared__ float tot[NV + NM];
   __shared__ int has_last;
+  __shared__ int any_kept;   // PRESORTED: did this op keep any sample (HvpOp keeps none of an agent not updated)
   __shared__ int scan_a[8];
   __shared__ float scan_b[8][NV];
   uint32_t* key = reinterpret_cast<uint32_t*>(lds);   // [2048]
   float* vec = lds + 2048;                            // [T*W][NVP]
   const int a = blockIdx.x, tid = threadIdx.x, W = op.W, T = op.T, D = op.D, TW = T * W;
   const int lane = tid & 63, wv = tid >> 6;
-  if (tid == 0) has_last = 0;
+  if (tid == 0) { has_last = 0; any_kept = 0; }
   float part[NV + NM];
 #pragma unroll
   for (int j = 0; j < NV + NM; ++j) part[j] = 0.0f;
@@ -1553,6 +1574,11 @@ TOUED_DEV void rows_sorted_body(const Op& op) {
 #pragma unroll
         for (int j = 0; j < NV; ++j) { vec[sl * NVP + j] = v[j]; part[j] += c * v[j]; }
         if (idx == D - 1) has_last = 1;
+        if (PRESORTED) any_kept = 1;
+      } else if (PRESORTED) {
+        // a sample the first op kept and this one drops: its slot in the shared sort adds zeros
+#pragma unroll
+        for (int j = 0; j < NV; ++j) vec[sl * NVP + j] = 0.0f;
       }
 #pragma unroll
       for (int j = 0; j < NM; ++j) part[NV + j] += m[j];
@@ -1582,10 +1608,16 @@ TOUED_DEV void rows_sorted_body(const Op& op) {
   uint32_t kc[CH];
   {
     const uint4 x = reinterpret_cast<const uint4*>(key)[tid];
-    kc[0] = x.x; kc[1] = x.y; kc[2] = x.z; kc[3] = x.w;
+    // PRESORTED with every sample dropped: the segments of a sort with no keys (exactly as a launch of its own)
+    if (PRESORTED && !any_kept) {
+      kc[0] = kc[1] = kc[2] = kc[3] = NONE;
+    } else {
+      kc[0] = x.x; kc[1] = x.y; kc[2] = x.z; kc[3] = x.w;
+    }
   }
-  const uint32_t prow = tid == 0 ? NONE : rowof(key[CH * tid - 1]);
-  const uint32_t nrow = tid == 511 ? NONE : rowof(key[CH * tid + CH]);
+  const bool keys_live = !PRESORTED || any_kept;
+  const uint32_t prow = tid == 0 || !keys_live ? NONE : rowof(key[CH * tid - 1]);
+  const uint32_t nrow = tid == 511 || !keys_live ? NONE : rowof(key[CH * tid + CH]);
   uint32_t endm = 0u;
 #pragma unroll
   for (int e = 0; e < CH; ++e) {
@@ -2180,14 +2212,18 @@ int toued_hvp(int N, int W, int T, int D, int K, const float* theta, const float
   return 0;
 }
 
-int toued_embed_bwd(int N, int W, int T, int D, int K, const float* phi_hist, long phi_stride, const int* tidx_hist,
+int toued_embed_bwd(int N, int W, int T, int D, int K, const float* phi_hist, long phi_stride, int phi_slot0,
+                    const int* tidx_hist,
                     long tidx_stride, const int* ttime_hist, const uint8_t* tdone_hist, long tstep_stride,
                     const float* dX3, const float* dX4, long dx_stride_k, const float* e1w, const float* e1b,
                     const float* e2w, float* partial, int n_blocks, hipStream_t stream) {
   if ((long)K * N * T * W == 0) return 0;
   TOUED_REQUIRE((long)K * N * (T + 1) * W < (1L << 31), "toued_embed_bwd: K*N*(T+1)*W = %ld samples exceed 2^31",
                 (long)K * N * (T + 1) * W);
+  TOUED_REQUIRE(phi_slot0 >= 0 && phi_slot0 <= K, "toued_embed_bwd: phi_slot0=%d outside the K+1=%d slots", phi_slot0,
+                K + 1);
 #define L_(KER) hipLaunchKernelGGL(KER, dim3(n_blocks), dim3(256), 0, stream, N, W, T, D, K, phi_hist, phi_stride,     \
+                                   phi_slot0,                                                                       \
                                    tidx_hist, tidx_stride, ttime_hist, tdone_hist, tstep_stride, dX3, dX4, dx_stride_k, \
                                    e1w, e1b, e2w, partial)
   if (EMBED_V == 3) {
@@ -2216,8 +2252,7 @@ int toued_init_tables_masked(const uint32_t* keys, int n, int cols, int D, float
   TOUED_REQUIRE(mask != nullptr, "toued_init_tables_masked: mask required");
   const long tot = (long)n * D * cols;
   if (tot == 0) return 0;
-  hipLaunchKernelGGL(k_init_tables, dim3(nb256((long)D * cols), n), dim3(256), 0, stream, keys, n, cols, D, lo, hi,
-                     stddev, out, mask);
+  hipLaunchKernelGGL(k_init_tables_blk, dim3(n), dim3(256), 0, stream, keys, n, cols, D, lo, hi, stddev, out, mask);
   TOUED_CHECK_LAUNCH();
   return 0;
 }

@@ -63,7 +63,7 @@ _SIGS = {
     "toued_clip_dot": [_I, _I, _P, _P, _P, _P, _P, _F, _F, _F, _P, _P],
     "toued_hvp": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F,
                   _P, _P, _P, _P, _P],
-    "toued_embed_bwd": [_I, _I, _I, _I, _I, _P, _L, _P, _L, _P, _P, _L, _P, _P, _L, _P, _P, _P, _P, _I, _P],
+    "toued_embed_bwd": [_I, _I, _I, _I, _I, _P, _L, _I, _P, _L, _P, _P, _L, _P, _P, _L, _P, _P, _P, _P, _I, _P],
     "toued_init_tables": [_P, _I, _I, _I, _F, _F, _F, _P, _P],
     "toued_init_tables_masked": [_P, _I, _I, _I, _F, _F, _F, _P, _P, _P],
     "toued_adam": [_I, _P, _P, _P, _P, _F, _F, ctypes.c_double, ctypes.c_double, _F, _I, _P],

@@ -164,10 +164,13 @@ class MetaGradStep:
         self.R = R
         f32, i32, u8 = torch.float32, torch.int32, torch.uint8
         z = lambda *s, dt=f32: torch.zeros(s, dtype=dt, device=dev)
-        # parameter history theta_0 .. theta_K; slot 0 doubles as the agents' own table storage (AgentBatch.theta is
-        # bound to it at the first step), so after a step it holds theta_K
-        self.theta_h = z(K + 1, N, D, 5)
-        self.phi_h = z(K + 1, N, D, Y)
+        # parameter history theta_0 .. theta_K as a ring of K + 1 slots: a step keeps theta_k in slot (r + k) % (K + 1),
+        # r = self._ring; the agents' own tables are bound to slot r (theta_0) and after the step to slot r + K
+        # (theta_K), which is the next step's theta_0 -- no copy back into a fixed slot
+        self._theta_store = z(K + 1, N, D, 5)
+        self._phi_store = z(K + 1, N, D, Y)
+        self._ring = 0        # this step's slot of theta_0
+        self._ring_last = 0   # the last step's (theta_h / phi_h below)
         self.G_th = z(K, N, D, 5)
         self.G_ph = z(K, N, D, Y)
         # inner updates as toued_agent_step (sparse: theta_{k+1} copied on a side stream beside rollout k and the
@@ -215,6 +218,16 @@ class MetaGradStep:
         self._draws = None      # the K + 1 train rollouts' draws (rollout.train_draws), reused every step
 
     # ------------------------------------------------------------------ helpers
+    @property
+    def theta_h(self) -> torch.Tensor:
+        """theta_0 .. theta_K of the last step [K + 1, N, D, 5] (copied out of the ring in that order; slot K holds the
+        agents' tables, which the level sampler rewrites in place for terminated agents)."""
+        return torch.roll(self._theta_store, -self._ring_last, dims=0)
+
+    @property
+    def phi_h(self) -> torch.Tensor:
+        return torch.roll(self._phi_store, -self._ring_last, dims=0)
+
     def _t(self, k: int) -> Transition:
         tr = self.traj
         return Transition(tr.obs_idx[k], tr.obs_time[k], tr.action[k], tr.reward[k], tr.done[k])
@@ -235,7 +248,15 @@ class MetaGradStep:
         n_all = self.n_total_local if rank_slice is None else rank_slice[2]
         lo = 0 if rank_slice is None else rank_slice[0]
         keys_all = prng.split(rng, n_all)
-        self.gru.pack(eta)
+        # the GRU fragments of eta (six small launches) on the side stream, beside the step's key, level and draws
+        # launches; the first LPG forward waits for them
+        main = torch.cuda.current_stream()
+        pack_stream = self.side if os.environ.get("TOUED_PACK_SIDE", "1") != "0" else main
+        pack_stream.wait_stream(main)
+        with torch.cuda.stream(pack_stream):
+            self.gru.pack(eta)
+            self._packed = torch.cuda.Event()
+            self._packed.record(pack_stream)
         self.grad.zero_()
         parts = []
         for c in range(self.n_chunks):
@@ -272,17 +293,24 @@ class MetaGradStep:
         ptr = L.ptr
         L.call("toued_meta_keys", ptr(agent_keys), N, K, ptr(self.keys_roll), ptr(self.keys_eval),
                ptr(self.keys_ea_reset), ptr(self.keys_ea_roll), st)
-        if self.n_chunks == 1 and isinstance(agents, AgentBatch):
-            # the agents' tables live in history slot 0 (bound there at the first step): theta_0 needs no copy, and the
-            # step ends by writing theta_K back into it
-            if agents.theta.data_ptr() != self.theta_h[0].data_ptr():
-                self.theta_h[0].copy_(agents.theta)
-                self.phi_h[0].copy_(agents.phi)
-                agents.theta = self.theta_h[0]
-                agents.phi = self.phi_h[0]
+        # the history ring's slots in this step's order (theta_k = th[k])
+        bound = self.n_chunks == 1 and isinstance(agents, AgentBatch)
+        ring = bound and os.environ.get("TOUED_HIST_RING", "1") != "0"
+        r0 = self._ring if ring else 0
+        th = [self._theta_store[(r0 + k) % (K + 1)] for k in range(K + 1)]
+        ph = [self._phi_store[(r0 + k) % (K + 1)] for k in range(K + 1)]
+        self._ring_last = r0
+        if bound:
+            # the agents' tables live in the ring (bound at the first step): theta_0 needs no copy, and theta_K's slot
+            # becomes the agents' tables (and the next step's theta_0) at the end
+            if agents.theta.data_ptr() != th[0].data_ptr():
+                th[0].copy_(agents.theta)
+                ph[0].copy_(agents.phi)
+                agents.theta = th[0]
+                agents.phi = ph[0]
         else:
-            self.theta_h[0].copy_(agents.theta)
-            self.phi_h[0].copy_(agents.phi)
+            th[0].copy_(agents.theta)
+            ph[0].copy_(agents.phi)
         if not self.fused_step:   # the fused step writes the touched gradient rows, and nothing reads the others
             self.G_th.zero_()
             self.G_ph.zero_()
@@ -307,20 +335,22 @@ class MetaGradStep:
                 # theta_{k+1} <- theta_k beside this update's rollout and LPG forward (theta_k is final here)
                 self.side.wait_stream(main)
                 with torch.cuda.stream(self.side):
-                    self.theta_h[k + 1].copy_(self.theta_h[k])
-                    self.phi_h[k + 1].copy_(self.phi_h[k])
+                    th[k + 1].copy_(th[k])
+                    ph[k + 1].copy_(ph[k])
             tok = self.timers.start("rollout")
             if draws is not None:
-                self.ro.rollout_from_draws(draws, k, self.theta_h[k], agents.levels, state, tk)
+                self.ro.rollout_from_draws(draws, k, th[k], agents.levels, state, tk)
             else:
-                self.ro.batch_rollout(self.keys_roll[k], self.theta_h[k], agents.levels, state, out=tk,
+                self.ro.batch_rollout(self.keys_roll[k], th[k], agents.levels, state, out=tk,
                                       inplace_state=True)
             self.timers.stop(tok)
             nan_checker().check("rollout_rewards", tk.reward)
-            L.call(lpg_inputs_fn(R, W), N, W, T, D, self.F, ptr(self.theta_h[k]), ptr(self.phi_h[k]),
+            L.call(lpg_inputs_fn(R, W), N, W, T, D, self.F, ptr(th[k]), ptr(ph[k]),
                    ptr(tk.obs_idx), ptr(tk.obs_time), ptr(tk.action), ptr(tk.reward), ptr(tk.done),
                    ptr(e1w), ptr(e1b), ptr(e2w), ptr(e2b), ptr(agents.step), ptr(agents.levels),
                    ptr(self.X) + 4 * k * T * R, self.gru.M, 1, 0, st)
+            if k == 0:
+                main.wait_event(self._packed)
             tok = self.timers.start("gru_fwd")
             self.gru.forward(k, self.X, tk.done, eta, self.pi_hat, self.y_hat)
             self.timers.stop(tok)
@@ -330,26 +360,26 @@ class MetaGradStep:
             if self.fused_step:
                 # the update and the new policy's entropy metrics (toued_entropy's metric mode) in one launch
                 main.wait_stream(self.side)
-                L.call("toued_agent_step_entropy" if self.step_entropy else "toued_agent_step", N, W, T, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]),
-                       ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(tk.obs_idx), ptr(tk.obs_time),
+                L.call("toued_agent_step_entropy" if self.step_entropy else "toued_agent_step", N, W, T, D, ptr(th[k]), ptr(ph[k]),
+                       ptr(th[k + 1]), ptr(ph[k + 1]), ptr(tk.obs_idx), ptr(tk.obs_time),
                        ptr(tk.action), ptr(tk.reward), ptr(tk.done), ptr(self.pi_hat[k]), ptr(self.y_hat[k]),
                        hyp.agent_target_coeff, hyp.actor_lr, hyp.critic_lr, hyp.max_grad_norm, ptr(self.G_th[k]),
                        ptr(self.G_ph[k]), ptr(self.met[k]), ptr(agents.step), ptr(agents.levels), ptr(self.gstat[k]),
                        st)
                 if not self.step_entropy:
-                    L.call("toued_entropy", N, W, T, D, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]),
+                    L.call("toued_entropy", N, W, T, D, ptr(th[k + 1]), ptr(ph[k + 1]),
                            ptr(tk.obs_idx), ptr(tk.obs_time), ptr(self.met[k]), 0.0, 0.0, None, None, st)
             else:
-                L.call("toued_agent_grad", N, W, T, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(tk.obs_idx),
+                L.call("toued_agent_grad", N, W, T, D, ptr(th[k]), ptr(ph[k]), ptr(tk.obs_idx),
                        ptr(tk.obs_time), ptr(tk.action), ptr(tk.reward), ptr(tk.done), ptr(self.pi_hat[k]),
                        ptr(self.y_hat[k]), hyp.agent_target_coeff, ptr(self.G_th[k]), ptr(self.G_ph[k]),
                        ptr(self.met[k]), ptr(agents.step), ptr(agents.levels), ptr(self.gstat[k]), st)
-                L.call("toued_agent_apply", N, D, ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(self.G_th[k]),
+                L.call("toued_agent_apply", N, D, ptr(th[k]), ptr(ph[k]), ptr(self.G_th[k]),
                        ptr(self.G_ph[k]), hyp.actor_lr, hyp.critic_lr, hyp.max_grad_norm, ptr(agents.step),
-                       ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]), ptr(self.gstat[k]), st)
-                L.call("toued_entropy", N, W, T, D, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]),
+                       ptr(th[k + 1]), ptr(ph[k + 1]), ptr(self.gstat[k]), st)
+                L.call("toued_entropy", N, W, T, D, ptr(th[k + 1]), ptr(ph[k + 1]),
                        ptr(tk.obs_idx), ptr(tk.obs_time), ptr(self.met[k]), 0.0, 0.0, None, None, st)
-            nan_checker().check("agent_params", self.theta_h[k + 1], self.phi_h[k + 1])
+            nan_checker().check("agent_params", th[k + 1], ph[k + 1])
         # ---------------- value critic on the train rollouts (--fix_value_critic), eval rollout, lpg loss
         if hyp.fix_value_critic:
             self.vc_loss.zero_()
@@ -357,10 +387,10 @@ class MetaGradStep:
                 self._value_critic_update(self._t(k), agents)
         te = self._t(K)
         if draws is not None:
-            self.ro.rollout_from_draws(draws, K, self.theta_h[K], agents.levels, state, te)
+            self.ro.rollout_from_draws(draws, K, th[K], agents.levels, state, te)
         else:
-            self.ro.batch_rollout(self.keys_eval, self.theta_h[K], agents.levels, state, out=te, inplace_state=True)
-        L.call("toued_eval_loss", N, W, T, D, ptr(self.theta_h[K]), ptr(agents.vcrit), ptr(te.obs_idx),
+            self.ro.batch_rollout(self.keys_eval, th[K], agents.levels, state, out=te, inplace_state=True)
+        L.call("toued_eval_loss", N, W, T, D, ptr(th[K]), ptr(agents.vcrit), ptr(te.obs_idx),
                ptr(te.obs_time), ptr(te.action), ptr(te.reward), ptr(te.done), hyp.gamma, hyp.gae_lambda,
                ptr(self.adv), ptr(self.abar), ptr(self.loss_out), st)
         if hyp.fix_value_critic:
@@ -404,7 +434,7 @@ class MetaGradStep:
             small_done.record(main)
             self.side.wait_event(small_done)
             with torch.cuda.stream(self.side):
-                ea["cum"] = self.ro.eval_returns_from_draws(self._ea_draws, self.theta_h[K], agents.levels,
+                ea["cum"] = self.ro.eval_returns_from_draws(self._ea_draws, th[K], agents.levels,
                                                             ea["state"])
             main.wait_event(ea["draws_done"])
             L.lib().toued_set_reserved_cus(eval_cus)
@@ -424,15 +454,15 @@ class MetaGradStep:
         a_in = 0
         self.adj_th[a_in].zero_()
         self.adj_ph[a_in].zero_()
-        L.call("toued_lpgloss_grad", N, W, T, D, ptr(self.theta_h[K]), ptr(te.obs_idx), ptr(te.obs_time),
+        L.call("toued_lpgloss_grad", N, W, T, D, ptr(th[K]), ptr(te.obs_idx), ptr(te.obs_time),
                ptr(te.action), ptr(self.abar), ptr(self.adj_th[a_in]), st)
         for k in range(K - 1, -1, -1):
             tk = self._t(k)
             # d(-b0*H_pi - b1*H_y)/K at (theta_{k+1}, phi_{k+1}) on rollout k, then the clip-VJP coefficients
             if self.fused_step and self.reverse_pair:
                 # entropy adjoint + clip coefficients, then the HVP rows, in one launch (one sort of rollout k)
-                L.call("toued_entropy_clip_hvp", N, W, T, D, K, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]),
-                       ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(tk.obs_idx), ptr(tk.obs_time), ptr(tk.action),
+                L.call("toued_entropy_clip_hvp", N, W, T, D, K, ptr(th[k + 1]), ptr(ph[k + 1]),
+                       ptr(th[k]), ptr(ph[k]), ptr(tk.obs_idx), ptr(tk.obs_time), ptr(tk.action),
                        ptr(self.pi_hat[k]), ptr(self.y_hat[k]), -hyp.policy_entropy_coeff / K,
                        -hyp.target_entropy_coeff / K, ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]),
                        ptr(self.G_th[k]), ptr(self.G_ph[k]), ptr(self.gstat[k]), hyp.actor_lr, hyp.critic_lr,
@@ -442,13 +472,13 @@ class MetaGradStep:
             if self.fused_step:
                 # one kernel: the entropy gradient's rows are the rows update k touched, so their owners add
                 # <G_k, adjoint> as they write them (toued_clip_dot's dot up to the summation order)
-                L.call("toued_entropy_clip", N, W, T, D, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]),
+                L.call("toued_entropy_clip", N, W, T, D, ptr(th[k + 1]), ptr(ph[k + 1]),
                        ptr(tk.obs_idx), ptr(tk.obs_time), -hyp.policy_entropy_coeff / K,
                        -hyp.target_entropy_coeff / K, ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]),
                        ptr(self.G_th[k]), ptr(self.G_ph[k]), ptr(self.gstat[k]), hyp.actor_lr, hyp.critic_lr,
                        hyp.max_grad_norm, ptr(self.coef), st)
             else:
-                L.call("toued_entropy", N, W, T, D, ptr(self.theta_h[k + 1]), ptr(self.phi_h[k + 1]),
+                L.call("toued_entropy", N, W, T, D, ptr(th[k + 1]), ptr(ph[k + 1]),
                        ptr(tk.obs_idx), ptr(tk.obs_time), None, -hyp.policy_entropy_coeff / K,
                        -hyp.target_entropy_coeff / K, ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]), st)
                 L.call("toued_clip_dot", N, D, ptr(self.G_th[k]), ptr(self.G_ph[k]), ptr(self.adj_th[a_in]),
@@ -457,7 +487,7 @@ class MetaGradStep:
             # theta_bar_k = theta_bar_{k+1} + (sparse second-order rows): accumulated in place.  k_rows_sorted reads
             # every sample's adjoint rows before its first row write (the sort's barriers separate the phases), and
             # each agent's tables belong to one workgroup, so no copy of the 144 MB adjoint is needed.
-            L.call("toued_hvp", N, W, T, D, K, ptr(self.theta_h[k]), ptr(self.phi_h[k]), ptr(tk.obs_idx),
+            L.call("toued_hvp", N, W, T, D, K, ptr(th[k]), ptr(ph[k]), ptr(tk.obs_idx),
                    ptr(tk.obs_time), ptr(tk.action), ptr(self.pi_hat[k]), ptr(self.y_hat[k]), ptr(self.G_th[k]),
                    ptr(self.G_ph[k]), ptr(self.adj_th[a_in]), ptr(self.adj_ph[a_in]), ptr(self.coef), hyp.actor_lr,
                    hyp.critic_lr, hyp.agent_target_coeff, hyp.policy_l2_coeff, hyp.target_l2_coeff,
@@ -473,7 +503,7 @@ class MetaGradStep:
         if "cum" not in ea:
             raise RuntimeError("MetaGradStep: the GRU backward returned without launching eval_agent")
         tr = self.traj
-        L.call("toued_embed_bwd", N, W, T, D, K, ptr(self.phi_h), self.phi_h[0].numel(), ptr(tr.obs_idx),
+        L.call("toued_embed_bwd", N, W, T, D, K, ptr(self._phi_store), self._phi_store[0].numel(), r0, ptr(tr.obs_idx),
                tr.obs_idx[0].numel(), ptr(tr.obs_time), ptr(tr.done), tr.done[0].numel(), ptr(self.gru.dX3),
                ptr(self.gru.dX4), T * R, ptr(e1w), ptr(e1b), ptr(e2w), ptr(self.embed_partial), self.embed_blocks, st)
         emb = self.embed_partial.sum(dim=0)
@@ -487,8 +517,13 @@ class MetaGradStep:
         ea_cum.record_stream(main)
         ea["state"].record_stream(main)
         nan_checker().check("eval_returns", ea_cum)
-        agents.theta.copy_(self.theta_h[K])
-        agents.phi.copy_(self.phi_h[K])
+        if ring:
+            agents.theta = th[K]
+            agents.phi = ph[K]
+            self._ring = (r0 + K) % (K + 1)
+        else:
+            agents.theta.copy_(th[K])
+            agents.phi.copy_(ph[K])
         # (met * inv_wt).mean over the K updates and the regularised loss, one launch (toued_meta_metrics)
         mo = torch.empty((6, N), dtype=torch.float32, device=self.dev)
         L.call("toued_meta_metrics", N, K, ptr(self.met), 1.0 / (W * T), ptr(self.loss_out),
@@ -612,10 +647,10 @@ def make_lpg_train_step(args, level_sampler, n_agents: int | None = None, world=
     ``(lpg_train_state, agent_states, value_critic_states, metrics)``.
 
     agent_states: agents.AgentBatch of this rank's agents (``rank_slice`` = (lo, hi, n_total) under data
-    parallelism; n_agents defaults to its size).  The meta-gradient step rebinds ``agent_states.theta`` / ``.phi`` at
-    its first call to its own history slot 0 (copying the tables once) and updates them there in place, so the
-    returned states alias the inputs from then on; a tensor reference taken to the tables BEFORE the first step is
-    not updated.  value_critic_states: ValueCriticStates or None (then the ones
+    parallelism; n_agents defaults to its size).  The meta-gradient step binds ``agent_states.theta`` / ``.phi`` to
+    slots of its parameter-history ring (copying the tables once at the first call) and rebinds them to theta_K's
+    slot at the end of every call (no copy back), so the returned states are the inputs with updated attributes; a
+    tensor reference taken to the tables before a call is not updated by it.  value_critic_states: ValueCriticStates or None (then the ones
     inside agent_states are used); ignored by the ES step, as in the reference.  ``impl``: an already built
     MetaGradStep / ESTrainStep to drive (train.Trainer keeps its instance for timers and buffers)."""
     n_local = n_agents if n_agents is not None else (args.num_agents if rank_slice is None

@@ -42,7 +42,8 @@ def main():
         part = torch.zeros(nb, 161, device="cuda")
 
         def run():
-            L.call("toued_embed_bwd", N, W, T, D, K, L.ptr(s.phi_h), s.phi_h[0].numel(), L.ptr(t.obs_idx),
+            L.call("toued_embed_bwd", N, W, T, D, K, L.ptr(s._phi_store), s._phi_store[0].numel(), s._ring_last,
+                   L.ptr(t.obs_idx),
                    t.obs_idx[0].numel(), L.ptr(t.obs_time), L.ptr(t.done), t.done[0].numel(), L.ptr(s.gru.dX3),
                    L.ptr(s.gru.dX4), T * R, L.ptr(e1w), L.ptr(e1b), L.ptr(e2w), L.ptr(part), nb, L.stream_ptr())
         run()
