@@ -90,7 +90,7 @@ def main():
     for r in rows[:12]:
         print(r)
     print(json.dumps(out["calibration"]))
-    for k in ("k_gru_bwd6n<true>", "k_gru_fwd6<true>", "k_wgrad_h3<8, 2>"):
+    for k in ("k_gru_bwd6n<true>", "k_gru_fwd6<true>", "k_wgrad_h3<8, 2, 3>"):
         print(k, out["kernels"].get(k))
 
 
