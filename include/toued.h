@@ -296,6 +296,12 @@ int toued_embed_bwd(int N, int W, int T, int D, int K, const float* phi_hist, lo
                     long tidx_stride, const int* ttime_hist, const uint8_t* tdone_hist, long tstep_stride,
                     const float* dX3, const float* dX4, long dx_stride_k, const float* e1w, const float* e1b,
                     const float* e2w, float* partial, int n_blocks, hipStream_t stream);
+/* out[dst_idx[i]] += src[src_idx[i]] for i < n, the dst indices distinct (index_add_ with unique indices): the GRU
+ * weight-gradient blocks (G | GI) into eta's flat gradient layout in one launch */
+int toued_gather_add(float* out, const float* src, const int* src_idx, const int* dst_idx, int n, hipStream_t stream);
+/* out[j] += sum_{i < rows} part[i * cols + j], summed in ascending i (deterministic): the embedding gradient's per-block
+ * partials (toued_embed_bwd) into the flat gradient */
+int toued_sum_rows_add(const float* part, int rows, int cols, float* out, hipStream_t stream);
 /* optax 0.1.5 chain(scale_by_adam(b1, b2, eps), scale(lr), scale(-1)) on the flat eta (models/optim.py:12-17),
    applied to grad / n_mean (the agent mean, meta/train.py:128).  b1, b2 are the python floats (double) so that
    (1 - b) rounds to f32 once, as jax's weak-typed constants do; count is the post-increment step (>= 1). */

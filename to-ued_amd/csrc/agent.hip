@@ -1253,6 +1253,25 @@ __global__ void __launch_bounds__(256) k_init_tables_blk(const uint32_t* __restr
   }
 }
 
+// out[dst[i]] += src[si[i]], every dst index distinct (one plain read-modify-write per element, as index_add_ with
+// unique indices): the GRU weight-gradient blocks into eta's flat layout in one launch
+__global__ void __launch_bounds__(256) k_gather_add(float* __restrict__ out, const float* __restrict__ src,
+                                                    const int* __restrict__ si, const int* __restrict__ di, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[di[i]] += src[si[i]];
+}
+
+// out[j] += sum over i = 0 .. rows-1 (ascending) of part[i][j]: the embedding gradient's per-block partials, one thread
+// per column, a fixed order (deterministic)
+__global__ void __launch_bounds__(256) k_sum_rows_add(const float* __restrict__ part, int rows, int cols,
+                                                      float* __restrict__ out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= cols) return;
+  float acc = 0.0f;
+  for (int i = 0; i < rows; ++i) acc += part[(size_t)i * cols + j];
+  out[j] += acc;
+}
+
 }  // namespace
 
 // ============================================================================ C ABI
@@ -2253,6 +2272,22 @@ int toued_init_tables_masked(const uint32_t* keys, int n, int cols, int D, float
   const long tot = (long)n * D * cols;
   if (tot == 0) return 0;
   hipLaunchKernelGGL(k_init_tables_blk, dim3(n), dim3(256), 0, stream, keys, n, cols, D, lo, hi, stddev, out, mask);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_gather_add(float* out, const float* src, const int* src_idx, const int* dst_idx, int n, hipStream_t stream) {
+  TOUED_REQUIRE(n >= 0, "toued_gather_add: n=%d", n);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_gather_add, dim3((n + 255) / 256), dim3(256), 0, stream, out, src, src_idx, dst_idx, n);
+  TOUED_CHECK_LAUNCH();
+  return 0;
+}
+
+int toued_sum_rows_add(const float* part, int rows, int cols, float* out, hipStream_t stream) {
+  TOUED_REQUIRE(rows >= 0 && cols >= 0, "toued_sum_rows_add: rows=%d cols=%d", rows, cols);
+  if (cols == 0) return 0;
+  hipLaunchKernelGGL(k_sum_rows_add, dim3((cols + 255) / 256), dim3(256), 0, stream, part, rows, cols, out);
   TOUED_CHECK_LAUNCH();
   return 0;
 }

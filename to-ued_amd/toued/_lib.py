@@ -98,6 +98,8 @@ _SIGS = {
     "toued_agent_update": [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _F, _P, _P, _P, _P, _P],
     "toued_agent_step": [_I, _I, _I, _I] + [_P] * 11 + [_F] * 4 + [_P] * 7,
     "toued_agent_step_entropy": [_I, _I, _I, _I] + [_P] * 11 + [_F] * 4 + [_P] * 7,
+    "toued_gather_add": [_P, _P, _P, _P, _I, _P],
+    "toued_sum_rows_add": [_P, _I, _I, _P, _P],
     "toued_sample_random_keys": [_P, _I, _I, _I, _P, _P, _P, _U, _P, _P, _P],
     "toued_entropy_clip_hvp": [_I] * 5 + [_P] * 9 + [_F] * 2 + [_P] * 5 + [_F] * 3 + [_P] + [_F] * 3 + [_P] * 3,
     "toued_meta_metrics": [_I, _I, _P, _F, _P, _F, _F, _F, _F, _P, _P],

@@ -250,7 +250,7 @@ class LPGGRU:
             assert t.numel() == n, (name, t.shape, lay.shapes[name])
             src.append(t.reshape(-1))
             dst.append(lay.offsets[name] + torch.arange(n))
-        return torch.cat(src).to(dev), torch.cat(dst).to(dev)
+        return torch.cat(src).to(dev, torch.int32), torch.cat(dst).to(dev, torch.int32)
 
     def pack(self, eta: torch.Tensor):
         _lib.call("toued_gru_pack", _lib.ptr(eta), self.lay.c_offsets, self.lay.F, _lib.ptr(self.fwdA),
@@ -362,6 +362,7 @@ class LPGGRU:
         if self._scatter is None:
             self._scatter = self._scatter_indices(grad.device)
         src, dst = self._scatter
-        grad.index_add_(0, dst, self._ggi[src])
+        _lib.call("toued_gather_add", _lib.ptr(grad), _lib.ptr(self._ggi), _lib.ptr(src), _lib.ptr(dst), src.numel(),
+                  _lib.stream_ptr())
         if timers is not None:
             timers.stop(tok)

@@ -506,11 +506,10 @@ class MetaGradStep:
         L.call("toued_embed_bwd", N, W, T, D, K, ptr(self._phi_store), self._phi_store[0].numel(), r0, ptr(tr.obs_idx),
                tr.obs_idx[0].numel(), ptr(tr.obs_time), ptr(tr.done), tr.done[0].numel(), ptr(self.gru.dX3),
                ptr(self.gru.dX4), T * R, ptr(e1w), ptr(e1b), ptr(e2w), ptr(self.embed_partial), self.embed_blocks, st)
-        emb = self.embed_partial.sum(dim=0)
-        # e1_b, e1_w, e2_b, e2_w are contiguous in eta in the partials' order: one add
+        # e1_b, e1_w, e2_b, e2_w are contiguous in eta in the partials' order: the block sums added in one launch
         o = self.lay.offsets["e1_b"]
         assert self.lay.offsets["e2_w"] + 16 == o + 161
-        self.grad[o:o + 161].add_(emb[0:161])
+        L.call("toued_sum_rows_add", ptr(self.embed_partial), self.embed_blocks, 161, ptr(self.grad) + 4 * o, st)
         # ---------------- agent state out + metrics
         main.wait_stream(self.side)
         ea_cum = ea["cum"]
