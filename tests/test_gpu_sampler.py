@@ -166,3 +166,39 @@ def test_flax_lpg_init_matches_oracle(F):
         args.append("--lifetime_conditioning")
     tr = Trainer(parse_args(args))
     assert np.array_equal(tr.eta.cpu().numpy(), got)
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_sample_random_rank_slice_matches_full_batch(monkeypatch, fused):
+    """sample() of one rank's agent slice (sl = (lo, hi, n_total), as each rank runs it under data parallelism) equals
+    that slice of the full-batch sample: levels, tables, value critics, env states and step counters, with agents
+    terminated on both sides of the slice; the random branch as toued_sample_random_keys (1) and launch per
+    operation (0)."""
+    monkeypatch.setenv("TOUED_SAMPLE_FUSED", fused)
+    from toued.agents import AgentBatch
+    from toued.env import L_LIFETIME
+    from toued.level_sampler import LevelSampler
+    from toued.parse_args import parse_args
+    N, W, lo, hi = 8, 64, 3, 7
+    args = parse_args(["--env_mode", "all_shortlife", "--score_function", "random", "--num_agents", str(N),
+                       "--num_mini_batches", "1"])
+    smp = LevelSampler(args)
+    k_init, k_s = jr.split(jr.PRNGKey(77), 2)
+    _, full = smp.initial_sample(dk(k_init), None, N, True)
+    life = full.levels[:, L_LIFETIME]
+    term = torch.tensor([1, 0, 1, 1, 0, 1, 0, 1], dtype=torch.bool, device="cuda")
+    full.step = torch.where(term, life, torch.ones_like(life)).to(torch.int32)
+    full.vstep = full.step.clone()
+    full.theta.add_(0.5)
+    part = AgentBatch(full.levels[lo:hi].clone(), full.theta[lo:hi].clone(), full.phi[lo:hi].clone(),
+                      full.step[lo:hi].clone(), full.state[:, lo * W:hi * W].clone(), full.vcrit[lo:hi].clone(),
+                      full.vstep[lo:hi].clone())
+    _, full = smp.sample(dk(k_s), None, full)
+    _, part = smp.sample(dk(k_s), None, part, (lo, hi, N))
+    torch.cuda.synchronize()
+    assert torch.equal(part.levels, full.levels[lo:hi])
+    assert torch.equal(part.theta, full.theta[lo:hi]) and torch.equal(part.phi, full.phi[lo:hi])
+    assert torch.equal(part.vcrit, full.vcrit[lo:hi])
+    assert torch.equal(part.step, full.step[lo:hi]) and torch.equal(part.vstep, full.vstep[lo:hi])
+    assert torch.equal(part.state, full.state[:, lo * W:hi * W])
+    assert bool((full.step[term] == 0).all()) and bool((full.step[~term] == 1).all())   # only terminated ones reset
