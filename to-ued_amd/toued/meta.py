@@ -328,6 +328,19 @@ class MetaGradStep:
                                     for _ in range(2))
             draws = self.ro.train_draws(self.keys_train, agents.levels, W,
                                         self._draws)
+        ea = {}
+
+        def start_eval_prep():
+            # eval_agent's worker reset, key chain and draws read only the step's keys and the levels; only the env
+            # chain on the draws waits for theta_K and the backward
+            self.side.wait_stream(main)
+            with torch.cuda.stream(self.side):
+                (_, _), ea["state"] = self.ro.batch_reset(self.keys_ea_reset, agents.levels, hyp.eval_workers)
+                self._ea_draws = self.ro.eval_draws(self.keys_ea_roll, agents.levels, hyp.eval_workers,
+                                                    self._ea_draws)
+                ea["draws_done"] = torch.cuda.Event()
+                ea["draws_done"].record(self.side)
+
         # ---------------- forward: K inner updates (agents/lpg_agent.py:88-140)
         for k in range(K):
             tk = self._t(k)
@@ -337,6 +350,8 @@ class MetaGradStep:
                 with torch.cuda.stream(self.side):
                     th[k + 1].copy_(th[k])
                     ph[k + 1].copy_(ph[k])
+                    copy_done = torch.cuda.Event()
+                    copy_done.record(self.side)
             tok = self.timers.start("rollout")
             if draws is not None:
                 self.ro.rollout_from_draws(draws, k, th[k], agents.levels, state, tk)
@@ -354,14 +369,17 @@ class MetaGradStep:
             tok = self.timers.start("gru_fwd")
             self.gru.forward(k, self.X, tk.done, eta, self.pi_hat, self.y_hat)
             self.timers.stop(tok)
+            if k == K - 1 and eval_keys_early() and eval_prep_after_forwards():
+                start_eval_prep()
             if nan_checker().enabled:   # the update's saved GRU states h_in [256][T*R] (a column block of the operand)
                 nan_checker().check("lpg_gru_states", self.gru.hin_block(k))
             nan_checker().check("lpg_outputs", self.pi_hat[k], self.y_hat[k])
             if self.fused_step:
-                # the update and the new policy's entropy metrics (toued_entropy's metric mode) in one launch
-                main.wait_stream(self.side)
-                L.call("toued_agent_step_entropy" if self.step_entropy else "toued_agent_step", N, W, T, D, ptr(th[k]), ptr(ph[k]),
-                       ptr(th[k + 1]), ptr(ph[k + 1]), ptr(tk.obs_idx), ptr(tk.obs_time),
+                # the update and the new policy's entropy metrics (toued_entropy's metric mode) in one launch, once
+                # theta_{k+1}'s copy is done (an event: the side stream may hold eval_agent's chain behind it)
+                main.wait_event(copy_done)
+                L.call("toued_agent_step_entropy" if self.step_entropy else "toued_agent_step", N, W, T, D,
+                       ptr(th[k]), ptr(ph[k]), ptr(th[k + 1]), ptr(ph[k + 1]), ptr(tk.obs_idx), ptr(tk.obs_time),
                        ptr(tk.action), ptr(tk.reward), ptr(tk.done), ptr(self.pi_hat[k]), ptr(self.y_hat[k]),
                        hyp.agent_target_coeff, hyp.actor_lr, hyp.critic_lr, hyp.max_grad_norm, ptr(self.G_th[k]),
                        ptr(self.G_ph[k]), ptr(self.met[k]), ptr(agents.step), ptr(agents.levels), ptr(self.gstat[k]),
@@ -410,7 +428,6 @@ class MetaGradStep:
         # latency-bound agent kernels the key chain slowed them by more than it took.)
         key_cus = 2 * -(-N * hyp.eval_workers // 256)   # the key chain: two lanes per eval worker (k_eval_keys_pairs)
         eval_cus = int(L.lib().toued_eval_returns_cus(N * hyp.eval_workers))
-        ea = {}
 
         def launch_eval():
             self.side.wait_stream(main)
@@ -438,18 +455,11 @@ class MetaGradStep:
                                                             ea["state"])
             main.wait_event(ea["draws_done"])
             L.lib().toued_set_reserved_cus(eval_cus)
-        if eval_keys_early():
-            # eval_agent's worker reset, key chain and draws read only the step's keys and the levels: beside the
-            # reverse agent loop (latency-bound per-agent kernels) instead of in front of the weight-gradient
-            # reduction, which waits for the draws (with the small products fused into the backward nothing else
-            # covers them there); only the env chain on the draws waits for theta_K and the backward
-            self.side.wait_stream(main)
-            with torch.cuda.stream(self.side):
-                (_, _), ea["state"] = self.ro.batch_reset(self.keys_ea_reset, agents.levels, hyp.eval_workers)
-                self._ea_draws = self.ro.eval_draws(self.keys_ea_roll, agents.levels, hyp.eval_workers,
-                                                    self._ea_draws)
-                ea["draws_done"] = torch.cuda.Event()
-                ea["draws_done"].record(self.side)
+        if eval_keys_early() and "draws_done" not in ea:
+            # eval_agent's reset, key chain and draws beside the reverse agent loop (latency-bound per-agent kernels)
+            # instead of in front of the weight-gradient reduction, which waits for the draws (with the small
+            # products fused into the backward nothing else covers them there)
+            start_eval_prep()
         # ---------------- reverse: explicit adjoint w.r.t. eta
         a_in = 0
         self.adj_th[a_in].zero_()
@@ -632,6 +642,14 @@ def create_lpg_train_state(rng: torch.Tensor, args) -> LpgTrainState:
     from .lpg import flax_init_lpg_params
     eta = flax_init_lpg_params(rng, 7 if args.lifetime_conditioning else 5)
     return LpgTrainState(eta, None if args.use_es else AdamState(eta.numel(), eta.device))
+
+
+def eval_prep_after_forwards() -> bool:
+    """With eval_keys_early: eval_agent's key chain starts right after the last LPG forward (default), beside that
+    update's agent kernels, the eval rollout and the reverse loop, so that it ends before the recurrent backward
+    starts (a CU still holding a chain wave when the backward's exactly-filled rounds begin finishes its last
+    round that much later).  TOUED_EVAL_PREP=reverse: at the reverse loop, as in round 4 (bit-identical)."""
+    return os.environ.get("TOUED_EVAL_PREP", "forwards") != "reverse"
 
 
 def eval_keys_early() -> bool:
