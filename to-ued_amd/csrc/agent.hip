@@ -1261,15 +1261,23 @@ __global__ void __launch_bounds__(256) k_gather_add(float* __restrict__ out, con
   if (i < n) out[di[i]] += src[si[i]];
 }
 
-// out[j] += sum over i = 0 .. rows-1 (ascending) of part[i][j]: the embedding gradient's per-block partials, one thread
-// per column, a fixed order (deterministic)
+// out[j] += the sum over i < rows of part[i][j]: the embedding gradient's per-block partials.  One workgroup per column:
+// thread t sums rows t, t + 256, ... (independent loads in flight), then a fixed-order tree over the 256 partial sums
+// (deterministic).  (One thread per column walking the 768 rows serially took 0.18 ms of dependent loads.)
 __global__ void __launch_bounds__(256) k_sum_rows_add(const float* __restrict__ part, int rows, int cols,
                                                       float* __restrict__ out) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= cols) return;
+  __shared__ float sred[256];
+  const int j = blockIdx.x, tid = threadIdx.x;
   float acc = 0.0f;
-  for (int i = 0; i < rows; ++i) acc += part[(size_t)i * cols + j];
-  out[j] += acc;
+  for (int i = tid; i < rows; i += 256) acc += part[(size_t)i * cols + j];
+  sred[tid] = acc;
+  __syncthreads();
+#pragma unroll
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) sred[tid] += sred[tid + o];
+    __syncthreads();
+  }
+  if (tid == 0) out[j] += sred[0];
 }
 
 }  // namespace
@@ -2287,7 +2295,7 @@ int toued_gather_add(float* out, const float* src, const int* src_idx, const int
 int toued_sum_rows_add(const float* part, int rows, int cols, float* out, hipStream_t stream) {
   TOUED_REQUIRE(rows >= 0 && cols >= 0, "toued_sum_rows_add: rows=%d cols=%d", rows, cols);
   if (cols == 0) return 0;
-  hipLaunchKernelGGL(k_sum_rows_add, dim3((cols + 255) / 256), dim3(256), 0, stream, part, rows, cols, out);
+  hipLaunchKernelGGL(k_sum_rows_add, dim3(cols), dim3(256), 0, stream, part, rows, cols, out);
   TOUED_CHECK_LAUNCH();
   return 0;
 }
