@@ -52,7 +52,10 @@ int toued_abi_version(void);
  * count, toued_set_reserved_cus).  A process-wide default context is current until a thread makes another one
  * current; the setting is then per thread, so two host threads driving separate streams plan independently.
  * toued_ctx_destroy of the calling thread's current context reverts that thread to the default; destroying a
- * context another thread still has current is refused (-1).  The settings are atomic, so threads sharing the
+ * context another thread still has current is refused (-1).  A thread that exits with a context current releases it
+ * (a thread-exit guard), so the context can then be destroyed; the check and the delete run under the same lock as
+ * toued_ctx_set_current, so no thread can make a context current while it is being destroyed.  The settings are
+ * atomic, so threads sharing the
  * default context do not race on them (each sees one of the values written).  Replaces no reference interface: the
  * reference's equivalent state lives in its jitted closures. */
 typedef struct toued_ctx toued_ctx;
@@ -66,7 +69,7 @@ toued_ctx* toued_ctx_current(void);
  * in it when the wait expires instead of hanging.  wait = 1: synchronise with `stream` and report any error of the
  * work enqueued before the call; wait = 0: never block -- report what the previous call's read-back saw (if it has
  * landed) and enqueue a new read-back.  Returns -3 and sets toued_last_error() when a bit was set (the word is then
- * cleared), 0 otherwise.  The first call allocates the word (do it outside graph capture: toued_a2c_chain_self
+ * cleared, and the next read-back is enqueued behind the clear, so an error is reported once), 0 otherwise.  The first call allocates the word (do it outside graph capture: toued_a2c_chain_self
  * refuses to launch before it).  Replaces no reference interface: XLA's scan cannot starve. */
 int toued_device_error_check(hipStream_t stream, int wait);
 /* --debug (experiments/parse_args.py:7, util/jax.py:12-14 `jax.disable_jit`): hipDeviceSynchronize + hipGetLastError,
@@ -299,8 +302,9 @@ int toued_embed_bwd(int N, int W, int T, int D, int K, const float* phi_hist, lo
 /* out[dst_idx[i]] += src[src_idx[i]] for i < n, the dst indices distinct (index_add_ with unique indices): the GRU
  * weight-gradient blocks (G | GI) into eta's flat gradient layout in one launch */
 int toued_gather_add(float* out, const float* src, const int* src_idx, const int* dst_idx, int n, hipStream_t stream);
-/* out[j] += sum_{i < rows} part[i * cols + j], summed in ascending i (deterministic): the embedding gradient's per-block
- * partials (toued_embed_bwd) into the flat gradient */
+/* out[j] += sum_{i < rows} part[i * cols + j]: the embedding gradient's per-block partials (toued_embed_bwd) into the
+ * flat gradient.  Deterministic but not a serial sum: 256 strided partials (partial t sums rows t, t + 256, ... in
+ * ascending order), then a fixed pairwise tree over the 256 partials (t += t + 128, then + 64, ... + 1). */
 int toued_sum_rows_add(const float* part, int rows, int cols, float* out, hipStream_t stream);
 /* optax 0.1.5 chain(scale_by_adam(b1, b2, eps), scale(lr), scale(-1)) on the flat eta (models/optim.py:12-17),
    applied to grad / n_mean (the agent mean, meta/train.py:128).  b1, b2 are the python floats (double) so that

@@ -710,7 +710,7 @@ def test_gru_backward_fused_small_matches_unfused(N, wscale, F):
     from toued.lpg import LPGGRU, LPGLayout, init_lpg_params
     W, T, K = 64, 6, 2
     R = N * W
-    lay = LPGLayout(F)
+    lay = LPGLayout(F, kernel_test=True)
     eta = init_lpg_params(7, F)
     gen = torch.Generator(device="cuda").manual_seed(5)
     eta += torch.randn(eta.shape, device="cuda", generator=gen) * 0.05

@@ -12,6 +12,18 @@ static thread_local char g_err[512] = "";
 static toued_ctx g_default_ctx;
 static thread_local toued_ctx* g_current_ctx = nullptr;
 toued_ctx* current_ctx() { return g_current_ctx ? g_current_ctx : &g_default_ctx; }
+// toued_ctx_set_current / toued_ctx_destroy / thread exit change a context's users count under this lock, so a destroy
+// cannot delete a context between another thread's check and its set_current
+static std::mutex g_ctx_m;
+// a thread that exits with a context current gives it back (else its users count stays raised and destroy refuses)
+struct CtxExitGuard {
+  ~CtxExitGuard() {
+    std::lock_guard<std::mutex> lk(g_ctx_m);
+    if (g_current_ctx) g_current_ctx->users.fetch_sub(1);
+    g_current_ctx = nullptr;
+  }
+};
+static thread_local CtxExitGuard g_ctx_exit_guard;
 void set_error(const char* fmt, ...) {
   va_list ap;
   va_start(ap, fmt);
@@ -70,6 +82,7 @@ int toued_abi_version(void) { return 1; }
 toued_ctx* toued_ctx_create(void) { return new (std::nothrow) toued_ctx(); }
 int toued_ctx_destroy(toued_ctx* ctx) {
   if (!ctx) return 0;
+  std::lock_guard<std::mutex> lk(toued::g_ctx_m);
   const int mine = toued::g_current_ctx == ctx ? 1 : 0;
   // refused while another host thread still has it current (that thread would keep a dangling pointer)
   TOUED_REQUIRE(ctx->users.load() <= mine, "toued_ctx_destroy: context is current on %d other thread(s)",
@@ -79,6 +92,8 @@ int toued_ctx_destroy(toued_ctx* ctx) {
   return 0;
 }
 int toued_ctx_set_current(toued_ctx* ctx) {
+  (void)&toued::g_ctx_exit_guard;   // odr-use: constructs this thread's exit guard
+  std::lock_guard<std::mutex> lk(toued::g_ctx_m);
   toued_ctx* old = toued::g_current_ctx;
   if (old == ctx) return 0;
   if (ctx) ctx->users.fetch_add(1);
@@ -118,19 +133,27 @@ int toued_device_error_check(hipStream_t stream, int wait) {
       TOUED_REQUIRE(q == hipErrorNotReady, "toued_device_error_check: %s", hipGetErrorString(q));
     }
   }
-  if (!g_de.pending) {
+  auto enqueue_readback = [&] {
     TOUED_REQUIRE(hipMemcpyAsync(g_de.host, g_de.word, sizeof(unsigned), hipMemcpyDeviceToHost, stream) == hipSuccess &&
                       hipEventRecord(g_de.ev, stream) == hipSuccess,
                   "toued_device_error_check: cannot enqueue the read-back");
     g_de.pending = true;
-    if (wait) {
-      TOUED_REQUIRE(hipEventSynchronize(g_de.ev) == hipSuccess, "toued_device_error_check: read-back failed");
-      code |= *g_de.host;
-      g_de.pending = false;
-    }
+    return 0;
+  };
+  if (!g_de.pending && wait) {
+    if (enqueue_readback()) return -1;
+    TOUED_REQUIRE(hipEventSynchronize(g_de.ev) == hipSuccess, "toued_device_error_check: read-back failed");
+    code |= *g_de.host;
+    g_de.pending = false;
   }
+  // the clear goes in front of the next read-back, so that read-back cannot report the same bits again (an error a
+  // kernel sets between the landed read-back and the clear is lost: the word only carries expired bounded waits)
+  if (code)
+    TOUED_REQUIRE(hipMemsetAsync(g_de.word, 0, sizeof(unsigned), stream) == hipSuccess,
+                  "toued_device_error_check: cannot clear the device error word (device error 0x%x: %s)", code,
+                  deverr_text(code));
+  if (!g_de.pending && !wait && enqueue_readback()) return -1;
   if (code) {
-    hipMemsetAsync(g_de.word, 0, sizeof(unsigned), stream);
     set_error("device error 0x%x: %s", code, deverr_text(code));
     return -3;
   }

@@ -675,6 +675,9 @@ __device__ unsigned long long g_fwd_stamps[64 * 32 * 6];
 #ifndef FWD_XFIRST
 #define FWD_XFIRST 0   // comparison runs: x(t) issued before the ring's lead fragments (the round-4 order)
 #endif
+#ifndef FWD_CAND0
+#define FWD_CAND0 0    // timing study only: the per-candidate instance reads candidate 0's fragments everywhere
+#endif
 template <bool SAVE>
 __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   constexpr bool A32 = FWD_AUG32 && !SAVE;   // the per-candidate (ES) instance: f32-MFMA augmented k-step
@@ -701,7 +704,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
   // per-candidate parameters in the ES inference mode (rows [c * rpc, (c + 1) * rpc) use candidate c)
   const int cand = SAVE ? 0 : r0 / p.rpc;
   const float* eta = p.eta + (long)cand * p.eta_stride;
-  const float* A6c = reinterpret_cast<const float*>(p.A6) + (long)cand * p.a_stride4 * 4;
+  // FWD_CAND0 (timing study only, wrong results): every workgroup streams candidate 0's packed fragments, which then
+  // stay L2-resident -- the per-candidate fragment stream's cost is the difference to the production kernel
+  const float* A6c = reinterpret_cast<const float*>(p.A6) + (long)(FWD_CAND0 ? 0 : cand) * p.a_stride4 * 4;
   for (int i = tid; i < HU * 12; i += 512) {
     const int u = i / 12, oo = i - u * 12;
     wh[i] = oo == 0 ? eta[p.o.pi_w + u] : oo < 9 ? eta[p.o.y_w + u * 8 + (oo - 1)] : 0.0f;
@@ -1520,6 +1525,13 @@ __device__ int g_bwd_wsimd[64 * 8];
 #ifndef BWD_TNOTR
 #define BWD_TNOTR 0   // timing study only (wrong results): r, z, hn used without their lane-quad transposes
 #endif
+// BWD_TRECOMP (timing study only, wrong results): the gate pre-activations W_hr h, W_hz h and
+// W_hn h recomputed on the matrix pipe at the top of every step (the forward's 16 carry k-steps: 3 gates x 2 row tiles
+// x scaled fp16 pairs, A fragments through a two-k-step L2 ring, B from the image) and the memory part loading only
+// h_in: a lower bound on the step of a recompute backward (no h_in image build, no augmented input k-step)
+#ifndef BWD_TRECOMP
+#define BWD_TRECOMP 0
+#endif
 template <bool SMALL>
 __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   constexpr int RBT = 2 * RB;
@@ -1843,9 +1855,11 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     if (HIN_SLAB) ld4(rs_hin, vs, ss, v[0]);
     else ld4(rs_hin, (unsigned)((((long)(ub + (col & 3))) * p.M + r0 + RB * h + (col & 28)) * 4),
              (unsigned)(((long)8 * g4 * p.M + ctr_) * 4), v[0]);
-    ld4(rs_r, vs, ss, v[1]);
-    ld4(rs_z, vs, ss, v[2]);
-    ld4(rs_hn, vs, ss, v[3]);
+    if (!BWD_TRECOMP) {
+      ld4(rs_r, vs, ss, v[1]);
+      ld4(rs_z, vs, ss, v[2]);
+      ld4(rs_hn, vs, ss, v[3]);
+    }
   };
   // the rows' inputs x(t) as gate_ain's B fragments (lane = row RB h + col, k = 2 kk + hi): n is recomputed.
   // Tile 0's go out with the first quads, tile 1's beside the ring loads of quad 3.
@@ -1888,6 +1902,53 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     lds_barrier();
     BWD_STAMP(1);
     BWD_WSTAMP(0);
+    floatx16 rc[3][2];   // BWD_TRECOMP: the recomputed r, z, W_hn h (+ b_hn) accumulators
+    if (BWD_TRECOMP) {
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int q = 0; q < 16; ++q) rc[g][h][q] = 0.0f;
+      f16x8 Ra0[3][2], Ra1[3][2], Rb[2][2];
+      const int ln = lane_now(), bl = (ln & 31) * PP + 8 * (ln >> 5);
+      auto ldRB = [&](int ks, int h) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) Rb[h][q] = *reinterpret_cast<const f16x8*>(&dgB[q][bl + RB * h * PP + 16 * ks]);
+      };
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          Ra0[g][q] = ldAh(0, g, q);
+          Ra1[g][q] = ldAh(1, g, q);
+        }
+      ldRB(0, 0);
+      ldRB(0, 1);
+      auto rstep = [&](int ks, f16x8 (&Ar)[3][2], bool reload) {
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            rc[g][h] = mfma3h(Ar[g], Rb[h], rc[g][h]);
+            if (g == 2 && ks + 1 < 16) ldRB(ks + 1, h);
+          }
+          if (reload) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) Ar[g][q] = ldAh(ks + 2, g, q);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      };
+#pragma nounroll
+      for (int kp = 0; kp < 7; ++kp) {
+        rstep(2 * kp, Ra0, true);
+        rstep(2 * kp + 1, Ra1, true);
+      }
+      rstep(14, Ra0, false);
+      rstep(15, Ra1, false);
+      lds_barrier();   // the image read before the memory part's f32 dr staging overwrites it
+    }
     // ---- memory part: the eight unit quads (two row tiles x four) as a software pipeline, quad i+1's five
     // 16-byte loads in flight while quad i is transposed and processed (twice the bytes in flight per wave)
     float dz_r[2][16], dhn_r[2][16];
@@ -1939,13 +2000,16 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         dx4 = 0.0f;
       }
 #pragma unroll
-      for (int a = 0; a < (BWD_TNOTR ? 1 : 4); ++a) quad_transpose(v[a], lane);
+      for (int a = 0; a < (BWD_TNOTR || BWD_TRECOMP ? 1 : 4); ++a) quad_transpose(v[a], lane);
       const float* wil = wi34 + ubn();
       float drq[4], rhq[4], dnq[4];
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int q = 4 * g4 + jj;
-        const float hin = v[0][jj], rg = v[1][jj], zg = v[2][jj], hn = v[3][jj];
+        const float hin = v[0][jj];
+        const float rg = BWD_TRECOMP ? sigm_r(rc[0][h][q] * 0.5f) : v[1][jj];
+        const float zg = BWD_TRECOMP ? sigm_r(rc[1][h][q] * 0.5f) : v[2][jj];
+        const float hn = BWD_TRECOMP ? rc[2][h][q] * 0.5f : v[3][jj];
         const float ng = gate_n(ain[q], rg, hn);
         const float hout = (1.0f - zg) * ng + zg * hin;
         const float d = dh[h][q] + (hout > 0.0f ? hacc[q] : 0.0f);

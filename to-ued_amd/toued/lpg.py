@@ -41,11 +41,15 @@ def layout(F: int) -> "OrderedDict[str, tuple]":
 
 
 class LPGLayout:
-    def __init__(self, F: int):
-        # the model's input width is 5, or 7 with lifetime conditioning; the GRU kernels take 1..7 (the augmented k-step
-        # holds x and the bias row in 8), which the kernel tests use for the edges of the fused small products' A table
-        if not 1 <= F <= 7:
-            raise ValueError(f"LPG input width F={F} (5, or 7 with lifetime conditioning; the kernels take 1..7)")
+    def __init__(self, F: int, kernel_test: bool = False):
+        # the model's input width is 5, or 7 with lifetime conditioning (models/lpg.py:38-85); the GRU kernels take
+        # 1..7 (the augmented k-step holds x and the bias row in 8), which the kernel tests use for the edges of the
+        # fused small products' A table -- only through kernel_test=True, so a wrong width fails on the product path
+        if kernel_test:
+            if not 1 <= F <= 7:
+                raise ValueError(f"LPG input width F={F}: the GRU kernels take 1..7")
+        elif F not in (5, 7):
+            raise ValueError(f"LPG input width F={F}: the model defines 5, or 7 with lifetime conditioning")
         self.F = F
         self.shapes = layout(F)
         self.offsets = {}
