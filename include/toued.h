@@ -325,10 +325,12 @@ size_t toued_gru_packed_floats(int which);
 /* repack eta's GRU weights into MFMA A-fragment order (fwdA / bwdA) */
 int toued_gru_pack(const float* eta, const int* off, int F, float* fwdA, float* bwdA, hipStream_t stream);
 /* forward over R rows x T steps (t = T-1 .. 0, h reset on done); X[f*xs_f + (t*R + r)*xs_col];
- * heads pi_hat [T][R], y_hat [T][8][R]; saves h_in, r, z, n, W_hn h + b_hn for the backward: h_in as [256][M]
- * rows (pointer at this update's first column, row stride M); r, z, W_hn h + b_hn likewise, or -- where
- * toued_gru_slab_saves(R) -- in 32-column slab blocks [M/32][256][32] (element (u, m) at ((m >> 5)*256 + u)*32 +
- * (m & 31); pointer at this update's first block, base + 256 * first column); n only by the f32 kernels (rows) */
+ * heads pi_hat [T][R], y_hat [T][8][R]; saves h_in, r, z, n, W_hn h + b_hn for the backward: as [256][M] rows
+ * (pointer at this update's first column, row stride M) on the f32 kernels, or -- where toued_gru_slab_saves(R) --
+ * h_in in 32-column slab blocks [M/32][256][32] (element (u, m) at ((m >> 5)*256 + u)*32 + (m & 31)) and r, z,
+ * W_hn h + b_hn in 32-column unit-quad blocks [M/32][64][32][4] (element (u, m) at (m >> 5)*8192 + ((u >> 2)*32 +
+ * (m & 31))*4 + (u & 3)); pointers at this update's first block, base + 256 * first column; n only by the f32
+ * kernels (rows) */
 int toued_gru_fwd(int R, int T, int W, int F, const float* X, long xs_f, long xs_col, const uint8_t* done,
                   const float* fwdA, const float* eta, const int* off, float* pi_hat, float* y_hat, float* s_hin,
                   float* s_r, float* s_z, float* s_n, float* s_hn, long M, hipStream_t stream);
@@ -342,10 +344,10 @@ int toued_gru_bwd(int R, int T, int W, int K, const uint8_t* done, long done_str
                   float* DG, float* RH, float* DH, float* dX3, float* dX4, int8_t* col_exp, hipStream_t stream);
 /* 1 when toued_gru_bwd runs its lockstep split-precision kernel for R rows (the one that writes col_exp) */
 int toued_gru_bwd_col_exp(int R);
-/* 1 when the forward and backward for R rows keep r, z, W_hn h + b_hn in 32-column slab blocks (see toued_gru_fwd):
- * the split-precision pair's 1 KB-contiguous loads and stores instead of 128-byte rows */
+/* 1 when the forward and backward for R rows keep r, z, W_hn h + b_hn in 32-column unit-quad blocks (see
+ * toued_gru_fwd): the split-precision pair's 16-byte stores and loads of a lane's four consecutive units */
 int toued_gru_slab_saves(int R);
-/* 1 when those slab blocks include h_in (A's first 256 rows' region; 0 only in HIN_SLAB=0 comparison builds) */
+/* 1 when h_in is in slab blocks (A's first 256 rows' region; 0 only in HIN_SLAB=0 comparison builds) */
 int toued_gru_hin_slab(void);
 /* 1 when toued_gru_bwd_fused applies: the lockstep kernel for R rows and LPG input width F <= 6 */
 int toued_gru_bwd_fused_fits(int R, int F);

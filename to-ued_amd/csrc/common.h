@@ -38,6 +38,23 @@ struct EnvSpec {
 
 // ----------------------------------------------------------------------------
 // threefry2x32-20 (jax/_src/prng.py _threefry2x32_lowering)
+// 4x4 transpose between a lane quad (four consecutive rows: lanes 4i..4i+3) and a register quad (four
+// consecutive units): before, lane row j holds units u0..u0+3; after, lane u0+i's data (for rows j0..j0+3)
+// sits in lane j0+i.  Two DPP quad_perm exchange stages; the transpose is its own inverse.
+TOUED_DEV float dpp_swap(float v, int ctrl_sel) {
+  const int x = __float_as_int(v);
+  return __int_as_float(ctrl_sel == 2 ? __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false)     // [2,3,0,1]
+                                      : __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false));   // [1,0,3,2]
+}
+TOUED_DEV void quad_transpose(float* a, int lane) {
+  const bool b1 = (lane & 2) != 0, b0 = (lane & 1) != 0;
+  float r0 = dpp_swap(b1 ? a[0] : a[2], 2), r1 = dpp_swap(b1 ? a[1] : a[3], 2);
+  if (b1) { a[0] = r0; a[1] = r1; } else { a[2] = r0; a[3] = r1; }
+  r0 = dpp_swap(b0 ? a[0] : a[1], 1);
+  r1 = dpp_swap(b0 ? a[2] : a[3], 1);
+  if (b0) { a[0] = r0; a[2] = r1; } else { a[1] = r0; a[3] = r1; }
+}
+
 TOUED_DEV uint32_t rotl32(uint32_t v, uint32_t r) { return (v << r) | (v >> (32u - r)); }
 
 // Workgroup barrier for LDS-only communication: waits for this wave's LDS (and scalar) accesses and meets the other

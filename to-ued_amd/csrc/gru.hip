@@ -91,22 +91,7 @@ TOUED_DEV void ld4(__amdgpu_buffer_rsrc_t r, unsigned vbyte, unsigned soff, floa
   const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)vbyte, (int)soff, GRU_LD_AUX);
   v[0] = __uint_as_float(x.x); v[1] = __uint_as_float(x.y); v[2] = __uint_as_float(x.z); v[3] = __uint_as_float(x.w);
 }
-// 4x4 transpose between a lane quad (four consecutive rows: lanes 4i..4i+3) and a register quad (four
-// consecutive units): before, lane row j holds units u0..u0+3; after, lane u0+i's data (for rows j0..j0+3)
-// sits in lane j0+i.  Two DPP quad_perm exchange stages; the transpose is its own inverse.
-TOUED_DEV float dpp_swap(float v, int ctrl_sel) {
-  const int x = __float_as_int(v);
-  return __int_as_float(ctrl_sel == 2 ? __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false)     // [2,3,0,1]
-                                      : __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false));   // [1,0,3,2]
-}
-TOUED_DEV void quad_transpose(float* a, int lane) {
-  const bool b1 = (lane & 2) != 0, b0 = (lane & 1) != 0;
-  float r0 = dpp_swap(b1 ? a[0] : a[2], 2), r1 = dpp_swap(b1 ? a[1] : a[3], 2);
-  if (b1) { a[0] = r0; a[1] = r1; } else { a[2] = r0; a[3] = r1; }
-  r0 = dpp_swap(b0 ? a[0] : a[1], 1);
-  r1 = dpp_swap(b0 ? a[2] : a[3], 1);
-  if (b0) { a[0] = r0; a[2] = r1; } else { a[1] = r0; a[3] = r1; }
-}
+// (quad_transpose, the 4x4 lane-quad / register-quad transpose: common.h)
 
 TOUED_DEV float sigm(float x) { return 1.0f / (1.0f + __expf(-x)); }
 // v_rcp_f32 (1 ulp) instead of the IEEE division sequence: the forward's gate maths is on the critical path
@@ -237,20 +222,43 @@ TOUED_DEV void store_gate_lds(const float* buf, __amdgpu_buffer_rsrc_t rs, long 
   }
 }
 
-// The split-precision pair's saves h_in, r, z, W_hn h + b_hn (k_gru_fwd6 / k_gru_fwd6h write them, k_gru_bwd6n reads
-// them; h_in is also the main weight-gradient reduction's A operand, toued_wgrad_bfp_slab layout bit 0) live in
-// 32-column slab blocks, [M / 32][256][32] per array (element (u, c) at ((c >> 5) * 256 + u) * 32 + (c & 31); the
-// forward's pointers at its update's first block; the input rows x that follow h_in stay [F][M] rows): the backward's
-// per-quad loads (eight consecutive units x 32 rows) are then 1 KB of contiguous memory instead of eight 128-byte rows
-// 4 M bytes apart, and a wave's stores fill 4 KB regions (HBM serves 128-byte row segments at ~4.0 TB/s, contiguous
-// KBs at ~5.9: tools/load_probe2.hip).  Byte offsets of unit ub_ + uq, column c0 + 32 h + col_ (c0 a multiple of
-// 32): lane part slab_vbyte, uniform part slab_soff.
+// The split-precision pair's saves (k_gru_fwd6 writes them, k_gru_bwd6n reads them; the forward's pointers at its
+// update's first block; the input rows x that follow h_in stay [F][M] rows):
+//  * h_in -- also the main weight-gradient reduction's A operand (toued_wgrad_bfp_slab layout bit 0) -- in 32-column
+//    slab blocks [M / 32][256][32] (element (u, c) at ((c >> 5) * 256 + u) * 32 + (c & 31)): the reduction's A slab
+//    (256 units x 32 columns) is 32 KB of contiguous memory and each of its 16-byte loads four columns of one unit.
+//    Byte offsets of unit ub_ + uq, column c0 + 32 h + col_ (c0 a multiple of 32): lane part slab_vbyte, uniform part
+//    slab_soff.  The backward loads four rows of one unit per lane and transposes them across a lane quad.
+//  * r, z, W_hn h + b_hn -- read only by the backward -- in 32-column unit-quad blocks [M / 32][64][32][4] (element
+//    (u, c) at (c >> 5) * 8192 + ((u >> 2) * 32 + (c & 31)) * 4 + (u & 3)): a lane of the forward's gate maths and of
+//    the backward's memory part holds four consecutive units (a register quad) of one batch row, so each (array, quad)
+//    is one 16-byte load with no lane transposes (round 6: the backward 7.78 -> 7.35 ms with all four arrays so; the
+//    reduction's A staging then needed a lane-quad transpose per load and lost 3.77 -> 4.15 ms, so h_in stays in
+//    slab blocks).  Byte offsets of register quad g4 of unit base ub_ (a multiple of 4), column c0 + 32 h + col_: lane
+//    part quad_vbyte, uniform part quad_soff.
+// Both keep a wave instruction's accesses in 512-byte or longer contiguous runs (HBM serves 128-byte row segments at
+// ~4.0 TB/s, contiguous KBs at ~5.9: tools/load_probe2.hip).
 // HIN_SLAB=0 (comparison builds): h_in in [256][M] rows (toued_gru_hin_slab() reports it to the host)
 #ifndef HIN_SLAB
 #define HIN_SLAB 1
 #endif
 TOUED_DEV unsigned slab_vbyte(int ub_, int col_) { return (unsigned)(ub_ * 128 + col_ * 4); }
 TOUED_DEV unsigned slab_soff(long c0, int h, int uq) { return (unsigned)(((c0 >> 5) + h) * 32768L + uq * 128); }
+TOUED_DEV unsigned quad_vbyte(int ub_, int col_) { return (unsigned)(((ub_ >> 2) * 32 + col_) * 16); }
+TOUED_DEV unsigned quad_soff(long c0, int h, int g4) { return (unsigned)(((c0 >> 5) + h) * 32768L + g4 * 1024); }
+// 16-byte store of a register quad (the r, z, hn saves).  Two wait states follow it before the scheduler may place
+// anything that rewrites its data registers: on gfx950 a buffer_store_dwordx4 whose data VGPRs the next one or two
+// instructions overwrite stored nondeterministic values (round 6, tools/det_fwd_diff.py: thousands of saved r / z / hn
+// elements differed between identical forwards; the compiler inserts no wait state there).  b64 / b32 stores and
+// b128 followed by s_nop 1 or s_nop 4 were bit-identical over repeated runs; the s_nop 1 form keeps b128's speed
+// (forward 1.166-1.168 ms, b64 pairs 1.218-1.226, profiles/r06/r06t7_ab.log).
+TOUED_DEV void st4(__amdgpu_buffer_rsrc_t r, unsigned vbyte, unsigned soff, const float (&v)[4]) {
+  const u32x4 x = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+  __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)vbyte, (int)soff, GRU_ST_AUX);
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 1");
+  __builtin_amdgcn_sched_barrier(0);
+}
 
 // ------------------------------------------------------------------ forward
 struct FwdArgs {
@@ -928,7 +936,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     for (int h = 0; h < 2; ++h) {
       const int row = RB * h + col;
       const bool dn = dnf[h];
-      const unsigned vslab = slab_vbyte(ub, col);
+      const unsigned vq = quad_vbyte(ub, col), vslab = slab_vbyte(ub, col);
       float hp_loc[9];
 #pragma unroll
       for (int oo = 0; oo < 9; ++oo) hp_loc[oo] = 0.0f;
@@ -939,6 +947,10 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
         const f16x4 h0 = *reinterpret_cast<const f16x4*>(&hB[0][ho]);
         const f16x4 h1 = *reinterpret_cast<const f16x4*>(&hB[1][ho]);
         const bf16x4 hr = *reinterpret_cast<const bf16x4*>(&hB[2][ho]);
+        // the saves of this register quad: h_in (rebuilt exactly from its pieces) per unit in its slab blocks; r, z,
+        // hn one 16-byte store each in their unit-quad blocks (quad_soff) after the gate maths
+        const unsigned sq = quad_soff(cbase + r0, h, g4);
+        float sv[3][4];
         float us[3][4];
 #pragma unroll
         for (int g = 0; g < 3; ++g) {
@@ -957,24 +969,23 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
           const float hin = (((float)h0[e] + (float)h1[e]) + (float)hr[e]) * (1.0f / HSCALE);   // exact
           const float hh = (1.0f - zg) * ng + zg * hin;
           split_carry(dn ? 0.0f : hh, n0, n1, nr, e);   // carry h_in(t-1) = where(d_{t-1}, 0, h_out(t))
-          if (SAVE && FWD_NOSAVE == 1) {
-            // timing study: no saves
-          } else if (SAVE && FWD_NOSAVE == 2) {
-            st_u(rs_hin, vslab, slab_soff(cbase + r0, h, qunit(q)), hin);   // timing study: h_in only
-          } else if (SAVE) {
-            // h_in, r, z, hn in slab blocks (see slab_soff)
-            const unsigned ss = slab_soff(cbase + r0, h, qunit(q));
-            if (HIN_SLAB) st_u(rs_hin, vslab, ss, hin);
+          sv[0][e] = rg;
+          sv[1][e] = zg;
+          sv[2][e] = hn;   // n is recomputed by the backward (gate_n)
+          if (SAVE && FWD_NOSAVE != 1) {   // (FWD_NOSAVE, timing studies only: 1 = no saves, 2 = h_in only)
+            if (HIN_SLAB) st_u(rs_hin, vslab, slab_soff(cbase + r0, h, qunit(q)), hin);
             else st_u(rs_hin, (unsigned)(((long)ub * p.M + r0 + row) * 4), (unsigned)(((long)qunit(q) * p.M + cbase) * 4), hin);
-            st_u(rs_r, vslab, ss, rg);
-            st_u(rs_z, vslab, ss, zg);
-            st_u(rs_hn, vslab, ss, hn);   // n is recomputed by the backward (gate_n)
           }
           const float rl = fmaxf(hh, 0.0f);
           const float4 w0 = whl[qunit(q) * 3], w1 = whl[qunit(q) * 3 + 1], w2 = whl[qunit(q) * 3 + 2];
           hp_loc[0] += rl * w0.x; hp_loc[1] += rl * w0.y; hp_loc[2] += rl * w0.z;
           hp_loc[3] += rl * w0.w; hp_loc[4] += rl * w1.x; hp_loc[5] += rl * w1.y;
           hp_loc[6] += rl * w1.z; hp_loc[7] += rl * w1.w; hp_loc[8] += rl * w2.x;
+        }
+        if (SAVE && FWD_NOSAVE == 0) {   // (FWD_NOSAVE, timing studies only: 1 = no saves, 2 = h_in only)
+          st4(rs_r, vq, sq, sv[0]);
+          st4(rs_z, vq, sq, sv[1]);
+          st4(rs_hn, vq, sq, sv[2]);
         }
         *reinterpret_cast<f16x4*>(&hB[0][ho]) = n0;
         *reinterpret_cast<f16x4*>(&hB[1][ho]) = n1;
@@ -1016,248 +1027,6 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     FWD_STAMP(5);
   }
   if (FWD_HDEFER && wave == 0) head_out(T - 1);   // the last step's heads (its partials visible: the loop's barrier)
-}
-
-// Forward, half-row workgroups (k_gru_fwd6h, the SAVE instance: the meta-gradient's forward).  k_gru_fwd6 runs one
-// 512-thread workgroup of 64 rows per CU, all eight waves in the same phase: the contraction (matrix pipe) and then the
-// gate maths and saves (VALU), so one pipe idles at a time (stamps: 23 k + 24 k cycles of a 47 k step).  Here a
-// 256-thread workgroup holds ONE 32-row tile and wave w owns units [64 w, 64 w + 64) (two unit tiles); two workgroups
-// share a CU, each wave beside a wave of the other workgroup on its SIMD, so one workgroup's gate maths can run in
-// the other's contraction.  The price: each A fragment (L2) now feeds one row tile instead of two (twice the
-// fragment bytes per FLOP).  Same arithmetic as k_gru_fwd6 (the augmented k-step on the f32 MFMA, FWD_AUG32), the
-// same saves, bit-compatible outputs within the forward's tolerance.
-#ifndef FWD_H2
-#define FWD_H2 1
-#endif
-__global__ void __launch_bounds__(256, 2) k_gru_fwd6h(FwdArgs p) {
-  __shared__ __attribute__((aligned(16))) __bf16 hB[3][32 * F6_HP];   // carry image [piece][row][unit]: 50.7 KB
-  __shared__ __attribute__((aligned(16))) float wh[HU * 12];          // head weights [unit][pi | y0..y7 | pad]
-  __shared__ __attribute__((aligned(16))) float usc[3 * HU];          // accumulator unscale 2^-(s + 14) [gate][unit]
-  __shared__ float hp[4 * 9 * 32];      // head partials [wave][output][row]
-  __shared__ float wIs[8 * 4 * 64];     // gate_ain's W_in fragments [unit tile][kk][lane]
-  const int tid = threadIdx.x, lane = tid & 63, hi = lane >> 5, col = lane & 31;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r0 = blockIdx.x * RB;
-  const int R = p.R, T = p.T, W = p.W, F = p.F;
-  const int a_ = r0 / W;                  // (W % 32 == 0: the tile's rows are one agent's workers)
-  const int w_ = r0 + col - a_ * W;
-  const float* eta = p.eta;
-  const float* A6c = reinterpret_cast<const float*>(p.A6);
-  for (int i = tid; i < HU * 12; i += 256) {
-    const int u = i / 12, oo = i - u * 12;
-    wh[i] = oo == 0 ? eta[p.o.pi_w + u] : oo < 9 ? eta[p.o.y_w + u * 8 + (oo - 1)] : 0.0f;
-  }
-  for (int i = tid; i < 3 * HU; i += 256) usc[i] = 1.0f / (A6c[F6_SCALES + i] * HSCALE);   // powers of two: exact
-#pragma unroll
-  for (int ut = 0; ut < 2; ++ut) {
-    float wI[4];
-    load_win_frags(wI, eta, p.o, F, 2 * wave + ut, lane);
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) wIs[((2 * wave + ut) * 4 + kk) * 64 + lane] = wI[kk];
-  }
-  {
-    uint4* z = reinterpret_cast<uint4*>(&hB[0][0]);
-    for (int i = tid; i < 3 * 32 * F6_HP / 8; i += 256) z[i] = make_uint4(0u, 0u, 0u, 0u);
-  }
-  const __amdgpu_buffer_rsrc_t rs_X = rsrc_of(p.X);
-  const __amdgpu_buffer_rsrc_t rs_done = rsrc_of(reinterpret_cast<const float*>(p.done));
-  __syncthreads();
-  const float bpi = eta[p.o.pi_b];
-  const __amdgpu_buffer_rsrc_t rs_A = rsrc_of(A6c);
-  const unsigned vA = (unsigned)lane * 16;
-  auto ldAh = [&](int frag) {
-    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs_A, (int)vA, frag * 1024, 0);
-    return __builtin_bit_cast(f16x8, x);
-  };
-  const __amdgpu_buffer_rsrc_t rs_hin = rsrc_of(p.s_hin), rs_r = rsrc_of(p.s_r), rs_z = rsrc_of(p.s_z),
-                               rs_hn = rsrc_of(p.s_hn);
-  for (int s = 0; s < T; ++s) {
-    const int t = T - 1 - s;
-    floatx16 acc[3][2];   // r, z, W_hn h + b_hn of the wave's two unit tiles
-#pragma unroll
-    for (int g = 0; g < 3; ++g)
-#pragma unroll
-      for (int ut = 0; ut < 2; ++ut)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[g][ut][q] = 0.0f;
-    // this lane's row inputs x(t) (the augmented k-step's B and gate_ain's)
-    float xv[7];
-#pragma unroll
-    for (int f = 0; f < 7; ++f) {
-      const int fc = f < F ? f : F - 1;
-      xv[f] = ld_u(rs_X, (unsigned)(col * p.xs_col * 4), (unsigned)((fc * p.xs_f + ((long)t * R + r0) * p.xs_col) * 4));
-    }
-    // A fragments (unit tile U = 2 wave + ut): FWD_H2_RING k-steps in flight (1: each fragment reloaded for the next
-    // k-step right after its MFMAs; the other workgroup's waves on the SIMD cover the latency); B (the carry, one row
-    // tile) double-buffered
-#ifndef FWD_H2_RING
-#define FWD_H2_RING 1
-#endif
-    f16x8 A0[3][2][2], A1[FWD_H2_RING == 2 ? 3 : 1][2][2], B[2][2];
-    auto fragA = [&](int ks, int g, int ut, int q) { return ((ks * 8 + 2 * wave + ut) * 3 + g) * 2 + q; };
-    auto load_B = [&](int ks, f16x8 (&b)[2]) {
-#pragma unroll
-      for (int q = 0; q < 2; ++q) b[q] = *reinterpret_cast<const f16x8*>(&hB[q][col * F6_HP + 16 * ks + 8 * hi]);
-    };
-    constexpr int RD = FWD_H2_RING;
-    auto slot = [&](int ks) -> f16x8 (&)[3][2][2] {
-      return (RD == 2 && (ks & 1)) ? reinterpret_cast<f16x8 (&)[3][2][2]>(A1) : A0;
-    };
-#pragma unroll
-    for (int g = 0; g < 3; ++g)
-#pragma unroll
-      for (int ut = 0; ut < 2; ++ut)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          A0[g][ut][q] = ldAh(fragA(0, g, ut, q));
-          if (RD == 2) reinterpret_cast<f16x8 (&)[3][2][2]>(A1)[g][ut][q] = ldAh(fragA(1, g, ut, q));
-        }
-    load_B(0, B[0]);
-    auto kstep = [&](int ks, f16x8 (&Ar)[3][2][2], f16x8 (&Bc)[2], f16x8 (&Bn)[2], bool reload) {
-#pragma unroll
-      for (int g = 0; g < 3; ++g) {
-#pragma unroll
-        for (int ut = 0; ut < 2; ++ut) {
-          acc[g][ut] = mfma3h(Ar[g][ut], Bc, acc[g][ut]);
-          if (reload) {
-#pragma unroll
-            for (int q = 0; q < 2; ++q) Ar[g][ut][q] = ldAh(fragA(ks + RD, g, ut, q));
-          }
-        }
-        if (g == 0 && ks + 1 < 16) load_B(ks + 1, Bn);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    };
-    // (rolled over k-step pairs: the ring slots and B buffers stay named statically)
-#pragma nounroll
-    for (int kp = 0; kp < 7; ++kp) {
-      kstep(2 * kp, slot(0), B[0], B[1], true);
-      kstep(2 * kp + 1, slot(1), B[1], B[0], 2 * kp + 1 + RD < 16);
-    }
-    kstep(14, slot(0), B[0], B[1], 14 + RD < 16);
-    f16x8 (&A1r)[3][2][2] = slot(1);   // k-step 15
-    {
-      // k-step 15, then the augmented k-step on the f32 MFMA (exact products): A = the scaled input weights and
-      // biases (one 16-byte fragment per gate and unit tile), B = 2^14 [x_k (k < F), 1 (k = 7)]
-      float4 a32[3][2];
-#pragma unroll
-      for (int g = 0; g < 3; ++g)
-#pragma unroll
-        for (int ut = 0; ut < 2; ++ut)
-          a32[g][ut] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                      rs_A, (int)vA, (F6_A32 + ((2 * wave + ut) * 3 + g) * 256) * 4, 0));
-#pragma unroll
-      for (int g = 0; g < 3; ++g) {
-#pragma unroll
-        for (int ut = 0; ut < 2; ++ut) acc[g][ut] = mfma3h(A1r[g][ut], B[1], acc[g][ut]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const int k = 2 * kk + hi;
-        const float bx = (k < F ? xv[k < 7 ? k : 6] : (k == 7 ? 1.0f : 0.0f)) * HSCALE;
-#pragma unroll
-        for (int g = 0; g < 3; ++g)
-#pragma unroll
-          for (int ut = 0; ut < 2; ++ut) {
-            const float av = kk == 0 ? a32[g][ut].x : kk == 1 ? a32[g][ut].y : kk == 2 ? a32[g][ut].z : a32[g][ut].w;
-            acc[g][ut] = mfma32(av, bx, acc[g][ut]);
-          }
-      }
-    }
-    lds_barrier();   // every wave done reading hB: the carry overwrites it in place
-    // ---- gate maths (lane = row col, register q = unit 32 U + 4 hi + qunit(q))
-    const bool dn = (t >= 1) ? __builtin_amdgcn_raw_buffer_load_b8(
-                                   rs_done, lane_now() & 31, (int)(((long)a_ * T + (t - 1)) * W + r0 - a_ * W), 0) != 0
-                             : false;
-    const long cbase = (long)t * R;
-#pragma unroll
-    for (int ut = 0; ut < 2; ++ut) {
-      const int U = 2 * wave + ut;
-      float hp_loc[9];
-#pragma unroll
-      for (int oo = 0; oo < 9; ++oo) hp_loc[oo] = 0.0f;
-      float wI[4];
-      {
-        const int ln = lane_now();
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) wI[kk] = wIs[(U * 4 + kk) * 64 + ln];
-      }
-      const floatx16 ain = gate_ain(wI, F, hi, [&](int k) { return xv[k < 7 ? k : 6]; });
-      const int ub = 32 * U + 4 * hi;
-      const float4* whl = reinterpret_cast<const float4*>(wh + ub * 12);
-      const unsigned vslab = slab_vbyte(ub, col);
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int ho = col * F6_HP + ub + 8 * g4;
-        const f16x4 h0 = *reinterpret_cast<const f16x4*>(&hB[0][ho]);
-        const f16x4 h1 = *reinterpret_cast<const f16x4*>(&hB[1][ho]);
-        const bf16x4 hr = *reinterpret_cast<const bf16x4*>(&hB[2][ho]);
-        float us[3][4];
-#pragma unroll
-        for (int g = 0; g < 3; ++g) {
-          const float4 v = *reinterpret_cast<const float4*>(&usc[g * HU + ub + 8 * g4]);
-          us[g][0] = v.x; us[g][1] = v.y; us[g][2] = v.z; us[g][3] = v.w;
-        }
-        f16x4 n0, n1;
-        bf16x4 nr;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int q = 4 * g4 + e;
-          const float rg = sigm_r(acc[0][ut][q] * us[0][e]);
-          const float zg = sigm_r(acc[1][ut][q] * us[1][e]);
-          const float hn = acc[2][ut][q] * us[2][e];
-          const float ng = gate_n(ain[q], rg, hn);
-          const float hin = (((float)h0[e] + (float)h1[e]) + (float)hr[e]) * (1.0f / HSCALE);   // exact
-          const float hh = (1.0f - zg) * ng + zg * hin;
-          split_carry(dn ? 0.0f : hh, n0, n1, nr, e);   // carry h_in(t-1) = where(d_{t-1}, 0, h_out(t))
-          const unsigned ss = slab_soff(cbase + r0, 0, qunit(q));   // h_in, r, z, hn in slab blocks
-          if (HIN_SLAB) st_u(rs_hin, vslab, ss, hin);
-          else st_u(rs_hin, (unsigned)(((long)ub * p.M + r0 + col) * 4), (unsigned)(((long)qunit(q) * p.M + cbase) * 4), hin);
-          st_u(rs_r, vslab, ss, rg);
-          st_u(rs_z, vslab, ss, zg);
-          st_u(rs_hn, vslab, ss, hn);   // n is recomputed by the backward (gate_n)
-          const float rl = fmaxf(hh, 0.0f);
-          const float4 w0 = whl[qunit(q) * 3], w1 = whl[qunit(q) * 3 + 1], w2 = whl[qunit(q) * 3 + 2];
-          hp_loc[0] += rl * w0.x; hp_loc[1] += rl * w0.y; hp_loc[2] += rl * w0.z;
-          hp_loc[3] += rl * w0.w; hp_loc[4] += rl * w1.x; hp_loc[5] += rl * w1.y;
-          hp_loc[6] += rl * w1.z; hp_loc[7] += rl * w1.w; hp_loc[8] += rl * w2.x;
-        }
-        *reinterpret_cast<f16x4*>(&hB[0][ho]) = n0;
-        *reinterpret_cast<f16x4*>(&hB[1][ho]) = n1;
-        *reinterpret_cast<bf16x4*>(&hB[2][ho]) = nr;
-      }
-      // lanes l and l + 32 hold the same row: fold the two halves; the second unit tile adds onto the first's (the
-      // same lane wrote it)
-#pragma unroll
-      for (int oo = 0; oo < 9; ++oo) {
-        const float o = __shfl_xor(hp_loc[oo], 32);
-        float* hq = &hp[(wave * 9 + oo) * 32 + lane_now()];
-        if (hi == 0) *hq = ut == 0 ? hp_loc[oo] + o : *hq + (hp_loc[oo] + o);
-      }
-    }
-    lds_barrier();   // head partials and the carry visible
-    if (tid < 32) {
-      const int tl = lane_now();   // == tid (wave 0)
-      float hv[9];
-#pragma unroll
-      for (int oo = 0; oo < 9; ++oo) {
-        float v = oo == 0 ? bpi : eta[p.o.y_b + oo - 1];
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) v += hp[(gq * 9 + oo) * 32 + tl];
-        hv[oo] = v;
-      }
-      const long ob = (long)t * R + r0 + tl;
-      p.pi_hat[ob] = hv[0];
-      float m = -__builtin_inff();
-      for (int j = 0; j < 8; ++j) m = fmaxf(m, hv[j + 1]);
-      float e[8], ssum = 0.0f;
-      for (int j = 0; j < 8; ++j) { e[j] = __expf(hv[j + 1] - m); ssum += e[j]; }
-      const float inv = 1.0f / ssum;
-      for (int j = 0; j < 8; ++j) p.y_hat[((long)t * 8 + j) * R + r0 + tl] = e[j] * inv;
-    }
-  }
-  (void)w_;
 }
 
 // ------------------------------------------------------------------ backward
@@ -1521,9 +1290,6 @@ __device__ int g_bwd_wsimd[64 * 8];
 //     reduction: see small_mfma below.
 #ifndef BWD_MPRIO
 #define BWD_MPRIO 0
-#endif
-#ifndef BWD_TNOTR
-#define BWD_TNOTR 0   // timing study only (wrong results): r, z, hn used without their lane-quad transposes
 #endif
 // BWD_TRECOMP (timing study only, wrong results): the gate pre-activations W_hr h, W_hz h and
 // W_hn h recomputed on the matrix pipe at the top of every step (the forward's 16 carry k-steps: 3 gates x 2 row tiles
@@ -1850,15 +1616,18 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   const int ub = 32 * wave + 4 * hi;               // lane's unit base (register q adds qunit(q))
   float vr[NR][4][4];   // NR-slot ring: quads i+1 .. i+NR-1 in flight while quad i is processed (NR = 2: 10.11 ms)
   auto load_q = [&](long ctr_, int h, int g4, float (&v)[4][4]) {
-    // h_in, r, z, hn from their slab blocks (slab_soff): eight consecutive units x 32 rows, 1 KB contiguous
-    const unsigned vs = slab_vbyte(ub + (col & 3), col & 28), ss = slab_soff(ctr_ + r0, h, 8 * g4);
-    if (HIN_SLAB) ld4(rs_hin, vs, ss, v[0]);
+    // r, z, hn of the lane's register quad g4 (its row, four consecutive units) from their unit-quad blocks
+    // (quad_soff): one 16-byte load each; h_in from its slab blocks (slab_soff): four rows of unit ub + (col & 3) +
+    // 8 g4 per lane (eight consecutive units x 32 rows, 1 KB contiguous per wave instruction), lane-quad transposed
+    // in the memory part
+    const unsigned vq = quad_vbyte(ub, col), sq = quad_soff(ctr_ + r0, h, g4);
+    if (HIN_SLAB) ld4(rs_hin, slab_vbyte(ub + (col & 3), col & 28), slab_soff(ctr_ + r0, h, 8 * g4), v[0]);
     else ld4(rs_hin, (unsigned)((((long)(ub + (col & 3))) * p.M + r0 + RB * h + (col & 28)) * 4),
              (unsigned)(((long)8 * g4 * p.M + ctr_) * 4), v[0]);
     if (!BWD_TRECOMP) {
-      ld4(rs_r, vs, ss, v[1]);
-      ld4(rs_z, vs, ss, v[2]);
-      ld4(rs_hn, vs, ss, v[3]);
+      ld4(rs_r, vq, sq, v[1]);
+      ld4(rs_z, vq, sq, v[2]);
+      ld4(rs_hn, vq, sq, v[3]);
     }
   };
   // the rows' inputs x(t) as gate_ain's B fragments (lane = row RB h + col, k = 2 kk + hi): n is recomputed.
@@ -1999,8 +1768,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
         dx3 = 0.0f;
         dx4 = 0.0f;
       }
-#pragma unroll
-      for (int a = 0; a < (BWD_TNOTR || BWD_TRECOMP ? 1 : 4); ++a) quad_transpose(v[a], lane);
+      quad_transpose(v[0], lane);   // h_in: four rows of one unit -> four units of the lane's row
       const float* wil = wi34 + ubn();
       float drq[4], rhq[4], dnq[4];
 #pragma unroll
@@ -2352,11 +2120,9 @@ static int gru_fwd_launch(int R, int T, int W, int F, const float* X, long xs_f,
   // two row tiles per workgroup when the rows (and, for per-candidate parameters, each candidate's rows)
   // split into 64-row blocks
   const bool nt2 = R % (2 * RB) == 0 && (rpc == 0 || rpc % (2 * RB) == 0);
-  // the SAVE instance as two 32-row workgroups per CU (k_gru_fwd6h, TOUED_FWD_H2=1) or one 64-row workgroup
-  static const bool h2 = FWD_H2 && getenv("TOUED_FWD_H2") && getenv("TOUED_FWD_H2")[0] == '1';
-  if (save && h2 && nt2 && !gru_f32_forced()) {   // (the f32 fallback pair below keeps its own saves, n included)
-    hipLaunchKernelGGL(k_gru_fwd6h, dim3(R / RB), dim3(256), 0, stream, p);
-  } else if (nt2 && !gru_f32_forced()) {
+  // (round 5's k_gru_fwd6h, the SAVE instance as two 32-row workgroups per CU, measured 1.24 vs 1.18 ms and was
+  // removed in round 6; the f32 fallback pair below keeps its own saves, n included)
+  if (nt2 && !gru_f32_forced()) {
     if (save) hipLaunchKernelGGL(k_gru_fwd6<true>, dim3(R / (2 * RB)), dim3(512), 0, stream, p);
     else hipLaunchKernelGGL(k_gru_fwd6<false>, dim3(R / (2 * RB)), dim3(512), 0, stream, p);
   } else if (save) {

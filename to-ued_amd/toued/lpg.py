@@ -140,6 +140,12 @@ def init_lpg_params(seed: int, F: int, device=None) -> torch.Tensor:
     return torch.from_numpy(flat).to(dev)
 
 
+def quad_blocks_to_rows(flat: torch.Tensor, M: int) -> torch.Tensor:
+    """[256][M] rows of an array in 32-column unit-quad blocks [M/32][64][32][4] (the split-precision GRU pair's saves:
+    element (u, m) at (m >> 5) * 8192 + ((u >> 2) * 32 + (m & 31)) * 4 + (u & 3), gru.hip quad_soff)."""
+    return flat.view(M // 32, 64, 32, 4).permute(1, 3, 0, 2).reshape(256, M)
+
+
 class LPGGRU:
     """MFMA GRU forward/backward over K x R rows (csrc/gru.hip) with saved activations.
 
@@ -163,8 +169,9 @@ class LPGGRU:
         self.A[H + lay.F].fill_(1.0)
         self.X = self.A[H:H + lay.F].view(lay.F, K, T, R)
         self.S = torch.empty((4, H, M), dtype=f32, device=dev)          # r, z, n (f32 fallback only), hn
-        # the split-precision pair keeps h_in (A's first 256 rows' region) and r, z, hn in 32-column slab blocks
-        # [M/32][256][32] (hin_rows(), a_rows(), s_rows() give rows); A's rows 256.. (x, ones) stay rows
+        # the split-precision pair keeps h_in (A's first 256 rows' region) in 32-column slab blocks [M/32][256][32] and
+        # r, z, hn in 32-column unit-quad blocks [M/32][64][32][4] (gru.hip slab_soff / quad_soff; hin_rows(),
+        # a_rows(), s_rows() give rows); A's rows 256.. (x, ones) stay rows
         self.slab = bool(L.toued_gru_slab_saves(R))
         self.hin_slab = self.slab and bool(L.toued_gru_hin_slab())
         # the small weight-gradient products fused into the backward (toued_gru_bwd_fused) where the lockstep kernel
@@ -221,11 +228,10 @@ class LPGGRU:
         return self.A.view(-1)[256 * c0:256 * (c0 + n)] if self.hin_slab else self.A[:256, c0:c0 + n]
 
     def s_rows(self, i: int):
-        """Saved array i (0 r, 1 z, 2 n, 3 hn) as [256][M] rows (a copy of its slab blocks for r, z, hn)."""
+        """Saved array i (0 r, 1 z, 2 n, 3 hn) as [256][M] rows (a copy of its unit-quad blocks for r, z, hn)."""
         if not self.slab or i == 2:
             return self.S[i]
-        H, M = self.S.shape[1], self.S.shape[2]
-        return self.S[i].view(M // 32, H, 32).permute(1, 0, 2).reshape(H, M)
+        return quad_blocks_to_rows(self.S[i].reshape(-1), self.S.shape[2])
 
     def dg_rows(self):
         """The gate cotangents as [gates][256][M] rows: DG itself (unfused), or a row-major copy of the fused
