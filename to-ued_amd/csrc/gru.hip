@@ -87,6 +87,7 @@ TOUED_DEV int qunit(int q) { return (q & 3) + 8 * (q >> 2); }
 
 // 16-byte raw buffer ops: the four consecutive units (q & 3) of a register quad in the m-major layout
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));   // packed FP32 pairs (v_pk_*_f32)
 TOUED_DEV void ld4(__amdgpu_buffer_rsrc_t r, unsigned vbyte, unsigned soff, float* v) {
   const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)vbyte, (int)soff, GRU_LD_AUX);
   v[0] = __uint_as_float(x.x); v[1] = __uint_as_float(x.y); v[2] = __uint_as_float(x.z); v[3] = __uint_as_float(x.w);
@@ -1298,6 +1299,12 @@ __device__ int g_bwd_wsimd[64 * 8];
 #ifndef BWD_TRECOMP
 #define BWD_TRECOMP 0
 #endif
+// BWD_PK: the memory part's per-element gate maths on element pairs (packed FP32: v_pk_{add,mul,fma}_f32, two
+// elements per instruction; 350 fewer VALU instructions in the kernel, k_gru_bwd6n 7.42 -> 7.27-7.34 ms, round 6
+// profiles/r06/r06t12_ab.log; the same head-partial pairing in the forward measured no gain and was dropped)
+#ifndef BWD_PK
+#define BWD_PK 1
+#endif
 template <bool SMALL>
 __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
   constexpr int RBT = 2 * RB;
@@ -1333,7 +1340,9 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
     g_bwd_wsimd[blockIdx.x * 8 + wave] = __builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4);   // HW_ID SIMD_ID
 #endif
   for (int i = tid; i < 2 * 3 * HU; i += 512) {
-    const int f = 3 + i / (3 * HU), g = (i / HU) % 3, u = i % HU;
+    // BWD_PK: [gate][unit] pairs (input 3, input 4) for the packed dX3 / dX4 accumulation; else [input][gate][unit]
+    const int f = BWD_PK ? 3 + (i & 1) : 3 + i / (3 * HU), g = BWD_PK ? (i >> 1) / HU : (i / HU) % 3,
+              u = BWD_PK ? (i >> 1) % HU : i % HU;
     const int base = g == 0 ? p.o.ir_w : g == 1 ? p.o.iz_w : p.o.in_w;
     wi34[i] = f < p.F ? p.eta[base + f * HU + u] : 0.0f;   // (inputs 3, 4 exist when F >= 5)
   }
@@ -1771,8 +1780,46 @@ __global__ void __launch_bounds__(512, 1) k_gru_bwd6n(BwdArgs p) {
       quad_transpose(v[0], lane);   // h_in: four rows of one unit -> four units of the lane's row
       const float* wil = wi34 + ubn();
       float drq[4], rhq[4], dnq[4];
+      if (BWD_PK) {
+        // the same gate maths on element pairs: v_pk_{add,mul,fma}_f32 carry two elements per instruction (the
+        // transcendentals and selects stay per element)
+        const f2v* wil2 = reinterpret_cast<const f2v*>(wi34) + ubn();
+        f2v dx34 = {dx3, dx4};
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
+        for (int pp = 0; pp < 2; ++pp) {
+          const int j0 = 2 * pp, q0 = 4 * g4 + j0;
+          const f2v hin = {v[0][j0], v[0][j0 + 1]}, rg = {v[1][j0], v[1][j0 + 1]}, zg = {v[2][j0], v[2][j0 + 1]},
+                    hn = {v[3][j0], v[3][j0 + 1]};
+          const f2v ng = {gate_n(ain[q0], rg.x, hn.x), gate_n(ain[q0 + 1], rg.y, hn.y)};
+          const f2v omz = 1.0f - zg;
+          const f2v hout = omz * ng + zg * hin;
+          const f2v hac = {hout.x > 0.0f ? hacc[q0] : 0.0f, hout.y > 0.0f ? hacc[q0 + 1] : 0.0f};
+          const f2v d = f2v{dh[h][q0], dh[h][q0 + 1]} + hac;
+          const f2v dn_ = d * omz;
+          const f2v dz = d * (hin - ng);
+          const f2v dnp = dn_ * (1.0f - ng * ng);
+          const f2v dhn = dnp * rg;
+          const f2v drp = dnp * hn * rg * (1.0f - rg);
+          const f2v dzp = dz * zg * omz;
+          const f2v dhv = d * zg;   // direct path; the W_h^T contraction accumulates onto it below
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int q = q0 + e, qu = qunit(q);
+            dh[h][q] = dhv[e];
+            drq[j0 + e] = drp[e];
+            dz_r[h][q] = dzp[e];
+            dhn_r[h][q] = dhn[e];
+            rhq[j0 + e] = fmaxf(hout[e], 0.0f);
+            dnq[j0 + e] = dnp[e];
+            dx34 += f2v{drp[e], drp[e]} * wil2[0 * HU + qu] + f2v{dzp[e], dzp[e]} * wil2[1 * HU + qu] +
+                    f2v{dnp[e], dnp[e]} * wil2[2 * HU + qu];
+          }
+        }
+        dx3 = dx34.x;
+        dx4 = dx34.y;
+      }
+#pragma unroll
+      for (int jj = 0; jj < (BWD_PK ? 0 : 4); ++jj) {
         const int q = 4 * g4 + jj;
         const float hin = v[0][jj];
         const float rg = BWD_TRECOMP ? sigm_r(rc[0][h][q] * 0.5f) : v[1][jj];

@@ -454,6 +454,10 @@ class MetaGradStep:
                 ea["cum"] = self.ro.eval_returns_from_draws(self._ea_draws, th[K], agents.levels,
                                                             ea["state"])
             main.wait_event(ea["draws_done"])
+            if os.environ.get("TOUED_EVAL_ALONE") == "1":
+                # timing study: the env chain alone, the main reduction after it on every CU (bit-identical)
+                main.wait_stream(self.side)
+                return
             L.lib().toued_set_reserved_cus(eval_cus)
         if eval_keys_early() and "draws_done" not in ea:
             # eval_agent's reset, key chain and draws beside the reverse agent loop (latency-bound per-agent kernels)
