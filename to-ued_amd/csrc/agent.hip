@@ -41,7 +41,7 @@ TOUED_DEV void probs_of(const float* __restrict__ tab, const float* __restrict__
   float m = -__builtin_inff();
 #pragma unroll
   for (int j = 0; j < K; ++j) {
-    l[j] = tab[(size_t)idx * K + j] + c * last[j];
+    l[j] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(tab) + ((unsigned)idx * K + j) * 4u) + c * last[j];
     m = fmaxf(m, l[j]);
   }
   float s = 0.0f;
@@ -53,6 +53,21 @@ TOUED_DEV void probs_of(const float* __restrict__ tab, const float* __restrict__
   const float inv = 1.0f / s;
 #pragma unroll
   for (int j = 0; j < K; ++j) p[j] *= inv;
+}
+
+// base[elem] with a 32-bit byte offset: a load (or store) off a uniform base pointer takes the scalar-base form
+// (one offset register, no 64-bit address pair per table)
+template <class T>
+TOUED_DEV T ld32(const T* base, unsigned elem) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + elem * (unsigned)sizeof(T));
+}
+// element j of the row at byte offset rowb from base (j in the instruction's immediate offset)
+TOUED_DEV float ldrow(const float* base, unsigned rowb, int j) {
+  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + rowb + j * 4);
+}
+template <class T>
+TOUED_DEV void st32(T* base, unsigned elem, T v) {
+  *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + elem * (unsigned)sizeof(T)) = v;
 }
 
 // Scatter a K-vector d into rows idx and D-1 (times c) of a dense per-agent table.
@@ -523,6 +538,58 @@ TOUED_DEV void entropy_metric_agent(int a, int tid, int W, int T, int D, const f
       for (int j = 0; j < 5; ++j) ha -= (p[j] + EPSF) * __logf(p[j] + EPSF);
 #pragma unroll
       for (int j = 0; j < 8; ++j) hc -= (y[j] + EPSF) * __logf(y[j] + EPSF);
+    }
+    ha = wave_sum(ha);
+    hc = wave_sum(hc);
+    if ((tid & 63) == 0) { red[0][tid >> 6] = ha; red[1][tid >> 6] = hc; }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    met[a * 8 + 3] += (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    met[a * 8 + 4] += (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  }
+}
+
+// entropy_metric_agent for a 512-thread block with T*W * 13 floats of LDS (`terms`): all 512 threads compute the
+// samples' 13 entropy terms (p + eps) log(p + eps) into LDS, then the same 256 threads as entropy_metric_agent
+// subtract them in the same order -- the same values and sums, with half the dependent gathers per thread
+TOUED_DEV void entropy_metric_block(int a, int tid, int W, int T, int D, const float* __restrict__ theta,
+                                    const float* __restrict__ phi, const int* __restrict__ tidx,
+                                    const int* __restrict__ ttime, float* __restrict__ met, float (*red)[4],
+                                    float* terms) {
+  const int TW = T * W;
+  {
+    const float* th = theta + (size_t)a * D * 5;
+    const float* ph = phi + (size_t)a * D * 8;
+    float lastA[5], lastC[8];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
+    const int* ti = tidx + (size_t)a * (T + 1) * W;   // sample i = t W + w
+    const int* tt = ttime + (size_t)a * (T + 1) * W;
+    for (int i = tid; i < TW; i += 512) {
+      const int idx = ld32(ti, (unsigned)i);
+      const float c = (float)ld32(tt, (unsigned)i) * 0.001f;
+      float p[5], y[8];
+      probs_of<5>(th, lastA, idx, c, p);
+      probs_of<8>(ph, lastC, idx, c, y);
+      float* e = terms + (size_t)i * 13;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) e[j] = (p[j] + EPSF) * __logf(p[j] + EPSF);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) e[5 + j] = (y[j] + EPSF) * __logf(y[j] + EPSF);
+    }
+  }
+  __syncthreads();
+  if (tid < 256) {
+    float ha = 0.0f, hc = 0.0f;
+    for (int i = tid; i < TW; i += 256) {
+      const float* e = terms + (size_t)i * 13;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) ha -= e[j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) hc -= e[5 + j];
     }
     ha = wave_sum(ha);
     hc = wave_sum(hc);
@@ -1299,18 +1366,19 @@ struct GradOp {   // k_agent_grad (+ the global norms and the lifetime test of t
   const uint8_t* tdone; const float* pi_hat; const float* y_hat; float alpha_y; float* Gth; float* Gph; float* met;
   const int* step; const int* levels; float* gstat;
   int N, W, T, D;
-  TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* v, float* m) const {
+  static constexpr int NLAST = 13;   // the time rows theta[D-1], phi[D-1]: the same for every sample of the agent
+  TOUED_DEV float last_val(int a, int i) const {
+    return i < 5 ? theta[((size_t)a * D + D - 1) * 5 + i] : phi[((size_t)a * D + D - 1) * 8 + (i - 5)];
+  }
+  TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* v, float* m, const float* lastv) const {
     const long s = ((long)a * T + t) * W + w;
     const SampleRef q = load_sample(s, T, W, tidx, ttime, tact, trew, tdone, true);
     const int R = N * W;
     const float inv_wt = 1.0f / (float)(W * T);
     const float* th = theta + (size_t)a * D * 5;
     const float* ph = phi + (size_t)a * D * 8;
-    float lastA[5], lastC[8];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
+    const float* lastA = lastv;
+    const float* lastC = lastv + 5;
     float p[5], y[8], yh[8];
     probs_of<5>(th, lastA, q.idx, q.c, p);
     probs_of<8>(ph, lastC, q.idx, q.c, y);
@@ -1368,6 +1436,11 @@ struct GradStepOp : GradApplyOp {
 struct GradStepEntOp : GradStepOp {
   static constexpr bool ENTROPY_AFTER = true;
 };
+// ops whose sample is register-heavy accumulate the time row's partial sums after the sample loop (HvpOp)
+template <class Op, class = void>
+struct defer_time_row : std::false_type {};
+template <class Op>
+struct defer_time_row<Op, std::void_t<decltype(Op::DEFER_TIME_ROW)>> : std::bool_constant<Op::DEFER_TIME_ROW> {};
 template <class Op, class = void>
 struct entropy_after : std::false_type {};
 template <class Op>
@@ -1379,17 +1452,18 @@ struct EntropyBwdOp {   // k_entropy, gradient mode
   const float* theta; const float* phi; const int* tidx; const int* ttime; float coef_a, coef_c;
   float* adj_th; float* adj_ph;
   int N, W, T, D;
-  TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* v, float* m) const {
+  static constexpr int NLAST = 13;   // the time rows theta[D-1], phi[D-1]: the same for every sample of the agent
+  TOUED_DEV float last_val(int a, int i) const {
+    return i < 5 ? theta[((size_t)a * D + D - 1) * 5 + i] : phi[((size_t)a * D + D - 1) * 8 + (i - 5)];
+  }
+  TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* v, float* m, const float* lastv) const {
     const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
     idx = tidx[o0];
     c = (float)ttime[o0] * 0.001f;
     const float* th = theta + (size_t)a * D * 5;
     const float* ph = phi + (size_t)a * D * 8;
-    float lastA[5], lastC[8];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
+    const float* lastA = lastv;
+    const float* lastC = lastv + 5;
     float p[5], y[8];
     probs_of<5>(th, lastA, idx, c, p);
     probs_of<8>(ph, lastC, idx, c, y);
@@ -1433,15 +1507,15 @@ struct LpgLossOp {   // k_lpgloss_grad
   static constexpr bool NORMS = false, APPLY = false, WRITE_G = false, CLIPDOT = false;
   const float* theta; const int* tidx; const int* ttime; const uint8_t* tact; const float* abar; float* adj_th;
   int N, W, T, D;
-  TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* v, float* m) const {
+  static constexpr int NLAST = 5;   // the time row theta[D-1]
+  TOUED_DEV float last_val(int a, int i) const { return theta[((size_t)a * D + D - 1) * 5 + i]; }
+  TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* v, float* m, const float* lastv) const {
     const long s = ((long)a * T + t) * W + w;
     const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
     idx = tidx[o0];
     c = (float)ttime[o0] * 0.001f;
     const float* th = theta + (size_t)a * D * 5;
-    float lastA[5];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
+    const float* lastA = lastv;
     float p[5];
     probs_of<5>(th, lastA, idx, c, p);
     const int act = tact[s];
@@ -1462,50 +1536,60 @@ struct LpgLossOp {   // k_lpgloss_grad
 };
 
 struct HvpOp {   // k_hvp
-  static constexpr int NA = 5, NC = 8, NM = 1;
+  static constexpr int NA = 5, NC = 8, NM = 0;   // (no metrics)
+  static constexpr bool DEFER_TIME_ROW = true;
   static constexpr bool NORMS = false, APPLY = false, WRITE_G = false, CLIPDOT = false;
   const float* theta; const float* phi; const int* tidx; const int* ttime; const uint8_t* tact;
   const float* pi_hat; const float* y_hat; const float* Gth; const float* Gph; const float* adj_th_in;
   const float* adj_ph_in; const float* coef; float lr_a, lr_c, alpha_y, b2, b3;
   float* adj_th_out; float* adj_ph_out; float* d_pi_hat; float* d_y_hat;
   int N, W, T, D, K;
-  TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* vout, float* m) const {
-    m[0] = 0.0f;
-    const long s = ((long)a * T + t) * W + w;
-    const int R = N * W, r = a * W + w;
+  // per-agent values every sample reads: theta[D-1] (0..4), phi[D-1] (5..12), adj_th_in[D-1] (13..17),
+  // Gth[D-1] (18..22), adj_ph_in[D-1] (23..30), Gph[D-1] (31..38), coef[a] (39..42)
+  static constexpr int NLAST = 43;
+  TOUED_DEV float last_val(int a, int i) const {
+    const size_t rA = ((size_t)a * D + D - 1) * 5, rC = ((size_t)a * D + D - 1) * 8;
+    if (i < 5) return theta[rA + i];
+    if (i < 13) return phi[rC + (i - 5)];
+    if (i < 18) return adj_th_in[rA + (i - 13)];
+    if (i < 23) return Gth[rA + (i - 18)];
+    if (i < 31) return adj_ph_in[rC + (i - 23)];
+    if (i < 39) return Gph[rC + (i - 31)];
+    return coef[a * 4 + (i - 39)];
+  }
+  // The sample's loads go through per-agent base pointers (uniform in the block: scalar registers) plus 32-bit
+  // element offsets, so every gather is a scalar-base load with one offset register per table shape instead of a
+  // 64-bit address pair per table (toued_hvp / toued_entropy_clip_hvp check that the offsets fit)
+  TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* vout, float* m, const float* lastv) const {
+    const unsigned R = (unsigned)(N * W), tw = (unsigned)(t * W + w), tr = (unsigned)t * R + (unsigned)w;
     const float inv_wt = 1.0f / (float)(W * T);
-    const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
-    idx = tidx[o0];
-    c = (float)ttime[o0] * 0.001f;
-    const int act = tact[s];
-    const size_t o = (size_t)t * R + r;
-    const float pih = pi_hat[o];
-    float yh[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) yh[j] = y_hat[((size_t)t * 8 + j) * R + r];
+    const size_t oa = (size_t)a * (T + 1) * W, ow = (size_t)a * W;
+    idx = ld32(tidx + oa, tw);
+    c = (float)ld32(ttime + oa, tw) * 0.001f;
+    const int act = ld32(tact + (size_t)a * T * W, tw);
+    const float pih = ld32(pi_hat + ow, tr);
     float dpih = (b2 / (float)K) * 2.0f * pih * inv_wt;
-    float dyh[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dyh[j] = (b3 / (float)K) * 2.0f * yh[j] * inv_wt;
-    const float aa = coef[a * 4 + 0], ba = coef[a * 4 + 1], ac = coef[a * 4 + 2], bc = coef[a * 4 + 3];
+    const float aa = lastv[39], ba = lastv[40], ac = lastv[41], bc = lastv[42];
     const bool applied = aa != 0.0f;
+    const size_t baseA = (size_t)a * D * 5, baseC = (size_t)a * D * 8;
+    // two stages, each issuing its rows' loads together: the policy half (rows idx of theta, adj_th, G_th), then
+    // the critic half (phi, adj_ph, G_ph rows and y_hat); fenced so the two halves' registers are never live at once
     if (applied) {
-      const size_t baseA = (size_t)a * D * 5, baseC = (size_t)a * D * 8;
-      const float* th = theta + baseA;
-      const float* ph = phi + baseC;
-      float lastA[5], lastC[8];
+      const unsigned bA = (unsigned)idx * 20u;
+      float thr[5], adA[5], gA[5];
 #pragma unroll
-      for (int j = 0; j < 5; ++j) lastA[j] = th[(size_t)(D - 1) * 5 + j];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
-      float p[5], y[8];
-      probs_of<5>(th, lastA, idx, c, p);
-      probs_of<8>(ph, lastC, idx, c, y);
+      for (int j = 0; j < 5; ++j) {
+        thr[j] = ldrow(theta + baseA, bA, j);
+        adA[j] = ldrow(adj_th_in + baseA, bA, j);
+        gA[j] = ldrow(Gth + baseA, bA, j);
+      }
+      float p[5];
+      probs_regs<5>(thr, lastv, c, p);
       float v[5];
 #pragma unroll
       for (int j = 0; j < 5; ++j) {
-        const float adj = adj_th_in[baseA + (size_t)idx * 5 + j] + c * adj_th_in[baseA + (size_t)(D - 1) * 5 + j];
-        const float g = Gth[baseA + (size_t)idx * 5 + j] + c * Gth[baseA + (size_t)(D - 1) * 5 + j];
+        const float adj = adA[j] + c * lastv[13 + j];
+        const float g = gA[j] + c * lastv[18 + j];
         v[j] = -lr_a * aa * adj + ba * g;
       }
       float pa = 0.0f, va = 0.0f, pv = 0.0f;
@@ -1524,11 +1608,30 @@ struct HvpOp {   // k_hvp
         const float drho = drs * ((k == act ? 1.0f : 0.0f) - p[k]);
         vout[k] = ws * (drho * (va - pv) - rho * p[k] * (v[k] - pv));
       }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    float yh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) yh[j] = ld32(y_hat + ow, (unsigned)(8 * t + j) * R + (unsigned)w);
+    float dyh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dyh[j] = (b3 / (float)K) * 2.0f * yh[j] * inv_wt;
+    if (applied) {
+      const unsigned bC = (unsigned)idx * 32u;
+      float phr[8], adC[8], gC[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        phr[j] = ldrow(phi + baseC, bC, j);
+        adC[j] = ldrow(adj_ph_in + baseC, bC, j);
+        gC[j] = ldrow(Gph + baseC, bC, j);
+      }
+      float y[8];
+      probs_regs<8>(phr, lastv + 5, c, y);
       float vc[8], av[8], ay = 0.0f, yv = 0.0f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float adj = adj_ph_in[baseC + (size_t)idx * 8 + j] + c * adj_ph_in[baseC + (size_t)(D - 1) * 8 + j];
-        const float g = Gph[baseC + (size_t)idx * 8 + j] + c * Gph[baseC + (size_t)(D - 1) * 8 + j];
+        const float adj = adC[j] + c * lastv[23 + j];
+        const float g = gC[j] + c * lastv[31 + j];
         vc[j] = -lr_c * ac * adj + bc * g;
         av[j] = __logf(y[j] + EPSF) - __logf(yh[j] + EPSF) + y[j] / (y[j] + EPSF);
         ay += av[j] * y[j];
@@ -1548,9 +1651,9 @@ struct HvpOp {   // k_hvp
 #pragma unroll
       for (int j = 0; j < 8; ++j) vout[5 + j] = scale * y[j] * (sv[j] - ys);
     }
-    d_pi_hat[o] = dpih;
+    st32(d_pi_hat + ow, tr, dpih);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) d_y_hat[((size_t)t * 8 + j) * R + r] = dyh[j];
+    for (int j = 0; j < 8; ++j) st32(d_y_hat + ow, (unsigned)(8 * t + j) * R + (unsigned)w, dyh[j]);
     return applied;
   }
   TOUED_DEV float* rowA(int a, int r) const { return adj_th_out + ((size_t)a * D + r) * 5; }
@@ -1565,7 +1668,45 @@ struct HvpOp {   // k_hvp
 // One agent's block (k_rows_sorted below).  PRESORTED: `key` already holds the block's sorted sample keys from an
 // earlier body over the same samples (every sample kept by both ops, as EntropyClipOp and HvpOp do), so only the row
 // vectors and partial sums are rebuilt and the sort is skipped.
-template <class Op, bool PRESORTED>
+#ifdef ROWS_STAMPS
+// timing instrumentation (tools/rows_stamps.py, built by tools/build_variant.py agent.hip ROWS_STAMPS=1): thread 0 of
+// blocks < 64 records the shader clock at 7 points of the body (slot 0 = k_rows_sorted's body, 1 and 2 =
+// k_rows_sorted2's first and second, of the last launch of each); every block records the 100 MHz real-time clock at
+// its body's start and end and its placement (XCC_ID, HW_ID), per launch (a ring of 8 launches per slot).  The clock
+// reads are volatile asm with their waits, so they stay between the phases they bracket.
+__device__ unsigned long long g_rows_stamps[3 * 64 * 8];
+__device__ unsigned long long g_rows_span[3 * 8 * 1024 * 4];
+__device__ unsigned g_rows_ctr[3];
+TOUED_DEV unsigned long long rs_clock() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t));
+  return t;
+}
+TOUED_DEV unsigned long long rs_rtc() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t));
+  return t;
+}
+#define ROWS_STAMP(ph)                                                                                 \
+  do {                                                                                                 \
+    if (tid == 0) {                                                                                    \
+      const unsigned long long tc = rs_clock(), tr = rs_rtc();                                         \
+      if (blockIdx.x < 64) g_rows_stamps[(SLOT * 64 + blockIdx.x) * 8 + (ph)] = tc;                    \
+      if ((ph) == 0) rs_launch = (atomicAdd(&g_rows_ctr[SLOT], 1u) / gridDim.x) & 7u;                 \
+      if (blockIdx.x < 1024 && ((ph) == 0 || (ph) == 6)) {                                             \
+        unsigned long long* e = g_rows_span + (((size_t)SLOT * 8 + rs_launch) * 1024 + blockIdx.x) * 4; \
+        e[(ph) == 6] = tr;                                                                             \
+        if ((ph) == 0) {                                                                               \
+          e[2] = (unsigned)__builtin_amdgcn_s_getreg((3 << 11) | 20);                                  \
+          e[3] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);                                  \
+        }                                                                                              \
+      }                                                                                                \
+    }                                                                                                  \
+  } while (0)
+#else
+#define ROWS_STAMP(ph) do {} while (0)
+#endif
+template <class Op, bool PRESORTED, int SLOT = 0>
 TOUED_DEV void rows_sorted_body(const Op& op) {
   constexpr int NA = Op::NA, NC = Op::NC, NV = NA + NC, NM = Op::NM;
   constexpr uint32_t NONE = 0xFFFFFFFFu, SMASK = 4095u;
@@ -1580,26 +1721,46 @@ TOUED_DEV void rows_sorted_body(const Op& op) {
   __shared__ int any_kept;   // PRESORTED: did this op keep any sample (HvpOp keeps none of an agent not updated)
   __shared__ int scan_a[8];
   __shared__ float scan_b[8][NV];
+  __shared__ float lastv[Op::NLAST];   // the op's per-agent values (time rows ...), read once per block
   uint32_t* key = reinterpret_cast<uint32_t*>(lds);   // [2048]
   float* vec = lds + 2048;                            // [T*W][NVP]
-  const int a = blockIdx.x, tid = threadIdx.x, W = op.W, T = op.T, D = op.D, TW = T * W;
+  // (the thread index through an opaque move: two bodies in one kernel share no tid-derived addresses, which the
+  // compiler would otherwise keep live from the first body into the second)
+  int tid_l;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(tid_l) : "v"((int)threadIdx.x));
+  const int a = blockIdx.x, tid = tid_l, W = op.W, T = op.T, D = op.D, TW = T * W;
   const int lane = tid & 63, wv = tid >> 6;
+  constexpr bool DEFER = defer_time_row<Op>::value;
   if (tid == 0) { has_last = 0; any_kept = 0; }
+  if (tid < Op::NLAST) lastv[tid] = op.last_val(a, tid);
+#ifdef ROWS_STAMPS
+  unsigned rs_launch = 0;
+#endif
+  ROWS_STAMP(0);
   float part[NV + NM];
 #pragma unroll
   for (int j = 0; j < NV + NM; ++j) part[j] = 0.0f;
   __syncthreads();
   // 1) per-sample row vectors -> LDS, sort keys, time-row and metric partial sums
-  for (int sl = tid; sl < 2048; sl += 512) {
+  uint32_t kept = 0u;   // DEFER: the iterations whose sample was kept
+  for (int sl = tid, it = 0; sl < 2048; sl += 512, ++it) {
     uint32_t kk = NONE;
     if (sl < TW) {
       const int t = sl / W, w = sl - t * W;
       int idx;
-      float c, v[NV], m[NM];
-      if (op.sample(a, t, w, idx, c, v, m)) {
+      float c, v[NV], m[NM > 0 ? NM : 1];
+      // (an opaque zero offset keeps the per-agent values' LDS reads in the iteration that uses them: hoisted out
+      // of the loop they would hold up to 43 registers across it)
+      int z0;
+      asm volatile("s_mov_b32 %0, 0" : "=s"(z0));
+      if (op.sample(a, t, w, idx, c, v, m, lastv + z0)) {
         kk = ((uint32_t)idx << 12) | (uint32_t)sl;
 #pragma unroll
-        for (int j = 0; j < NV; ++j) { vec[sl * NVP + j] = v[j]; part[j] += c * v[j]; }
+        for (int j = 0; j < NV; ++j) {
+          vec[sl * NVP + j] = v[j];
+          if constexpr (!DEFER) part[j] += c * v[j];
+        }
+        if constexpr (DEFER) kept |= 1u << it;
         if (idx == D - 1) has_last = 1;
         if (PRESORTED) any_kept = 1;
       } else if (PRESORTED) {
@@ -1612,6 +1773,18 @@ TOUED_DEV void rows_sorted_body(const Op& op) {
     }
     if (!PRESORTED) key[sl] = kk;
   }
+  if constexpr (DEFER) {
+    // the time row's partial sums after the loop, from the stored row vectors: the same products in the same order,
+    // with 13 fewer registers live across the sample loop
+    const int* tt = op.ttime + (size_t)a * (T + 1) * W;   // c of sample sl = t W + w
+    for (int sl = tid, it = 0; sl < TW; sl += 512, ++it) {
+      if ((kept >> it) & 1u) {
+        const float c = (float)ld32(tt, (unsigned)sl) * 0.001f;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) part[j] += c * vec[sl * NVP + j];
+      }
+    }
+  }
 #pragma unroll
   for (int j = 0; j < NV + NM; ++j) {
     const float r = wsum_dpp(part[j]);
@@ -1623,9 +1796,11 @@ TOUED_DEV void rows_sorted_body(const Op& op) {
     for (int w = 0; w < 8; ++w) r += red[w][tid];
     tot[tid] = r;
   }
+  ROWS_STAMP(1);
   // 2) sort by (row, sample)
   if constexpr (PRESORTED) __syncthreads();   // (tot and the row vectors before phase 3)
   else sort2048_reg<512>(key, tid);
+  ROWS_STAMP(2);
   // 3) segmented row sums, deterministic (a fixed combination tree): thread t owns the sorted entries
   //    [CH t, CH t + CH) as runs of equal rows; the part of a segment in earlier chunks (the carry) reaches the chunk
   //    where the segment ends through a segmented scan over the 512 chunks (carry_t = a_t carry_{t-1} + b_t, b_t the
@@ -1710,6 +1885,7 @@ TOUED_DEV void rows_sorted_body(const Op& op) {
     if (lane == 0) cj = pb[j];
     run[j] = cont0 ? cj : 0.0f;
   }
+  ROWS_STAMP(3);
   float na2 = 0.0f, nc2 = 0.0f;
   {
     uint32_t rr = r0;
@@ -1766,6 +1942,7 @@ TOUED_DEV void rows_sorted_body(const Op& op) {
       }
     }
   }
+  ROWS_STAMP(4);
   // APPLY: the step counter and lifetime test before any thread writes them
   bool applied = false;
   if constexpr (Op::APPLY) applied = (op.step[a] + 1) <= op.levels[(size_t)a * LEVEL_WORDS + L_LIFETIME];
@@ -1865,11 +2042,14 @@ TOUED_DEV void rows_sorted_body(const Op& op) {
       op.finish(a, x, y);
     }
   }
+  ROWS_STAMP(5);
   if constexpr (entropy_after<Op>::value) {
     __syncthreads();   // the rewritten rows (and red's last readers) before the entropies read them
-    entropy_metric_agent(a, tid, W, T, D, op.theta_w, op.phi_w, op.tidx, op.ttime, op.met,
-                         reinterpret_cast<float (*)[4]>(&red[0][0]));
+    static_assert(NVP == 13, "entropy_metric_block keeps 13 terms per sample in the row-vector area");
+    entropy_metric_block(a, tid, W, T, D, op.theta_w, op.phi_w, op.tidx, op.ttime, op.met,
+                         reinterpret_cast<float (*)[4]>(&red[0][0]), vec);
   }
+  ROWS_STAMP(6);
 }
 
 template <class Op>
@@ -1880,14 +2060,17 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   rows_sorted_body<Op, false>(op);
 }
 
+#ifndef ROWS2_WPE
+#define ROWS2_WPE 4
+#endif
 // Two ops over the same samples in one block: the second reuses the first's sort (and reads what the first wrote:
 // its rows and, through global memory, anything its thread 0 wrote -- the barrier orders them within the block).
 template <class Op1, class Op2>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k_rows_sorted2(Op1 op1, Op2 op2) {
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(ROWS2_WPE))) k_rows_sorted2(Op1 op1, Op2 op2) {
   if (ROWS_PRIO > 0) __builtin_amdgcn_s_setprio(ROWS_PRIO);
-  rows_sorted_body<Op1, false>(op1);
+  rows_sorted_body<Op1, false, 1>(op1);
   __syncthreads();
-  rows_sorted_body<Op2, true>(op2);
+  rows_sorted_body<Op2, true, 2>(op2);
 }
 
 // launch the sorted variant when one agent's samples fit (T*W <= SORT_MAX_TW, D < 2^19); false otherwise
@@ -2291,6 +2474,15 @@ int toued_gather_add(float* out, const float* src, const int* src_idx, const int
   TOUED_CHECK_LAUNCH();
   return 0;
 }
+
+#ifdef ROWS_STAMPS
+int toued_dbg_rows_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rows_stamps), sizeof(g_rows_stamps)) == hipSuccess ? 0 : 1;
+}
+int toued_dbg_rows_span(unsigned long long* host) {   // [3][8][1024][4]: start, end, XCC_ID, HW_ID
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rows_span), sizeof(g_rows_span)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 int toued_sum_rows_add(const float* part, int rows, int cols, float* out, hipStream_t stream) {
   TOUED_REQUIRE(rows >= 0 && cols >= 0, "toued_sum_rows_add: rows=%d cols=%d", rows, cols);
