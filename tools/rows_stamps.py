@@ -67,7 +67,9 @@ def main():
                 "start_us_p50_p90_max": np.percentile(st_us, [50, 90, 100]).round(2).tolist(),
                 "end_us_p50_p90_max": np.percentile(en_us, [50, 90, 100]).round(2).tolist(),
                 "body_us_p50_p90_max": np.percentile(en_us - st_us, [50, 90, 100]).round(2).tolist(),
-                "late_start_us": sorted(st_us[late].round(1).tolist())[:12]}), flush=True)
+                "late_start_us": sorted(st_us[late].round(1).tolist())[:12],
+                "abs_start_end_us": [round(float(s0) / 100.0, 2), round(float(e[:, 1].max()) / 100.0, 2)]}),
+                flush=True)
 
 if __name__ == "__main__":
     main()
