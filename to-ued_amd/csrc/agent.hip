@@ -1370,28 +1370,28 @@ struct GradOp {   // k_agent_grad (+ the global norms and the lifetime test of t
   TOUED_DEV float last_val(int a, int i) const {
     return i < 5 ? theta[((size_t)a * D + D - 1) * 5 + i] : phi[((size_t)a * D + D - 1) * 8 + (i - 5)];
   }
-  TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* v, float* m, const float* lastv) const {
+  TOUED_DEV bool sample(int a, int t, int w, int idx, float c, float* v, float* m, const float* lastv) const {
     const long s = ((long)a * T + t) * W + w;
-    const SampleRef q = load_sample(s, T, W, tidx, ttime, tact, trew, tdone, true);
     const int R = N * W;
+    const int qr = a * W + w, qact = tact[s];
     const float inv_wt = 1.0f / (float)(W * T);
     const float* th = theta + (size_t)a * D * 5;
     const float* ph = phi + (size_t)a * D * 8;
     const float* lastA = lastv;
     const float* lastC = lastv + 5;
     float p[5], y[8], yh[8];
-    probs_of<5>(th, lastA, q.idx, q.c, p);
-    probs_of<8>(ph, lastC, q.idx, q.c, y);
-    const size_t o = (size_t)q.t * R + q.r;
+    probs_of<5>(th, lastA, idx, c, p);
+    probs_of<8>(ph, lastC, idx, c, y);
+    const size_t o = (size_t)t * R + qr;
     const float pih = pi_hat[o];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) yh[j] = y_hat[((size_t)q.t * 8 + j) * R + q.r];
+    for (int j = 0; j < 8; ++j) yh[j] = y_hat[((size_t)t * 8 + j) * R + qr];
     float pa = 0.0f;
 #pragma unroll
-    for (int j = 0; j < 5; ++j) pa = (j == q.act) ? p[j] : pa;
+    for (int j = 0; j < 5; ++j) pa = (j == qact) ? p[j] : pa;
     const float rho = pa / (pa + EPSF);
 #pragma unroll
-    for (int j = 0; j < 5; ++j) v[j] = pih * inv_wt * rho * ((j == q.act ? 1.0f : 0.0f) - p[j]);
+    for (int j = 0; j < 5; ++j) v[j] = pih * inv_wt * rho * ((j == qact ? 1.0f : 0.0f) - p[j]);
     float av[8], ya = 0.0f, kl = 0.0f, y2 = 0.0f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -1404,7 +1404,6 @@ struct GradOp {   // k_agent_grad (+ the global norms and the lifetime test of t
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[5 + j] = alpha_y * inv_wt * y[j] * (av[j] - ya);
     m[0] = kl; m[1] = pih * pih; m[2] = y2;
-    idx = q.idx; c = q.c;
     return true;
   }
   TOUED_DEV float* rowA(int a, int r) const { return Gth + ((size_t)a * D + r) * 5; }
@@ -1456,10 +1455,7 @@ struct EntropyBwdOp {   // k_entropy, gradient mode
   TOUED_DEV float last_val(int a, int i) const {
     return i < 5 ? theta[((size_t)a * D + D - 1) * 5 + i] : phi[((size_t)a * D + D - 1) * 8 + (i - 5)];
   }
-  TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* v, float* m, const float* lastv) const {
-    const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
-    idx = tidx[o0];
-    c = (float)ttime[o0] * 0.001f;
+  TOUED_DEV bool sample(int a, int t, int w, int idx, float c, float* v, float* m, const float* lastv) const {
     const float* th = theta + (size_t)a * D * 5;
     const float* ph = phi + (size_t)a * D * 8;
     const float* lastA = lastv;
@@ -1509,11 +1505,8 @@ struct LpgLossOp {   // k_lpgloss_grad
   int N, W, T, D;
   static constexpr int NLAST = 5;   // the time row theta[D-1]
   TOUED_DEV float last_val(int a, int i) const { return theta[((size_t)a * D + D - 1) * 5 + i]; }
-  TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* v, float* m, const float* lastv) const {
+  TOUED_DEV bool sample(int a, int t, int w, int idx, float c, float* v, float* m, const float* lastv) const {
     const long s = ((long)a * T + t) * W + w;
-    const size_t o0 = ((size_t)a * (T + 1) + t) * W + w;
-    idx = tidx[o0];
-    c = (float)ttime[o0] * 0.001f;
     const float* th = theta + (size_t)a * D * 5;
     const float* lastA = lastv;
     float p[5];
@@ -1560,12 +1553,10 @@ struct HvpOp {   // k_hvp
   // The sample's loads go through per-agent base pointers (uniform in the block: scalar registers) plus 32-bit
   // element offsets, so every gather is a scalar-base load with one offset register per table shape instead of a
   // 64-bit address pair per table (toued_hvp / toued_entropy_clip_hvp check that the offsets fit)
-  TOUED_DEV bool sample(int a, int t, int w, int& idx, float& c, float* vout, float* m, const float* lastv) const {
+  TOUED_DEV bool sample(int a, int t, int w, int idx, float c, float* vout, float* m, const float* lastv) const {
     const unsigned R = (unsigned)(N * W), tw = (unsigned)(t * W + w), tr = (unsigned)t * R + (unsigned)w;
     const float inv_wt = 1.0f / (float)(W * T);
-    const size_t oa = (size_t)a * (T + 1) * W, ow = (size_t)a * W;
-    idx = ld32(tidx + oa, tw);
-    c = (float)ld32(ttime + oa, tw) * 0.001f;
+    const size_t ow = (size_t)a * W;
     const int act = ld32(tact + (size_t)a * T * W, tw);
     const float pih = ld32(pi_hat + ow, tr);
     float dpih = (b2 / (float)K) * 2.0f * pih * inv_wt;
@@ -1671,10 +1662,10 @@ struct HvpOp {   // k_hvp
 #ifdef ROWS_STAMPS
 // timing instrumentation (tools/rows_stamps.py, built by tools/build_variant.py agent.hip ROWS_STAMPS=1): thread 0 of
 // blocks < 64 records the shader clock at 7 points of the body (slot 0 = k_rows_sorted's body, 1 and 2 =
-// k_rows_sorted2's first and second, of the last launch of each); every block records the 100 MHz real-time clock at
-// its body's start and end and its placement (XCC_ID, HW_ID), per launch (a ring of 8 launches per slot).  The clock
+// k_rows_sorted2's first and second); every block records the 100 MHz real-time clock at its body's start and end
+// and its placement (XCC_ID, HW_ID); both per launch (a ring of 8 launches per slot).  The clock
 // reads are volatile asm with their waits, so they stay between the phases they bracket.
-__device__ unsigned long long g_rows_stamps[3 * 64 * 8];
+__device__ unsigned long long g_rows_stamps[3 * 8 * 64 * 8];   // [slot][launch ring][block][stamp]
 __device__ unsigned long long g_rows_span[3 * 8 * 1024 * 4];
 __device__ unsigned g_rows_ctr[3];
 TOUED_DEV unsigned long long rs_clock() {
@@ -1691,8 +1682,8 @@ TOUED_DEV unsigned long long rs_rtc() {
   do {                                                                                                 \
     if (tid == 0) {                                                                                    \
       const unsigned long long tc = rs_clock(), tr = rs_rtc();                                         \
-      if (blockIdx.x < 64) g_rows_stamps[(SLOT * 64 + blockIdx.x) * 8 + (ph)] = tc;                    \
       if ((ph) == 0) rs_launch = (atomicAdd(&g_rows_ctr[SLOT], 1u) / gridDim.x) & 7u;                 \
+      if (blockIdx.x < 64) g_rows_stamps[((SLOT * 8 + rs_launch) * 64 + blockIdx.x) * 8 + (ph)] = tc;  \
       if (blockIdx.x < 1024 && ((ph) == 0 || (ph) == 6)) {                                             \
         unsigned long long* e = g_rows_span + (((size_t)SLOT * 8 + rs_launch) * 1024 + blockIdx.x) * 4; \
         e[(ph) == 6] = tr;                                                                             \
@@ -1743,12 +1734,31 @@ TOUED_DEV void rows_sorted_body(const Op& op) {
   __syncthreads();
   // 1) per-sample row vectors -> LDS, sort keys, time-row and metric partial sums
   uint32_t kept = 0u;   // DEFER: the iterations whose sample was kept
+  // every op's sample sl = t W + w is row tidx[a][t][w] at time c = ttime[a][t][w] / 1000 (the [N][T + 1][W] index
+  // arrays): the body loads them, one iteration ahead, so a sample's row gathers do not wait behind its own index load
+  // (only in the one-op kernel, SLOT 0, and not for HvpOp: with the two more live registers k_rows_sorted2's two
+  // bodies and k_rows_sorted<HvpOp> spill)
+  constexpr bool AHEAD = SLOT == 0 && !DEFER;
+  int nidx = 0, ntt = 0;
+  if (AHEAD && tid < TW) {
+    nidx = ld32(op.tidx + (size_t)a * (T + 1) * W, (unsigned)tid);
+    ntt = ld32(op.ttime + (size_t)a * (T + 1) * W, (unsigned)tid);
+  }
   for (int sl = tid, it = 0; sl < 2048; sl += 512, ++it) {
     uint32_t kk = NONE;
+    if (!AHEAD && sl < TW) {
+      nidx = ld32(op.tidx + (size_t)a * (T + 1) * W, (unsigned)sl);
+      ntt = ld32(op.ttime + (size_t)a * (T + 1) * W, (unsigned)sl);
+    }
+    const int idx = nidx, tcur = ntt;
+    if (AHEAD && sl + 512 < TW) {
+      nidx = ld32(op.tidx + (size_t)a * (T + 1) * W, (unsigned)(sl + 512));
+      ntt = ld32(op.ttime + (size_t)a * (T + 1) * W, (unsigned)(sl + 512));
+    }
     if (sl < TW) {
       const int t = sl / W, w = sl - t * W;
-      int idx;
-      float c, v[NV], m[NM > 0 ? NM : 1];
+      const float c = (float)tcur * 0.001f;
+      float v[NV], m[NM > 0 ? NM : 1];
       // (an opaque zero offset keeps the per-agent values' LDS reads in the iteration that uses them: hoisted out
       // of the loop they would hold up to 43 registers across it)
       int z0;

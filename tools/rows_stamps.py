@@ -3,8 +3,8 @@
     python tools/build_variant.py agent.hip ROWS_STAMPS=1
     TOUED_LIB=to-ued_amd/exp/libtoued_ROWS_STAMPS_1.so python tools/rows_stamps.py
 
-Runs two C2 meta-steps (512 agents, tabular, K = 5) and prints, for the first 64 blocks of the last launch of each
-kind, the mean shader cycles of each phase: per-sample rows + partial sums, sort, segmented scan, the row writes
+Runs two C2 meta-steps (512 agents, tabular, K = 5) and prints, for the first 64 blocks of each of the last step's
+launches, the mean shader cycles of each phase: per-sample rows + partial sums, sort, segmented scan, the row writes
 (read-modify-write of the touched rows), norms / clip / apply, entropy metrics.  Slot 0: the inner update
 (k_rows_sorted<GradStepEntOp>); slots 1, 2: the reverse step's two bodies (k_rows_sorted2<EntropyClipOp, HvpOp>)."""
 import ctypes
@@ -30,16 +30,22 @@ def main():
     torch.cuda.synchronize()
     fn = _lib.lib().toued_dbg_rows_stamps
     fn.argtypes = [ctypes.c_void_p]
-    buf = np.zeros(3 * 64 * 8, np.uint64)
+    buf = np.zeros(3 * 8 * 64 * 8, np.uint64)
     assert fn(buf.ctypes.data) == 0
-    st = buf.reshape(3, 64, 8).astype(np.int64)
+    st = buf.reshape(3, 8, 64, 8).astype(np.int64)
     names = ["rows + partials", "sort", "segmented scan", "row writes", "norms / clip / apply", "entropy metrics"]
-    for slot, kind in enumerate(["k_rows_sorted<GradStepEntOp>", "k_rows_sorted2 body 1 (EntropyClipOp)",
+    # per slot, the last step's launches (ring entries 5, 6, 7, 0, 1 of 10 launches per slot over the two steps; slot
+    # 0 also holds k_rows_sorted<LpgLossOp>, the step's sixth one-op launch)
+    for slot, kind in enumerate(["k_rows_sorted (GradStepEntOp; LpgLossOp)", "k_rows_sorted2 body 1 (EntropyClipOp)",
                                  "k_rows_sorted2 body 2 (HvpOp)"]):
-        ph = np.diff(st[slot], axis=1)[:, :6]
-        res = {n: round(float(ph[:, i].mean())) for i, n in enumerate(names)}
-        res["total"] = round(float((st[slot, :, 6] - st[slot, :, 0]).mean()))
-        print(json.dumps({"kernel": kind, **res}), flush=True)
+        for ln in (5, 6, 7, 0, 1):
+            e = st[slot, ln]
+            if not e[:, 0].all():
+                continue
+            ph = np.diff(e, axis=1)[:, :6]
+            res = {n: round(float(ph[:, i].mean())) for i, n in enumerate(names)}
+            res["total"] = round(float((e[:, 6] - e[:, 0]).mean()))
+            print(json.dumps({"kernel": kind, "launch": ln, **res}), flush=True)
     # every block's body start / end on the 100 MHz real-time clock and its placement, per launch: dispatch spread,
     # body durations, and how the late-starting blocks sit on the CUs (ring of 8 launches per slot; the last step's 5)
     sf = _lib.lib().toued_dbg_rows_span
