@@ -568,17 +568,28 @@ TOUED_DEV void entropy_metric_block(int a, int tid, int W, int T, int D, const f
     for (int j = 0; j < 8; ++j) lastC[j] = ph[(size_t)(D - 1) * 8 + j];
     const int* ti = tidx + (size_t)a * (T + 1) * W;   // sample i = t W + w
     const int* tt = ttime + (size_t)a * (T + 1) * W;
-    for (int i = tid; i < TW; i += 512) {
-      const int idx = ld32(ti, (unsigned)i);
-      const float c = (float)ld32(tt, (unsigned)i) * 0.001f;
-      float p[5], y[8];
-      probs_of<5>(th, lastA, idx, c, p);
-      probs_of<8>(ph, lastC, idx, c, y);
-      float* e = terms + (size_t)i * 13;
+    // the thread's (at most four: T W <= 2048) samples' indices first, then their row gathers: two dependent trips
+    int ix[4];
+    float cx[4];
 #pragma unroll
-      for (int j = 0; j < 5; ++j) e[j] = (p[j] + EPSF) * __logf(p[j] + EPSF);
+    for (int q = 0; q < 4; ++q) {
+      const int i = tid + 512 * q;
+      ix[q] = i < TW ? ld32(ti, (unsigned)i) : 0;
+      cx[q] = i < TW ? (float)ld32(tt, (unsigned)i) * 0.001f : 0.0f;
+    }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) e[5 + j] = (y[j] + EPSF) * __logf(y[j] + EPSF);
+    for (int q = 0; q < 4; ++q) {
+      const int i = tid + 512 * q;
+      if (i < TW) {
+        float p[5], y[8];
+        probs_of<5>(th, lastA, ix[q], cx[q], p);
+        probs_of<8>(ph, lastC, ix[q], cx[q], y);
+        float* e = terms + (size_t)i * 13;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) e[j] = (p[j] + EPSF) * __logf(p[j] + EPSF);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) e[5 + j] = (y[j] + EPSF) * __logf(y[j] + EPSF);
+      }
     }
   }
   __syncthreads();
@@ -1722,6 +1733,12 @@ TOUED_DEV void rows_sorted_body(const Op& op) {
   const int a = blockIdx.x, tid = tid_l, W = op.W, T = op.T, D = op.D, TW = T * W;
   const int lane = tid & 63, wv = tid >> 6;
   constexpr bool DEFER = defer_time_row<Op>::value;
+  // APPLY: the step counter and lifetime (the lifetime test below), loaded at the start, off the critical path
+  int app_step = 0, app_life = 0;
+  if constexpr (Op::APPLY) {
+    app_step = op.step[a];
+    app_life = op.levels[(size_t)a * LEVEL_WORDS + L_LIFETIME];
+  }
   if (tid == 0) { has_last = 0; any_kept = 0; }
   if (tid < Op::NLAST) lastv[tid] = op.last_val(a, tid);
 #ifdef ROWS_STAMPS
@@ -1953,9 +1970,24 @@ TOUED_DEV void rows_sorted_body(const Op& op) {
     }
   }
   ROWS_STAMP(4);
+  // APPLY: the theta_k / phi_k rows this thread will rewrite (its segments' rows; thread 0 also the time row when no
+  // segment holds it), loaded here so that they arrive during the norm reduction instead of after it
+  float srcv[Op::APPLY ? CH + 1 : 1][Op::APPLY ? NV : 1];
+  if constexpr (Op::APPLY) {
+    auto load_row = [&](size_t r, float* dst) {
+#pragma unroll
+      for (int j = 0; j < NA; ++j) dst[j] = op.theta[((size_t)a * D + r) * NA + j];
+#pragma unroll
+      for (int j = 0; j < NC; ++j) dst[NA + j] = op.phi[((size_t)a * D + r) * NC + j];
+    };
+#pragma unroll
+    for (int e = 0; e < CH; ++e)
+      if ((endm >> e) & 1u) load_row(kc[e] >> 12, srcv[e]);
+    if (tid == 0 && !has_last) load_row((size_t)(D - 1), srcv[CH]);
+  }
   // APPLY: the step counter and lifetime test before any thread writes them
   bool applied = false;
-  if constexpr (Op::APPLY) applied = (op.step[a] + 1) <= op.levels[(size_t)a * LEVEL_WORDS + L_LIFETIME];
+  if constexpr (Op::APPLY) applied = app_step + 1 <= app_life;
   if (Op::APPLY && tid == 0 && !has_last) {
     float* ga = nullptr;
     float* gc = nullptr;
@@ -2018,26 +2050,24 @@ TOUED_DEV void rows_sorted_body(const Op& op) {
           const float gg = clip ? (g / gn) * op.max_norm : g;
           return p0 + (-(lr * gg));
         };
-        // read theta / phi (theta_k), write theta_w / phi_w (the same tables in place, or theta_{k+1})
-        auto apply_row = [&](size_t r, const float* g) {
-          const float* src_a = op.theta + ((size_t)a * D + r) * NA;
-          const float* src_c = op.phi + ((size_t)a * D + r) * NC;
+        // theta_k / phi_k (srcv, loaded above) -> theta_w / phi_w (the same tables in place, or theta_{k+1})
+        auto apply_row = [&](size_t r, const float* src, const float* g) {
           float* ta = op.theta_w + ((size_t)a * D + r) * NA;
           float* tc = op.phi_w + ((size_t)a * D + r) * NC;
 #pragma unroll
-          for (int j = 0; j < NA; ++j) ta[j] = upd(src_a[j], g[j], clip_a, gna, op.lr_a);
+          for (int j = 0; j < NA; ++j) ta[j] = upd(src[j], g[j], clip_a, gna, op.lr_a);
 #pragma unroll
-          for (int j = 0; j < NC; ++j) tc[j] = upd(src_c[j], g[NA + j], clip_c, gnc, op.lr_c);
+          for (int j = 0; j < NC; ++j) tc[j] = upd(src[NA + j], g[NA + j], clip_c, gnc, op.lr_c);
         };
         if (applied) {
 #pragma unroll
           for (int e = 0; e < CH; ++e)
-            if ((endm >> e) & 1u) apply_row(kc[e] >> 12, vec + (size_t)(kc[e] & SMASK) * NVP);
+            if ((endm >> e) & 1u) apply_row(kc[e] >> 12, srcv[e], vec + (size_t)(kc[e] & SMASK) * NVP);
           if (tid == 0 && !has_last) {
             float g[NV];
 #pragma unroll
             for (int j = 0; j < NV; ++j) g[j] = 0.0f + tot[j];
-            apply_row((size_t)(D - 1), g);
+            apply_row((size_t)(D - 1), srcv[CH], g);
           }
         }
         if (tid == 0) {
