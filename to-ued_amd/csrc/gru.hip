@@ -668,8 +668,23 @@ __device__ unsigned long long g_fwd_stamps[64 * 32 * 6];
     if (blockIdx.x < 64 && tid == 0 && s < 32)                                                         \
       g_fwd_stamps[(blockIdx.x * 32 + s) * 6 + (ph)] = __builtin_amdgcn_s_memtime();                   \
   } while (0)
+// the ping-pong schedule (FWD_PP): lane 0 of waves 0 and 4 record the start and end of each of their three pieces of
+// work per step (half 0: contraction k 0-7, k 8-15 + heads, gate maths; half 1: gate maths of the step before,
+// k 0-7, k 8-15), ordered clock reads
+__device__ unsigned long long g_fwd_pp[64 * 32 * 2 * 6];
+TOUED_DEV unsigned long long fwd_clock() {
+  unsigned long long c;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c));
+  return c;
+}
+#define PP_STAMP(s_, k)                                                                                \
+  do {                                                                                                 \
+    if (blockIdx.x < 64 && lane == 0 && (wave & 3) == 0 && (s_) >= 0 && (s_) < 32)                     \
+      g_fwd_pp[((blockIdx.x * 32 + (s_)) * 2 + grp) * 6 + (k)] = fwd_clock();                          \
+  } while (0)
 #else
 #define FWD_STAMP(ph) do {} while (0)
+#define PP_STAMP(s_, k) do {} while (0)
 #endif
 
 #ifndef FWD_AUG32
@@ -683,6 +698,12 @@ __device__ unsigned long long g_fwd_stamps[64 * 32 * 6];
 #endif
 #ifndef FWD_XFIRST
 #define FWD_XFIRST 0   // comparison runs: x(t) issued before the ring's lead fragments (the round-4 order)
+#endif
+#ifndef FWD_PP
+#define FWD_PP 0       // the two halves of the workgroup one interval apart (gate maths beside the partner's MFMAs)
+#endif
+#ifndef FWD_PP_PRIO
+#define FWD_PP_PRIO 0  // FWD_PP: the gate maths' issue priority over the partner wave's contraction
 #endif
 #ifndef FWD_CAND0
 #define FWD_CAND0 0    // timing study only: the per-candidate instance reads candidate 0's fragments everywhere
@@ -775,6 +796,288 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     const float inv = 1.0f / ssum;
     for (int j = 0; j < 8; ++j) p.y_hat[((long)t_ * 8 + j) * R + r0 + tl] = e[j] * inv;
   };
+if constexpr (FWD_PP && SAVE) {   // (C2 instance only: the per-candidate one spills with it)
+  // ---- ping-pong schedule: the workgroup's two halves (waves 0-3 own units 0-127 = k-steps 0-7 of the carry, waves
+  // 4-7 units 128-255 = k-steps 8-15) run one interval apart, three intervals per step with a barrier after each:
+  //   interval   waves 0-3 (half 0)                          waves 4-7 (half 1)
+  //   1          contraction k 0-7 of step s (own units)     gate maths of step s-1: writes units 128-255
+  //   2          contraction k 8-15 + augmented of step s    contraction k 0-7 of step s
+  //   3          gate maths of step s: writes units 0-127    contraction k 8-15 + augmented of step s
+  // so each SIMD (waves w and w + 4) has one wave's gate maths (VALU, saves) beside its partner's matrix work in two
+  // of the three intervals, where the lockstep order runs them one after the other.  Every interval reads carry units
+  // that no wave writes in it (the table above), so the carry stays single-buffered in place; the k-order of the
+  // contraction is unchanged.  Heads: step s's partials (both halves) are complete after interval 1 of step s + 1;
+  // wave 0 reduces them in its interval 2 (FWD_HDEFER's double buffer).
+  static_assert(FWD_HDEFER, "FWD_PP defers the heads");
+  const int grp = wave >> 2;
+  floatx16 acc[3][2];   // r, z, W_hn h + b_hn (the n gate's input part is gate_ain, on the VALU)
+  float xv[2][7];
+  f16x8 A0[3][2], A1[3][2], B[2][2];
+  auto fragA = [&](int ks, int g, int q) { return ((ks * 8 + wave) * 3 + g) * 2 + q; };
+  auto fragAug = [&](int g, int q) { return F6_NFH + (wave * 4 + g) * 3 + q; };
+  auto load_B = [&](int ks, int h) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      B[h][q] = *reinterpret_cast<const f16x8*>(&hB[q][(RB * h + col) * F6_HP + 16 * ks + 8 * hi]);
+  };
+  // one k-step: refill its A ring slot two k-steps ahead (reload), load the next k-step's B fragments (nextB)
+  auto kstep = [&](int ks, f16x8 (&Ar)[3][2], bool reload, bool nextB) {
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        acc[g][h] = mfma3h(Ar[g], B[h], acc[g][h]);
+        if (g == 2 && nextB) load_B(ks + 1, h);
+      }
+      if (reload) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) Ar[g][q] = ldAh(fragA(ks + 2, g, q));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // the contraction's first half: x(t), the ring's lead fragments, k-steps 0-7 (carry units 0-127)
+  auto c_first = [&](int s) {
+    const int t = T - 1 - s;
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[g][h][q] = 0.0f;
+      {
+        auto ring = [&] {
+  #pragma unroll
+          for (int g = 0; g < 3; ++g)
+  #pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              A0[g][q] = ldAh(fragA(0, g, q));
+              A1[g][q] = ldAh(fragA(1, g, q));
+            }
+        };
+        if (!FWD_XFIRST) ring();
+  #pragma unroll
+        for (int h = 0; h < 2; ++h)
+  #pragma unroll
+          for (int f = 0; f < 7; ++f) {
+            const int fc = f < F ? f : F - 1;
+            xv[h][f] = ld_u(rs_X, (unsigned)((RB * h + col) * p.xs_col * 4),
+                            (unsigned)((fc * p.xs_f + ((long)t * R + r0) * p.xs_col) * 4));
+          }
+        if (FWD_XFIRST) ring();
+      }
+    load_B(0, 0);
+    load_B(0, 1);
+#pragma nounroll
+    for (int kp = 0; kp < 3; ++kp) {
+      kstep(2 * kp, A0, true, true);
+      kstep(2 * kp + 1, A1, true, true);
+    }
+    kstep(6, A0, true, true);
+    kstep(7, A1, true, false);   // (k-step 8's B: units 128-143, written by the other half in this interval)
+  };
+  // the second half: k-steps 8-15 (carry units 128-255) and the augmented k-step
+  auto c_second = [&](int s) {
+    load_B(8, 0);
+    load_B(8, 1);
+#pragma nounroll
+    for (int kp = 4; kp < 7; ++kp) {
+      kstep(2 * kp, A0, true, true);
+      kstep(2 * kp + 1, A1, true, true);
+    }
+    kstep(14, A0, false, true);
+      f16x8 (&A)[3][2] = A1;   // k-step 15
+      if (A32) {
+        // the augmented k-step on the f32 MFMA (exact products): A = the scaled input weights and biases (one 16-byte
+        // fragment per gate, 3 KB per wave-step instead of the bf16 triple's 12 KB: the ES candidates' per-step stream
+        // from the Infinity Cache is what this kernel waits on), B = 2^14 [x_k (k < F), 1 (k = 7)]
+        float4 a32[3];
+  #pragma unroll
+        for (int g = 0; g < 3; ++g)
+          a32[g] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  rs_A, (int)vA, (F6_A32 + (wave * 3 + g) * 256) * 4, 0));
+  #pragma unroll
+        for (int g = 0; g < 3; ++g) {
+  #pragma unroll
+          for (int h = 0; h < 2; ++h) acc[g][h] = mfma3h(A[g], B[h], acc[g][h]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+  #pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int k = 2 * kk + hi;
+          float bx[2];
+  #pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            // static indices: the lane's k = 2 kk + hi picks between two registers (a lane-dependent index puts xv in
+            // scratch: 64 bytes per lane, C4's forward 2.22 -> 2.65 ms while xv lived outside the step loop)
+            const float xs = hi ? xv[h][2 * kk + 1 < 7 ? 2 * kk + 1 : 6] : xv[h][2 * kk];
+            bx[h] = (k < F ? xs : (k == 7 ? 1.0f : 0.0f)) * HSCALE;
+          }
+  #pragma unroll
+          for (int g = 0; g < 3; ++g) {
+            const float av = kk == 0 ? a32[g].x : kk == 1 ? a32[g].y : kk == 2 ? a32[g].z : a32[g].w;
+  #pragma unroll
+            for (int h = 0; h < 2; ++h) acc[g][h] = mfma32(av, bx[h], acc[g][h]);
+          }
+        }
+      } else {
+      // last carry k-step; each gate's augmented fragments (three bf16 pieces) load behind its MFMAs
+      bf16x8 Aa[3][3], Ba[2][3];
+  #pragma unroll
+      for (int g = 0; g < 3; ++g) {
+  #pragma unroll
+        for (int h = 0; h < 2; ++h) acc[g][h] = mfma3h(A[g], B[h], acc[g][h]);
+  #pragma unroll
+        for (int q = 0; q < 3; ++q) Aa[g][q] = ldA(fragAug(g, q));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // augmented k-step: B = bf16 pieces of 2^14 [x, 1, 0 ...]
+  #pragma unroll
+      for (int h = 0; h < 2; ++h)
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = hi ? 0.0f : e < F ? xv[h][e < 7 ? e : 6] : (e == F ? 1.0f : 0.0f);
+          split3v(v * HSCALE, Ba[h][0], Ba[h][1], Ba[h][2], e);
+        }
+  #pragma unroll
+      for (int g = 0; g < 3; ++g) {
+  #pragma unroll
+        for (int h = 0; h < 2; ++h) acc[g][h] = mfma6(Aa[g], Ba[h], acc[g][h]);
+      }
+      }
+  };
+  auto g_maths = [&](int s) {
+    const int t = T - 1 - s;
+    // (FWD_PP_PRIO: the gate maths' VALU ahead of the partner's MFMA issue on the SIMD)
+    if (FWD_PP_PRIO) __builtin_amdgcn_s_setprio(FWD_PP_PRIO);
+      // ---- gate maths (lane = row 32h + col, register q = unit 32 wave + 4 hi + qunit(q))
+      floatx16 ain[2];
+      // done flags d_{t-1} of the lane's two rows, issued before the saves so their wait drains nothing else
+      // (lane offset re-derived here: a spilled copy's reload would wait on every outstanding access)
+      bool dnf[2];
+  #pragma unroll
+      for (int h = 0; h < 2; ++h)
+        dnf[h] = (t >= 1) ? __builtin_amdgcn_raw_buffer_load_b8(
+                                rs_done, lane_now() & 31, (int)(((long)a_[h] * T + (t - 1)) * W + r0 + RB * h - a_[h] * W),
+                                0) != 0
+                          : false;
+      float wI[4];
+      {
+        const int ln = lane_now();
+  #pragma unroll
+        for (int kk = 0; kk < 4; ++kk) wI[kk] = wIs[(wave * 4 + kk) * 64 + ln];
+      }
+  #pragma unroll
+      for (int h = 0; h < 2; ++h) ain[h] = gate_ain(wI, F, hi, [&](int k) { return xv[h][k < 7 ? k : 6]; });
+      const long cbase = (long)t * R;
+      const int ub = 32 * wave + 4 * hi;
+      const float4* whl = reinterpret_cast<const float4*>(wh + ub * 12);
+  #pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = RB * h + col;
+        const bool dn = dnf[h];
+        const unsigned vq = quad_vbyte(ub, col), vslab = slab_vbyte(ub, col);
+        float hp_loc[9];
+  #pragma unroll
+        for (int oo = 0; oo < 9; ++oo) hp_loc[oo] = 0.0f;
+  #pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          // four consecutive units ub + 8 g4 .. +3 of this row: h_in pieces, then the new carry's pieces
+          const int ho = row * F6_HP + ub + 8 * g4;
+          const f16x4 h0 = *reinterpret_cast<const f16x4*>(&hB[0][ho]);
+          const f16x4 h1 = *reinterpret_cast<const f16x4*>(&hB[1][ho]);
+          const bf16x4 hr = *reinterpret_cast<const bf16x4*>(&hB[2][ho]);
+          // the saves of this register quad: h_in (rebuilt exactly from its pieces) per unit in its slab blocks; r, z,
+          // hn one 16-byte store each in their unit-quad blocks (quad_soff) after the gate maths
+          const unsigned sq = quad_soff(cbase + r0, h, g4);
+          float sv[3][4];
+          float us[3][4];
+  #pragma unroll
+          for (int g = 0; g < 3; ++g) {
+            const float4 v = *reinterpret_cast<const float4*>(&usc[g * HU + ub + 8 * g4]);
+            us[g][0] = v.x; us[g][1] = v.y; us[g][2] = v.z; us[g][3] = v.w;
+          }
+          f16x4 n0, n1;
+          bf16x4 nr;
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int q = 4 * g4 + e;
+            const float rg = sigm_r(acc[0][h][q] * us[0][e]);
+            const float zg = sigm_r(acc[1][h][q] * us[1][e]);
+            const float hn = acc[2][h][q] * us[2][e];
+            const float ng = gate_n(ain[h][q], rg, hn);
+            const float hin = (((float)h0[e] + (float)h1[e]) + (float)hr[e]) * (1.0f / HSCALE);   // exact
+            const float hh = (1.0f - zg) * ng + zg * hin;
+            split_carry(dn ? 0.0f : hh, n0, n1, nr, e);   // carry h_in(t-1) = where(d_{t-1}, 0, h_out(t))
+            sv[0][e] = rg;
+            sv[1][e] = zg;
+            sv[2][e] = hn;   // n is recomputed by the backward (gate_n)
+            if (SAVE && FWD_NOSAVE != 1) {   // (FWD_NOSAVE, timing studies only: 1 = no saves, 2 = h_in only)
+              if (HIN_SLAB) st_u(rs_hin, vslab, slab_soff(cbase + r0, h, qunit(q)), hin);
+              else st_u(rs_hin, (unsigned)(((long)ub * p.M + r0 + row) * 4), (unsigned)(((long)qunit(q) * p.M + cbase) * 4), hin);
+            }
+            const float rl = fmaxf(hh, 0.0f);
+            const float4 w0 = whl[qunit(q) * 3], w1 = whl[qunit(q) * 3 + 1], w2 = whl[qunit(q) * 3 + 2];
+            hp_loc[0] += rl * w0.x; hp_loc[1] += rl * w0.y; hp_loc[2] += rl * w0.z;
+            hp_loc[3] += rl * w0.w; hp_loc[4] += rl * w1.x; hp_loc[5] += rl * w1.y;
+            hp_loc[6] += rl * w1.z; hp_loc[7] += rl * w1.w; hp_loc[8] += rl * w2.x;
+          }
+          if (SAVE && FWD_NOSAVE == 0) {   // (FWD_NOSAVE, timing studies only: 1 = no saves, 2 = h_in only)
+            st4(rs_r, vq, sq, sv[0]);
+            st4(rs_z, vq, sq, sv[1]);
+            st4(rs_hn, vq, sq, sv[2]);
+          }
+          *reinterpret_cast<f16x4*>(&hB[0][ho]) = n0;
+          *reinterpret_cast<f16x4*>(&hB[1][ho]) = n1;
+          *reinterpret_cast<bf16x4*>(&hB[2][ho]) = nr;
+        }
+        // lanes l and l + 32 hold the same row: fold the two halves, one lane writes
+  #pragma unroll
+        for (int oo = 0; oo < 9; ++oo) {
+          const float o = __shfl_xor(hp_loc[oo], 32);
+          if (hi == 0) hp[(FWD_HDEFER ? (s & 1) * 4608 : 0) + (wave * 9 + oo) * 64 + row] = hp_loc[oo] + o;
+        }
+      }
+    if (FWD_PP_PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+  // (each half's three roles in program order, so the ring and B registers are dead across the gate maths)
+  if (grp == 0) {
+    for (int s = 0; s < T; ++s) {
+      PP_STAMP(s, 0);
+      c_first(s);
+      PP_STAMP(s, 1);
+      lds_barrier();
+      PP_STAMP(s, 2);
+      c_second(s);
+      if (wave == 0 && s > 0) head_out(s - 1);
+      PP_STAMP(s, 3);
+      lds_barrier();
+      PP_STAMP(s, 4);
+      g_maths(s);
+      PP_STAMP(s, 5);
+      lds_barrier();
+    }
+    lds_barrier();   // (the other half's last gate maths)
+    if (wave == 0) head_out(T - 1);
+  } else {
+    for (int s = 0; s < T; ++s) {
+      PP_STAMP(s, 0);
+      if (s > 0) g_maths(s - 1);
+      PP_STAMP(s, 1);
+      lds_barrier();
+      PP_STAMP(s, 2);
+      c_first(s);
+      PP_STAMP(s, 3);
+      lds_barrier();
+      PP_STAMP(s, 4);
+      c_second(s);
+      PP_STAMP(s, 5);
+      lds_barrier();
+    }
+    g_maths(T - 1);
+    lds_barrier();
+  }
+} else {
   for (int s = 0; s < T; ++s) {
     const int t = T - 1 - s;
     FWD_STAMP(0);
@@ -1028,6 +1331,7 @@ __global__ void __launch_bounds__(512, 1) k_gru_fwd6(FwdArgs p) {
     FWD_STAMP(5);
   }
   if (FWD_HDEFER && wave == 0) head_out(T - 1);   // the last step's heads (its partials visible: the loop's barrier)
+}
 }
 
 // ------------------------------------------------------------------ backward
@@ -2346,6 +2650,9 @@ int toued_gru_bwd_fused(int R, int T, int W, int K, const uint8_t* done, long do
 #ifdef FWD_STAMPS
 int toued_dbg_fwd_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd_stamps), sizeof(g_fwd_stamps)) == hipSuccess ? 0 : 1;
+}
+int toued_dbg_fwd_pp_stamps(unsigned long long* host) {   // [64 workgroups][32 steps][2 halves][6]
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd_pp), sizeof(g_fwd_pp)) == hipSuccess ? 0 : 1;
 }
 #endif
 

@@ -53,6 +53,22 @@ def main():
         for _ in range(3):
             gru.forward(0, gru.X, done[0], eta, pi_hat, y_hat)
     torch.cuda.synchronize()
+    if "--pp" in sys.argv:
+        # the ping-pong schedule (FWD_PP=1 FWD_STAMPS=1): per half, its three pieces of work and the barrier waits
+        buf = np.zeros(64 * 32 * 2 * 6, np.uint64)
+        fn = _lib.lib().toued_dbg_fwd_pp_stamps
+        fn.argtypes = [ctypes.c_void_p]
+        assert fn(buf.ctypes.data) == 0
+        st = buf.reshape(64, 32, 2, 6)[:, 1:T - 1].astype(np.int64)   # steps 1 .. T-2 (both halves busy)
+        names = {0: ["k 0-7", "k 8-15 + aug (+ heads)", "gate maths s"], 1: ["gate maths s-1", "k 0-7", "k 8-15 + aug"]}
+        for grp in range(2):
+            e = st[:, :, grp]
+            work = [float((e[..., 2 * j + 1] - e[..., 2 * j]).mean()) for j in range(3)]
+            wait = [float((e[..., 2 * j + 2] - e[..., 2 * j + 1]).mean()) for j in range(2)]
+            step = float((e[:, 1:, 0] - e[:, :-1, 0]).mean())
+            print(json.dumps({"half": grp, **{n: round(w) for n, w in zip(names[grp], work)},
+                              "barrier waits (1st, 2nd)": [round(w) for w in wait], "step": round(step)}), flush=True)
+        return
     buf = np.zeros(64 * 32 * 6, np.uint64)
     fn = _lib.lib().toued_dbg_fwd_stamps
     fn.argtypes = [ctypes.c_void_p]
