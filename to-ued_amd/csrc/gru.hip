@@ -672,6 +672,12 @@ __device__ unsigned long long g_fwd_stamps[64 * 32 * 6];
 // work per step (half 0: contraction k 0-7, k 8-15 + heads, gate maths; half 1: gate maths of the step before,
 // k 0-7, k 8-15), ordered clock reads
 __device__ unsigned long long g_fwd_pp[64 * 32 * 2 * 6];
+// the lockstep gate maths' inside (thread 0): after the done flags + gate_ain, after row tile 0, after row tile 1
+__device__ unsigned long long g_fwd_gm[64 * 32 * 4];
+#define GM_STAMP(k)                                                                                    \
+  do {                                                                                                 \
+    if (blockIdx.x < 64 && tid == 0 && s < 32) g_fwd_gm[(blockIdx.x * 32 + s) * 4 + (k)] = fwd_clock(); \
+  } while (0)
 TOUED_DEV unsigned long long fwd_clock() {
   unsigned long long c;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c));
@@ -685,6 +691,7 @@ TOUED_DEV unsigned long long fwd_clock() {
 #else
 #define FWD_STAMP(ph) do {} while (0)
 #define PP_STAMP(s_, k) do {} while (0)
+#define GM_STAMP(k) do {} while (0)
 #endif
 
 #ifndef FWD_AUG32
@@ -1099,6 +1106,7 @@ if constexpr (FWD_PP && SAVE) {   // (C2 instance only: the per-candidate one sp
     // wait for x's HBM loads; 1.207-1.216 ms either order at C2)
     float xv[2][7];
     f16x8 A0[3][2], A1[3][2], B[2][2];
+
     auto fragA = [&](int ks, int g, int q) { return ((ks * 8 + wave) * 3 + g) * 2 + q; };
     auto fragAug = [&](int g, int q) { return F6_NFH + (wave * 4 + g) * 3 + q; };
     {
@@ -1236,6 +1244,7 @@ if constexpr (FWD_PP && SAVE) {   // (C2 instance only: the per-candidate one sp
     const long cbase = (long)t * R;
     const int ub = 32 * wave + 4 * hi;
     const float4* whl = reinterpret_cast<const float4*>(wh + ub * 12);
+    GM_STAMP(0);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int row = RB * h + col;
@@ -1301,6 +1310,7 @@ if constexpr (FWD_PP && SAVE) {   // (C2 instance only: the per-candidate one sp
         const float o = __shfl_xor(hp_loc[oo], 32);
         if (hi == 0) hp[(FWD_HDEFER ? (s & 1) * 4608 : 0) + (wave * 9 + oo) * 64 + row] = hp_loc[oo] + o;
       }
+      GM_STAMP(1 + h);
     }
     FWD_STAMP(3);
     lds_barrier();   // head partials, the carry and x(t-1) visible
@@ -2650,6 +2660,9 @@ int toued_gru_bwd_fused(int R, int T, int W, int K, const uint8_t* done, long do
 #ifdef FWD_STAMPS
 int toued_dbg_fwd_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd_stamps), sizeof(g_fwd_stamps)) == hipSuccess ? 0 : 1;
+}
+int toued_dbg_fwd_gm_stamps(unsigned long long* host) {   // [64 workgroups][32 steps][4]
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd_gm), sizeof(g_fwd_gm)) == hipSuccess ? 0 : 1;
 }
 int toued_dbg_fwd_pp_stamps(unsigned long long* host) {   // [64 workgroups][32 steps][2 halves][6]
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd_pp), sizeof(g_fwd_pp)) == hipSuccess ? 0 : 1;

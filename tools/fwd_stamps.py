@@ -80,6 +80,15 @@ def main():
     res = {n: float(ph[:, :, i].mean()) for i, n in enumerate(names)}
     res["step total"] = float((st[:, 1:, 0] - st[:, :-1, 0]).mean())
     print(json.dumps({k: round(v) for k, v in res.items()}), flush=True)
+    if "--gm" in sys.argv:   # inside the gate maths: done flags + gate_ain, row tile 0, row tile 1, to the barrier
+        gb = np.zeros(64 * 32 * 4, np.uint64)
+        fg = _lib.lib().toued_dbg_fwd_gm_stamps
+        fg.argtypes = [ctypes.c_void_p]
+        assert fg(gb.ctypes.data) == 0
+        gm = gb.reshape(64, 32, 4)[:, :T].astype(np.int64)
+        parts = {"done flags + gate_ain": gm[..., 0] - st[..., 2], "row tile 0": gm[..., 1] - gm[..., 0],
+                 "row tile 1": gm[..., 2] - gm[..., 1], "head fold to barrier": st[..., 3] - gm[..., 2]}
+        print(json.dumps({k: round(float(v.mean())) for k, v in parts.items()}), flush=True)
 
 
 if __name__ == "__main__":
