@@ -148,6 +148,11 @@ TOUED_DEV int lane_now() {
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
   return l;
 }
+// x of lane l ^ 32, with the source lane re-derived here (__shfl_xor's lane arithmetic, kept live across the step loop
+// by the compiler, was spilled; its reload in the gate maths waited for every outstanding save store)
+TOUED_DEV float xor32(float x) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute((lane_now() ^ 32) << 2, __float_as_int(x)));
+}
 
 // ------------------------------------------------------------------ packing
 // fwdA[(tile*KQF + kq)*64 + lane] = float4 over kk = 4kq..4kq+3 of A[i=l&31][k=2kk+(l>>5)]
@@ -712,6 +717,12 @@ TOUED_DEV unsigned long long fwd_clock() {
 #ifndef FWD_PP_PRIO
 #define FWD_PP_PRIO 0  // FWD_PP: the gate maths' issue priority over the partner wave's contraction
 #endif
+#ifndef FWD_XOR32
+#define FWD_XOR32 0    // the gate maths' head-partial fold through xor32 (no spilled lane index, no store drain)
+#endif
+#ifndef FWD_LANEB
+#define FWD_LANEB 0
+#endif
 #ifndef FWD_CAND0
 #define FWD_CAND0 0    // timing study only: the per-candidate instance reads candidate 0's fragments everywhere
 #endif
@@ -1131,9 +1142,13 @@ if constexpr (FWD_PP && SAVE) {   // (C2 instance only: the per-candidate one sp
       if (FWD_XFIRST) ring();
     }
     auto load_B = [&](int ks, int h) {
+      // (FWD_LANEB: the lane's row and half re-derived instead of a register kept across the step loop -- no spill,
+      // but the contraction issued slower: 1.150-1.152 vs 1.131-1.136 ms, r06t34)
+      const int ln = FWD_LANEB ? lane_now() : lane;
+      const int cl = ln & 31, hl = ln >> 5;
 #pragma unroll
       for (int q = 0; q < 2; ++q)
-        B[h][q] = *reinterpret_cast<const f16x8*>(&hB[q][(RB * h + col) * F6_HP + 16 * ks + 8 * hi]);
+        B[h][q] = *reinterpret_cast<const f16x8*>(&hB[q][(RB * h + cl) * F6_HP + 16 * ks + 8 * hl]);
     };
     load_B(0, 0);
     load_B(0, 1);
@@ -1307,8 +1322,9 @@ if constexpr (FWD_PP && SAVE) {   // (C2 instance only: the per-candidate one sp
       // lanes l and l + 32 hold the same row: fold the two halves, one lane writes
 #pragma unroll
       for (int oo = 0; oo < 9; ++oo) {
-        const float o = __shfl_xor(hp_loc[oo], 32);
-        if (hi == 0) hp[(FWD_HDEFER ? (s & 1) * 4608 : 0) + (wave * 9 + oo) * 64 + row] = hp_loc[oo] + o;
+        const float o = FWD_XOR32 ? xor32(hp_loc[oo]) : __shfl_xor(hp_loc[oo], 32);
+        const int rw = FWD_XOR32 ? RB * h + (lane_now() & 31) : row;   // (re-derived: no spilled address either)
+        if (hi == 0) hp[(FWD_HDEFER ? (s & 1) * 4608 : 0) + (wave * 9 + oo) * 64 + rw] = hp_loc[oo] + o;
       }
       GM_STAMP(1 + h);
     }
